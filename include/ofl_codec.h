@@ -1,0 +1,117 @@
+/*
+ * ofl_codec.h -- C ABI of libofl_codec.so, the MI355X (gfx950) tensor-codec
+ * library behind openfl_amd.pipelines.
+ *
+ * Every entry point is plain C: integers, sizes and raw pointers.  Device
+ * pointers are HIP device addresses on the current device (e.g. a
+ * torch.Tensor's data_ptr()); `stream` is a hipStream_t (e.g.
+ * torch.cuda.current_stream().cuda_stream) passed as void*.  Functions return
+ * 0 on success and a negative OFL_E* code on failure; ofl_last_error() then
+ * returns a thread-local message.  No entry point allocates, frees or
+ * synchronises inside encode/decode, so they are reentrant and
+ * graph-capturable; concurrent calls need separate workspaces.
+ *
+ * The codec replaces the per-tensor Eden transformer of the reference
+ * (securefederatedai/openfl v1.6, /root/reference):
+ *   openfl/pipelines/eden_pipeline.py:555-611  Eden.compress     -> ofl_eden_encode
+ *   openfl/pipelines/eden_pipeline.py:632-659  Eden.decompress   -> ofl_eden_decode
+ *   openfl/pipelines/eden_pipeline.py:569-606  slicing rule      -> ofl_eden_slice_plan
+ *   openfl/pipelines/eden_pipeline.py:771      seed `sum()` term -> ofl_serial_sum_f32/_f64
+ * The Python plugin surface (EdenTransformer.forward/backward,
+ * eden_pipeline.py:761-818) is mirrored by openfl_amd/pipelines/eden_pipeline.py
+ * on top of these calls.  Byte layout of the output planes and the meaning of
+ * every metadata value are identical to the reference's.
+ */
+#ifndef OFL_CODEC_H
+#define OFL_CODEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OFL_OK 0
+#define OFL_EINVAL -1  /* bad argument (n_bits outside 1..8, dims not powers of two, ...) */
+#define OFL_EHIP -2    /* a HIP runtime call failed */
+#define OFL_ESPACE -3  /* workspace too small */
+
+/* Library version string. */
+const char* ofl_version(void);
+
+/* Thread-local message for the last failing call on this thread. */
+const char* ofl_last_error(void);
+
+/* ---- slicing rule (eden_pipeline.py:569-606) ------------------------------
+ * Splits n elements into power-of-two slices: while
+ * (next_po2(rem) - rem) / n > 0.1 take prev_po2(rem); the last slice takes the
+ * remainder.  Each slice is padded to max(next_po2(len), 8) (:541-546).
+ * Writes up to max_slices padded sizes to P_out and valid lengths to len_out
+ * (either may be NULL) and returns the slice count (> max_slices means the
+ * arrays were too small). */
+int ofl_eden_slice_plan(int64_t n, int64_t* P_out, int64_t* len_out, int max_slices);
+
+/* ---- plans ----------------------------------------------------------------
+ * A plan describes a batch of `ntensors` fp32 tensors laid out in one fp32
+ * arena (tensor t starts at element elem_offset[t] and has numel[t] elements)
+ * and their Eden bit planes laid out in one byte arena (tensor t's planes
+ * start at byte ofl_eden_plan_tensor_info(...).planes_offset and hold
+ * n_bits * P_tot(t) / 8 bytes: plane i of tensor t is the byte range
+ * [i * P_tot/8, (i+1) * P_tot/8), byte j bit b = bit i of bin[8j + b], the
+ * reference's to_bits layout, eden_pipeline.py:661-690).
+ *
+ * slice_dims: NULL -> the reference slicing rule; otherwise nslices[t]
+ * padded slice sizes per tensor, concatenated (the P_k values of a received
+ * metadata dict, eden_pipeline.py:650-654).  Slice k of tensor t then holds
+ * elements [sum_{k'<k} P_k', ...) truncated to numel[t] (:656-657).
+ * Creating a plan allocates and uploads its descriptor tables (one
+ * synchronous copy); encode/decode with it do not allocate. */
+typedef struct ofl_eden_plan* ofl_eden_plan_t;
+
+int ofl_eden_plan_create(int ntensors, const int64_t* numel, const int64_t* elem_offset,
+                         const int32_t* nslices, const int64_t* slice_dims, int n_bits,
+                         ofl_eden_plan_t* plan_out);
+void ofl_eden_plan_destroy(ofl_eden_plan_t plan);
+
+/* Totals: slices (= length of the scales array), planes-arena bytes,
+ * workspace bytes needed by encode and decode. */
+int64_t ofl_eden_plan_num_slices(ofl_eden_plan_t plan);
+int64_t ofl_eden_plan_planes_bytes(ofl_eden_plan_t plan);
+int64_t ofl_eden_plan_workspace_bytes(ofl_eden_plan_t plan);
+
+/* Per-tensor placement inside the arenas.  Any out pointer may be NULL. */
+int ofl_eden_plan_tensor_info(ofl_eden_plan_t plan, int t, int64_t* planes_offset,
+                              int64_t* planes_bytes, int32_t* first_slice, int32_t* nslices);
+/* Padded size of every slice of tensor t (nslices entries). */
+int ofl_eden_plan_tensor_dims(ofl_eden_plan_t plan, int t, int64_t* dims_out);
+
+/* ---- encode / decode -------------------------------------------------------
+ * seeds: DEVICE array of ntensors uint32 seeds (the metadata key 0 value,
+ *        eden_pipeline.py:771-779; slices use seed and seed+1, :548-549).
+ * scales: DEVICE float array of ofl_eden_plan_num_slices() entries, slice
+ *        order (metadata keys 2,4,6,... :781-785).
+ * Encode: x_arena (fp32, read only) -> planes_arena (every plane byte of every
+ *        tensor is written) + scales.
+ * Decode: planes_arena + scales -> y_arena (only the numel[t] elements of each
+ *        tensor are written).
+ * ws: DEVICE workspace of at least ofl_eden_plan_workspace_bytes() bytes.
+ * Everything is enqueued on `stream`; nothing synchronises. */
+int ofl_eden_encode(ofl_eden_plan_t plan, const float* x_arena, const uint32_t* seeds,
+                    uint8_t* planes_arena, float* scales, void* ws, size_t ws_bytes,
+                    void* stream);
+int ofl_eden_decode(ofl_eden_plan_t plan, const uint8_t* planes_arena, const uint32_t* seeds,
+                    const float* scales, float* y_arena, void* ws, size_t ws_bytes,
+                    void* stream);
+
+/* ---- host helpers ----------------------------------------------------------
+ * Left-to-right serial sums in the array's own precision: the
+ * `sum(data.flatten())` term of the reference seed formula
+ * (eden_pipeline.py:771, NumPy scalar arithmetic).  Host pointers. */
+float ofl_serial_sum_f32(const float* x, int64_t n);
+double ofl_serial_sum_f64(const double* x, int64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OFL_CODEC_H */

@@ -1,0 +1,77 @@
+"""ctypes binding of libofl_codec.so (include/ofl_codec.h).
+
+The product path has no CPU fallback: if the library is missing or no GPU is
+visible, the codec raises.  torch is imported before the library is loaded so
+that the library binds to the HIP runtime torch already loaded (both carry the
+SONAME libamdhip64.so.7), making torch streams and device pointers valid here.
+"""
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libofl_codec.so")
+_lock = threading.Lock()
+_lib = None
+
+OFL_OK = 0
+
+EXPORTS = (
+    "ofl_version", "ofl_last_error", "ofl_eden_slice_plan", "ofl_eden_plan_create",
+    "ofl_eden_plan_destroy", "ofl_eden_plan_num_slices", "ofl_eden_plan_planes_bytes",
+    "ofl_eden_plan_workspace_bytes", "ofl_eden_plan_tensor_info", "ofl_eden_plan_tensor_dims",
+    "ofl_eden_encode", "ofl_eden_decode", "ofl_serial_sum_f32", "ofl_serial_sum_f64",
+)
+
+
+class CodecError(RuntimeError):
+    pass
+
+
+def _bind(L):
+    i64, i32, vp, sz = ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t
+    L.ofl_version.restype = ctypes.c_char_p
+    L.ofl_last_error.restype = ctypes.c_char_p
+    L.ofl_eden_slice_plan.argtypes = [i64, vp, vp, i32]
+    L.ofl_eden_slice_plan.restype = i32
+    L.ofl_eden_plan_create.argtypes = [i32, vp, vp, vp, vp, i32, ctypes.POINTER(vp)]
+    L.ofl_eden_plan_create.restype = i32
+    L.ofl_eden_plan_destroy.argtypes = [vp]
+    L.ofl_eden_plan_destroy.restype = None
+    for f in ("ofl_eden_plan_num_slices", "ofl_eden_plan_planes_bytes", "ofl_eden_plan_workspace_bytes"):
+        getattr(L, f).argtypes = [vp]
+        getattr(L, f).restype = i64
+    L.ofl_eden_plan_tensor_info.argtypes = [vp, i32, vp, vp, vp, vp]
+    L.ofl_eden_plan_tensor_info.restype = i32
+    L.ofl_eden_plan_tensor_dims.argtypes = [vp, i32, vp]
+    L.ofl_eden_plan_tensor_dims.restype = i32
+    L.ofl_eden_encode.argtypes = [vp, vp, vp, vp, vp, vp, sz, vp]
+    L.ofl_eden_encode.restype = i32
+    L.ofl_eden_decode.argtypes = [vp, vp, vp, vp, vp, vp, sz, vp]
+    L.ofl_eden_decode.restype = i32
+    L.ofl_serial_sum_f32.argtypes = [vp, i64]
+    L.ofl_serial_sum_f32.restype = ctypes.c_float
+    L.ofl_serial_sum_f64.argtypes = [vp, i64]
+    L.ofl_serial_sum_f64.restype = ctypes.c_double
+    return L
+
+
+def lib():
+    """Load (once) and return the bound library; raise if it is not built."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                import torch  # noqa: F401  (HIP runtime first; see module doc)
+                if not os.path.exists(LIB_PATH):
+                    raise CodecError(
+                        f"{LIB_PATH} is missing: build it with `python -m openfl_amd.build` "
+                        "(hipcc --offload-arch=gfx950); openfl_amd has no CPU fallback")
+                _lib = _bind(ctypes.CDLL(LIB_PATH))
+    return _lib
+
+
+def check(rc):
+    if rc != OFL_OK:
+        raise CodecError(lib().ofl_last_error().decode() or f"libofl_codec error {rc}")
+    return rc

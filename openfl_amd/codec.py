@@ -1,0 +1,202 @@
+"""Device-level Eden codec: batch plans over PyTorch-ROCm buffers.
+
+This is the layer the plugin (openfl_amd.pipelines.eden_pipeline) and
+bench.py sit on.  A batch of tensors lives in one fp32 arena (tensor t at
+element offset ``plan.elem_offsets[t]``); its Eden bit planes live in one byte
+arena (tensor t at ``plan.planes_offsets[t]``, ``plan.planes_nbytes[t]``
+bytes, the reference's to_bits layout, eden_pipeline.py:661-690) and its
+per-slice scales in one float array (tensor t's slices start at
+``plan.first_slice[t]``).  Encode/decode are asynchronous on the given HIP
+stream; nothing here synchronises.
+"""
+import ctypes
+import threading
+
+import numpy as np
+import torch
+
+from openfl_amd import _lib
+
+_ALIGN = 64  # elements: every tensor starts 256-B aligned in the fp32 arena
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if isinstance(a, np.ndarray) else ctypes.c_void_p(a)
+
+
+def slice_plan(n):
+    """Reference slicing rule (eden_pipeline.py:569-606): (padded sizes, valid lengths)."""
+    L = _lib.lib()
+    ns = L.ofl_eden_slice_plan(int(n), None, None, 0)
+    P = np.zeros(max(ns, 1), np.int64)
+    ln = np.zeros(max(ns, 1), np.int64)
+    L.ofl_eden_slice_plan(int(n), _ptr(P), _ptr(ln), ns)
+    return [int(v) for v in P[:ns]], [int(v) for v in ln[:ns]]
+
+
+class EdenPlan:
+    """Layout + launch plan for one batch shape (list of numels, optional dims)."""
+
+    def __init__(self, numels, n_bits=8, dims=None, elem_offsets=None):
+        L = _lib.lib()
+        self.n_bits = int(n_bits)
+        self.numels = [int(n) for n in numels]
+        nt = len(self.numels)
+        if elem_offsets is None:
+            offs, acc = [], 0
+            for n in self.numels:
+                offs.append(acc)
+                acc += (n + _ALIGN - 1) // _ALIGN * _ALIGN
+        else:
+            offs = [int(o) for o in elem_offsets]
+        self.arena_numel = max([o + n for o, n in zip(offs, self.numels)] + [0])
+        self.elem_offsets = offs
+        numel_a = np.asarray(self.numels, np.int64)
+        off_a = np.asarray(offs, np.int64)
+        if dims is not None:
+            ns_a = np.asarray([len(d) for d in dims], np.int32)
+            dims_a = np.asarray([int(v) for d in dims for v in d] or [0], np.int64)
+            args = (_ptr(ns_a), _ptr(dims_a))
+        else:
+            args = (None, None)
+        h = ctypes.c_void_p()
+        _lib.check(L.ofl_eden_plan_create(nt, _ptr(numel_a), _ptr(off_a), args[0], args[1],
+                                          self.n_bits, ctypes.byref(h)))
+        self._h = h
+        self._L = L
+        self.n_slices = int(L.ofl_eden_plan_num_slices(h))
+        self.planes_bytes = int(L.ofl_eden_plan_planes_bytes(h))
+        self.ws_bytes = int(L.ofl_eden_plan_workspace_bytes(h))
+        self.planes_offsets, self.planes_nbytes, self.first_slice, self.dims = [], [], [], []
+        for t in range(nt):
+            po, pb = ctypes.c_int64(), ctypes.c_int64()
+            fs, ns = ctypes.c_int32(), ctypes.c_int32()
+            _lib.check(L.ofl_eden_plan_tensor_info(h, t, ctypes.byref(po), ctypes.byref(pb),
+                                                   ctypes.byref(fs), ctypes.byref(ns)))
+            d = np.zeros(max(ns.value, 1), np.int64)
+            _lib.check(L.ofl_eden_plan_tensor_dims(h, t, _ptr(d)))
+            self.planes_offsets.append(po.value)
+            self.planes_nbytes.append(pb.value)
+            self.first_slice.append(fs.value)
+            self.dims.append([int(v) for v in d[:ns.value]])
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            self._L.ofl_eden_plan_destroy(h)
+            self._h = None
+
+    # -- raw launches (all pointers are device tensors) --
+    def encode(self, x_arena, seeds, planes, scales, ws, stream=None):
+        """x_arena fp32[arena_numel] -> planes u8[planes_bytes], scales f32[n_slices]."""
+        self._check(x_arena, torch.float32, self.arena_numel)
+        self._check(planes, torch.uint8, self.planes_bytes)
+        self._check(scales, torch.float32, self.n_slices)
+        self._check(seeds, torch.int32, len(self.numels))
+        st = stream if stream is not None else torch.cuda.current_stream(x_arena.device)
+        _lib.check(self._L.ofl_eden_encode(self._h, x_arena.data_ptr(), seeds.data_ptr(),
+                                           planes.data_ptr(), scales.data_ptr(),
+                                           ws.data_ptr() if ws is not None else None,
+                                           ws.numel() if ws is not None else 0, st.cuda_stream))
+
+    def decode(self, planes, seeds, scales, y_arena, ws, stream=None):
+        """planes u8 + scales f32 -> y_arena fp32 (numel[t] elements of each tensor)."""
+        self._check(y_arena, torch.float32, self.arena_numel)
+        self._check(planes, torch.uint8, self.planes_bytes)
+        self._check(scales, torch.float32, self.n_slices)
+        self._check(seeds, torch.int32, len(self.numels))
+        st = stream if stream is not None else torch.cuda.current_stream(y_arena.device)
+        _lib.check(self._L.ofl_eden_decode(self._h, planes.data_ptr(), seeds.data_ptr(),
+                                           scales.data_ptr(), y_arena.data_ptr(),
+                                           ws.data_ptr() if ws is not None else None,
+                                           ws.numel() if ws is not None else 0, st.cuda_stream))
+
+    @staticmethod
+    def _check(t, dtype, min_numel):
+        if not t.is_cuda:
+            raise _lib.CodecError("openfl_amd codec buffers must be device tensors")
+        if t.dtype != dtype or not t.is_contiguous() or t.numel() < min_numel:
+            raise _lib.CodecError(f"buffer must be contiguous {dtype} with >= {min_numel} elements")
+
+
+class Workspace:
+    """Per-(thread, device) growable device scratch buffer."""
+
+    def __init__(self):
+        self._tls = threading.local()
+
+    def get(self, nbytes, device):
+        bufs = getattr(self._tls, "bufs", None)
+        if bufs is None:
+            bufs = self._tls.bufs = {}
+        key = str(device)
+        b = bufs.get(key)
+        if b is None or b.numel() < nbytes:
+            b = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+            bufs[key] = b
+        return b
+
+
+def resolve_device(device):
+    """Map a reference `device` setting to a ROCm device.
+
+    The reference's Eden defaults to device="cpu" (eden_pipeline.py:738,834).
+    This package only has the gfx950 path, so "cpu"/None select the current
+    GPU; "cuda:N" selects GPU N.  No GPU -> CodecError (no CPU fallback).
+    """
+    if not torch.cuda.is_available():
+        raise _lib.CodecError("openfl_amd Eden codec needs a ROCm GPU (no CPU fallback)")
+    if device is None or str(device) == "cpu":
+        return torch.device("cuda", torch.cuda.current_device())
+    d = torch.device(device)
+    if d.type != "cuda":
+        raise _lib.CodecError(f"unsupported device {device!r}")
+    return d if d.index is not None else torch.device("cuda", torch.cuda.current_device())
+
+
+class EdenCodec:
+    """Batch Eden codec on one device with a plan cache.
+
+    encode(list of fp32 device tensors, seeds) -> (planes u8, scales f32, plan)
+    decode(planes, scales, seeds, plan) -> fp32 arena (slice per tensor with plan).
+    """
+
+    def __init__(self, n_bits=8, device=None, max_plans=256):
+        if n_bits not in (1, 2, 3, 4, 5, 6, 7, 8):
+            raise Exception("nbits value is not supported")  # eden_pipeline.py:389-390
+        self.n_bits = int(n_bits)
+        self.device = resolve_device(device)
+        self._plans = {}
+        self._order = []
+        self._max = max_plans
+        self._lock = threading.Lock()
+        self.ws = Workspace()
+
+    def plan(self, numels, dims=None):
+        key = (tuple(int(n) for n in numels), None if dims is None else tuple(tuple(d) for d in dims))
+        with self._lock:
+            p = self._plans.get(key)
+            if p is None:
+                p = EdenPlan(key[0], self.n_bits, dims=None if dims is None else [list(d) for d in key[1]])
+                self._plans[key] = p
+                self._order.append(key)
+                if len(self._order) > self._max:
+                    self._plans.pop(self._order.pop(0), None)
+            return p
+
+    def seeds_tensor(self, seeds):
+        return torch.tensor([int(s) for s in seeds], dtype=torch.int32).to(self.device, non_blocking=True)
+
+    def encode_arena(self, plan, x_arena, seeds_dev, stream=None):
+        planes = torch.empty(max(plan.planes_bytes, 1), dtype=torch.uint8, device=self.device)
+        scales = torch.empty(max(plan.n_slices, 1), dtype=torch.float32, device=self.device)
+        ws = self.ws.get(plan.ws_bytes, self.device)
+        plan.encode(x_arena, seeds_dev, planes, scales, ws, stream)
+        return planes, scales
+
+    def decode_arena(self, plan, planes, scales, seeds_dev, stream=None, out=None):
+        y = out if out is not None else torch.empty(max(plan.arena_numel, 1), dtype=torch.float32,
+                                                    device=self.device)
+        ws = self.ws.get(plan.ws_bytes, self.device)
+        plan.decode(planes, seeds_dev, scales, y, ws, stream)
+        return y

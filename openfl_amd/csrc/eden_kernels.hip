@@ -1,0 +1,1268 @@
+// eden_kernels.hip -- gfx950 (MI355X / CDNA4) kernels of the Eden codec.
+//
+// Eden (reference: /root/reference/openfl/pipelines/eden_pipeline.py) encodes
+// a slice x of P = 2^p fp32 values as
+//     y = H D2 H D1 x / P           (rht twice, :548-549, :475-488)
+//     bins = bucketize(y sqrt(P) / |y|, B)  scale = |y|^2 / <C[bins], y>  (:505-525)
+// with H the Sylvester Hadamard matrix (:451-473), D1/D2 the rand_diag sign
+// diagonals for seed and seed+1 (:403-449), and packs bins into the global
+// bit-plane layout (:661-690).  Decode is x' = scale * D1 H D2 H C[bins] / P
+// (:613-630).
+//
+// MI355X design (see DESIGN.md for the roofline):
+//  * Every transform is a sequence of FWHT "stages" (one per index bit).  A
+//    workgroup owns a 2^13 / 2^14-element tile; each thread keeps 32 elements
+//    in VGPRs ("layout" = which 5 index bits live in registers) and runs the
+//    stages of those bits as register butterflies.  Between layouts the tile
+//    is transposed through LDS with an XOR swizzle that keeps every ds_write /
+//    ds_read_b32 wave access bank-conflict-free.
+//  * Slices with P <= 2^14 are done in ONE kernel, one workgroup per slice,
+//    straight from HBM to bit planes (encode) or planes to HBM (decode).
+//  * Larger slices use H_P = H_rows (x) H_cols: a row pass (contiguous 2^13
+//    rows), column passes over the remaining bits (2^14-element tiles of
+//    2^m rows x 2^(14-m) contiguous columns) and a final row pass.  The two
+//    Hadamards meet in the middle column pass, which fuses F1's last stages,
+//    D2 and F2's first stages, so a 2-Hadamard encode is 3 HBM passes for
+//    P <= 2^22.
+//  * D1/D2 signs are regenerated on the fly (no sign tensors in HBM); the two
+//    LCG steps are folded into one affine map r2 = A*j + B(seed).
+//  * Normalisation uses exact powers of two (2^-floor(p/2) at D2, 2^-ceil(p/2)
+//    at the end) instead of the reference's two divisions by float32(sqrt P):
+//    identical for even p, < 1e-7 relative apart for odd p.
+//  * bucketize is exact with one compare: a 1/64 grid over z (every cell
+//    holds <= 1 boundary) stored in LDS with {count, 64*B, C_lo, C_hi}.
+//  * Bit planes are produced by an in-register 8x8 bit-matrix transpose of 32
+//    contiguous bins per thread -> one 32-bit store per plane per thread.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "eden_tables.h"
+#include "ofl_codec.h"
+
+#define DEVI __device__ __forceinline__
+
+namespace ofl {
+
+// ---------------------------------------------------------------------------
+// Descriptors (host-built once per plan, uploaded once)
+// ---------------------------------------------------------------------------
+struct SliceDesc {
+    int64_t x_off;      // encode: element offset of the slice's input in the fp32 arena
+    int64_t y_off;      // decode: element offset of the slice's output in the fp32 arena
+    int64_t ylen;       // decode: elements of this slice that land in the output
+    int64_t ws_off;     // element offset of the slice's intermediate in ws (large slices)
+    int64_t pl_off;     // byte offset of the slice's first byte of plane 0
+    int64_t pl_stride;  // bytes between planes of this tensor (= P_tot(t) / 8)
+    int64_t len;        // encode: valid input elements (<= P), zero padded to P
+    int32_t logp;
+    int32_t tensor;
+    int32_t scale_idx;
+    int32_t part_off;   // offset of this slice's partials (large slices)
+};
+
+struct KArgs {
+    const SliceDesc* d;
+    const int32_t* list;    // slice indices for this launch
+    const int32_t* tstart;  // per-list-entry tile prefix (count + 1), multi-tile kernels
+    int32_t count;
+    int32_t nbits;
+    int32_t lo;             // column passes: first transformed bit
+    int32_t pad_;
+    const float* xin;       // fp32 arena in (encode) / ws in
+    float* xout;            // fp32 arena out (decode) / ws out
+    float* ws;              // intermediate buffer base
+    const uint8_t* pin;     // planes in (decode)
+    uint8_t* pout;          // planes out (encode)
+    const uint32_t* seeds;
+    float* scales;          // encode: out
+    const float* scales_in; // decode: in
+    float* part;            // partial sums
+    float* nu;              // per-slice norms (large)
+};
+
+// Eden tables in global memory (read into LDS per workgroup)
+__device__ const float g_centroids[8][256] = {
+#include "eden_centroids.inc"
+};
+
+// ---------------------------------------------------------------------------
+// rand_diag (eden_pipeline.py:403-449)
+// ---------------------------------------------------------------------------
+constexpr uint32_t kLcgA = (uint32_t)(1140671485ull * 1103515245ull);
+
+DEVI uint32_t seed_hash(uint32_t seed) {
+    uint32_t s = seed * 1664525u + 1013904223u;  // & mask32 (:423)
+    return s * 8121u + 28411u;                    // & mask32 (:424)
+}
+// r2 = LCG2(LCG1(j + s)) = A*j + B(s)  (:426-430)
+DEVI uint32_t seed_b(uint32_t seed) {
+    uint32_t s = seed_hash(seed);
+    return 1140671485u * (1103515245u * s + 12345u + s) + 12820163u + s;
+}
+// SplitMix finaliser with the reference's unmasked 33-bit add (:433-436)
+DEVI uint32_t rd_mix(uint32_t r2) {
+    uint32_t lo = r2 + 0x9E3779B9u;
+    uint32_t carry = lo < r2 ? 1u : 0u;
+    uint32_t t = lo ^ (lo >> 16) ^ (carry << 16);
+    t *= 0x85EBCA6Bu;
+    t = (t ^ (t >> 13)) * 0xC2B2AE35u;
+    return t ^ (t >> 16);
+}
+DEVI uint32_t rd_word(uint32_t j, uint32_t b) { return rd_mix(kLcgA * j + b); }
+// sign of element with nibble index nib, word w: +1 iff nibble >= 8 (:440-447)
+DEVI float sgn_apply(float v, uint32_t w, uint32_t nib) {
+    uint32_t bit = (w >> (4u * nib + 3u)) & 1u;
+    return __uint_as_float(__float_as_uint(v) ^ ((bit ^ 1u) << 31));
+}
+DEVI float sgn_elem(float v, uint64_t e, int p, uint32_t b) {
+    const uint64_t S = 1ull << (p - 3);
+    return sgn_apply(v, rd_word((uint32_t)(e & (S - 1)), b), (uint32_t)(e >> (p - 3)));
+}
+
+// ---------------------------------------------------------------------------
+// Register-layout engine
+// ---------------------------------------------------------------------------
+struct Lay { int nb, r0, r1, r2, r3, r4; };
+
+template <Lay L> struct LT {
+    static constexpr int rb(int i) { return i == 0 ? L.r0 : i == 1 ? L.r1 : i == 2 ? L.r2 : i == 3 ? L.r3 : L.r4; }
+    static constexpr uint32_t rmask() { uint32_t m = 0; for (int i = 0; i < 5; ++i) m |= 1u << rb(i); return m; }
+    static constexpr uint32_t off(int r) {
+        uint32_t o = 0;
+        for (int i = 0; i < 5; ++i) if ((r >> i) & 1) o |= 1u << rb(i);
+        return o;
+    }
+    // deposit tid into the non-register bit positions, lowest first
+    DEVI static uint32_t base(uint32_t tid) {
+        uint32_t b = 0;
+        int t = 0;
+#pragma unroll
+        for (int q = 0; q < L.nb; ++q) {
+            if (!((rmask() >> q) & 1u)) { b |= ((tid >> t) & 1u) << q; ++t; }
+        }
+        return b;
+    }
+};
+
+constexpr uint32_t cswz(uint32_t e) { return e ^ (((e >> 5) ^ (e >> 10)) & 31u); }
+DEVI uint32_t swz(uint32_t e) { return e ^ (((e >> 5) ^ (e >> 10)) & 31u); }
+
+// butterflies on every register bit whose element bit is in ACT
+template <Lay L, uint32_t ACT>
+DEVI void stages(float (&v)[32]) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        if ((ACT >> LT<L>::rb(i)) & 1u) {
+#pragma unroll
+            for (int r = 0; r < 32; ++r) {
+                if (!((r >> i) & 1)) {
+                    const float a = v[r], b = v[r | (1 << i)];
+                    v[r] = a + b;
+                    v[r | (1 << i)] = a - b;
+                }
+            }
+        }
+    }
+}
+
+template <Lay A, Lay B>
+DEVI void exchange(float (&v)[32], float* s, uint32_t tid) {
+    const uint32_t ba = swz(LT<A>::base(tid));
+#pragma unroll
+    for (int r = 0; r < 32; ++r) s[ba ^ cswz(LT<A>::off(r))] = v[r];
+    __syncthreads();
+    const uint32_t bb = swz(LT<B>::base(tid));
+#pragma unroll
+    for (int r = 0; r < 32; ++r) v[r] = s[bb ^ cswz(LT<B>::off(r))];
+    __syncthreads();
+}
+
+constexpr uint32_t bits_mask(std::initializer_list<int> l) { uint32_t m = 0; for (int b : l) m |= 1u << b; return m; }
+
+// ---------------------------------------------------------------------------
+// Reductions
+// ---------------------------------------------------------------------------
+DEVI float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+template <int NT>
+DEVI float block_sum(float v, float* red) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) t += red[i];
+    __syncthreads();
+    return t;
+}
+
+// ---------------------------------------------------------------------------
+// Quantiser table in LDS: cell k of z*64 in [k-288, k-287):
+//   {lo = #B < (k-288)/64, 64*B[lo], C[lo], C[lo+1]}
+// ---------------------------------------------------------------------------
+struct QEnt { int lo; float b64; float clo; float chi; };
+__device__ const unsigned char g_grid[8][EDEN_GRID_CELLS] = {
+#include "eden_grid.inc"
+};
+__device__ const float g_bounds[8][256] = {
+#include "eden_bounds.inc"
+};
+
+template <int NT>
+DEVI void load_qtable(QEnt* q, int nbits) {
+    const int nb = (1 << nbits) - 1;
+    for (int k = threadIdx.x; k < EDEN_GRID_CELLS; k += NT) {
+        const int lo = g_grid[nbits - 1][k];
+        QEnt e;
+        e.lo = lo;
+        e.b64 = lo < nb ? g_bounds[nbits - 1][lo] * 64.0f : __int_as_float(0x7f800000);
+        e.clo = g_centroids[nbits - 1][lo];
+        e.chi = g_centroids[nbits - 1][lo < nb ? lo + 1 : lo];
+        q[k] = e;
+    }
+}
+
+// bucketize + centroid: returns bin, writes centroid
+DEVI int quant(float z64, const QEnt* q, float& c) {
+    float f = floorf(z64);
+    f = fminf(fmaxf(f, -288.0f), 287.0f);
+    const int k = (int)f + EDEN_GRID_OFF;  // NaN -> clamp gives 287 or -288 path; harmless
+    const QEnt e = q[k];
+    const bool up = e.b64 < z64;
+    c = up ? e.chi : e.clo;
+    return e.lo + (up ? 1 : 0);
+}
+
+// ---------------------------------------------------------------------------
+// 32 contiguous bins <-> nbits 32-bit plane words (8x8 bit transposes)
+// ---------------------------------------------------------------------------
+DEVI uint64_t tr8x8(uint64_t x) {
+    uint64_t t;
+    t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;  x ^= t ^ (t << 7);
+    t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull; x ^= t ^ (t << 14);
+    t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull; x ^= t ^ (t << 28);
+    return x;
+}
+// bins[32] (each < 256) -> w[8]: bit t of w[i] = bit i of bins[t]
+DEVI void pack32(const int (&bins)[32], uint32_t (&w)[8]) {
+    uint64_t g[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        uint64_t x = 0;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) x |= (uint64_t)(uint32_t)bins[8 * q + t] << (8 * t);
+        g[q] = tr8x8(x);  // byte i of g[q] = plane i bits of elements 8q..8q+7
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint32_t r = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) r |= (uint32_t)((g[q] >> (8 * i)) & 0xffu) << (8 * q);
+        w[i] = r;
+    }
+}
+DEVI void unpack32(const uint32_t (&w)[8], int (&bins)[32]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        uint64_t x = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x |= (uint64_t)((w[i] >> (8 * q)) & 0xffu) << (8 * i);
+        x = tr8x8(x);  // transpose is an involution
+#pragma unroll
+        for (int t = 0; t < 8; ++t) bins[8 * q + t] = (int)((x >> (8 * t)) & 0xffu);
+    }
+}
+DEVI void store_plane_word(uint8_t* p, uint32_t w) {
+    if ((reinterpret_cast<uintptr_t>(p) & 3u) == 0) {
+        *reinterpret_cast<uint32_t*>(p) = w;
+    } else {
+        p[0] = (uint8_t)w; p[1] = (uint8_t)(w >> 8); p[2] = (uint8_t)(w >> 16); p[3] = (uint8_t)(w >> 24);
+    }
+}
+DEVI uint32_t load_plane_word(const uint8_t* p) {
+    if ((reinterpret_cast<uintptr_t>(p) & 3u) == 0) return *reinterpret_cast<const uint32_t*>(p);
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+DEVI float pow2i(int e) { return __int_as_float((127 + e) << 23); }  // 2^e, |e| < 127
+
+// ---------------------------------------------------------------------------
+// fp32 element I/O with valid-length bound (zero padding, :541-546)
+// ---------------------------------------------------------------------------
+DEVI void load4(const float* base, int64_t i, int64_t len, float* v) {
+    if (i + 3 < len && ((reinterpret_cast<uintptr_t>(base + i) & 15u) == 0)) {
+        const float4 f = *reinterpret_cast<const float4*>(base + i);
+        v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = (i + q < len) ? base[i + q] : 0.0f;
+    }
+}
+DEVI void store4(float* base, int64_t i, int64_t len, const float* v) {
+    if (i + 3 < len && ((reinterpret_cast<uintptr_t>(base + i) & 15u) == 0)) {
+        *reinterpret_cast<float4*>(base + i) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) if (i + q < len) base[i + q] = v[q];
+    }
+}
+
+// block-uniform slice lookup for multi-tile launches
+DEVI void find_tile(const KArgs& a, int& slice, int64_t& tile) {
+    const int64_t b = blockIdx.x;
+    int lo = 0, hi = a.count - 1;
+    while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if (a.tstart[mid] <= b) lo = mid; else hi = mid - 1;
+    }
+    slice = a.list[lo];
+    tile = b - a.tstart[lo];
+}
+
+// ===========================================================================
+// Layout sets.  Small slices: one set per p in 11..14 (tile = slice, NT =
+// 2^(p-5)).  Row passes of large slices reuse the p = 13 set.
+//   encode: L1 (load, D1) F1 -> L2 F1 -> L3 F1 | D2 | L3 F2 -> L4 F2 -> L5 F2 (pack)
+//   decode: the reverse.
+// Lanes 0..31 of every layout vary 5 index bits with distinct residues mod 5,
+// so swz() keeps every exchange bank-conflict-free.
+// ===========================================================================
+template <int P> struct SmallSet;
+template <> struct SmallSet<11> {
+    static constexpr Lay L1{11, 0, 1, 8, 9, 10}, L2{11, 2, 3, 4, 5, 6}, L3{11, 5, 7, 8, 9, 10},
+                         L4{11, 6, 7, 8, 9, 10}, L5{11, 0, 1, 2, 3, 4};
+    static constexpr uint32_t F1a = bits_mask({0, 1, 8, 9, 10}), F1b = bits_mask({2, 3, 4, 5, 6}),
+                              F1c = bits_mask({7}), F2c = bits_mask({5, 7, 8, 9, 10}),
+                              F2d = bits_mask({6}), F2e = bits_mask({0, 1, 2, 3, 4});
+};
+template <> struct SmallSet<12> {
+    static constexpr Lay L1{12, 0, 1, 9, 10, 11}, L2{12, 2, 3, 4, 5, 6}, L3{12, 7, 8, 9, 10, 11},
+                         L4{12, 5, 6, 9, 10, 11}, L5{12, 0, 1, 2, 3, 4};
+    static constexpr uint32_t F1a = bits_mask({0, 1, 9, 10, 11}), F1b = bits_mask({2, 3, 4, 5, 6}),
+                              F1c = bits_mask({7, 8}), F2c = bits_mask({7, 8, 9, 10, 11}),
+                              F2d = bits_mask({5, 6}), F2e = bits_mask({0, 1, 2, 3, 4});
+};
+template <> struct SmallSet<13> {
+    static constexpr Lay L1{13, 0, 1, 10, 11, 12}, L2{13, 2, 3, 4, 5, 6}, L3{13, 7, 8, 9, 10, 11},
+                         L4{13, 5, 6, 10, 11, 12}, L5{13, 0, 1, 2, 3, 4};
+    static constexpr uint32_t F1a = bits_mask({0, 1, 10, 11, 12}), F1b = bits_mask({2, 3, 4, 5, 6}),
+                              F1c = bits_mask({7, 8, 9}), F2c = bits_mask({7, 8, 9, 10, 11}),
+                              F2d = bits_mask({5, 6, 12}), F2e = bits_mask({0, 1, 2, 3, 4});
+};
+template <> struct SmallSet<14> {
+    static constexpr Lay L1{14, 0, 1, 11, 12, 13}, L2{14, 2, 3, 4, 5, 6}, L3{14, 7, 8, 9, 10, 11},
+                         L4{14, 5, 6, 11, 12, 13}, L5{14, 0, 1, 2, 3, 4};
+    static constexpr uint32_t F1a = bits_mask({0, 1, 11, 12, 13}), F1b = bits_mask({2, 3, 4, 5, 6}),
+                              F1c = bits_mask({7, 8, 9, 10}), F2c = bits_mask({7, 8, 9, 10, 11}),
+                              F2d = bits_mask({5, 6, 12, 13}), F2e = bits_mask({0, 1, 2, 3, 4});
+};
+
+// signs of the 32 register elements of layout L from an LDS word table
+template <Lay L>
+DEVI void apply_signs_tab(float (&v)[32], uint32_t base, const uint32_t* tab, int p, float mul) {
+    const uint32_t jm = (1u << (p - 3)) - 1u;
+#pragma unroll
+    for (int r = 0; r < 32; ++r) {
+        const uint32_t e = base | LT<L>::off(r);
+        v[r] = sgn_apply(v[r] * mul, tab[e & jm], e >> (p - 3));
+    }
+}
+// signs of the 32 register elements computed directly (rows of large slices)
+template <Lay L>
+DEVI void apply_signs_direct(float (&v)[32], uint64_t ebase, uint32_t base, int p, uint32_t b,
+                             float mul) {
+#pragma unroll
+    for (int r = 0; r < 32; ++r) v[r] = sgn_elem(v[r] * mul, ebase + (base | LT<L>::off(r)), p, b);
+}
+
+// quantise 32 contiguous values: bins + partial dot <C[bins], y>
+DEVI float quant32(const float (&v)[32], float ysc, float zm64, const QEnt* q, int (&bins)[32]) {
+    float dot = 0.f;
+#pragma unroll
+    for (int r = 0; r < 32; ++r) {
+        const float y = v[r] * ysc;
+        float c;
+        bins[r] = quant(y * zm64, q, c);
+        dot += c * y;
+    }
+    return dot;
+}
+// pack 32 contiguous bins starting at slice element `e` into every plane
+DEVI void pack_store(int (&bins)[32], bool zero, uint8_t* plane0, int64_t e, int64_t stride, int nbits) {
+    if (zero) {
+#pragma unroll
+        for (int r = 0; r < 32; ++r) bins[r] = 0;
+    }
+    uint32_t w[8];
+    pack32(bins, w);
+    uint8_t* p = plane0 + (e >> 3);
+    for (int i = 0; i < nbits; ++i) store_plane_word(p + (int64_t)i * stride, w[i]);
+}
+
+// ===========================================================================
+// Small slices (2^11 <= P <= 2^14): one workgroup per slice, whole codec.
+// ===========================================================================
+template <int P_LOG>
+__global__ __launch_bounds__(1 << (P_LOG - 5)) void k_enc_small(KArgs a) {
+    using S = SmallSet<P_LOG>;
+    constexpr int NT = 1 << (P_LOG - 5);
+    constexpr int NS = 1 << (P_LOG - 3);
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float* s = reinterpret_cast<float*>(smem);                       // 4 * 2^p
+    uint32_t* tab1 = reinterpret_cast<uint32_t*>(s + (1 << P_LOG));  // NS words
+    uint32_t* tab2 = tab1 + NS;                                      // NS words
+    QEnt* qt = reinterpret_cast<QEnt*>(tab2 + NS);                   // 576 * 16 B
+    float* red = reinterpret_cast<float*>(qt + EDEN_GRID_CELLS);     // NT/64
+
+    const SliceDesc D = a.d[a.list[blockIdx.x]];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t seed = a.seeds[D.tensor];
+    const uint32_t b1 = seed_b(seed), b2 = seed_b(seed + 1u);
+    for (int j = tid; j < NS; j += NT) { tab1[j] = rd_word(j, b1); tab2[j] = rd_word(j, b2); }
+    load_qtable<NT>(qt, a.nbits);
+
+    float v[32];
+    const float* x = a.xin + D.x_off;
+    {
+        const uint32_t base = LT<S::L1>::base(tid);
+#pragma unroll
+        for (int r = 0; r < 32; r += 4) load4(x, base | LT<S::L1>::off(r), D.len, &v[r]);
+    }
+    __syncthreads();  // tables ready
+    apply_signs_tab<S::L1>(v, LT<S::L1>::base(tid), tab1, P_LOG, 1.0f);
+    stages<S::L1, S::F1a>(v);
+    exchange<S::L1, S::L2>(v, s, tid);
+    stages<S::L2, S::F1b>(v);
+    exchange<S::L2, S::L3>(v, s, tid);
+    stages<S::L3, S::F1c>(v);
+    apply_signs_tab<S::L3>(v, LT<S::L3>::base(tid), tab2, P_LOG, pow2i(-(P_LOG / 2)));
+    stages<S::L3, S::F2c>(v);
+    exchange<S::L3, S::L4>(v, s, tid);
+    stages<S::L4, S::F2d>(v);
+    exchange<S::L4, S::L5>(v, s, tid);
+    stages<S::L5, S::F2e>(v);
+
+    const float ysc = pow2i(-((P_LOG + 1) / 2));
+    float ss = 0.f;
+#pragma unroll
+    for (int r = 0; r < 32; ++r) { const float y = v[r] * ysc; ss += y * y; }
+    ss = block_sum<NT>(ss, red);
+    const float nu = sqrtf(ss);
+    const bool pos = nu > 0.0f;
+    const float zm64 = 64.0f * (sqrtf((float)(1 << P_LOG)) / nu);
+    int bins[32];
+    float dot = quant32(v, ysc, zm64, qt, bins);
+    if (!pos) dot = 0.f;
+    dot = block_sum<NT>(dot, red);
+    float scale = pos ? (nu * nu) / dot : 0.0f;
+    const bool zero = !pos || isnan(scale);  // reference zero fallback (:517-525)
+    if (zero) scale = 0.0f;
+    pack_store(bins, zero, a.pout + D.pl_off, LT<S::L5>::base(tid), D.pl_stride, a.nbits);
+    if (tid == 0) a.scales[D.scale_idx] = scale;
+}
+
+template <int P_LOG>
+__global__ __launch_bounds__(1 << (P_LOG - 5)) void k_dec_small(KArgs a) {
+    using S = SmallSet<P_LOG>;
+    constexpr int NT = 1 << (P_LOG - 5);
+    constexpr int NS = 1 << (P_LOG - 3);
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float* s = reinterpret_cast<float*>(smem);
+    uint32_t* tab1 = reinterpret_cast<uint32_t*>(s + (1 << P_LOG));
+    uint32_t* tab2 = tab1 + NS;
+    float* cen = reinterpret_cast<float*>(tab2 + NS);  // 256
+
+    const SliceDesc D = a.d[a.list[blockIdx.x]];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t seed = a.seeds[D.tensor];
+    const uint32_t b1 = seed_b(seed), b2 = seed_b(seed + 1u);
+    for (int j = tid; j < NS; j += NT) { tab1[j] = rd_word(j, b1); tab2[j] = rd_word(j, b2); }
+    for (int j = tid; j < 256; j += NT) cen[j] = g_centroids[a.nbits - 1][j];
+    float v[32];
+    {
+        const uint32_t base = LT<S::L5>::base(tid);
+        const uint8_t* p = a.pin + D.pl_off + (base >> 3);
+        uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int i = 0; i < a.nbits; ++i) w[i] = load_plane_word(p + (int64_t)i * D.pl_stride);
+        int bins[32];
+        unpack32(w, bins);
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 32; ++r) v[r] = cen[bins[r]];
+    }
+    stages<S::L5, S::F2e>(v);
+    exchange<S::L5, S::L4>(v, s, tid);
+    stages<S::L4, S::F2d>(v);
+    exchange<S::L4, S::L3>(v, s, tid);
+    stages<S::L3, S::F2c>(v);
+    apply_signs_tab<S::L3>(v, LT<S::L3>::base(tid), tab2, P_LOG, pow2i(-(P_LOG / 2)));
+    stages<S::L3, S::F1c>(v);
+    exchange<S::L3, S::L2>(v, s, tid);
+    stages<S::L2, S::F1b>(v);
+    exchange<S::L2, S::L1>(v, s, tid);
+    stages<S::L1, S::F1a>(v);
+    const float sc = a.scales_in[D.scale_idx];
+    const uint32_t base = LT<S::L1>::base(tid);
+    apply_signs_tab<S::L1>(v, base, tab1, P_LOG, pow2i(-((P_LOG + 1) / 2)));
+#pragma unroll
+    for (int r = 0; r < 32; ++r) v[r] = sc * v[r];
+    float* y = a.xout + D.y_off;
+#pragma unroll
+    for (int r = 0; r < 32; r += 4) store4(y, base | LT<S::L1>::off(r), D.ylen, &v[r]);
+}
+
+// ===========================================================================
+// Tiny slices (P <= 2^10): one 64-thread workgroup per slice, LDS-resident.
+// ===========================================================================
+DEVI void fwht_lds_generic(float* s, int P) {
+    for (int h = 1; h < P; h <<= 1) {
+        for (int q = threadIdx.x; q < (P >> 1); q += 64) {
+            const int i = ((q & ~(h - 1)) << 1) | (q & (h - 1));
+            const float a = s[i], b = s[i + h];
+            s[i] = a + b;
+            s[i + h] = a - b;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(64) void k_enc_tiny(KArgs a) {
+    __shared__ float s[1024];
+    __shared__ unsigned char bins[1024];
+    __shared__ QEnt qt[EDEN_GRID_CELLS];
+    __shared__ float red[1];
+    const SliceDesc D = a.d[a.list[blockIdx.x]];
+    const int p = D.logp, P = 1 << p;
+    const uint32_t seed = a.seeds[D.tensor];
+    const uint32_t b1 = seed_b(seed), b2 = seed_b(seed + 1u);
+    load_qtable<64>(qt, a.nbits);
+    const float* x = a.xin + D.x_off;
+    for (int e = threadIdx.x; e < P; e += 64)
+        s[e] = sgn_elem(e < D.len ? x[e] : 0.0f, (uint64_t)e, p, b1);
+    __syncthreads();
+    fwht_lds_generic(s, P);
+    const float m2 = pow2i(-(p / 2));
+    for (int e = threadIdx.x; e < P; e += 64) s[e] = sgn_elem(s[e] * m2, (uint64_t)e, p, b2);
+    __syncthreads();
+    fwht_lds_generic(s, P);
+    const float ysc = pow2i(-((p + 1) / 2));
+    float ss = 0.f;
+    for (int e = threadIdx.x; e < P; e += 64) { const float y = s[e] * ysc; s[e] = y; ss += y * y; }
+    ss = block_sum<64>(ss, red);
+    const float nu = sqrtf(ss);
+    const bool pos = nu > 0.0f;
+    const float zm64 = 64.0f * (sqrtf((float)P) / nu);
+    float dot = 0.f;
+    for (int e = threadIdx.x; e < P; e += 64) {
+        float c;
+        const int b = pos ? quant(s[e] * zm64, qt, c) : 0;
+        if (pos) dot += c * s[e];
+        bins[e] = (unsigned char)b;
+    }
+    dot = block_sum<64>(dot, red);
+    float scale = pos ? (nu * nu) / dot : 0.0f;
+    const bool zero = !pos || isnan(scale);
+    if (zero) scale = 0.0f;
+    __syncthreads();
+    uint8_t* pl = a.pout + D.pl_off;
+    for (int q = threadIdx.x; q < (P >> 3) * a.nbits; q += 64) {
+        const int i = q / (P >> 3), j = q % (P >> 3);
+        uint32_t by = 0;
+        if (!zero)
+            for (int t = 0; t < 8; ++t) by |= ((uint32_t)(bins[8 * j + t] >> i) & 1u) << t;
+        pl[(int64_t)i * D.pl_stride + j] = (uint8_t)by;
+    }
+    if (threadIdx.x == 0) a.scales[D.scale_idx] = scale;
+}
+
+__global__ __launch_bounds__(64) void k_dec_tiny(KArgs a) {
+    __shared__ float s[1024];
+    const SliceDesc D = a.d[a.list[blockIdx.x]];
+    const int p = D.logp, P = 1 << p;
+    const uint32_t seed = a.seeds[D.tensor];
+    const uint32_t b1 = seed_b(seed), b2 = seed_b(seed + 1u);
+    const uint8_t* pl = a.pin + D.pl_off;
+    for (int e = threadIdx.x; e < P; e += 64) {
+        int b = 0;
+        for (int i = 0; i < a.nbits; ++i) b |= ((pl[(int64_t)i * D.pl_stride + (e >> 3)] >> (e & 7)) & 1) << i;
+        s[e] = g_centroids[a.nbits - 1][b];
+    }
+    __syncthreads();
+    fwht_lds_generic(s, P);
+    const float m2 = pow2i(-(p / 2));
+    for (int e = threadIdx.x; e < P; e += 64) s[e] = sgn_elem(s[e] * m2, (uint64_t)e, p, b2);
+    __syncthreads();
+    fwht_lds_generic(s, P);
+    const float m1 = pow2i(-((p + 1) / 2));
+    const float sc = a.scales_in[D.scale_idx];
+    float* y = a.xout + D.y_off;
+    for (int e = threadIdx.x; e < P; e += 64)
+        if (e < D.ylen) y[e] = sc * sgn_elem(s[e] * m1, (uint64_t)e, p, b1);
+}
+
+// ===========================================================================
+// Large slices (P >= 2^15): row passes (2^13 contiguous, NT = 256)
+// ===========================================================================
+using RS = SmallSet<13>;
+constexpr int kRowLog = 13;
+constexpr int kRowNT = 256;
+
+// encode pass A: x -> D1 -> F1 row stages -> ws ; partial sum of x^2
+__global__ __launch_bounds__(kRowNT) void k_enc_rowA(KArgs a) {
+    __shared__ __attribute__((aligned(16))) float s[1 << kRowLog];
+    __shared__ float red[kRowNT / 64];
+    int si; int64_t tile;
+    find_tile(a, si, tile);
+    const SliceDesc D = a.d[si];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t b1 = seed_b(a.seeds[D.tensor]);
+    const int64_t e0 = tile << kRowLog;
+    float v[32];
+    const uint32_t base1 = LT<RS::L1>::base(tid);
+    const float* x = a.xin + D.x_off + e0;
+    const int64_t len = D.len - e0;
+#pragma unroll
+    for (int r = 0; r < 32; r += 4) load4(x, base1 | LT<RS::L1>::off(r), len, &v[r]);
+    float ss = 0.f;
+#pragma unroll
+    for (int r = 0; r < 32; ++r) ss += v[r] * v[r];
+    apply_signs_direct<RS::L1>(v, (uint64_t)e0, base1, D.logp, b1, 1.0f);
+    stages<RS::L1, RS::F1a>(v);
+    exchange<RS::L1, RS::L2>(v, s, tid);
+    stages<RS::L2, RS::F1b>(v);
+    exchange<RS::L2, RS::L3>(v, s, tid);
+    stages<RS::L3, RS::F1c>(v);
+    float* w = a.ws + D.ws_off + e0;
+    const uint32_t base3 = LT<RS::L3>::base(tid);
+#pragma unroll
+    for (int r = 0; r < 32; ++r) w[base3 | LT<RS::L3>::off(r)] = v[r];
+    ss = block_sum<kRowNT>(ss, red);
+    if (tid == 0) a.part[D.part_off + tile] = ss;
+}
+
+// encode pass C: ws -> F2 row stages -> y -> quantise, pack ; partial dot
+__global__ __launch_bounds__(kRowNT) void k_enc_rowC(KArgs a) {
+    __shared__ __attribute__((aligned(16))) float s[1 << kRowLog];
+    __shared__ QEnt qt[EDEN_GRID_CELLS];
+    __shared__ float red[kRowNT / 64];
+    int si; int64_t tile;
+    find_tile(a, si, tile);
+    const SliceDesc D = a.d[si];
+    const uint32_t tid = threadIdx.x;
+    load_qtable<kRowNT>(qt, a.nbits);
+    const int64_t e0 = tile << kRowLog;
+    float v[32];
+    const float* w = a.ws + D.ws_off + e0;
+    const uint32_t base3 = LT<RS::L3>::base(tid);
+#pragma unroll
+    for (int r = 0; r < 32; ++r) v[r] = w[base3 | LT<RS::L3>::off(r)];
+    stages<RS::L3, RS::F2c>(v);
+    exchange<RS::L3, RS::L4>(v, s, tid);
+    stages<RS::L4, RS::F2d>(v);
+    exchange<RS::L4, RS::L5>(v, s, tid);  // also orders qt writes before use
+    stages<RS::L5, RS::F2e>(v);
+    const float nu = a.nu[si];
+    const bool pos = nu > 0.0f;
+    const float ysc = pow2i(-((D.logp + 1) / 2));
+    const float zm64 = 64.0f * (sqrtf((float)(1ll << D.logp)) / nu);
+    int bins[32];
+    float dot = quant32(v, ysc, zm64, qt, bins);
+    pack_store(bins, !pos, a.pout + D.pl_off, e0 + LT<RS::L5>::base(tid), D.pl_stride, a.nbits);
+    if (!pos) dot = 0.f;
+    dot = block_sum<kRowNT>(dot, red);
+    if (tid == 0) a.part[D.part_off + tile] = dot;
+}
+
+// decode pass A: planes -> C[bins] -> G1 row stages -> ws
+__global__ __launch_bounds__(kRowNT) void k_dec_rowA(KArgs a) {
+    __shared__ __attribute__((aligned(16))) float s[1 << kRowLog];
+    __shared__ float cen[256];
+    int si; int64_t tile;
+    find_tile(a, si, tile);
+    const SliceDesc D = a.d[si];
+    const uint32_t tid = threadIdx.x;
+    cen[tid] = g_centroids[a.nbits - 1][tid];
+    const int64_t e0 = tile << kRowLog;
+    float v[32];
+    const uint32_t base5 = LT<RS::L5>::base(tid);
+    {
+        const uint8_t* p = a.pin + D.pl_off + (e0 >> 3) + (base5 >> 3);
+        uint32_t wd[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int i = 0; i < a.nbits; ++i) wd[i] = load_plane_word(p + (int64_t)i * D.pl_stride);
+        int bins[32];
+        unpack32(wd, bins);
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 32; ++r) v[r] = cen[bins[r]];
+    }
+    stages<RS::L5, RS::F2e>(v);
+    exchange<RS::L5, RS::L4>(v, s, tid);
+    stages<RS::L4, RS::F2d>(v);
+    exchange<RS::L4, RS::L3>(v, s, tid);
+    stages<RS::L3, RS::F2c>(v);
+    float* w = a.ws + D.ws_off + e0;
+    const uint32_t base3 = LT<RS::L3>::base(tid);
+#pragma unroll
+    for (int r = 0; r < 32; ++r) w[base3 | LT<RS::L3>::off(r)] = v[r];
+}
+
+// decode pass C: ws -> G2 row stages -> D1, scale -> y
+__global__ __launch_bounds__(kRowNT) void k_dec_rowC(KArgs a) {
+    __shared__ __attribute__((aligned(16))) float s[1 << kRowLog];
+    int si; int64_t tile;
+    find_tile(a, si, tile);
+    const SliceDesc D = a.d[si];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t b1 = seed_b(a.seeds[D.tensor]);
+    const int64_t e0 = tile << kRowLog;
+    float v[32];
+    const float* w = a.ws + D.ws_off + e0;
+    const uint32_t base3 = LT<RS::L3>::base(tid);
+#pragma unroll
+    for (int r = 0; r < 32; ++r) v[r] = w[base3 | LT<RS::L3>::off(r)];
+    stages<RS::L3, RS::F1c>(v);
+    exchange<RS::L3, RS::L2>(v, s, tid);
+    stages<RS::L2, RS::F1b>(v);
+    exchange<RS::L2, RS::L1>(v, s, tid);
+    stages<RS::L1, RS::F1a>(v);
+    const uint32_t base1 = LT<RS::L1>::base(tid);
+    apply_signs_direct<RS::L1>(v, (uint64_t)e0, base1, D.logp, b1, pow2i(-((D.logp + 1) / 2)));
+    const float sc = a.scales_in[D.scale_idx];
+#pragma unroll
+    for (int r = 0; r < 32; ++r) v[r] = sc * v[r];
+    float* y = a.xout + D.y_off + e0;
+    const int64_t len = D.ylen - e0;
+#pragma unroll
+    for (int r = 0; r < 32; r += 4) store4(y, base1 | LT<RS::L1>::off(r), len, &v[r]);
+}
+
+// ===========================================================================
+// Column passes: tile = 2^M rows (index bits [lo, lo+M)) x 2^(14-M)
+// contiguous columns (bits [0, 14-M)), NT = 512.  MID fuses F1 | D2 | F2.
+// ===========================================================================
+constexpr int kColNT = 512;
+template <int M> struct ColSet {
+    static constexpr int K = 14 - M;
+    static constexpr int m1 = M < 5 ? M : 5;
+    // L1: rows K..K+m1-1, filled with top columns K-1, K-2, ...
+    static constexpr int l1(int i) { return i < m1 ? K + i : K - 1 - (i - m1); }
+    static constexpr Lay L1{14, l1(0), l1(1), l1(2), l1(3), l1(4)};
+    // L2: rows K+5..K+M-1, filled with rows K, K+1, ...
+    static constexpr int l2(int i) { return i < M - 5 ? K + 5 + i : K + (i - (M - 5)); }
+    static constexpr Lay L2{14, l2(0), l2(1), l2(2), l2(3), l2(4)};
+    static constexpr uint32_t A1 = ((1u << m1) - 1u) << K;
+    static constexpr uint32_t A2 = M > 5 ? ((1u << (M - 5)) - 1u) << (K + 5) : 0u;
+};
+
+template <int M, bool MID>
+__global__ __launch_bounds__(kColNT) void k_col(KArgs a) {
+    using CS = ColSet<M>;
+    constexpr int K = CS::K;
+    __shared__ __attribute__((aligned(16))) float s[M > 5 ? (1 << 14) : 1];
+    int si; int64_t tile;
+    find_tile(a, si, tile);
+    const SliceDesc D = a.d[si];
+    const uint32_t tid = threadIdx.x;
+    const int lo = a.lo;
+    // tile -> slice bits: [K, lo) from tile low bits, [lo+M, p) from the rest
+    const int64_t tl = tile & ((1ll << (lo - K)) - 1);
+    const int64_t th = tile >> (lo - K);
+    const int64_t tb = (tl << K) | (th << (lo + M));
+    float* w = a.ws + D.ws_off;
+    auto map = [&](uint32_t t) -> int64_t {
+        return tb | (int64_t)(t & ((1u << K) - 1u)) | ((int64_t)(t >> K) << lo);
+    };
+    float v[32];
+    const uint32_t base1 = LT<CS::L1>::base(tid);
+#pragma unroll
+    for (int r = 0; r < 32; ++r) v[r] = w[map(base1 | LT<CS::L1>::off(r))];
+    stages<CS::L1, CS::A1>(v);
+    if constexpr (M > 5) {
+        exchange<CS::L1, CS::L2>(v, s, tid);
+        stages<CS::L2, CS::A2>(v);
+    }
+    if constexpr (MID) {
+        const uint32_t b2 = seed_b(a.seeds[D.tensor] + 1u);
+        const float m2 = pow2i(-(D.logp / 2));
+        if constexpr (M > 5) {
+            const uint32_t base2 = LT<CS::L2>::base(tid);
+#pragma unroll
+            for (int r = 0; r < 32; ++r)
+                v[r] = sgn_elem(v[r] * m2, (uint64_t)map(base2 | LT<CS::L2>::off(r)), D.logp, b2);
+            stages<CS::L2, CS::A2>(v);
+            exchange<CS::L2, CS::L1>(v, s, tid);
+            stages<CS::L1, CS::A1>(v);
+        } else {
+#pragma unroll
+            for (int r = 0; r < 32; ++r)
+                v[r] = sgn_elem(v[r] * m2, (uint64_t)map(base1 | LT<CS::L1>::off(r)), D.logp, b2);
+            stages<CS::L1, CS::A1>(v);
+        }
+#pragma unroll
+        for (int r = 0; r < 32; ++r) w[map(base1 | LT<CS::L1>::off(r))] = v[r];
+    } else {
+        if constexpr (M > 5) {
+            const uint32_t base2 = LT<CS::L2>::base(tid);
+#pragma unroll
+            for (int r = 0; r < 32; ++r) w[map(base2 | LT<CS::L2>::off(r))] = v[r];
+        } else {
+#pragma unroll
+            for (int r = 0; r < 32; ++r) w[map(base1 | LT<CS::L1>::off(r))] = v[r];
+        }
+    }
+}
+
+// ===========================================================================
+// Per-slice reductions (large slices): norms before pass C, scales after.
+// ===========================================================================
+__global__ __launch_bounds__(256) void k_norms(KArgs a) {
+    __shared__ float red[4];
+    const int si = a.list[blockIdx.x];
+    const SliceDesc D = a.d[si];
+    const int64_t ntile = 1ll << (D.logp - kRowLog);
+    float ss = 0.f;
+    for (int64_t t = threadIdx.x; t < ntile; t += 256) ss += a.part[D.part_off + t];
+    ss = block_sum<256>(ss, red);
+    if (threadIdx.x == 0) a.nu[si] = sqrtf(ss);
+}
+
+__global__ __launch_bounds__(256) void k_finalize(KArgs a) {
+    __shared__ float red[4];
+    const int si = a.list[blockIdx.x];
+    const SliceDesc D = a.d[si];
+    const int64_t ntile = 1ll << (D.logp - kRowLog);
+    float dot = 0.f;
+    for (int64_t t = threadIdx.x; t < ntile; t += 256) dot += a.part[D.part_off + t];
+    dot = block_sum<256>(dot, red);
+    const float nu = a.nu[si];
+    const bool pos = nu > 0.0f;
+    float scale = pos ? (nu * nu) / dot : 0.0f;
+    const bool zero = !pos || isnan(scale);
+    if (threadIdx.x == 0) a.scales[D.scale_idx] = zero ? 0.0f : scale;
+    if (pos && zero) {  // rare: NaN scale -> reference returns all-zero bins (:522-525)
+        const int64_t nbytes = 1ll << (D.logp - 3);
+        for (int i = 0; i < a.nbits; ++i)
+            for (int64_t q = threadIdx.x; q < nbytes; q += 256) a.pout[D.pl_off + i * D.pl_stride + q] = 0;
+    }
+}
+
+}  // namespace ofl
+
+// ===========================================================================
+// Host side: plans and the C ABI
+// ===========================================================================
+namespace {
+
+thread_local std::string g_err;
+int fail(int code, const std::string& msg) { g_err = msg; return code; }
+#define HIP_TRY(x)                                                                  \
+    do {                                                                            \
+        hipError_t e_ = (x);                                                        \
+        if (e_ != hipSuccess) return fail(OFL_EHIP, std::string(#x " failed: ") + hipGetErrorString(e_)); \
+    } while (0)
+
+struct Launch {
+    int kind;        // see enum below
+    int param;       // p (small) / M (column)
+    int lo;          // column passes
+    int mid;         // column: fused middle pass
+    int list_off;    // into d_list
+    int tstart_off;  // into d_tstart (multi-tile kernels), -1 otherwise
+    int count;       // list entries
+    int64_t blocks;  // grid size
+};
+enum Kind { K_TINY, K_SMALL, K_ROWA, K_ROWC, K_COL, K_NORMS, K_FINAL };
+
+}  // namespace
+
+struct ofl_eden_plan {
+    int nbits = 8;
+    int ntensors = 0;
+    std::vector<ofl::SliceDesc> slices;
+    std::vector<int64_t> t_planes_off, t_planes_bytes;
+    std::vector<int32_t> t_first, t_nslices;
+    int64_t planes_bytes = 0;
+    int64_t ws_floats = 0;      // intermediates
+    int64_t part_floats = 0;    // partials
+    int64_t nlarge = 0;
+    std::vector<Launch> enc, dec;
+    std::vector<int32_t> ints;  // launch lists and tile prefixes (host copy)
+    ofl::SliceDesc* d_slices = nullptr;
+    int32_t* d_ints = nullptr;
+    int device = -1;
+    bool uploaded = false;
+    std::mutex mu;
+};
+
+namespace {
+
+int64_t low_po2(int64_t n) { int64_t p = 1; while (p * 2 <= n) p *= 2; return n ? p : 0; }
+int64_t high_po2(int64_t n) { int64_t p = 1; while (p < n) p *= 2; return n ? p : 0; }
+int ilog2(int64_t v) { int l = 0; while ((1ll << l) < v) ++l; return l; }
+
+template <typename K>
+hipError_t launch(K kern, int64_t blocks, int threads, size_t shmem, hipStream_t st, const ofl::KArgs& a) {
+    if (blocks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(threads), shmem, st, a);
+    return hipGetLastError();
+}
+
+size_t small_smem(int p, bool enc) {
+    size_t s = sizeof(float) * (1u << p) + 2 * sizeof(uint32_t) * (1u << (p - 3));
+    if (enc) s += sizeof(ofl::QEnt) * EDEN_GRID_CELLS + sizeof(float) * 16;
+    else s += sizeof(float) * 256;
+    return s;
+}
+
+template <int P>
+hipError_t set_smem_attr() {
+    hipError_t e = hipFuncSetAttribute((const void*)ofl::k_enc_small<P>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)small_smem(P, true));
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute((const void*)ofl::k_dec_small<P>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)small_smem(P, false));
+}
+
+int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t st) {
+    static bool attrs_done = false;
+    if (!attrs_done) {
+        HIP_TRY(set_smem_attr<11>());
+        HIP_TRY(set_smem_attr<12>());
+        HIP_TRY(set_smem_attr<13>());
+        HIP_TRY(set_smem_attr<14>());
+        attrs_done = true;
+    }
+    const std::vector<Launch>& L = enc ? pl->enc : pl->dec;
+    for (const Launch& l : L) {
+        ofl::KArgs a = base;
+        a.list = pl->d_ints + l.list_off;
+        a.tstart = l.tstart_off >= 0 ? pl->d_ints + l.tstart_off : nullptr;
+        a.count = l.count;
+        a.lo = l.lo;
+        hipError_t e = hipSuccess;
+        switch (l.kind) {
+        case K_TINY:
+            e = enc ? launch(ofl::k_enc_tiny, l.blocks, 64, 0, st, a) : launch(ofl::k_dec_tiny, l.blocks, 64, 0, st, a);
+            break;
+        case K_SMALL: {
+            const int p = l.param;
+            const int nt = 1 << (p - 5);
+            const size_t sm = small_smem(p, enc);
+            if (enc) {
+                if (p == 11) e = launch(ofl::k_enc_small<11>, l.blocks, nt, sm, st, a);
+                else if (p == 12) e = launch(ofl::k_enc_small<12>, l.blocks, nt, sm, st, a);
+                else if (p == 13) e = launch(ofl::k_enc_small<13>, l.blocks, nt, sm, st, a);
+                else e = launch(ofl::k_enc_small<14>, l.blocks, nt, sm, st, a);
+            } else {
+                if (p == 11) e = launch(ofl::k_dec_small<11>, l.blocks, nt, sm, st, a);
+                else if (p == 12) e = launch(ofl::k_dec_small<12>, l.blocks, nt, sm, st, a);
+                else if (p == 13) e = launch(ofl::k_dec_small<13>, l.blocks, nt, sm, st, a);
+                else e = launch(ofl::k_dec_small<14>, l.blocks, nt, sm, st, a);
+            }
+            break;
+        }
+        case K_ROWA:
+            e = enc ? launch(ofl::k_enc_rowA, l.blocks, ofl::kRowNT, 0, st, a)
+                    : launch(ofl::k_dec_rowA, l.blocks, ofl::kRowNT, 0, st, a);
+            break;
+        case K_ROWC:
+            e = enc ? launch(ofl::k_enc_rowC, l.blocks, ofl::kRowNT, 0, st, a)
+                    : launch(ofl::k_dec_rowC, l.blocks, ofl::kRowNT, 0, st, a);
+            break;
+        case K_COL: {
+#define COLCASE(MM)                                                                                  \
+    case MM:                                                                                         \
+        e = l.mid ? launch(ofl::k_col<MM, true>, l.blocks, ofl::kColNT, 0, st, a)                    \
+                  : launch(ofl::k_col<MM, false>, l.blocks, ofl::kColNT, 0, st, a);                  \
+        break;
+            switch (l.param) {
+                COLCASE(1) COLCASE(2) COLCASE(3) COLCASE(4) COLCASE(5) COLCASE(6) COLCASE(7) COLCASE(8) COLCASE(9)
+            default: return fail(OFL_EINVAL, "column pass height out of range");
+            }
+#undef COLCASE
+            break;
+        }
+        case K_NORMS: e = launch(ofl::k_norms, l.blocks, 256, 0, st, a); break;
+        case K_FINAL: e = launch(ofl::k_finalize, l.blocks, 256, 0, st, a); break;
+        }
+        if (e != hipSuccess) return fail(OFL_EHIP, std::string("kernel launch failed: ") + hipGetErrorString(e));
+    }
+    return OFL_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* ofl_version(void) { return "openfl_amd-codec 0.1 (gfx950)"; }
+const char* ofl_last_error(void) { return g_err.c_str(); }
+
+int ofl_eden_slice_plan(int64_t n, int64_t* P_out, int64_t* len_out, int max_slices) {
+    if (n <= 0) return 0;
+    int64_t rem = n;
+    int ns = 0;
+    while ((double)(high_po2(rem) - rem) / (double)n > 0.1) {
+        const int64_t low = low_po2(rem);
+        if (ns < max_slices) {
+            if (P_out) P_out[ns] = std::max<int64_t>(low, 8);
+            if (len_out) len_out[ns] = low;
+        }
+        ++ns;
+        rem -= low;
+    }
+    if (ns < max_slices) {
+        if (P_out) P_out[ns] = std::max<int64_t>(high_po2(rem), 8);
+        if (len_out) len_out[ns] = rem;
+    }
+    return ns + 1;
+}
+
+int ofl_eden_plan_create(int ntensors, const int64_t* numel, const int64_t* elem_offset,
+                         const int32_t* nslices, const int64_t* slice_dims, int n_bits,
+                         ofl_eden_plan_t* plan_out) {
+    if (!plan_out || ntensors < 0 || !numel || !elem_offset) return fail(OFL_EINVAL, "null argument");
+    if (n_bits < 1 || n_bits > 8) return fail(OFL_EINVAL, "nbits value is not supported");
+    auto* pl = new ofl_eden_plan();
+    pl->nbits = n_bits;
+    pl->ntensors = ntensors;
+    int64_t dims_pos = 0;
+    // per-class slice lists
+    std::vector<int32_t> tiny, small[4], large;
+    for (int t = 0; t < ntensors; ++t) {
+        const int64_t n = numel[t];
+        std::vector<int64_t> Ps, Ls;  // padded sizes, valid input lengths
+        if (slice_dims) {
+            int64_t rem = n;
+            for (int k = 0; k < nslices[t]; ++k) {
+                const int64_t P = slice_dims[dims_pos + k];
+                Ps.push_back(P);
+                Ls.push_back(std::max<int64_t>(0, std::min<int64_t>(P, rem)));
+                rem -= Ls.back();
+            }
+            dims_pos += nslices[t];
+        } else {
+            int ns = ofl_eden_slice_plan(n, nullptr, nullptr, 0);
+            Ps.resize(ns);
+            Ls.resize(ns);
+            ofl_eden_slice_plan(n, Ps.data(), Ls.data(), ns);
+        }
+        int64_t Ptot = 0;
+        for (int64_t P : Ps) {
+            if (P < 8 || (P & (P - 1)) || P > (1ll << 29)) {
+                delete pl;
+                return fail(OFL_EINVAL, "slice size must be a power of two in [8, 2^29]");
+            }
+            Ptot += P;
+        }
+        pl->t_first.push_back((int32_t)pl->slices.size());
+        pl->t_nslices.push_back((int32_t)Ps.size());
+        const int64_t poff = (pl->planes_bytes + 255) & ~255ll;
+        pl->t_planes_off.push_back(poff);
+        pl->t_planes_bytes.push_back(Ptot / 8 * n_bits);
+        pl->planes_bytes = poff + Ptot / 8 * n_bits;
+        // Encode reads slice k from input offset sum(len_k') (Eden.compress
+        // advances by the valid length, :599-602); decode writes slice k's P
+        // outputs at sum(P_k') and truncates to total_dim (:650-657).  The two
+        // differ only for n < ~150 with a sub-8 non-final slice (reproduced).
+        int64_t off = 0, xoff = 0;
+        for (size_t k = 0; k < Ps.size(); ++k) {
+            const int64_t P = Ps[k];
+            ofl::SliceDesc D{};
+            D.x_off = elem_offset[t] + xoff;
+            D.len = Ls[k];
+            D.y_off = elem_offset[t] + off;
+            D.ylen = std::max<int64_t>(0, std::min<int64_t>(P, n - off));
+            D.pl_off = poff + off / 8;
+            D.pl_stride = Ptot / 8;
+            D.logp = ilog2(P);
+            D.tensor = t;
+            D.scale_idx = (int32_t)pl->slices.size();
+            const int si = (int)pl->slices.size();
+            if (D.logp <= 10) tiny.push_back(si);
+            else if (D.logp <= 14) small[D.logp - 11].push_back(si);
+            else {
+                D.ws_off = pl->ws_floats;
+                pl->ws_floats += P;
+                D.part_off = (int32_t)pl->part_floats;
+                pl->part_floats += P >> ofl::kRowLog;
+                large.push_back(si);
+            }
+            pl->slices.push_back(D);
+            off += P;
+            xoff += D.len;
+        }
+    }
+    pl->nlarge = (int64_t)large.size();
+    // ---- launch lists ----
+    std::vector<int32_t>& ints = pl->ints;
+    auto add_list = [&](const std::vector<int32_t>& l) { int o = (int)ints.size(); ints.insert(ints.end(), l.begin(), l.end()); return o; };
+    auto add_prefix = [&](const std::vector<int32_t>& l, int log_tile, int64_t& total) {
+        int o = (int)ints.size();
+        int64_t acc = 0;
+        for (int32_t si : l) { ints.push_back((int32_t)acc); acc += 1ll << (pl->slices[si].logp - log_tile); }
+        ints.push_back((int32_t)acc);
+        total = acc;
+        return o;
+    };
+    std::vector<Launch> common;
+    if (!tiny.empty()) common.push_back({K_TINY, 0, 0, 0, add_list(tiny), -1, (int)tiny.size(), (int64_t)tiny.size()});
+    for (int k = 0; k < 4; ++k)
+        if (!small[k].empty())
+            common.push_back({K_SMALL, 11 + k, 0, 0, add_list(small[k]), -1, (int)small[k].size(), (int64_t)small[k].size()});
+    pl->enc = common;
+    pl->dec = common;
+    if (!large.empty()) {
+        int64_t rows = 0;
+        const int lo_l = add_list(large);
+        const int rp = add_prefix(large, ofl::kRowLog, rows);
+        // column launches grouped by p
+        std::map<int, std::vector<int32_t>> byp;
+        for (int32_t si : large) byp[pl->slices[si].logp].push_back(si);
+        std::vector<Launch> colseq;
+        for (auto& kv : byp) {
+            const int p = kv.first, r = p - ofl::kRowLog;
+            int64_t tiles = 0;
+            const int lo_c = add_list(kv.second);
+            const int tp = add_prefix(kv.second, 14, tiles);
+            const int cnt = (int)kv.second.size();
+            if (r <= 9) {
+                colseq.push_back({K_COL, r, ofl::kRowLog, 1, lo_c, tp, cnt, tiles});
+            } else {
+                const int m1 = r / 2, m2 = r - m1;
+                colseq.push_back({K_COL, m1, ofl::kRowLog, 0, lo_c, tp, cnt, tiles});
+                colseq.push_back({K_COL, m2, ofl::kRowLog + m1, 1, lo_c, tp, cnt, tiles});
+                colseq.push_back({K_COL, m1, ofl::kRowLog, 0, lo_c, tp, cnt, tiles});
+            }
+        }
+        const int nl = (int)large.size();
+        pl->enc.push_back({K_ROWA, 0, 0, 0, lo_l, rp, nl, rows});
+        pl->enc.push_back({K_NORMS, 0, 0, 0, lo_l, -1, nl, nl});
+        pl->enc.insert(pl->enc.end(), colseq.begin(), colseq.end());
+        pl->enc.push_back({K_ROWC, 0, 0, 0, lo_l, rp, nl, rows});
+        pl->enc.push_back({K_FINAL, 0, 0, 0, lo_l, -1, nl, nl});
+        pl->dec.push_back({K_ROWA, 0, 0, 0, lo_l, rp, nl, rows});
+        pl->dec.insert(pl->dec.end(), colseq.begin(), colseq.end());
+        pl->dec.push_back({K_ROWC, 0, 0, 0, lo_l, rp, nl, rows});
+    }
+    *plan_out = pl;
+    return OFL_OK;
+}
+
+// Descriptor tables go to the device on first use (one synchronous copy), so
+// plans can be built and inspected on hosts without a GPU.  The first
+// encode/decode of a plan must therefore not be inside a graph capture.
+static int ensure_device(ofl_eden_plan_t pl) {
+    std::lock_guard<std::mutex> g(pl->mu);
+    if (pl->uploaded) return OFL_OK;
+    HIP_TRY(hipGetDevice(&pl->device));
+    if (!pl->slices.empty()) {
+        HIP_TRY(hipMalloc(&pl->d_slices, sizeof(ofl::SliceDesc) * pl->slices.size()));
+        HIP_TRY(hipMemcpy(pl->d_slices, pl->slices.data(), sizeof(ofl::SliceDesc) * pl->slices.size(), hipMemcpyHostToDevice));
+    }
+    if (!pl->ints.empty()) {
+        HIP_TRY(hipMalloc(&pl->d_ints, sizeof(int32_t) * pl->ints.size()));
+        HIP_TRY(hipMemcpy(pl->d_ints, pl->ints.data(), sizeof(int32_t) * pl->ints.size(), hipMemcpyHostToDevice));
+    }
+    pl->uploaded = true;
+    return OFL_OK;
+}
+
+void ofl_eden_plan_destroy(ofl_eden_plan_t pl) {
+    if (!pl) return;
+    if (pl->d_slices) (void)hipFree(pl->d_slices);
+    if (pl->d_ints) (void)hipFree(pl->d_ints);
+    delete pl;
+}
+
+int64_t ofl_eden_plan_num_slices(ofl_eden_plan_t pl) { return pl ? (int64_t)pl->slices.size() : -1; }
+int64_t ofl_eden_plan_planes_bytes(ofl_eden_plan_t pl) { return pl ? pl->planes_bytes : -1; }
+int64_t ofl_eden_plan_workspace_bytes(ofl_eden_plan_t pl) {
+    if (!pl) return -1;
+    // intermediates | partials | norms, each 256-B aligned
+    auto al = [](int64_t b) { return (b + 255) & ~255ll; };
+    return al(pl->ws_floats * 4) + al(pl->part_floats * 4) + al(pl->nlarge * 4) + 256;
+}
+
+int ofl_eden_plan_tensor_info(ofl_eden_plan_t pl, int t, int64_t* planes_offset, int64_t* planes_bytes,
+                              int32_t* first_slice, int32_t* nslices) {
+    if (!pl || t < 0 || t >= pl->ntensors) return fail(OFL_EINVAL, "tensor index out of range");
+    if (planes_offset) *planes_offset = pl->t_planes_off[t];
+    if (planes_bytes) *planes_bytes = pl->t_planes_bytes[t];
+    if (first_slice) *first_slice = pl->t_first[t];
+    if (nslices) *nslices = pl->t_nslices[t];
+    return OFL_OK;
+}
+
+int ofl_eden_plan_tensor_dims(ofl_eden_plan_t pl, int t, int64_t* dims_out) {
+    if (!pl || t < 0 || t >= pl->ntensors) return fail(OFL_EINVAL, "tensor index out of range");
+    for (int k = 0; k < pl->t_nslices[t]; ++k) dims_out[k] = 1ll << pl->slices[pl->t_first[t] + k].logp;
+    return OFL_OK;
+}
+
+static int prep_args(ofl_eden_plan_t pl, ofl::KArgs& a, void* ws, size_t ws_bytes) {
+    if (int rc = ensure_device(pl)) return rc;
+    const int64_t need = ofl_eden_plan_workspace_bytes(pl);
+    if ((int64_t)ws_bytes < need || (need > 256 && !ws)) return fail(OFL_ESPACE, "workspace too small");
+    auto al = [](int64_t b) { return (b + 255) & ~255ll; };
+    char* w = static_cast<char*>(ws);
+    memset(&a, 0, sizeof(a));
+    a.d = pl->d_slices;
+    a.nbits = pl->nbits;
+    a.ws = reinterpret_cast<float*>(w);
+    a.part = reinterpret_cast<float*>(w + al(pl->ws_floats * 4));
+    a.nu = reinterpret_cast<float*>(w + al(pl->ws_floats * 4) + al(pl->part_floats * 4));
+    return OFL_OK;
+}
+
+int ofl_eden_encode(ofl_eden_plan_t pl, const float* x_arena, const uint32_t* seeds, uint8_t* planes_arena,
+                    float* scales, void* ws, size_t ws_bytes, void* stream) {
+    if (!pl) return fail(OFL_EINVAL, "null plan");
+    ofl::KArgs a;
+    int rc = prep_args(pl, a, ws, ws_bytes);
+    if (rc) return rc;
+    a.xin = x_arena;
+    a.pout = planes_arena;
+    a.seeds = seeds;
+    a.scales = scales;
+    return run(pl, true, a, static_cast<hipStream_t>(stream));
+}
+
+int ofl_eden_decode(ofl_eden_plan_t pl, const uint8_t* planes_arena, const uint32_t* seeds, const float* scales,
+                    float* y_arena, void* ws, size_t ws_bytes, void* stream) {
+    if (!pl) return fail(OFL_EINVAL, "null plan");
+    ofl::KArgs a;
+    int rc = prep_args(pl, a, ws, ws_bytes);
+    if (rc) return rc;
+    a.pin = planes_arena;
+    a.xout = y_arena;
+    a.seeds = seeds;
+    a.scales_in = scales;
+    return run(pl, false, a, static_cast<hipStream_t>(stream));
+}
+
+float ofl_serial_sum_f32(const float* x, int64_t n) {
+    volatile float s = 0.0f;
+    for (int64_t i = 0; i < n; ++i) s = s + x[i];
+    return s;
+}
+
+double ofl_serial_sum_f64(const double* x, int64_t n) {
+    volatile double s = 0.0;
+    for (int64_t i = 0; i < n; ++i) s = s + x[i];
+    return s;
+}
+
+}  // extern "C"

@@ -1,0 +1,172 @@
+"""EdenPipeline on MI355X: drop-in for openfl/pipelines/eden_pipeline.py.
+
+Same classes, constructor keywords, metadata schema and wire bytes as the
+reference (/root/reference/openfl/pipelines/eden_pipeline.py):
+
+  Eden.compress / Eden.decompress    :555-611 / :632-659   -> libofl_codec.so
+  EdenTransformer.forward            :761-793
+  EdenTransformer.backward           :795-818
+  EdenPipeline(n_bits, dim_threshold, device, **kw)  :821-851
+
+The numerics run in the gfx950 kernels of openfl_amd/csrc/eden_kernels.hip;
+this module only moves host NumPy buffers to/from the device and builds the
+metadata dict.  There is no CPU fallback: without a ROCm GPU and the built
+library every Eden call raises openfl_amd._lib.CodecError.
+
+Deliberate differences (DESIGN.md "Reference quirks"):
+  * backward() decides "compressed?" with the same `size > dim_threshold`
+    test as forward(); the reference uses `>=` there (:808), so a tensor of
+    exactly dim_threshold elements crashes it with KeyError.
+  * seed_mode="fast" (opt-in) replaces the O(n) serial Python sum in the
+    seed hash with a sum over the first 4096 elements; the default
+    "reference" reproduces the reference seed exactly.  The seed is carried
+    in the metadata either way, so decoding never depends on it.
+  * device="cpu" (the reference default) selects the current GPU.
+"""
+import threading
+
+import numpy as np
+import torch
+
+from openfl_amd import _lib
+from openfl_amd.codec import EdenCodec, resolve_device
+from openfl_amd.pipelines.pipeline import Float32NumpyArrayToBytes, TransformationPipeline, Transformer
+
+_FAST_SEED_PREFIX = 4096
+
+
+def _serial_sum(flat):
+    """`sum(data.flatten())` of the reference seed (:771): left-to-right, in
+    the array's own precision (NumPy scalar arithmetic)."""
+    L = _lib.lib()
+    if flat.dtype == np.float32:
+        a = np.ascontiguousarray(flat)
+        return np.float32(L.ofl_serial_sum_f32(a.ctypes.data, a.size))
+    if flat.dtype == np.float64:
+        a = np.ascontiguousarray(flat)
+        return np.float64(L.ofl_serial_sum_f64(a.ctypes.data, a.size))
+    return sum(flat)
+
+
+def eden_seed(data, mode="reference"):
+    """Seed of EdenTransformer.forward (:771-772); draws ONE np.random value."""
+    flat = data.reshape(-1)
+    if mode == "fast":
+        flat = flat[:_FAST_SEED_PREFIX]
+    s = _serial_sum(flat)
+    seed = (hash(s * 13 + 7) + np.random.randint(1, 2 ** 16)) % (2 ** 16)
+    return int(float(seed))
+
+
+class Eden:
+    """Device Eden codec with the reference Eden class's method surface."""
+
+    def __init__(self, nbits=8, device="cpu"):
+        if nbits not in [1, 2, 3, 4, 5, 6, 7, 8]:
+            raise Exception("nbits value is not supported")  # :389-390
+        self.nbits = int(nbits)
+        self.device = resolve_device(device)
+        self.num_hadamard = 2           # :394
+        self.max_padding_overhead = 0.1  # :397
+        self.codec = EdenCodec(self.nbits, self.device)
+        self._tls = threading.local()
+
+    def _stream(self):
+        st = getattr(self._tls, "stream", None)
+        if st is None:
+            st = self._tls.stream = torch.cuda.Stream(device=self.device)
+        return st
+
+    def compress(self, vec, seed):
+        """(planes uint8 ndarray, scales list[float], dims list[int], total_dim) (:555-611)."""
+        flat = np.ascontiguousarray(np.asarray(vec).reshape(-1), dtype=np.float32)
+        n = flat.size
+        plan = self.codec.plan([n])
+        st = self._stream()
+        with torch.cuda.stream(st):
+            x = torch.from_numpy(flat).to(self.device, non_blocking=False) if n else \
+                torch.empty(1, dtype=torch.float32, device=self.device)
+            seeds = torch.tensor([int(seed)], dtype=torch.int32).to(self.device)
+            planes, scales = self.codec.encode_arena(plan, x, seeds, stream=st)
+            planes_h = planes[:plan.planes_bytes].cpu().numpy()
+            scales_h = scales[:plan.n_slices].cpu().numpy()
+        return planes_h, [float(s) for s in scales_h], list(plan.dims[0]), n
+
+    def decompress(self, bins, metadata):
+        """bins: uint8 planes; metadata: int_to_float mapping (:632-659)."""
+        seed = int(metadata[0])
+        total_dim = int(metadata[1])
+        keys = list(metadata.keys())
+        scales, dims = [], []
+        for k in range(2, max(keys) + 1, 2):
+            scales.append(metadata[k])
+            dims.append(int(metadata[k + 1]))
+        if total_dim > sum(dims):
+            raise ValueError(f"Eden metadata: total_dim {total_dim} exceeds the slices ({sum(dims)})")
+        planes_h = np.frombuffer(bytes(bins) if not isinstance(bins, np.ndarray) else bins.tobytes(),
+                                 dtype=np.uint8)
+        plan = self.codec.plan([total_dim], dims=[dims])
+        if planes_h.size < plan.planes_bytes:
+            raise ValueError(f"Eden payload has {planes_h.size} bytes, expected {plan.planes_bytes}")
+        st = self._stream()
+        with torch.cuda.stream(st):
+            planes = torch.from_numpy(planes_h[:plan.planes_bytes].copy()).to(self.device)
+            sc = torch.tensor(np.asarray(scales, np.float32)).to(self.device)
+            seeds = torch.tensor([seed], dtype=torch.int32).to(self.device)
+            y = self.codec.decode_arena(plan, planes, sc, seeds, stream=st)
+            out = y[:total_dim].cpu().numpy()
+        return out
+
+
+class EdenTransformer(Transformer):
+    """Eden quantising transformer (:723-818)."""
+
+    def __init__(self, n_bits=8, dim_threshold=100, device="cpu", seed_mode="reference"):
+        self.lossy = True
+        self.eden = Eden(nbits=n_bits, device=device)
+        self.dim_threshold = dim_threshold
+        self.no_comp = Float32NumpyArrayToBytes()
+        if seed_mode not in ("reference", "fast"):
+            raise ValueError("seed_mode must be 'reference' or 'fast'")
+        self.seed_mode = seed_mode
+
+    def forward(self, data, **kwargs):
+        seed = eden_seed(data, self.seed_mode)
+        metadata = {"int_list": list(data.shape)}
+        if data.size > self.dim_threshold:
+            int_array, scale_list, dim_list, total_dim = self.eden.compress(data, seed)
+            metadata["int_to_float"] = {0: float(seed), 1: float(total_dim)}
+            k = 2
+            for scale, dim in zip(scale_list, dim_list):
+                metadata["int_to_float"][k] = scale
+                metadata["int_to_float"][k + 1] = float(dim)
+                k += 2
+            return int_array.tobytes(), metadata
+        return self.no_comp.forward(data)
+
+    def backward(self, data, metadata, **kwargs):
+        if np.prod(metadata["int_list"]) > self.dim_threshold:  # reference: >= (:808), see module doc
+            out = self.eden.decompress(np.frombuffer(data, dtype=np.uint8), metadata["int_to_float"])
+            out = out.reshape(list(metadata["int_list"]))
+        else:
+            out = self.no_comp.backward(data, metadata)
+        return out.astype(np.float32)
+
+
+class EdenPipeline(TransformationPipeline):
+    """plan.yaml: template openfl_amd.pipelines.EdenPipeline, settings n_bits /
+    dim_threshold / device (:821-851); extra keyword seed_mode."""
+
+    def __init__(self, n_bits=8, dim_threshold=100, device="cpu", seed_mode="reference", **kwargs):
+        transformers = [EdenTransformer(n_bits, dim_threshold, device, seed_mode)]
+        super().__init__(transformers=transformers, **kwargs)
+
+    def forward(self, data, **kwargs):
+        # The reference copies the input first (pipeline.py:144) to protect it
+        # from in-place transformers; EdenTransformer never writes its input,
+        # so the O(n) host copy is skipped.
+        transformer_metadata = []
+        for transformer in self.transformers:
+            data, metadata = transformer.forward(data=data, **kwargs)
+            transformer_metadata.append(metadata)
+        return data, transformer_metadata

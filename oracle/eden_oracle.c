@@ -1,0 +1,253 @@
+/*
+ * eden_oracle.c -- CPU restatement of the reference Eden codec.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the checker the parity tests, the
+ * smoke test and bench.py's cpu_baseline leg compare the HIP product path
+ * against.  The product (openfl_amd/) never links, loads or calls it.
+ *
+ * It restates, in plain scalar C, the algorithm of
+ *   /root/reference/openfl/pipelines/eden_pipeline.py
+ * function by function (citations are file:line in that file):
+ *   oracle_rand_signs     Eden.rand_diag            :403-449
+ *   oracle_fwht           Eden.hadamard             :451-473
+ *   oracle_slice_plan     Eden.compress slicing     :569-606
+ *   oracle_eden_compress  Eden.compress             :555-611
+ *                         (compress_slice :527-553, rht :475-488,
+ *                          quantize :505-525, to_bits :661-690)
+ *   oracle_eden_decompress Eden.decompress          :632-659
+ *                         (decompress_slice :613-630, irht :490-503,
+ *                          from_bits :692-720)
+ *   oracle_serial_sum_*   the `sum(data.flatten())` seed term   :771
+ *
+ * Floating-point order follows the reference's eager torch ops where they are
+ * elementwise (butterfly a'=a+b, b'=a'-2b; division by float32(sqrt(P)) per
+ * Hadamard; scale multiply in float32), so decode is bit-exact with the
+ * reference given the same bytes/metadata.  The two reductions (norm, dot)
+ * are accumulated in double here; torch's vectorised float sums differ in the
+ * last bits, which flips a bin on ~1e-3 of elements (|dbin| = 1) -- the
+ * tolerance recorded in SURVEY.md section 8(c) and asserted in tests/.
+ *
+ * Pinned by: tests/golden/eden_golden.{npz,json} generated from the reference
+ * itself by tests/golden/make_golden.py (see tests/test_oracle_golden.py).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ---- rand_diag (:403-449) ------------------------------------------------
+ * r_j = j + s for j < ceil(P/8), two LCG steps, SplitMix finaliser with the
+ * 33-bit (unmasked) add at :433, then sign(i) = +1 iff nibble floor(i/S) of
+ * r_{i mod S} is >= 8, S = ceil(P/8).  Output: packed bits, LSB-first,
+ * bit i = 1 <=> sign +1. */
+static uint32_t seed_hash(int64_t seed) {
+    uint64_t m = 0xFFFFFFFFull;
+    uint64_t s = ((uint64_t)seed * 1664525ull + 1013904223ull) & m;
+    s = (s * 8121ull + 28411ull) & m;
+    return (uint32_t)s;
+}
+
+static uint32_t rd_word(uint64_t j, uint64_t s) {
+    const uint64_t m = 0xFFFFFFFFull;
+    uint64_t r = j + s;
+    r = (1103515245ull * r + 12345ull + s) & m;
+    r = (1140671485ull * r + 12820163ull + s) & m;
+    r += 0x9E3779B9ull;                         /* no mask: 33-bit value */
+    r = ((r ^ (r >> 16)) * 0x85EBCA6Bull) & m;
+    r = ((r ^ (r >> 13)) * 0xC2B2AE35ull) & m;
+    r = (r ^ (r >> 16)) & m;
+    return (uint32_t)r;
+}
+
+void oracle_rand_signs(int64_t P, int64_t seed, uint8_t* bits) {
+    int64_t S = P / 8 + (P % 8 != 0);
+    uint64_t s = seed_hash(seed);
+    memset(bits, 0, (size_t)((P + 7) / 8));
+    for (int64_t j = 0; j < S; ++j) {
+        uint32_t r = rd_word((uint64_t)j, s);
+        for (int k = 0; k < 8; ++k) {
+            int64_t i = (int64_t)k * S + j;
+            if (i >= P) break;
+            if (((r >> (4 * k)) & 15u) >= 8u) bits[i >> 3] |= (uint8_t)(1u << (i & 7));
+        }
+    }
+}
+
+static void apply_signs(float* v, int64_t P, int64_t seed) {
+    int64_t S = P / 8 + (P % 8 != 0);
+    uint64_t s = seed_hash(seed);
+    for (int64_t j = 0; j < S; ++j) {
+        uint32_t r = rd_word((uint64_t)j, s);
+        for (int k = 0; k < 8; ++k) {
+            int64_t i = (int64_t)k * S + j;
+            if (i >= P) break;
+            if (((r >> (4 * k)) & 15u) < 8u) v[i] = v[i] * -1.0f;
+        }
+    }
+}
+
+/* ---- hadamard (:451-473): stride-1 stages first, a'=a+b, b'=a'-2b, then
+ * divide by float32(sqrt(P)) ---- */
+void oracle_fwht(float* v, int64_t P) {
+    for (int64_t h = 2; h <= P; h <<= 1) {
+        int64_t hf = h >> 1;
+        for (int64_t base = 0; base < P; base += h) {
+            for (int64_t k = 0; k < hf; ++k) {
+                float a = v[base + k], b = v[base + hf + k];
+                float s = a + b;
+                v[base + k] = s;
+                v[base + hf + k] = s - 2.0f * b;
+            }
+        }
+    }
+    float d = (float)sqrt((double)P);
+    for (int64_t i = 0; i < P; ++i) v[i] = v[i] / d;
+}
+
+/* ---- slicing (:569-606) ----
+ * while (high_po2(rem) - rem) / n > 0.1: take low_po2(rem);
+ * last slice = rem, padded to max(next_po2, 8) (:541-546).
+ * Returns the number of slices; out_len[k] = valid elements, out_P[k] =
+ * padded power of two. */
+static int64_t low_po2(int64_t n) { int64_t p = 1; while (p * 2 <= n) p *= 2; return n ? p : 0; }
+static int64_t high_po2(int64_t n) { int64_t p = 1; while (p < n) p *= 2; return n ? p : 0; }
+
+int oracle_slice_plan(int64_t n, int64_t* out_P, int64_t* out_len, int max_slices) {
+    int64_t rem = n;
+    int ns = 0;
+    while ((double)(high_po2(rem) - rem) / (double)n > 0.1) {
+        int64_t low = low_po2(rem);
+        if (ns < max_slices) { out_len[ns] = low; out_P[ns] = low < 8 ? 8 : low; }
+        ns++;
+        rem -= low;
+    }
+    if (ns < max_slices) {
+        int64_t P = high_po2(rem);
+        out_len[ns] = rem;
+        out_P[ns] = P < 8 ? 8 : P;
+    }
+    return ns + 1;
+}
+
+/* bucketize(right=False) (:519): number of boundaries strictly below z */
+static int bucketize(float z, const float* B, int nb) {
+    int lo = 0, hi = nb;
+    while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (!(B[mid] >= z)) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+/* ---- compress_slice + quantize (:527-553, :505-525) ----
+ * bins_out has P entries; returns scale (float32 value). */
+static float compress_slice(const float* x, int64_t len, int64_t P, int64_t seed,
+                            const float* C, const float* B, int nbits, int32_t* bins_out,
+                            float* work) {
+    memset(work, 0, sizeof(float) * (size_t)P);
+    memcpy(work, x, sizeof(float) * (size_t)len);
+    for (int i = 0; i < 2; ++i) {            /* num_hadamard = 2 (:394, :548-549) */
+        apply_signs(work, P, seed + i);
+        oracle_fwht(work, P);
+    }
+    /* torch.norm squares in float32 (under/overflow as in the reference, e.g.
+     * 1e-32 inputs give norm 0 and 1e28 inputs give norm inf), accumulates
+     * accurately; restated as float32 squares summed in double. */
+    double ss = 0.0;
+    for (int64_t i = 0; i < P; ++i) { float q = work[i] * work[i]; ss += (double)q; }
+    float nu = sqrtf((float)ss);          /* float32 sum: overflows to inf past FLT_MAX */
+    int nb = (1 << nbits) - 1;
+    if (nu > 0.0f) {
+        float rp = (float)sqrt((double)P);
+        double dot = 0.0;
+        for (int64_t i = 0; i < P; ++i) {
+            float z = (work[i] * rp) / nu;
+            int b = bucketize(z, B, nb);
+            bins_out[i] = b;
+            float pr = C[b] * work[i];       /* float32 products, as torch.dot */
+            dot += (double)pr;
+        }
+        float scale = (nu * nu) / (float)dot;
+        if (!isnan(scale)) return scale;
+    }
+    for (int64_t i = 0; i < P; ++i) bins_out[i] = 0;
+    return 0.0f;
+}
+
+/* ---- to_bits (:661-690): plane i at offset i*L, L = P_tot/8;
+ * byte j bit t = bit i of bin[8j+t] ---- */
+static void to_bits(const int32_t* bins, int64_t Ptot, int nbits, uint8_t* planes) {
+    int64_t L = Ptot / 8;
+    memset(planes, 0, (size_t)(L * nbits));
+    for (int64_t e = 0; e < Ptot; ++e)
+        for (int i = 0; i < nbits; ++i)
+            if ((bins[e] >> i) & 1) planes[i * L + (e >> 3)] |= (uint8_t)(1u << (e & 7));
+}
+
+/* Full Eden.compress.  planes must hold nbits*P_tot/8 bytes, scales/dims
+ * max_slices entries.  Returns the number of slices (or -needed if
+ * max_slices is too small). */
+int oracle_eden_compress(const float* x, int64_t n, int64_t seed, int nbits,
+                         const float* C, const float* B,
+                         uint8_t* planes, float* scales, int64_t* dims, int max_slices) {
+    int64_t* Ps = (int64_t*)malloc(sizeof(int64_t) * 64);
+    int64_t* Ls = (int64_t*)malloc(sizeof(int64_t) * 64);
+    int ns = oracle_slice_plan(n, Ps, Ls, 64);
+    if (ns > max_slices) { free(Ps); free(Ls); return -ns; }
+    int64_t Ptot = 0, maxP = 0;
+    for (int k = 0; k < ns; ++k) { Ptot += Ps[k]; if (Ps[k] > maxP) maxP = Ps[k]; }
+    int32_t* bins = (int32_t*)malloc(sizeof(int32_t) * (size_t)Ptot);
+    float* work = (float*)malloc(sizeof(float) * (size_t)maxP);
+    int64_t off = 0, src = 0;
+    for (int k = 0; k < ns; ++k) {
+        scales[k] = compress_slice(x + src, Ls[k], Ps[k], seed, C, B, nbits, bins + off, work);
+        dims[k] = Ps[k];
+        off += Ps[k];
+        src += Ls[k];
+    }
+    to_bits(bins, Ptot, nbits, planes);
+    free(bins); free(work); free(Ps); free(Ls);
+    return ns;
+}
+
+/* ---- decompress (:632-659, :613-630, :692-720) ---- */
+void oracle_eden_decompress(const uint8_t* planes, int64_t total_dim, const float* scales,
+                            const int64_t* dims, int nslices, int64_t seed, int nbits,
+                            const float* C, float* y) {
+    int64_t Ptot = 0, maxP = 0;
+    for (int k = 0; k < nslices; ++k) { Ptot += dims[k]; if (dims[k] > maxP) maxP = dims[k]; }
+    int64_t L = Ptot / 8;
+    float* work = (float*)malloc(sizeof(float) * (size_t)maxP);
+    int64_t off = 0, out = 0;
+    for (int k = 0; k < nslices; ++k) {
+        int64_t P = dims[k];
+        for (int64_t e = 0; e < P; ++e) {
+            int64_t g = off + e;
+            int b = 0;
+            for (int i = 0; i < nbits; ++i) b |= ((planes[i * L + (g >> 3)] >> (g & 7)) & 1) << i;
+            work[e] = C[b];
+        }
+        for (int i = 1; i >= 0; --i) {       /* irht(seed+1) then irht(seed) */
+            oracle_fwht(work, P);
+            apply_signs(work, P, seed + i);
+        }
+        float sc = scales[k];
+        for (int64_t e = 0; e < P && out < total_dim; ++e) y[out++] = sc * work[e];
+        off += P;
+    }
+    free(work);
+}
+
+/* the `sum(data.flatten())` seed term (:771): a left-to-right sum in the
+ * array's own precision (NumPy scalar arithmetic, NEP 50). */
+float oracle_serial_sum_f32(const float* x, int64_t n) {
+    volatile float s = 0.0f;
+    for (int64_t i = 0; i < n; ++i) s = s + x[i];
+    return s;
+}
+
+double oracle_serial_sum_f64(const double* x, int64_t n) {
+    volatile double s = 0.0;
+    for (int64_t i = 0; i < n; ++i) s = s + x[i];
+    return s;
+}
