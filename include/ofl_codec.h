@@ -7,8 +7,8 @@
  * torch.Tensor's data_ptr()); `stream` is a hipStream_t (e.g.
  * torch.cuda.current_stream().cuda_stream) passed as void*.  Functions return
  * 0 on success and a negative OFL_E* code on failure; ofl_last_error() then
- * returns a thread-local message.  No entry point allocates, frees or
- * synchronises inside encode/decode, so they are reentrant and
+ * returns a thread-local message.  After a plan's first use, encode/decode
+ * neither allocate nor synchronise, so they are reentrant and
  * graph-capturable; concurrent calls need separate workspaces.
  *
  * The codec replaces the per-tensor Eden transformer of the reference
@@ -65,8 +65,10 @@ int ofl_eden_slice_plan(int64_t n, int64_t* P_out, int64_t* len_out, int max_sli
  * padded slice sizes per tensor, concatenated (the P_k values of a received
  * metadata dict, eden_pipeline.py:650-654).  Slice k of tensor t then holds
  * elements [sum_{k'<k} P_k', ...) truncated to numel[t] (:656-657).
- * Creating a plan allocates and uploads its descriptor tables (one
- * synchronous copy); encode/decode with it do not allocate. */
+ * Creating a plan is host-only (works without a GPU).  The FIRST encode or
+ * decode with a plan uploads its descriptor tables (hipMalloc + one
+ * synchronous copy), so that first call must not be graph-captured; later
+ * calls neither allocate nor synchronise. */
 typedef struct ofl_eden_plan* ofl_eden_plan_t;
 
 int ofl_eden_plan_create(int ntensors, const int64_t* numel, const int64_t* elem_offset,
@@ -103,6 +105,21 @@ int ofl_eden_encode(ofl_eden_plan_t plan, const float* x_arena, const uint32_t* 
 int ofl_eden_decode(ofl_eden_plan_t plan, const uint8_t* planes_arena, const uint32_t* seeds,
                     const float* scales, float* y_arena, void* ws, size_t ws_bytes,
                     void* stream);
+
+/* ---- profiling (bench.py) --------------------------------------------------
+ * While enabled, every encode/decode of the plan records a HIP event before
+ * its first launch and after each launch on its stream.  collect() waits for
+ * the recorded calls of one direction, writes the summed per-launch
+ * milliseconds (launch order) and the call count, and drops the records.
+ * launch_info() names launch idx (kernel symbol as rocprofv3 shows it) with
+ * its grid size, the bytes it reads+writes in HBM and its share of the
+ * algorithmic bytes (input/output fp32 + bit planes; FWHT intermediates 0). */
+int ofl_eden_plan_profile(ofl_eden_plan_t plan, int enable);
+int ofl_eden_plan_num_launches(ofl_eden_plan_t plan, int encode);
+int ofl_eden_plan_launch_info(ofl_eden_plan_t plan, int encode, int idx, char* name, int cap,
+                              int64_t* blocks, int64_t* bytes_moved, int64_t* bytes_alg);
+int ofl_eden_plan_profile_collect(ofl_eden_plan_t plan, int encode, double* ms_sum, int max,
+                                  int* ncalls);
 
 /* ---- host helpers ----------------------------------------------------------
  * Left-to-right serial sums in the array's own precision: the

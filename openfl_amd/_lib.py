@@ -20,7 +20,9 @@ EXPORTS = (
     "ofl_version", "ofl_last_error", "ofl_eden_slice_plan", "ofl_eden_plan_create",
     "ofl_eden_plan_destroy", "ofl_eden_plan_num_slices", "ofl_eden_plan_planes_bytes",
     "ofl_eden_plan_workspace_bytes", "ofl_eden_plan_tensor_info", "ofl_eden_plan_tensor_dims",
-    "ofl_eden_encode", "ofl_eden_decode", "ofl_serial_sum_f32", "ofl_serial_sum_f64",
+    "ofl_eden_encode", "ofl_eden_decode", "ofl_eden_plan_profile", "ofl_eden_plan_num_launches",
+    "ofl_eden_plan_launch_info", "ofl_eden_plan_profile_collect", "ofl_serial_sum_f32",
+    "ofl_serial_sum_f64",
 )
 
 
@@ -49,6 +51,14 @@ def _bind(L):
     L.ofl_eden_encode.restype = i32
     L.ofl_eden_decode.argtypes = [vp, vp, vp, vp, vp, vp, sz, vp]
     L.ofl_eden_decode.restype = i32
+    L.ofl_eden_plan_profile.argtypes = [vp, i32]
+    L.ofl_eden_plan_profile.restype = i32
+    L.ofl_eden_plan_num_launches.argtypes = [vp, i32]
+    L.ofl_eden_plan_num_launches.restype = i32
+    L.ofl_eden_plan_launch_info.argtypes = [vp, i32, i32, ctypes.c_char_p, i32, vp, vp, vp]
+    L.ofl_eden_plan_launch_info.restype = i32
+    L.ofl_eden_plan_profile_collect.argtypes = [vp, i32, vp, i32, vp]
+    L.ofl_eden_plan_profile_collect.restype = i32
     L.ofl_serial_sum_f32.argtypes = [vp, i64]
     L.ofl_serial_sum_f32.restype = ctypes.c_float
     L.ofl_serial_sum_f64.argtypes = [vp, i64]

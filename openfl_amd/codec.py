@@ -111,6 +111,31 @@ class EdenPlan:
                                            ws.data_ptr() if ws is not None else None,
                                            ws.numel() if ws is not None else 0, st.cuda_stream))
 
+    # -- profiling (HIP events between launches; see ofl_codec.h) --
+    def profile(self, enable=True):
+        _lib.check(self._L.ofl_eden_plan_profile(self._h, 1 if enable else 0))
+
+    def launches(self, encode):
+        out = []
+        for i in range(self._L.ofl_eden_plan_num_launches(self._h, 1 if encode else 0)):
+            name = ctypes.create_string_buffer(128)
+            blocks, mv, al = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+            _lib.check(self._L.ofl_eden_plan_launch_info(self._h, 1 if encode else 0, i, name, 128,
+                                                         ctypes.byref(blocks), ctypes.byref(mv),
+                                                         ctypes.byref(al)))
+            out.append({"name": name.value.decode(), "blocks": blocks.value,
+                        "bytes_moved": mv.value, "bytes_alg": al.value})
+        return out
+
+    def profile_collect(self, encode):
+        """-> (per-launch summed ms, number of recorded calls)."""
+        n = self._L.ofl_eden_plan_num_launches(self._h, 1 if encode else 0)
+        ms = np.zeros(max(n, 1), np.float64)
+        calls = ctypes.c_int()
+        _lib.check(self._L.ofl_eden_plan_profile_collect(self._h, 1 if encode else 0, _ptr(ms), n,
+                                                         ctypes.byref(calls)))
+        return ms[:n], calls.value
+
     @staticmethod
     def _check(t, dtype, min_numel):
         if not t.is_cuda:

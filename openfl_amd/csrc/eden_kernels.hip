@@ -883,6 +883,8 @@ struct Launch {
     int tstart_off;  // into d_tstart (multi-tile kernels), -1 otherwise
     int count;       // list entries
     int64_t blocks;  // grid size
+    int64_t bytes_moved;  // fp32/plane bytes this launch reads + writes in HBM (intermediates included)
+    int64_t bytes_alg;    // its share of the SURVEY 8(d) algorithmic bytes (x/y fp32 + planes only)
 };
 enum Kind { K_TINY, K_SMALL, K_ROWA, K_ROWC, K_COL, K_NORMS, K_FINAL };
 
@@ -900,6 +902,10 @@ struct ofl_eden_plan {
     int64_t nlarge = 0;
     std::vector<Launch> enc, dec;
     std::vector<int32_t> ints;  // launch lists and tile prefixes (host copy)
+    // profiling: events around every launch of every call while enabled
+    bool prof = false;
+    std::vector<std::vector<hipEvent_t>> prof_ev[2];  // [dec, enc][call][launch+1]
+    std::vector<hipEvent_t> ev_pool;
     ofl::SliceDesc* d_slices = nullptr;
     int32_t* d_ints = nullptr;
     int device = -1;
@@ -946,7 +952,21 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t st) {
         attrs_done = true;
     }
     const std::vector<Launch>& L = enc ? pl->enc : pl->dec;
-    for (const Launch& l : L) {
+    std::vector<hipEvent_t>* evs = nullptr;
+    if (pl->prof) {
+        std::lock_guard<std::mutex> g(pl->mu);
+        pl->prof_ev[enc].emplace_back();
+        evs = &pl->prof_ev[enc].back();
+        for (size_t i = 0; i <= L.size(); ++i) {
+            hipEvent_t e;
+            if (!pl->ev_pool.empty()) { e = pl->ev_pool.back(); pl->ev_pool.pop_back(); }
+            else HIP_TRY(hipEventCreate(&e));
+            evs->push_back(e);
+        }
+        HIP_TRY(hipEventRecord((*evs)[0], st));
+    }
+    for (size_t li = 0; li < L.size(); ++li) {
+        const Launch& l = L[li];
         ofl::KArgs a = base;
         a.list = pl->d_ints + l.list_off;
         a.tstart = l.tstart_off >= 0 ? pl->d_ints + l.tstart_off : nullptr;
@@ -999,8 +1019,22 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t st) {
         case K_FINAL: e = launch(ofl::k_finalize, l.blocks, 256, 0, st, a); break;
         }
         if (e != hipSuccess) return fail(OFL_EHIP, std::string("kernel launch failed: ") + hipGetErrorString(e));
+        if (evs) HIP_TRY(hipEventRecord((*evs)[li + 1], st));
     }
     return OFL_OK;
+}
+
+std::string launch_name(const Launch& l, bool enc) {
+    const char* d = enc ? "enc" : "dec";
+    switch (l.kind) {
+    case K_TINY: return std::string("ofl::k_") + d + "_tiny";
+    case K_SMALL: return std::string("ofl::k_") + d + "_small<" + std::to_string(l.param) + ">";
+    case K_ROWA: return std::string("ofl::k_") + d + "_rowA";
+    case K_ROWC: return std::string("ofl::k_") + d + "_rowC";
+    case K_COL: return "ofl::k_col<" + std::to_string(l.param) + ", " + (l.mid ? "true" : "false") + ">";
+    case K_NORMS: return "ofl::k_norms";
+    default: return "ofl::k_finalize";
+    }
 }
 
 }  // namespace
@@ -1157,6 +1191,29 @@ int ofl_eden_plan_create(int ntensors, const int64_t* numel, const int64_t* elem
         pl->dec.insert(pl->dec.end(), colseq.begin(), colseq.end());
         pl->dec.push_back({K_ROWC, 0, 0, 0, lo_l, rp, nl, rows});
     }
+    // per-launch byte accounting (bench / DESIGN.md roofline)
+    for (int dir = 0; dir < 2; ++dir) {
+        const bool enc = dir == 1;
+        for (Launch& l : enc ? pl->enc : pl->dec) {
+            int64_t mv = 0, al = 0;
+            for (int i = 0; i < l.count; ++i) {
+                const ofl::SliceDesc& D = pl->slices[ints[l.list_off + i]];
+                const int64_t P = 1ll << D.logp, pb = (int64_t)n_bits * P / 8;
+                switch (l.kind) {
+                case K_TINY: case K_SMALL:
+                    mv += enc ? 4 * D.len + pb : pb + 4 * D.ylen; al = mv; break;
+                case K_ROWA:
+                    mv += enc ? 4 * D.len + 4 * P : pb + 4 * P; al += enc ? 4 * D.len : pb; break;
+                case K_ROWC:
+                    mv += enc ? 4 * P + pb : 4 * P + 4 * D.ylen; al += enc ? pb : 4 * D.ylen; break;
+                case K_COL: mv += 8 * P; break;
+                default: mv += 4 * (P >> ofl::kRowLog); break;
+                }
+            }
+            l.bytes_moved = mv;
+            l.bytes_alg = al;
+        }
+    }
     *plan_out = pl;
     return OFL_OK;
 }
@@ -1182,6 +1239,8 @@ static int ensure_device(ofl_eden_plan_t pl) {
 
 void ofl_eden_plan_destroy(ofl_eden_plan_t pl) {
     if (!pl) return;
+    ofl_eden_plan_profile(pl, 0);
+    for (hipEvent_t e : pl->ev_pool) (void)hipEventDestroy(e);
     if (pl->d_slices) (void)hipFree(pl->d_slices);
     if (pl->d_ints) (void)hipFree(pl->d_ints);
     delete pl;
@@ -1251,6 +1310,57 @@ int ofl_eden_decode(ofl_eden_plan_t pl, const uint8_t* planes_arena, const uint3
     a.seeds = seeds;
     a.scales_in = scales;
     return run(pl, false, a, static_cast<hipStream_t>(stream));
+}
+
+int ofl_eden_plan_profile(ofl_eden_plan_t pl, int enable) {
+    if (!pl) return fail(OFL_EINVAL, "null plan");
+    std::lock_guard<std::mutex> g(pl->mu);
+    for (int d = 0; d < 2; ++d) {
+        for (auto& call : pl->prof_ev[d]) pl->ev_pool.insert(pl->ev_pool.end(), call.begin(), call.end());
+        pl->prof_ev[d].clear();
+    }
+    pl->prof = enable != 0;
+    return OFL_OK;
+}
+
+int ofl_eden_plan_num_launches(ofl_eden_plan_t pl, int encode) {
+    if (!pl) return fail(OFL_EINVAL, "null plan");
+    return (int)(encode ? pl->enc.size() : pl->dec.size());
+}
+
+int ofl_eden_plan_launch_info(ofl_eden_plan_t pl, int encode, int idx, char* name, int cap, int64_t* blocks,
+                              int64_t* bytes_moved, int64_t* bytes_alg) {
+    if (!pl) return fail(OFL_EINVAL, "null plan");
+    const std::vector<Launch>& L = encode ? pl->enc : pl->dec;
+    if (idx < 0 || idx >= (int)L.size()) return fail(OFL_EINVAL, "launch index out of range");
+    if (name && cap > 0) {
+        const std::string s = launch_name(L[idx], encode != 0);
+        snprintf(name, (size_t)cap, "%s", s.c_str());
+    }
+    if (blocks) *blocks = L[idx].blocks;
+    if (bytes_moved) *bytes_moved = L[idx].bytes_moved;
+    if (bytes_alg) *bytes_alg = L[idx].bytes_alg;
+    return OFL_OK;
+}
+
+int ofl_eden_plan_profile_collect(ofl_eden_plan_t pl, int encode, double* ms_sum, int max, int* ncalls) {
+    if (!pl) return fail(OFL_EINVAL, "null plan");
+    std::lock_guard<std::mutex> g(pl->mu);
+    auto& calls = pl->prof_ev[encode ? 1 : 0];
+    const int nl = (int)(encode ? pl->enc.size() : pl->dec.size());
+    for (int i = 0; i < std::min(nl, max); ++i) ms_sum[i] = 0.0;
+    for (auto& call : calls) {
+        HIP_TRY(hipEventSynchronize(call.back()));
+        for (int i = 0; i < nl && i < max; ++i) {
+            float ms = 0.f;
+            HIP_TRY(hipEventElapsedTime(&ms, call[i], call[i + 1]));
+            ms_sum[i] += ms;
+        }
+        pl->ev_pool.insert(pl->ev_pool.end(), call.begin(), call.end());
+    }
+    if (ncalls) *ncalls = (int)calls.size();
+    calls.clear();
+    return OFL_OK;
 }
 
 float ofl_serial_sum_f32(const float* x, int64_t n) {

@@ -61,7 +61,7 @@ def gen_input(n, seed, scale=0.01):
 
 EDEN_NS = [1, 7, 8, 99, 100, 101, 500, 1000, 4096, 37000, 65537]
 BIG_N = 300000
-FULL_PLANES_MAX = 64 * 1024
+FULL_PLANES_MAX = 512 * 1024
 
 
 def eden_fixtures(ref):
