@@ -31,17 +31,6 @@ METRIC = "GiB/s device-resident Eden encode+decode, fp32 update tensors, 1/2/4/8
 PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 
-def lpt_partition(sizes, parts):
-    order = sorted(range(len(sizes)), key=lambda i: -sizes[i])
-    load = [0] * parts
-    out = [[] for _ in range(parts)]
-    for i in order:
-        r = min(range(parts), key=lambda k: load[k])
-        out[r].append(i)
-        load[r] += sizes[i]
-    return [sorted(o) for o in out]
-
-
 def cpu_baseline(shapes, x_host_fn, n_bits, sample_mib):
     """The C oracle (oracle/eden_oracle.c, single thread) on a bounded sample
     of the same workload: leading tensors (after a leading embedding, if any)
@@ -96,6 +85,7 @@ def main():
     import torch
     import torch.distributed as dist
     from openfl_amd.codec import EdenPlan
+    from openfl_amd.sharding import max_over_ranks, shard_indices, throughput_gib_s
     from openfl_amd.workloads import WORKLOADS, numel
 
     torch.cuda.set_device(local)
@@ -105,10 +95,7 @@ def main():
 
     shapes = WORKLOADS[args.workload]()
     sizes = [numel(s) for _, s in shapes]
-    if args.scaling == "strong" and world > 1:
-        mine = lpt_partition(sizes, world)[rank]
-    else:
-        mine = list(range(len(shapes)))
+    mine = shard_indices(sizes, rank, world, args.scaling)
     numels = [sizes[i] for i in mine]
     plan = EdenPlan(numels, args.n_bits)
 
@@ -154,10 +141,7 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     gpu_ms = ev0.elapsed_time(ev1)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, dev)
 
     # per-kernel breakdown from the events recorded inside the timed region
     kernels = {}
@@ -178,11 +162,7 @@ def main():
         rel = float(torch.linalg.vector_norm((y - x).double()) / torch.linalg.vector_norm(x.double()))
 
     in_bytes_rank = 4 * sum(numels)
-    if args.scaling == "weak":
-        total_bytes = in_bytes_rank * world
-    else:
-        total_bytes = 4 * sum(sizes)
-    value = total_bytes * args.steps / elapsed / 2 ** 30
+    value = throughput_gib_s(in_bytes_rank, world, args.steps, elapsed, args.scaling, 4 * sum(sizes))
 
     alg_step = sum(l["bytes_alg"] for e in (True, False) for l in plan.launches(e))
     step_s = gpu_ms / 1e3 / args.steps
