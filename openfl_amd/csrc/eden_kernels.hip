@@ -11,19 +11,19 @@
 //
 // MI355X design (see DESIGN.md for the roofline):
 //  * Every transform is a sequence of FWHT "stages" (one per index bit).  A
-//    workgroup owns a 2^13 / 2^14-element tile; each thread keeps 32 elements
-//    in VGPRs ("layout" = which 5 index bits live in registers) and runs the
-//    stages of those bits as register butterflies.  Between layouts the tile
-//    is transposed through LDS with an XOR swizzle that keeps every ds_write /
-//    ds_read_b32 wave access bank-conflict-free.
-//  * Slices with P <= 2^14 are done in ONE kernel, one workgroup per slice,
+//    workgroup owns a tile of up to 2^15 elements; each thread keeps 32
+//    elements in VGPRs ("layout" = which 5 index bits live in registers) and
+//    runs the stages of those bits as register butterflies.  Between layouts
+//    the tile is transposed through LDS with an XOR swizzle that keeps every
+//    ds_write / ds_read_b32 wave access bank-conflict-free.
+//  * Slices with P <= 2^15 are done in ONE kernel, one workgroup per slice,
 //    straight from HBM to bit planes (encode) or planes to HBM (decode).
-//  * Larger slices use H_P = H_rows (x) H_cols: a row pass (contiguous 2^13
-//    rows), column passes over the remaining bits (2^14-element tiles of
-//    2^m rows x 2^(14-m) contiguous columns) and a final row pass.  The two
+//  * Larger slices use H_P = H_rows (x) H_cols: a row pass (contiguous 2^15
+//    rows), column passes over the remaining bits (2^15-element tiles of
+//    2^M rows x 2^(15-M) contiguous columns) and a final row pass.  The two
 //    Hadamards meet in the middle column pass, which fuses F1's last stages,
 //    D2 and F2's first stages, so a 2-Hadamard encode is 3 HBM passes for
-//    P <= 2^22.
+//    P <= 2^25 (5 passes for 2^26..2^29).
 //  * D1/D2 signs are regenerated on the fly (no sign tensors in HBM); the two
 //    LCG steps are folded into one affine map r2 = A*j + B(seed).
 //  * Normalisation uses exact powers of two (2^-floor(p/2) at D2, 2^-ceil(p/2)
@@ -31,8 +31,9 @@
 //    identical for even p, < 1e-7 relative apart for odd p.
 //  * bucketize is exact with one compare: a 1/64 grid over z (every cell
 //    holds <= 1 boundary) stored in LDS with {count, 64*B, C_lo, C_hi}.
-//  * Bit planes are produced by an in-register 8x8 bit-matrix transpose of 32
+//  * Bit planes are produced by in-register 8x8 bit-matrix transposes of 32
 //    contiguous bins per thread -> one 32-bit store per plane per thread.
+//  * Global addressing: uniform 64-bit base + 32-bit per-lane offsets.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -53,7 +54,7 @@
 namespace ofl {
 
 // ---------------------------------------------------------------------------
-// Descriptors (host-built once per plan, uploaded once)
+// Descriptors (host-built once per plan, uploaded on first use)
 // ---------------------------------------------------------------------------
 struct SliceDesc {
     int64_t x_off;      // encode: element offset of the slice's input in the fp32 arena
@@ -77,8 +78,8 @@ struct KArgs {
     int32_t nbits;
     int32_t lo;             // column passes: first transformed bit
     int32_t pad_;
-    const float* xin;       // fp32 arena in (encode) / ws in
-    float* xout;            // fp32 arena out (decode) / ws out
+    const float* xin;       // fp32 arena in (encode)
+    float* xout;            // fp32 arena out (decode)
     float* ws;              // intermediate buffer base
     const uint8_t* pin;     // planes in (decode)
     uint8_t* pout;          // planes out (encode)
@@ -89,9 +90,15 @@ struct KArgs {
     float* nu;              // per-slice norms (large)
 };
 
-// Eden tables in global memory (read into LDS per workgroup)
+// Eden tables in global memory (copied to LDS per workgroup)
 __device__ const float g_centroids[8][256] = {
 #include "eden_centroids.inc"
+};
+__device__ const unsigned char g_grid[8][EDEN_GRID_CELLS] = {
+#include "eden_grid.inc"
+};
+__device__ const float g_bounds[8][256] = {
+#include "eden_bounds.inc"
 };
 
 // ---------------------------------------------------------------------------
@@ -118,14 +125,20 @@ DEVI uint32_t rd_mix(uint32_t r2) {
     return t ^ (t >> 16);
 }
 DEVI uint32_t rd_word(uint32_t j, uint32_t b) { return rd_mix(kLcgA * j + b); }
-// sign of element with nibble index nib, word w: +1 iff nibble >= 8 (:440-447)
-DEVI float sgn_apply(float v, uint32_t w, uint32_t nib) {
-    uint32_t bit = (w >> (4u * nib + 3u)) & 1u;
-    return __uint_as_float(__float_as_uint(v) ^ ((bit ^ 1u) << 31));
+// the 8 sign bits of word j: bit k = 1 <=> nibble k >= 8 <=> element k*S+j is +1 (:440-447)
+DEVI uint32_t rd_byte(uint32_t j, uint32_t b) {
+    const uint32_t w = rd_word(j, b) >> 3;
+    uint32_t r = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r |= ((w >> (4 * k)) & 1u) << k;
+    return r;
 }
-DEVI float sgn_elem(float v, uint64_t e, int p, uint32_t b) {
-    const uint64_t S = 1ull << (p - 3);
-    return sgn_apply(v, rd_word((uint32_t)(e & (S - 1)), b), (uint32_t)(e >> (p - 3)));
+DEVI float flip_unless(float v, uint32_t plus) {  // plus = 1 -> +v, 0 -> -v
+    return __uint_as_float(__float_as_uint(v) ^ ((plus ^ 1u) << 31));
+}
+DEVI float sgn_elem(float v, uint32_t e, int p, uint32_t b) {
+    const uint32_t jm = (1u << (p - 3)) - 1u;
+    return flip_unless(v, (rd_word(e & jm, b) >> (4u * (e >> (p - 3)) + 3u)) & 1u);
 }
 
 // ---------------------------------------------------------------------------
@@ -153,8 +166,14 @@ template <Lay L> struct LT {
     }
 };
 
-constexpr uint32_t cswz(uint32_t e) { return e ^ (((e >> 5) ^ (e >> 10)) & 31u); }
-DEVI uint32_t swz(uint32_t e) { return e ^ (((e >> 5) ^ (e >> 10)) & 31u); }
+// LDS address of tile element e: one pad word per 32 and per 1024 elements.
+// Additive over disjoint bit sets (pad(b | o) = pad(b) + pad(o)), so register
+// offsets become DS immediates, and conflict-free for every half-wave lane
+// pattern the layouts use: lanes varying index bits {0..4}, {5..9}, {2..6} or
+// {0,1,7,8,9} hit 32 distinct banks (bank = address mod 32 for b32 ops).
+constexpr uint32_t cpad(uint32_t e) { return e + (e >> 5) + (e >> 10); }
+DEVI uint32_t pad(uint32_t e) { return e + (e >> 5) + (e >> 10); }
+constexpr size_t lds_floats(int nb) { return ((size_t)1 << nb) + ((size_t)1 << nb >> 5) + ((size_t)1 << nb >> 10); }
 
 // butterflies on every register bit whose element bit is in ACT
 template <Lay L, uint32_t ACT>
@@ -176,13 +195,13 @@ DEVI void stages(float (&v)[32]) {
 
 template <Lay A, Lay B>
 DEVI void exchange(float (&v)[32], float* s, uint32_t tid) {
-    const uint32_t ba = swz(LT<A>::base(tid));
+    const uint32_t ba = pad(LT<A>::base(tid));
 #pragma unroll
-    for (int r = 0; r < 32; ++r) s[ba ^ cswz(LT<A>::off(r))] = v[r];
+    for (int r = 0; r < 32; ++r) s[ba + cpad(LT<A>::off(r))] = v[r];
     __syncthreads();
-    const uint32_t bb = swz(LT<B>::base(tid));
+    const uint32_t bb = pad(LT<B>::base(tid));
 #pragma unroll
-    for (int r = 0; r < 32; ++r) v[r] = s[bb ^ cswz(LT<B>::off(r))];
+    for (int r = 0; r < 32; ++r) v[r] = s[bb + cpad(LT<B>::off(r))];
     __syncthreads();
 }
 
@@ -210,40 +229,32 @@ DEVI float block_sum(float v, float* red) {
 }
 
 // ---------------------------------------------------------------------------
-// Quantiser table in LDS: cell k of z*64 in [k-288, k-287):
-//   {lo = #B < (k-288)/64, 64*B[lo], C[lo], C[lo+1]}
+// Quantiser tables in LDS.  Grid cell k of z*64 in [k-288, k-287):
+//   QEnt{lo = #B < (k-288)/64, 64*B[lo]}  (+inf when lo = 2^b - 1)
+// then bin = lo + (64 B[lo] < 64 z) exactly, and C[bin] from a 256-entry table.
 // ---------------------------------------------------------------------------
-struct QEnt { int lo; float b64; float clo; float chi; };
-__device__ const unsigned char g_grid[8][EDEN_GRID_CELLS] = {
-#include "eden_grid.inc"
-};
-__device__ const float g_bounds[8][256] = {
-#include "eden_bounds.inc"
-};
+struct QEnt { int lo; float b64; };
+struct QTab { QEnt grid[EDEN_GRID_CELLS]; float cen[256]; };
 
 template <int NT>
-DEVI void load_qtable(QEnt* q, int nbits) {
+DEVI void load_qtable(QTab* q, int nbits) {
     const int nb = (1 << nbits) - 1;
     for (int k = threadIdx.x; k < EDEN_GRID_CELLS; k += NT) {
         const int lo = g_grid[nbits - 1][k];
-        QEnt e;
-        e.lo = lo;
-        e.b64 = lo < nb ? g_bounds[nbits - 1][lo] * 64.0f : __int_as_float(0x7f800000);
-        e.clo = g_centroids[nbits - 1][lo];
-        e.chi = g_centroids[nbits - 1][lo < nb ? lo + 1 : lo];
-        q[k] = e;
+        q->grid[k] = QEnt{lo, lo < nb ? g_bounds[nbits - 1][lo] * 64.0f : __int_as_float(0x7f800000)};
     }
+    for (int k = threadIdx.x; k < 256; k += NT) q->cen[k] = g_centroids[nbits - 1][k];
 }
 
-// bucketize + centroid: returns bin, writes centroid
-DEVI int quant(float z64, const QEnt* q, float& c) {
+// bucketize + centroid (exact, one compare): returns bin, writes centroid
+DEVI int quant(float z64, const QTab* q, float& c) {
     float f = floorf(z64);
     f = fminf(fmaxf(f, -288.0f), 287.0f);
-    const int k = (int)f + EDEN_GRID_OFF;  // NaN -> clamp gives 287 or -288 path; harmless
-    const QEnt e = q[k];
-    const bool up = e.b64 < z64;
-    c = up ? e.chi : e.clo;
-    return e.lo + (up ? 1 : 0);
+    const int k = (int)f + EDEN_GRID_OFF;
+    const QEnt e = q->grid[k];
+    const int b = e.lo + (e.b64 < z64 ? 1 : 0);
+    c = q->cen[b];
+    return b;
 }
 
 // ---------------------------------------------------------------------------
@@ -256,33 +267,41 @@ DEVI uint64_t tr8x8(uint64_t x) {
     t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull; x ^= t ^ (t << 28);
     return x;
 }
-// bins[32] (each < 256) -> w[8]: bit t of w[i] = bit i of bins[t]
-DEVI void pack32(const int (&bins)[32], uint32_t (&w)[8]) {
-    uint64_t g[4];
+
+// quantise 32 contiguous values (registers r = element offset r) and build the
+// plane words: bit t of w[i] = bit i of bin(element t).  Returns <C[bins], y>.
+DEVI float quant_pack32(const float (&v)[32], float ysc, float zm64, const QTab* q, uint32_t (&w)[8]) {
+    float dot = 0.f;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int i = 0; i < 8; ++i) w[i] = 0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
         uint64_t x = 0;
 #pragma unroll
-        for (int t = 0; t < 8; ++t) x |= (uint64_t)(uint32_t)bins[8 * q + t] << (8 * t);
-        g[q] = tr8x8(x);  // byte i of g[q] = plane i bits of elements 8q..8q+7
-    }
+        for (int t = 0; t < 8; ++t) {
+            const float y = v[8 * g + t] * ysc;
+            float c;
+            const int b = quant(y * zm64, q, c);
+            dot += c * y;
+            x |= (uint64_t)(uint32_t)b << (8 * t);
+        }
+        x = tr8x8(x);  // byte i = plane-i bits of elements 8g..8g+7
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        uint32_t r = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) r |= (uint32_t)((g[q] >> (8 * i)) & 0xffu) << (8 * q);
-        w[i] = r;
+        for (int i = 0; i < 8; ++i) w[i] |= (uint32_t)((x >> (8 * i)) & 0xffu) << (8 * g);
+        asm volatile("" ::: "memory");  // keep each group's LDS-table reads in the group (VGPR cap 128)
     }
+    return dot;
 }
-DEVI void unpack32(const uint32_t (&w)[8], int (&bins)[32]) {
+// plane words -> centroid values of 32 contiguous elements
+DEVI void unpack_centroids32(const uint32_t (&w)[8], const float* cen, float (&v)[32]) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int g = 0; g < 4; ++g) {
         uint64_t x = 0;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) x |= (uint64_t)((w[i] >> (8 * q)) & 0xffu) << (8 * i);
-        x = tr8x8(x);  // transpose is an involution
+        for (int i = 0; i < 8; ++i) x |= (uint64_t)((w[i] >> (8 * g)) & 0xffu) << (8 * i);
+        x = tr8x8(x);  // involution: byte t = bin of element 8g+t
 #pragma unroll
-        for (int t = 0; t < 8; ++t) bins[8 * q + t] = (int)((x >> (8 * t)) & 0xffu);
+        for (int t = 0; t < 8; ++t) v[8 * g + t] = cen[(x >> (8 * t)) & 0xffu];
     }
 }
 DEVI void store_plane_word(uint8_t* p, uint32_t w) {
@@ -296,49 +315,65 @@ DEVI uint32_t load_plane_word(const uint8_t* p) {
     if ((reinterpret_cast<uintptr_t>(p) & 3u) == 0) return *reinterpret_cast<const uint32_t*>(p);
     return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
+// planes at plane0 + byte (e >> 3), stride between planes
+DEVI void store_planes(uint8_t* plane0, uint32_t e, int64_t stride, int nbits, const uint32_t (&w)[8]) {
+    uint8_t* p = plane0 + (e >> 3);
+    for (int i = 0; i < nbits; ++i) store_plane_word(p + (int64_t)i * stride, w[i]);
+}
+DEVI void load_planes(const uint8_t* plane0, uint32_t e, int64_t stride, int nbits, uint32_t (&w)[8]) {
+    const uint8_t* p = plane0 + (e >> 3);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = 0;
+    for (int i = 0; i < nbits; ++i) w[i] = load_plane_word(p + (int64_t)i * stride);
+}
 
 DEVI float pow2i(int e) { return __int_as_float((127 + e) << 23); }  // 2^e, |e| < 127
 
+// Hide a value from the optimiser so per-register addresses are recomputed
+// (cheap ALU) instead of being kept live across a whole pass (32 VGPRs).
+DEVI uint32_t opaque(uint32_t v) { asm volatile("" : "+v"(v)); return v; }
+
 // ---------------------------------------------------------------------------
-// fp32 element I/O with valid-length bound (zero padding, :541-546)
+// fp32 element I/O with valid-length bound (zero padding, :541-546); base is
+// block-uniform, offsets 32-bit.
 // ---------------------------------------------------------------------------
-DEVI void load4(const float* base, int64_t i, int64_t len, float* v) {
-    if (i + 3 < len && ((reinterpret_cast<uintptr_t>(base + i) & 15u) == 0)) {
+DEVI void load4(const float* base, uint32_t i, int64_t len, float* v) {
+    if ((int64_t)i + 3 < len && ((reinterpret_cast<uintptr_t>(base) & 15u) == 0)) {
         const float4 f = *reinterpret_cast<const float4*>(base + i);
         v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
     } else {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = (i + q < len) ? base[i + q] : 0.0f;
+        for (int q = 0; q < 4; ++q) v[q] = ((int64_t)i + q < len) ? base[i + q] : 0.0f;
     }
 }
-DEVI void store4(float* base, int64_t i, int64_t len, const float* v) {
-    if (i + 3 < len && ((reinterpret_cast<uintptr_t>(base + i) & 15u) == 0)) {
+DEVI void store4(float* base, uint32_t i, int64_t len, const float* v) {
+    if ((int64_t)i + 3 < len && ((reinterpret_cast<uintptr_t>(base) & 15u) == 0)) {
         *reinterpret_cast<float4*>(base + i) = make_float4(v[0], v[1], v[2], v[3]);
     } else {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) if (i + q < len) base[i + q] = v[q];
+        for (int q = 0; q < 4; ++q) if ((int64_t)i + q < len) base[i + q] = v[q];
     }
 }
 
 // block-uniform slice lookup for multi-tile launches
-DEVI void find_tile(const KArgs& a, int& slice, int64_t& tile) {
-    const int64_t b = blockIdx.x;
+DEVI void find_tile(const KArgs& a, int& slice, uint32_t& tile) {
+    const int b = (int)blockIdx.x;
     int lo = 0, hi = a.count - 1;
     while (lo < hi) {
         int mid = (lo + hi + 1) >> 1;
         if (a.tstart[mid] <= b) lo = mid; else hi = mid - 1;
     }
     slice = a.list[lo];
-    tile = b - a.tstart[lo];
+    tile = (uint32_t)(b - a.tstart[lo]);
 }
 
 // ===========================================================================
-// Layout sets.  Small slices: one set per p in 11..14 (tile = slice, NT =
-// 2^(p-5)).  Row passes of large slices reuse the p = 13 set.
+// Layout sets.  Small slices: one set per p in 11..15 (tile = slice, NT =
+// 2^(p-5)).  Row passes of large slices reuse the p = 15 set.
 //   encode: L1 (load, D1) F1 -> L2 F1 -> L3 F1 | D2 | L3 F2 -> L4 F2 -> L5 F2 (pack)
 //   decode: the reverse.
-// Lanes 0..31 of every layout vary 5 index bits with distinct residues mod 5,
-// so swz() keeps every exchange bank-conflict-free.
+// Lanes 0..31 of every layout vary index bits {0..4}, {5..9}, {2..6} or
+// {0,1,7,8,9}, so pad() keeps every exchange bank-conflict-free.
 // ===========================================================================
 template <int P> struct SmallSet;
 template <> struct SmallSet<11> {
@@ -369,69 +404,62 @@ template <> struct SmallSet<14> {
                               F1c = bits_mask({7, 8, 9, 10}), F2c = bits_mask({7, 8, 9, 10, 11}),
                               F2d = bits_mask({5, 6, 12, 13}), F2e = bits_mask({0, 1, 2, 3, 4});
 };
+template <> struct SmallSet<15> {
+    static constexpr Lay L1{15, 0, 1, 12, 13, 14}, L2{15, 2, 3, 4, 5, 6}, L3{15, 7, 8, 9, 10, 11},
+                         L4{15, 5, 6, 12, 13, 14}, L5{15, 0, 1, 2, 3, 4};
+    static constexpr uint32_t F1a = bits_mask({0, 1, 12, 13, 14}), F1b = bits_mask({2, 3, 4, 5, 6}),
+                              F1c = bits_mask({7, 8, 9, 10, 11}), F2c = bits_mask({7, 8, 9, 10, 11}),
+                              F2d = bits_mask({5, 6, 12, 13, 14}), F2e = bits_mask({0, 1, 2, 3, 4});
+};
 
-// signs of the 32 register elements of layout L from an LDS word table
+// signs of the 32 register elements of layout L from an LDS byte table
+// (byte j, bit k = sign of element k*S + j), times mul
 template <Lay L>
-DEVI void apply_signs_tab(float (&v)[32], uint32_t base, const uint32_t* tab, int p, float mul) {
+DEVI void apply_signs_tab(float (&v)[32], uint32_t base, const uint8_t* tab, int p, float mul) {
     const uint32_t jm = (1u << (p - 3)) - 1u;
 #pragma unroll
     for (int r = 0; r < 32; ++r) {
         const uint32_t e = base | LT<L>::off(r);
-        v[r] = sgn_apply(v[r] * mul, tab[e & jm], e >> (p - 3));
+        v[r] = flip_unless(v[r] * mul, ((uint32_t)tab[e & jm] >> (e >> (p - 3))) & 1u);
     }
 }
 // signs of the 32 register elements computed directly (rows of large slices)
 template <Lay L>
-DEVI void apply_signs_direct(float (&v)[32], uint64_t ebase, uint32_t base, int p, uint32_t b,
-                             float mul) {
+DEVI void apply_signs_direct(float (&v)[32], uint32_t ebase, uint32_t base, int p, uint32_t b, float mul) {
 #pragma unroll
     for (int r = 0; r < 32; ++r) v[r] = sgn_elem(v[r] * mul, ebase + (base | LT<L>::off(r)), p, b);
 }
 
-// quantise 32 contiguous values: bins + partial dot <C[bins], y>
-DEVI float quant32(const float (&v)[32], float ysc, float zm64, const QEnt* q, int (&bins)[32]) {
-    float dot = 0.f;
-#pragma unroll
-    for (int r = 0; r < 32; ++r) {
-        const float y = v[r] * ysc;
-        float c;
-        bins[r] = quant(y * zm64, q, c);
-        dot += c * y;
-    }
-    return dot;
-}
-// pack 32 contiguous bins starting at slice element `e` into every plane
-DEVI void pack_store(int (&bins)[32], bool zero, uint8_t* plane0, int64_t e, int64_t stride, int nbits) {
-    if (zero) {
-#pragma unroll
-        for (int r = 0; r < 32; ++r) bins[r] = 0;
-    }
-    uint32_t w[8];
-    pack32(bins, w);
-    uint8_t* p = plane0 + (e >> 3);
-    for (int i = 0; i < nbits; ++i) store_plane_word(p + (int64_t)i * stride, w[i]);
-}
+// LDS carve-up of the single-kernel small path
+template <int P_LOG> struct SmallSmem {
+    static constexpr int NT = 1 << (P_LOG - 5);
+    static constexpr int NS = 1 << (P_LOG - 3);
+    static constexpr size_t data = (sizeof(float) * lds_floats(P_LOG) + 15) & ~(size_t)15;
+    static constexpr size_t tabs = 2 * NS;                                   // bytes
+    static constexpr size_t enc = data + tabs + sizeof(QTab) + 4 * 16;
+    static constexpr size_t dec = data + tabs + sizeof(float) * 256;
+};
 
 // ===========================================================================
-// Small slices (2^11 <= P <= 2^14): one workgroup per slice, whole codec.
+// Small slices (2^11 <= P <= 2^15): one workgroup per slice, whole codec.
 // ===========================================================================
 template <int P_LOG>
 __global__ __launch_bounds__(1 << (P_LOG - 5)) void k_enc_small(KArgs a) {
     using S = SmallSet<P_LOG>;
-    constexpr int NT = 1 << (P_LOG - 5);
-    constexpr int NS = 1 << (P_LOG - 3);
+    using SM = SmallSmem<P_LOG>;
+    constexpr int NT = SM::NT, NS = SM::NS;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    float* s = reinterpret_cast<float*>(smem);                       // 4 * 2^p
-    uint32_t* tab1 = reinterpret_cast<uint32_t*>(s + (1 << P_LOG));  // NS words
-    uint32_t* tab2 = tab1 + NS;                                      // NS words
-    QEnt* qt = reinterpret_cast<QEnt*>(tab2 + NS);                   // 576 * 16 B
-    float* red = reinterpret_cast<float*>(qt + EDEN_GRID_CELLS);     // NT/64
+    float* s = reinterpret_cast<float*>(smem);
+    uint8_t* tab1 = smem + SM::data;
+    uint8_t* tab2 = tab1 + NS;
+    QTab* qt = reinterpret_cast<QTab*>(smem + SM::data + SM::tabs);
+    float* red = reinterpret_cast<float*>(qt + 1);
 
     const SliceDesc D = a.d[a.list[blockIdx.x]];
     const uint32_t tid = threadIdx.x;
     const uint32_t seed = a.seeds[D.tensor];
     const uint32_t b1 = seed_b(seed), b2 = seed_b(seed + 1u);
-    for (int j = tid; j < NS; j += NT) { tab1[j] = rd_word(j, b1); tab2[j] = rd_word(j, b2); }
+    for (int j = tid; j < NS; j += NT) { tab1[j] = (uint8_t)rd_byte(j, b1); tab2[j] = (uint8_t)rd_byte(j, b2); }
     load_qtable<NT>(qt, a.nbits);
 
     float v[32];
@@ -463,45 +491,44 @@ __global__ __launch_bounds__(1 << (P_LOG - 5)) void k_enc_small(KArgs a) {
     const float nu = sqrtf(ss);
     const bool pos = nu > 0.0f;
     const float zm64 = 64.0f * (sqrtf((float)(1 << P_LOG)) / nu);
-    int bins[32];
-    float dot = quant32(v, ysc, zm64, qt, bins);
+    uint32_t w[8];
+    float dot = quant_pack32(v, ysc, zm64, qt, w);
     if (!pos) dot = 0.f;
     dot = block_sum<NT>(dot, red);
     float scale = pos ? (nu * nu) / dot : 0.0f;
     const bool zero = !pos || isnan(scale);  // reference zero fallback (:517-525)
-    if (zero) scale = 0.0f;
-    pack_store(bins, zero, a.pout + D.pl_off, LT<S::L5>::base(tid), D.pl_stride, a.nbits);
+    if (zero) {
+        scale = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w[i] = 0;
+    }
+    store_planes(a.pout + D.pl_off, LT<S::L5>::base(tid), D.pl_stride, a.nbits, w);
     if (tid == 0) a.scales[D.scale_idx] = scale;
 }
 
 template <int P_LOG>
 __global__ __launch_bounds__(1 << (P_LOG - 5)) void k_dec_small(KArgs a) {
     using S = SmallSet<P_LOG>;
-    constexpr int NT = 1 << (P_LOG - 5);
-    constexpr int NS = 1 << (P_LOG - 3);
+    using SM = SmallSmem<P_LOG>;
+    constexpr int NT = SM::NT, NS = SM::NS;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float* s = reinterpret_cast<float*>(smem);
-    uint32_t* tab1 = reinterpret_cast<uint32_t*>(s + (1 << P_LOG));
-    uint32_t* tab2 = tab1 + NS;
-    float* cen = reinterpret_cast<float*>(tab2 + NS);  // 256
+    uint8_t* tab1 = smem + SM::data;
+    uint8_t* tab2 = tab1 + NS;
+    float* cen = reinterpret_cast<float*>(smem + SM::data + SM::tabs);
 
     const SliceDesc D = a.d[a.list[blockIdx.x]];
     const uint32_t tid = threadIdx.x;
     const uint32_t seed = a.seeds[D.tensor];
     const uint32_t b1 = seed_b(seed), b2 = seed_b(seed + 1u);
-    for (int j = tid; j < NS; j += NT) { tab1[j] = rd_word(j, b1); tab2[j] = rd_word(j, b2); }
+    for (int j = tid; j < NS; j += NT) { tab1[j] = (uint8_t)rd_byte(j, b1); tab2[j] = (uint8_t)rd_byte(j, b2); }
     for (int j = tid; j < 256; j += NT) cen[j] = g_centroids[a.nbits - 1][j];
     float v[32];
     {
-        const uint32_t base = LT<S::L5>::base(tid);
-        const uint8_t* p = a.pin + D.pl_off + (base >> 3);
-        uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int i = 0; i < a.nbits; ++i) w[i] = load_plane_word(p + (int64_t)i * D.pl_stride);
-        int bins[32];
-        unpack32(w, bins);
+        uint32_t w[8];
+        load_planes(a.pin + D.pl_off, LT<S::L5>::base(tid), D.pl_stride, a.nbits, w);
         __syncthreads();
-#pragma unroll
-        for (int r = 0; r < 32; ++r) v[r] = cen[bins[r]];
+        unpack_centroids32(w, cen, v);
     }
     stages<S::L5, S::F2e>(v);
     exchange<S::L5, S::L4>(v, s, tid);
@@ -542,7 +569,7 @@ DEVI void fwht_lds_generic(float* s, int P) {
 __global__ __launch_bounds__(64) void k_enc_tiny(KArgs a) {
     __shared__ float s[1024];
     __shared__ unsigned char bins[1024];
-    __shared__ QEnt qt[EDEN_GRID_CELLS];
+    __shared__ QTab qt[1];
     __shared__ float red[1];
     const SliceDesc D = a.d[a.list[blockIdx.x]];
     const int p = D.logp, P = 1 << p;
@@ -550,12 +577,11 @@ __global__ __launch_bounds__(64) void k_enc_tiny(KArgs a) {
     const uint32_t b1 = seed_b(seed), b2 = seed_b(seed + 1u);
     load_qtable<64>(qt, a.nbits);
     const float* x = a.xin + D.x_off;
-    for (int e = threadIdx.x; e < P; e += 64)
-        s[e] = sgn_elem(e < D.len ? x[e] : 0.0f, (uint64_t)e, p, b1);
+    for (int e = threadIdx.x; e < P; e += 64) s[e] = sgn_elem(e < D.len ? x[e] : 0.0f, e, p, b1);
     __syncthreads();
     fwht_lds_generic(s, P);
     const float m2 = pow2i(-(p / 2));
-    for (int e = threadIdx.x; e < P; e += 64) s[e] = sgn_elem(s[e] * m2, (uint64_t)e, p, b2);
+    for (int e = threadIdx.x; e < P; e += 64) s[e] = sgn_elem(s[e] * m2, e, p, b2);
     __syncthreads();
     fwht_lds_generic(s, P);
     const float ysc = pow2i(-((p + 1) / 2));
@@ -603,43 +629,47 @@ __global__ __launch_bounds__(64) void k_dec_tiny(KArgs a) {
     __syncthreads();
     fwht_lds_generic(s, P);
     const float m2 = pow2i(-(p / 2));
-    for (int e = threadIdx.x; e < P; e += 64) s[e] = sgn_elem(s[e] * m2, (uint64_t)e, p, b2);
+    for (int e = threadIdx.x; e < P; e += 64) s[e] = sgn_elem(s[e] * m2, e, p, b2);
     __syncthreads();
     fwht_lds_generic(s, P);
     const float m1 = pow2i(-((p + 1) / 2));
     const float sc = a.scales_in[D.scale_idx];
     float* y = a.xout + D.y_off;
     for (int e = threadIdx.x; e < P; e += 64)
-        if (e < D.ylen) y[e] = sc * sgn_elem(s[e] * m1, (uint64_t)e, p, b1);
+        if (e < D.ylen) y[e] = sc * sgn_elem(s[e] * m1, e, p, b1);
 }
 
 // ===========================================================================
-// Large slices (P >= 2^15): row passes (2^13 contiguous, NT = 256)
+// Large slices (P >= 2^16): row passes (2^15 contiguous, NT = 1024)
 // ===========================================================================
-using RS = SmallSet<13>;
-constexpr int kRowLog = 13;
-constexpr int kRowNT = 256;
+using RS = SmallSet<15>;
+constexpr int kRowLog = 15;
+constexpr int kRowNT = 1024;
+constexpr size_t kRowSmem = (sizeof(float) * lds_floats(kRowLog) + 15) & ~(size_t)15;
+constexpr size_t kRowSmemQ = kRowSmem + sizeof(QTab) + 4 * 16;
+constexpr size_t kRowSmemC = kRowSmem + sizeof(float) * 256;
 
 // encode pass A: x -> D1 -> F1 row stages -> ws ; partial sum of x^2
 __global__ __launch_bounds__(kRowNT) void k_enc_rowA(KArgs a) {
-    __shared__ __attribute__((aligned(16))) float s[1 << kRowLog];
-    __shared__ float red[kRowNT / 64];
-    int si; int64_t tile;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float* s = reinterpret_cast<float*>(smem);
+    float* red = reinterpret_cast<float*>(smem + kRowSmem);
+    int si; uint32_t tile;
     find_tile(a, si, tile);
     const SliceDesc D = a.d[si];
     const uint32_t tid = threadIdx.x;
     const uint32_t b1 = seed_b(a.seeds[D.tensor]);
-    const int64_t e0 = tile << kRowLog;
+    const uint32_t e0 = tile << kRowLog;
     float v[32];
     const uint32_t base1 = LT<RS::L1>::base(tid);
     const float* x = a.xin + D.x_off + e0;
-    const int64_t len = D.len - e0;
+    const int64_t len = D.len - (int64_t)e0;
 #pragma unroll
     for (int r = 0; r < 32; r += 4) load4(x, base1 | LT<RS::L1>::off(r), len, &v[r]);
     float ss = 0.f;
 #pragma unroll
     for (int r = 0; r < 32; ++r) ss += v[r] * v[r];
-    apply_signs_direct<RS::L1>(v, (uint64_t)e0, base1, D.logp, b1, 1.0f);
+    apply_signs_direct<RS::L1>(v, e0, base1, D.logp, b1, 1.0f);
     stages<RS::L1, RS::F1a>(v);
     exchange<RS::L1, RS::L2>(v, s, tid);
     stages<RS::L2, RS::F1b>(v);
@@ -655,15 +685,16 @@ __global__ __launch_bounds__(kRowNT) void k_enc_rowA(KArgs a) {
 
 // encode pass C: ws -> F2 row stages -> y -> quantise, pack ; partial dot
 __global__ __launch_bounds__(kRowNT) void k_enc_rowC(KArgs a) {
-    __shared__ __attribute__((aligned(16))) float s[1 << kRowLog];
-    __shared__ QEnt qt[EDEN_GRID_CELLS];
-    __shared__ float red[kRowNT / 64];
-    int si; int64_t tile;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float* s = reinterpret_cast<float*>(smem);
+    QTab* qt = reinterpret_cast<QTab*>(smem + kRowSmem);
+    float* red = reinterpret_cast<float*>(qt + 1);
+    int si; uint32_t tile;
     find_tile(a, si, tile);
     const SliceDesc D = a.d[si];
     const uint32_t tid = threadIdx.x;
     load_qtable<kRowNT>(qt, a.nbits);
-    const int64_t e0 = tile << kRowLog;
+    const uint32_t e0 = tile << kRowLog;
     float v[32];
     const float* w = a.ws + D.ws_off + e0;
     const uint32_t base3 = LT<RS::L3>::base(tid);
@@ -672,41 +703,41 @@ __global__ __launch_bounds__(kRowNT) void k_enc_rowC(KArgs a) {
     stages<RS::L3, RS::F2c>(v);
     exchange<RS::L3, RS::L4>(v, s, tid);
     stages<RS::L4, RS::F2d>(v);
-    exchange<RS::L4, RS::L5>(v, s, tid);  // also orders qt writes before use
+    exchange<RS::L4, RS::L5>(v, s, tid);  // its barriers also publish qt
     stages<RS::L5, RS::F2e>(v);
     const float nu = a.nu[si];
     const bool pos = nu > 0.0f;
     const float ysc = pow2i(-((D.logp + 1) / 2));
     const float zm64 = 64.0f * (sqrtf((float)(1ll << D.logp)) / nu);
-    int bins[32];
-    float dot = quant32(v, ysc, zm64, qt, bins);
-    pack_store(bins, !pos, a.pout + D.pl_off, e0 + LT<RS::L5>::base(tid), D.pl_stride, a.nbits);
-    if (!pos) dot = 0.f;
+    uint32_t wd[8];
+    float dot = quant_pack32(v, ysc, zm64, qt, wd);
+    if (!pos) {
+        dot = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) wd[i] = 0;
+    }
+    store_planes(a.pout + D.pl_off, e0 + LT<RS::L5>::base(tid), D.pl_stride, a.nbits, wd);
     dot = block_sum<kRowNT>(dot, red);
     if (tid == 0) a.part[D.part_off + tile] = dot;
 }
 
 // decode pass A: planes -> C[bins] -> G1 row stages -> ws
 __global__ __launch_bounds__(kRowNT) void k_dec_rowA(KArgs a) {
-    __shared__ __attribute__((aligned(16))) float s[1 << kRowLog];
-    __shared__ float cen[256];
-    int si; int64_t tile;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float* s = reinterpret_cast<float*>(smem);
+    float* cen = reinterpret_cast<float*>(smem + kRowSmem);
+    int si; uint32_t tile;
     find_tile(a, si, tile);
     const SliceDesc D = a.d[si];
     const uint32_t tid = threadIdx.x;
-    cen[tid] = g_centroids[a.nbits - 1][tid];
-    const int64_t e0 = tile << kRowLog;
+    if (tid < 256) cen[tid] = g_centroids[a.nbits - 1][tid];
+    const uint32_t e0 = tile << kRowLog;
     float v[32];
-    const uint32_t base5 = LT<RS::L5>::base(tid);
     {
-        const uint8_t* p = a.pin + D.pl_off + (e0 >> 3) + (base5 >> 3);
-        uint32_t wd[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int i = 0; i < a.nbits; ++i) wd[i] = load_plane_word(p + (int64_t)i * D.pl_stride);
-        int bins[32];
-        unpack32(wd, bins);
+        uint32_t wd[8];
+        load_planes(a.pin + D.pl_off, e0 + LT<RS::L5>::base(tid), D.pl_stride, a.nbits, wd);
         __syncthreads();
-#pragma unroll
-        for (int r = 0; r < 32; ++r) v[r] = cen[bins[r]];
+        unpack_centroids32(wd, cen, v);
     }
     stages<RS::L5, RS::F2e>(v);
     exchange<RS::L5, RS::L4>(v, s, tid);
@@ -721,13 +752,14 @@ __global__ __launch_bounds__(kRowNT) void k_dec_rowA(KArgs a) {
 
 // decode pass C: ws -> G2 row stages -> D1, scale -> y
 __global__ __launch_bounds__(kRowNT) void k_dec_rowC(KArgs a) {
-    __shared__ __attribute__((aligned(16))) float s[1 << kRowLog];
-    int si; int64_t tile;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float* s = reinterpret_cast<float*>(smem);
+    int si; uint32_t tile;
     find_tile(a, si, tile);
     const SliceDesc D = a.d[si];
     const uint32_t tid = threadIdx.x;
     const uint32_t b1 = seed_b(a.seeds[D.tensor]);
-    const int64_t e0 = tile << kRowLog;
+    const uint32_t e0 = tile << kRowLog;
     float v[32];
     const float* w = a.ws + D.ws_off + e0;
     const uint32_t base3 = LT<RS::L3>::base(tid);
@@ -739,30 +771,32 @@ __global__ __launch_bounds__(kRowNT) void k_dec_rowC(KArgs a) {
     exchange<RS::L2, RS::L1>(v, s, tid);
     stages<RS::L1, RS::F1a>(v);
     const uint32_t base1 = LT<RS::L1>::base(tid);
-    apply_signs_direct<RS::L1>(v, (uint64_t)e0, base1, D.logp, b1, pow2i(-((D.logp + 1) / 2)));
+    apply_signs_direct<RS::L1>(v, e0, base1, D.logp, b1, pow2i(-((D.logp + 1) / 2)));
     const float sc = a.scales_in[D.scale_idx];
 #pragma unroll
     for (int r = 0; r < 32; ++r) v[r] = sc * v[r];
     float* y = a.xout + D.y_off + e0;
-    const int64_t len = D.ylen - e0;
+    const int64_t len = D.ylen - (int64_t)e0;
 #pragma unroll
     for (int r = 0; r < 32; r += 4) store4(y, base1 | LT<RS::L1>::off(r), len, &v[r]);
 }
 
 // ===========================================================================
-// Column passes: tile = 2^M rows (index bits [lo, lo+M)) x 2^(14-M)
-// contiguous columns (bits [0, 14-M)), NT = 512.  MID fuses F1 | D2 | F2.
+// Column passes: tile = 2^M rows (index bits [lo, lo+M)) x 2^(15-M)
+// contiguous columns (bits [0, 15-M)), NT = 1024.  MID fuses F1 | D2 | F2.
 // ===========================================================================
-constexpr int kColNT = 512;
+constexpr int kColLog = 15;
+constexpr int kColNT = 1024;
+constexpr size_t kColSmem = (sizeof(float) * lds_floats(kColLog) + 15) & ~(size_t)15;
 template <int M> struct ColSet {
-    static constexpr int K = 14 - M;
+    static constexpr int K = kColLog - M;
     static constexpr int m1 = M < 5 ? M : 5;
     // L1: rows K..K+m1-1, filled with top columns K-1, K-2, ...
     static constexpr int l1(int i) { return i < m1 ? K + i : K - 1 - (i - m1); }
-    static constexpr Lay L1{14, l1(0), l1(1), l1(2), l1(3), l1(4)};
+    static constexpr Lay L1{kColLog, l1(0), l1(1), l1(2), l1(3), l1(4)};
     // L2: rows K+5..K+M-1, filled with rows K, K+1, ...
     static constexpr int l2(int i) { return i < M - 5 ? K + 5 + i : K + (i - (M - 5)); }
-    static constexpr Lay L2{14, l2(0), l2(1), l2(2), l2(3), l2(4)};
+    static constexpr Lay L2{kColLog, l2(0), l2(1), l2(2), l2(3), l2(4)};
     static constexpr uint32_t A1 = ((1u << m1) - 1u) << K;
     static constexpr uint32_t A2 = M > 5 ? ((1u << (M - 5)) - 1u) << (K + 5) : 0u;
 };
@@ -771,20 +805,19 @@ template <int M, bool MID>
 __global__ __launch_bounds__(kColNT) void k_col(KArgs a) {
     using CS = ColSet<M>;
     constexpr int K = CS::K;
-    __shared__ __attribute__((aligned(16))) float s[M > 5 ? (1 << 14) : 1];
-    int si; int64_t tile;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float* s = reinterpret_cast<float*>(smem);
+    int si; uint32_t tile;
     find_tile(a, si, tile);
     const SliceDesc D = a.d[si];
     const uint32_t tid = threadIdx.x;
     const int lo = a.lo;
     // tile -> slice bits: [K, lo) from tile low bits, [lo+M, p) from the rest
-    const int64_t tl = tile & ((1ll << (lo - K)) - 1);
-    const int64_t th = tile >> (lo - K);
-    const int64_t tb = (tl << K) | (th << (lo + M));
+    const uint32_t tl = tile & ((1u << (lo - K)) - 1u);
+    const uint32_t th = tile >> (lo - K);
+    const uint32_t tb = (tl << K) | (th << (lo + M));
     float* w = a.ws + D.ws_off;
-    auto map = [&](uint32_t t) -> int64_t {
-        return tb | (int64_t)(t & ((1u << K) - 1u)) | ((int64_t)(t >> K) << lo);
-    };
+    auto map = [&](uint32_t t) -> uint32_t { return tb | (t & ((1u << K) - 1u)) | ((t >> K) << lo); };
     float v[32];
     const uint32_t base1 = LT<CS::L1>::base(tid);
 #pragma unroll
@@ -798,29 +831,32 @@ __global__ __launch_bounds__(kColNT) void k_col(KArgs a) {
         const uint32_t b2 = seed_b(a.seeds[D.tensor] + 1u);
         const float m2 = pow2i(-(D.logp / 2));
         if constexpr (M > 5) {
-            const uint32_t base2 = LT<CS::L2>::base(tid);
+            const uint32_t base2 = opaque(LT<CS::L2>::base(tid));
 #pragma unroll
             for (int r = 0; r < 32; ++r)
-                v[r] = sgn_elem(v[r] * m2, (uint64_t)map(base2 | LT<CS::L2>::off(r)), D.logp, b2);
+                v[r] = sgn_elem(v[r] * m2, map(base2 | LT<CS::L2>::off(r)), D.logp, b2);
             stages<CS::L2, CS::A2>(v);
             exchange<CS::L2, CS::L1>(v, s, tid);
             stages<CS::L1, CS::A1>(v);
         } else {
+            const uint32_t base1s = opaque(base1);
 #pragma unroll
             for (int r = 0; r < 32; ++r)
-                v[r] = sgn_elem(v[r] * m2, (uint64_t)map(base1 | LT<CS::L1>::off(r)), D.logp, b2);
+                v[r] = sgn_elem(v[r] * m2, map(base1s | LT<CS::L1>::off(r)), D.logp, b2);
             stages<CS::L1, CS::A1>(v);
         }
+        const uint32_t base1w = opaque(base1);
 #pragma unroll
-        for (int r = 0; r < 32; ++r) w[map(base1 | LT<CS::L1>::off(r))] = v[r];
+        for (int r = 0; r < 32; ++r) w[map(base1w | LT<CS::L1>::off(r))] = v[r];
     } else {
         if constexpr (M > 5) {
-            const uint32_t base2 = LT<CS::L2>::base(tid);
+            const uint32_t base2 = opaque(LT<CS::L2>::base(tid));
 #pragma unroll
             for (int r = 0; r < 32; ++r) w[map(base2 | LT<CS::L2>::off(r))] = v[r];
         } else {
+            const uint32_t base1w = opaque(base1);
 #pragma unroll
-            for (int r = 0; r < 32; ++r) w[map(base1 | LT<CS::L1>::off(r))] = v[r];
+            for (int r = 0; r < 32; ++r) w[map(base1w | LT<CS::L1>::off(r))] = v[r];
         }
     }
 }
@@ -927,30 +963,54 @@ hipError_t launch(K kern, int64_t blocks, int threads, size_t shmem, hipStream_t
 }
 
 size_t small_smem(int p, bool enc) {
-    size_t s = sizeof(float) * (1u << p) + 2 * sizeof(uint32_t) * (1u << (p - 3));
-    if (enc) s += sizeof(ofl::QEnt) * EDEN_GRID_CELLS + sizeof(float) * 16;
-    else s += sizeof(float) * 256;
-    return s;
+    switch (p) {
+    case 11: return enc ? ofl::SmallSmem<11>::enc : ofl::SmallSmem<11>::dec;
+    case 12: return enc ? ofl::SmallSmem<12>::enc : ofl::SmallSmem<12>::dec;
+    case 13: return enc ? ofl::SmallSmem<13>::enc : ofl::SmallSmem<13>::dec;
+    case 14: return enc ? ofl::SmallSmem<14>::enc : ofl::SmallSmem<14>::dec;
+    default: return enc ? ofl::SmallSmem<15>::enc : ofl::SmallSmem<15>::dec;
+    }
+}
+
+hipError_t set_lds(const void* f, size_t bytes) {
+    return hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
 template <int P>
-hipError_t set_smem_attr() {
-    hipError_t e = hipFuncSetAttribute((const void*)ofl::k_enc_small<P>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)small_smem(P, true));
-    if (e != hipSuccess) return e;
-    return hipFuncSetAttribute((const void*)ofl::k_dec_small<P>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)small_smem(P, false));
+hipError_t set_small_attr() {
+    hipError_t e = set_lds((const void*)ofl::k_enc_small<P>, ofl::SmallSmem<P>::enc);
+    return e != hipSuccess ? e : set_lds((const void*)ofl::k_dec_small<P>, ofl::SmallSmem<P>::dec);
+}
+
+template <int M>
+hipError_t set_col_attr() {
+    hipError_t e = set_lds((const void*)ofl::k_col<M, true>, M > 5 ? ofl::kColSmem : 0);
+    return e != hipSuccess ? e : set_lds((const void*)ofl::k_col<M, false>, M > 5 ? ofl::kColSmem : 0);
+}
+
+hipError_t set_all_attrs() {
+    hipError_t e;
+    if ((e = set_small_attr<11>()) != hipSuccess) return e;
+    if ((e = set_small_attr<12>()) != hipSuccess) return e;
+    if ((e = set_small_attr<13>()) != hipSuccess) return e;
+    if ((e = set_small_attr<14>()) != hipSuccess) return e;
+    if ((e = set_small_attr<15>()) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_enc_rowA, ofl::kRowSmem + 64)) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_enc_rowC, ofl::kRowSmemQ)) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_dec_rowA, ofl::kRowSmemC)) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_dec_rowC, ofl::kRowSmem)) != hipSuccess) return e;
+    if ((e = set_col_attr<6>()) != hipSuccess) return e;
+    if ((e = set_col_attr<7>()) != hipSuccess) return e;
+    if ((e = set_col_attr<8>()) != hipSuccess) return e;
+    if ((e = set_col_attr<9>()) != hipSuccess) return e;
+    return set_col_attr<10>();
 }
 
 int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t st) {
-    static bool attrs_done = false;
-    if (!attrs_done) {
-        HIP_TRY(set_smem_attr<11>());
-        HIP_TRY(set_smem_attr<12>());
-        HIP_TRY(set_smem_attr<13>());
-        HIP_TRY(set_smem_attr<14>());
-        attrs_done = true;
-    }
+    static std::once_flag attrs_once;
+    static hipError_t attrs_err = hipSuccess;
+    std::call_once(attrs_once, [] { attrs_err = set_all_attrs(); });
+    if (attrs_err != hipSuccess) return fail(OFL_EHIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(attrs_err));
     const std::vector<Launch>& L = enc ? pl->enc : pl->dec;
     std::vector<hipEvent_t>* evs = nullptr;
     if (pl->prof) {
@@ -981,35 +1041,36 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t st) {
             const int p = l.param;
             const int nt = 1 << (p - 5);
             const size_t sm = small_smem(p, enc);
-            if (enc) {
-                if (p == 11) e = launch(ofl::k_enc_small<11>, l.blocks, nt, sm, st, a);
-                else if (p == 12) e = launch(ofl::k_enc_small<12>, l.blocks, nt, sm, st, a);
-                else if (p == 13) e = launch(ofl::k_enc_small<13>, l.blocks, nt, sm, st, a);
-                else e = launch(ofl::k_enc_small<14>, l.blocks, nt, sm, st, a);
-            } else {
-                if (p == 11) e = launch(ofl::k_dec_small<11>, l.blocks, nt, sm, st, a);
-                else if (p == 12) e = launch(ofl::k_dec_small<12>, l.blocks, nt, sm, st, a);
-                else if (p == 13) e = launch(ofl::k_dec_small<13>, l.blocks, nt, sm, st, a);
-                else e = launch(ofl::k_dec_small<14>, l.blocks, nt, sm, st, a);
+#define SMALLCASE(PP)                                                                         \
+    case PP:                                                                                  \
+        e = enc ? launch(ofl::k_enc_small<PP>, l.blocks, nt, sm, st, a)                       \
+                : launch(ofl::k_dec_small<PP>, l.blocks, nt, sm, st, a);                      \
+        break;
+            switch (p) {
+                SMALLCASE(11) SMALLCASE(12) SMALLCASE(13) SMALLCASE(14) SMALLCASE(15)
+            default: return fail(OFL_EINVAL, "small slice size out of range");
             }
+#undef SMALLCASE
             break;
         }
         case K_ROWA:
-            e = enc ? launch(ofl::k_enc_rowA, l.blocks, ofl::kRowNT, 0, st, a)
-                    : launch(ofl::k_dec_rowA, l.blocks, ofl::kRowNT, 0, st, a);
+            e = enc ? launch(ofl::k_enc_rowA, l.blocks, ofl::kRowNT, ofl::kRowSmem + 64, st, a)
+                    : launch(ofl::k_dec_rowA, l.blocks, ofl::kRowNT, ofl::kRowSmemC, st, a);
             break;
         case K_ROWC:
-            e = enc ? launch(ofl::k_enc_rowC, l.blocks, ofl::kRowNT, 0, st, a)
-                    : launch(ofl::k_dec_rowC, l.blocks, ofl::kRowNT, 0, st, a);
+            e = enc ? launch(ofl::k_enc_rowC, l.blocks, ofl::kRowNT, ofl::kRowSmemQ, st, a)
+                    : launch(ofl::k_dec_rowC, l.blocks, ofl::kRowNT, ofl::kRowSmem, st, a);
             break;
         case K_COL: {
+            const size_t sm = l.param > 5 ? ofl::kColSmem : 0;
 #define COLCASE(MM)                                                                                  \
     case MM:                                                                                         \
-        e = l.mid ? launch(ofl::k_col<MM, true>, l.blocks, ofl::kColNT, 0, st, a)                    \
-                  : launch(ofl::k_col<MM, false>, l.blocks, ofl::kColNT, 0, st, a);                  \
+        e = l.mid ? launch(ofl::k_col<MM, true>, l.blocks, ofl::kColNT, sm, st, a)                   \
+                  : launch(ofl::k_col<MM, false>, l.blocks, ofl::kColNT, sm, st, a);                 \
         break;
             switch (l.param) {
                 COLCASE(1) COLCASE(2) COLCASE(3) COLCASE(4) COLCASE(5) COLCASE(6) COLCASE(7) COLCASE(8) COLCASE(9)
+                COLCASE(10)
             default: return fail(OFL_EINVAL, "column pass height out of range");
             }
 #undef COLCASE
@@ -1074,7 +1135,7 @@ int ofl_eden_plan_create(int ntensors, const int64_t* numel, const int64_t* elem
     pl->ntensors = ntensors;
     int64_t dims_pos = 0;
     // per-class slice lists
-    std::vector<int32_t> tiny, small[4], large;
+    std::vector<int32_t> tiny, small[5], large;
     for (int t = 0; t < ntensors; ++t) {
         const int64_t n = numel[t];
         std::vector<int64_t> Ps, Ls;  // padded sizes, valid input lengths
@@ -1126,7 +1187,7 @@ int ofl_eden_plan_create(int ntensors, const int64_t* numel, const int64_t* elem
             D.scale_idx = (int32_t)pl->slices.size();
             const int si = (int)pl->slices.size();
             if (D.logp <= 10) tiny.push_back(si);
-            else if (D.logp <= 14) small[D.logp - 11].push_back(si);
+            else if (D.logp <= ofl::kRowLog) small[D.logp - 11].push_back(si);
             else {
                 D.ws_off = pl->ws_floats;
                 pl->ws_floats += P;
@@ -1153,7 +1214,7 @@ int ofl_eden_plan_create(int ntensors, const int64_t* numel, const int64_t* elem
     };
     std::vector<Launch> common;
     if (!tiny.empty()) common.push_back({K_TINY, 0, 0, 0, add_list(tiny), -1, (int)tiny.size(), (int64_t)tiny.size()});
-    for (int k = 0; k < 4; ++k)
+    for (int k = 0; k < 5; ++k)
         if (!small[k].empty())
             common.push_back({K_SMALL, 11 + k, 0, 0, add_list(small[k]), -1, (int)small[k].size(), (int64_t)small[k].size()});
     pl->enc = common;
@@ -1170,9 +1231,9 @@ int ofl_eden_plan_create(int ntensors, const int64_t* numel, const int64_t* elem
             const int p = kv.first, r = p - ofl::kRowLog;
             int64_t tiles = 0;
             const int lo_c = add_list(kv.second);
-            const int tp = add_prefix(kv.second, 14, tiles);
+            const int tp = add_prefix(kv.second, ofl::kColLog, tiles);
             const int cnt = (int)kv.second.size();
-            if (r <= 9) {
+            if (r <= 10) {
                 colseq.push_back({K_COL, r, ofl::kRowLog, 1, lo_c, tp, cnt, tiles});
             } else {
                 const int m1 = r / 2, m2 = r - m1;
