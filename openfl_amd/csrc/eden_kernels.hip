@@ -355,7 +355,16 @@ DEVI void store4(float* base, uint32_t i, int64_t len, const float* v) {
     }
 }
 
-// block-uniform slice lookup for multi-tile launches
+// block-uniform slice lookup for multi-tile launches (tile b of the launch)
+DEVI void find_tile_at(const KArgs& a, int b, int& slice, uint32_t& tile) {
+    int lo = 0, hi = a.count - 1;
+    while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if (a.tstart[mid] <= b) lo = mid; else hi = mid - 1;
+    }
+    slice = a.list[lo];
+    tile = (uint32_t)(b - a.tstart[lo]);
+}
 DEVI void find_tile(const KArgs& a, int& slice, uint32_t& tile) {
     const int b = (int)blockIdx.x;
     int lo = 0, hi = a.count - 1;
@@ -423,11 +432,23 @@ DEVI void apply_signs_tab(float (&v)[32], uint32_t base, const uint8_t* tab, int
         v[r] = flip_unless(v[r] * mul, ((uint32_t)tab[e & jm] >> (e >> (p - 3))) & 1u);
     }
 }
-// signs of the 32 register elements computed directly (rows of large slices)
+// signs of the 32 register elements computed directly (rows of large slices,
+// tile start ebase a multiple of 2^15).  For p >= 18 the tile lies inside one
+// nibble region (S = 2^(p-3) >= 2^15): j = (ebase mod S) + base + off(r), so
+// r2 = A*j + B is one add of the compile-time constant A*off(r) per element.
 template <Lay L>
 DEVI void apply_signs_direct(float (&v)[32], uint32_t ebase, uint32_t base, int p, uint32_t b, float mul) {
+    if (p >= 18) {
+        const uint32_t jm = (1u << (p - 3)) - 1u;
+        const uint32_t r2b = kLcgA * ((ebase & jm) + base) + b;
+        const uint32_t sh = 4u * (ebase >> (p - 3)) + 3u;
 #pragma unroll
-    for (int r = 0; r < 32; ++r) v[r] = sgn_elem(v[r] * mul, ebase + (base | LT<L>::off(r)), p, b);
+        for (int r = 0; r < 32; ++r)
+            v[r] = flip_unless(v[r] * mul, (rd_mix(r2b + kLcgA * LT<L>::off(r)) >> sh) & 1u);
+    } else {
+#pragma unroll
+        for (int r = 0; r < 32; ++r) v[r] = sgn_elem(v[r] * mul, ebase + (base | LT<L>::off(r)), p, b);
+    }
 }
 
 // LDS carve-up of the single-kernel small path
@@ -801,12 +822,20 @@ template <int M> struct ColSet {
     static constexpr uint32_t A2 = M > 5 ? ((1u << (M - 5)) - 1u) << (K + 5) : 0u;
 };
 
+// The middle pass's D2 signs: the tile spans the slice's top three index bits
+// (the rand_diag nibble index) whenever M >= 3, so each of its 2^12 distinct
+// words j serves 8 elements: one hash per 8 elements, kept as a byte table in
+// LDS (bit k of byte = sign of element k*S + j).  M < 3 hashes per element.
+constexpr size_t kColTab = 4096;
+
 template <int M, bool MID>
 __global__ __launch_bounds__(kColNT) void k_col(KArgs a) {
     using CS = ColSet<M>;
     constexpr int K = CS::K;
+    constexpr bool TAB = MID && M >= 3;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float* s = reinterpret_cast<float*>(smem);
+    uint8_t* tab = smem + (M > 5 ? kColSmem : 0);
     int si; uint32_t tile;
     find_tile(a, si, tile);
     const SliceDesc D = a.d[si];
@@ -818,31 +847,51 @@ __global__ __launch_bounds__(kColNT) void k_col(KArgs a) {
     const uint32_t tb = (tl << K) | (th << (lo + M));
     float* w = a.ws + D.ws_off;
     auto map = [&](uint32_t t) -> uint32_t { return tb | (t & ((1u << K) - 1u)) | ((t >> K) << lo); };
+    // sign-table index of tile element t: the tile bits below the nibble bits
+    // (columns, then rows lo .. p-4), i.e. t with its top 3 bits removed
+    constexpr uint32_t kTabMask = (1u << (kColLog - 3)) - 1u;
+    if constexpr (TAB) {
+        const uint32_t b2 = seed_b(a.seeds[D.tensor] + 1u);
+        for (uint32_t q = tid; q < (1u << (kColLog - 3)); q += kColNT)
+            tab[q] = (uint8_t)rd_byte(map(q) & ((1u << (D.logp - 3)) - 1u), b2);
+    }
     float v[32];
     const uint32_t base1 = LT<CS::L1>::base(tid);
 #pragma unroll
     for (int r = 0; r < 32; ++r) v[r] = w[map(base1 | LT<CS::L1>::off(r))];
     stages<CS::L1, CS::A1>(v);
     if constexpr (M > 5) {
-        exchange<CS::L1, CS::L2>(v, s, tid);
+        exchange<CS::L1, CS::L2>(v, s, tid);  // its barriers also publish tab
         stages<CS::L2, CS::A2>(v);
+    } else if constexpr (TAB) {
+        __syncthreads();
     }
     if constexpr (MID) {
-        const uint32_t b2 = seed_b(a.seeds[D.tensor] + 1u);
         const float m2 = pow2i(-(D.logp / 2));
         if constexpr (M > 5) {
             const uint32_t base2 = opaque(LT<CS::L2>::base(tid));
 #pragma unroll
-            for (int r = 0; r < 32; ++r)
-                v[r] = sgn_elem(v[r] * m2, map(base2 | LT<CS::L2>::off(r)), D.logp, b2);
+            for (int r = 0; r < 32; ++r) {
+                const uint32_t t = base2 | LT<CS::L2>::off(r);
+                v[r] = flip_unless(v[r] * m2, ((uint32_t)tab[t & kTabMask] >> (t >> (kColLog - 3))) & 1u);
+            }
             stages<CS::L2, CS::A2>(v);
             exchange<CS::L2, CS::L1>(v, s, tid);
             stages<CS::L1, CS::A1>(v);
         } else {
             const uint32_t base1s = opaque(base1);
+            if constexpr (TAB) {
 #pragma unroll
-            for (int r = 0; r < 32; ++r)
-                v[r] = sgn_elem(v[r] * m2, map(base1s | LT<CS::L1>::off(r)), D.logp, b2);
+                for (int r = 0; r < 32; ++r) {
+                    const uint32_t t = base1s | LT<CS::L1>::off(r);
+                    v[r] = flip_unless(v[r] * m2, ((uint32_t)tab[t & kTabMask] >> (t >> (kColLog - 3))) & 1u);
+                }
+            } else {
+                const uint32_t b2 = seed_b(a.seeds[D.tensor] + 1u);
+#pragma unroll
+                for (int r = 0; r < 32; ++r)
+                    v[r] = sgn_elem(v[r] * m2, map(base1s | LT<CS::L1>::off(r)), D.logp, b2);
+            }
             stages<CS::L1, CS::A1>(v);
         }
         const uint32_t base1w = opaque(base1);
@@ -982,10 +1031,12 @@ hipError_t set_small_attr() {
     return e != hipSuccess ? e : set_lds((const void*)ofl::k_dec_small<P>, ofl::SmallSmem<P>::dec);
 }
 
+size_t col_smem(int M, bool mid) { return (M > 5 ? ofl::kColSmem : 0) + (mid && M >= 3 ? ofl::kColTab : 0); }
+
 template <int M>
 hipError_t set_col_attr() {
-    hipError_t e = set_lds((const void*)ofl::k_col<M, true>, M > 5 ? ofl::kColSmem : 0);
-    return e != hipSuccess ? e : set_lds((const void*)ofl::k_col<M, false>, M > 5 ? ofl::kColSmem : 0);
+    hipError_t e = set_lds((const void*)ofl::k_col<M, true>, col_smem(M, true));
+    return e != hipSuccess ? e : set_lds((const void*)ofl::k_col<M, false>, col_smem(M, false));
 }
 
 hipError_t set_all_attrs() {
@@ -1062,7 +1113,7 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t st) {
                     : launch(ofl::k_dec_rowC, l.blocks, ofl::kRowNT, ofl::kRowSmem, st, a);
             break;
         case K_COL: {
-            const size_t sm = l.param > 5 ? ofl::kColSmem : 0;
+            const size_t sm = col_smem(l.param, l.mid != 0);
 #define COLCASE(MM)                                                                                  \
     case MM:                                                                                         \
         e = l.mid ? launch(ofl::k_col<MM, true>, l.blocks, ofl::kColNT, sm, st, a)                   \
