@@ -121,6 +121,40 @@ int ofl_eden_plan_launch_info(ofl_eden_plan_t plan, int encode, int idx, char* n
 int ofl_eden_plan_profile_collect(ofl_eden_plan_t plan, int encode, double* ms_sum, int max,
                                   int* ncalls);
 
+/* ---- lossy k-means / sparsify / ternary pipelines ---------------------------
+ * (openfl/pipelines/kc_pipeline.py, skc_pipeline.py, stc_pipeline.py).  Device
+ * pointers as above; scalar results come back in host memory, so these calls
+ * synchronise `stream`.  ws: DEVICE scratch of ofl_lossy_workspace_bytes(n).
+ *
+ * ofl_kmeans1d_fit   replaces sklearn KMeans(n_clusters=k, n_init).fit on a
+ *                    column vector (kc_pipeline.py:49-56, skc_pipeline.py:127-131):
+ *                    sorted centres, per-cluster counts, inertia.
+ * ofl_kmeans1d_label labels as float32 values: out[i] = rank_of_cluster[c(i)],
+ *                    c(i) = nearest centre (np.choose + _float_to_int, :55-61, :88-114)
+ * ofl_sparsify_topk  SparsityTransformer.forward (skc_pipeline.py:33-54,72-94):
+ *                    keep the k largest |x| (ties: lowest index), +1e-7 shift rule,
+ *                    dense float32 output + kept-set statistics
+ * ofl_ternary_stats  TernaryTransformer.forward mean/sign counts (stc_pipeline.py:120-123)
+ * ofl_ternary_ranks  TernaryTransformer.forward ranks (stc_pipeline.py:105-130)
+ * ofl_lut_decode     the sequential in-place key->value replacement of every
+ *                    lossy backward (kc_pipeline.py:81-83, stc_pipeline.py:139-142) */
+const char* ofl_lossy_last_error(void);
+size_t ofl_lossy_workspace_bytes(int64_t n);
+int ofl_kmeans1d_fit(const float* x, int64_t n, int k, int n_init, uint64_t seed, int max_exact,
+                     double* centres, int64_t* counts, double* inertia, void* ws, size_t ws_bytes,
+                     void* stream);
+int ofl_kmeans1d_label(const float* x, int64_t n, const double* centres, int k,
+                       const float* rank_of_cluster, float* out, void* stream);
+int ofl_sparsify_topk(const float* x, int64_t n, int64_t k, float* sparse_out, float* kept_min,
+                      int64_t* n_pos, int64_t* n_neg, int64_t* n_zero, double* abs_sum, int* shifted,
+                      void* ws, size_t ws_bytes, void* stream);
+int ofl_ternary_stats(const float* x, int64_t n, int64_t* n_pos, int64_t* n_neg, double* abs_sum, void* ws,
+                      size_t ws_bytes, void* stream);
+int ofl_ternary_ranks(const float* sparse, int64_t n, float rank_neg, float rank_zero, float rank_pos,
+                      float* out, void* stream);
+int ofl_lut_decode(const float* in, int64_t n, const float* keys, const float* vals, int nk, float* out,
+                   void* stream);
+
 /* ---- host helpers ----------------------------------------------------------
  * Left-to-right serial sums in the array's own precision: the
  * `sum(data.flatten())` term of the reference seed formula

@@ -22,7 +22,8 @@ EXPORTS = (
     "ofl_eden_plan_workspace_bytes", "ofl_eden_plan_tensor_info", "ofl_eden_plan_tensor_dims",
     "ofl_eden_encode", "ofl_eden_decode", "ofl_eden_plan_profile", "ofl_eden_plan_num_launches",
     "ofl_eden_plan_launch_info", "ofl_eden_plan_profile_collect", "ofl_serial_sum_f32",
-    "ofl_serial_sum_f64",
+    "ofl_serial_sum_f64", "ofl_lossy_last_error", "ofl_lossy_workspace_bytes", "ofl_kmeans1d_fit",
+    "ofl_kmeans1d_label", "ofl_sparsify_topk", "ofl_ternary_stats", "ofl_ternary_ranks", "ofl_lut_decode",
 )
 
 
@@ -59,6 +60,21 @@ def _bind(L):
     L.ofl_eden_plan_launch_info.restype = i32
     L.ofl_eden_plan_profile_collect.argtypes = [vp, i32, vp, i32, vp]
     L.ofl_eden_plan_profile_collect.restype = i32
+    L.ofl_lossy_last_error.restype = ctypes.c_char_p
+    L.ofl_lossy_workspace_bytes.argtypes = [i64]
+    L.ofl_lossy_workspace_bytes.restype = sz
+    L.ofl_kmeans1d_fit.argtypes = [vp, i64, i32, i32, ctypes.c_uint64, i32, vp, vp, vp, vp, sz, vp]
+    L.ofl_kmeans1d_fit.restype = i32
+    L.ofl_kmeans1d_label.argtypes = [vp, i64, vp, i32, vp, vp, vp]
+    L.ofl_kmeans1d_label.restype = i32
+    L.ofl_sparsify_topk.argtypes = [vp, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp]
+    L.ofl_sparsify_topk.restype = i32
+    L.ofl_ternary_stats.argtypes = [vp, i64, vp, vp, vp, vp, sz, vp]
+    L.ofl_ternary_stats.restype = i32
+    L.ofl_ternary_ranks.argtypes = [vp, i64, ctypes.c_float, ctypes.c_float, ctypes.c_float, vp, vp]
+    L.ofl_ternary_ranks.restype = i32
+    L.ofl_lut_decode.argtypes = [vp, i64, vp, vp, i32, vp, vp]
+    L.ofl_lut_decode.restype = i32
     L.ofl_serial_sum_f32.argtypes = [vp, i64]
     L.ofl_serial_sum_f32.restype = ctypes.c_float
     L.ofl_serial_sum_f64.argtypes = [vp, i64]
@@ -79,6 +95,12 @@ def lib():
                         "(hipcc --offload-arch=gfx950); openfl_amd has no CPU fallback")
                 _lib = _bind(ctypes.CDLL(LIB_PATH))
     return _lib
+
+
+def check_lossy(rc):
+    if rc != OFL_OK:
+        raise CodecError(lib().ofl_lossy_last_error().decode() or f"libofl_codec error {rc}")
+    return rc
 
 
 def check(rc):

@@ -1,0 +1,139 @@
+"""Device ops behind the KC / SKC / STC pipelines (libofl_codec.so lossy ABI).
+
+Each function takes/returns PyTorch-ROCm device tensors and host scalars; the
+heavy O(n) work runs in openfl_amd/csrc/lossy_kernels.hip.  Reference
+semantics are cited per function (paths relative to /root/reference).
+"""
+import ctypes
+import gzip
+import threading
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import torch
+
+from openfl_amd import _lib
+
+_tls = threading.local()
+GZIP_CHUNK = 8 << 20
+_pool = None
+
+
+def _ws(device, n):
+    need = int(_lib.lib().ofl_lossy_workspace_bytes(int(n)))
+    bufs = getattr(_tls, "ws", None)
+    if bufs is None:
+        bufs = _tls.ws = {}
+    b = bufs.get(str(device))
+    if b is None or b.numel() < need:
+        b = bufs[str(device)] = torch.empty(need, dtype=torch.uint8, device=device)
+    return b
+
+
+def _stream(device):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _check_dev(x):
+    if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous()):
+        raise _lib.CodecError("lossy ops take contiguous float32 device tensors")
+
+
+def kmeans_fit(x, k=6, n_init=6, seed=0, max_exact=8):
+    """1-D k-means of a float32 device vector (replaces sklearn KMeans.fit,
+    kc_pipeline.py:49-56): -> (sorted centres float64[k], counts int64[k], inertia)."""
+    _check_dev(x)
+    L = _lib.lib()
+    c = np.zeros(k, np.float64)
+    cnt = np.zeros(k, np.int64)
+    inertia = ctypes.c_double()
+    ws = _ws(x.device, x.numel())
+    _lib.check_lossy(L.ofl_kmeans1d_fit(x.data_ptr(), x.numel(), k, n_init, seed, max_exact,
+                                        c.ctypes.data, cnt.ctypes.data, ctypes.byref(inertia),
+                                        ws.data_ptr(), ws.numel(), _stream(x.device)))
+    return c, cnt, inertia.value
+
+
+def kmeans_label(x, centres, rank_of_cluster):
+    """out[i] = rank_of_cluster[nearest centre of x[i]] as float32 (device)."""
+    _check_dev(x)
+    c = np.ascontiguousarray(centres, np.float64)
+    r = np.ascontiguousarray(rank_of_cluster, np.float32)
+    out = torch.empty_like(x)
+    _lib.check_lossy(_lib.lib().ofl_kmeans1d_label(x.data_ptr(), x.numel(), c.ctypes.data, c.size,
+                                                   r.ctypes.data, out.data_ptr(), _stream(x.device)))
+    return out
+
+
+def sparsify_topk(x, k):
+    """SparsityTransformer top-k (skc_pipeline.py:33-54, 72-94) -> (sparse
+    float32 device array, stats dict)."""
+    _check_dev(x)
+    L = _lib.lib()
+    out = torch.empty_like(x)
+    kmin = ctypes.c_float()
+    npos, nneg, nzero = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    asum = ctypes.c_double()
+    shifted = ctypes.c_int()
+    ws = _ws(x.device, x.numel())
+    _lib.check_lossy(L.ofl_sparsify_topk(x.data_ptr(), x.numel(), int(k), out.data_ptr(), ctypes.byref(kmin),
+                                         ctypes.byref(npos), ctypes.byref(nneg), ctypes.byref(nzero),
+                                         ctypes.byref(asum), ctypes.byref(shifted), ws.data_ptr(), ws.numel(),
+                                         _stream(x.device)))
+    return out, {"kept_min": kmin.value, "n_pos": npos.value, "n_neg": nneg.value, "n_zero": nzero.value,
+                 "abs_sum": asum.value, "shifted": bool(shifted.value), "k": int(k)}
+
+
+def ternary_stats(x):
+    """(n_pos, n_neg, fp64 sum |x|) of a float32 device vector."""
+    _check_dev(x)
+    npos, nneg, asum = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_double()
+    ws = _ws(x.device, x.numel())
+    _lib.check_lossy(_lib.lib().ofl_ternary_stats(x.data_ptr(), x.numel(), ctypes.byref(npos), ctypes.byref(nneg),
+                                                  ctypes.byref(asum), ws.data_ptr(), ws.numel(),
+                                                  _stream(x.device)))
+    return npos.value, nneg.value, asum.value
+
+
+def ternary_ranks(sparse, rank_neg, rank_zero, rank_pos):
+    _check_dev(sparse)
+    out = torch.empty_like(sparse)
+    _lib.check_lossy(_lib.lib().ofl_ternary_ranks(sparse.data_ptr(), sparse.numel(), float(rank_neg),
+                                                  float(rank_zero), float(rank_pos), out.data_ptr(),
+                                                  _stream(sparse.device)))
+    return out
+
+
+def lut_decode(ranks, int_to_float):
+    """Reference backward: `for key in map: data[data == key] = map[key]` on a
+    float32 array, in the mapping's own iteration order (kc_pipeline.py:81-83)."""
+    _check_dev(ranks)
+    keys = np.asarray([float(k) for k in int_to_float.keys()], np.float32)
+    vals = np.asarray([float(int_to_float[k]) for k in int_to_float.keys()], np.float32)
+    out = torch.empty_like(ranks)
+    _lib.check_lossy(_lib.lib().ofl_lut_decode(ranks.data_ptr(), ranks.numel(), keys.ctypes.data,
+                                               vals.ctypes.data, keys.size, out.data_ptr(),
+                                               _stream(ranks.device)))
+    return out
+
+
+def rank_map(values):
+    """_float_to_int (kc_pipeline.py:88-114): sorted unique values -> ranks.
+    Returns (unique sorted values, rank index per input value)."""
+    u = np.unique(np.asarray(values))
+    return u, np.searchsorted(u, values)
+
+
+def gzip_compress(data_bytes, level=9, threads=8):
+    """gzip.compress (kc_pipeline.py:138-139) of float32 bytes.  Large payloads
+    are split into independent gzip members compressed in parallel; Python's
+    gzip.decompress (the reference GZIPTransformer.backward) reads
+    multi-member streams, so the bytes stay wire compatible."""
+    global _pool
+    mv = memoryview(data_bytes)
+    if len(mv) <= GZIP_CHUNK or threads <= 1:
+        return gzip.compress(bytes(mv), compresslevel=level)
+    if _pool is None:
+        _pool = ThreadPoolExecutor(max_workers=threads)
+    parts = [mv[i:i + GZIP_CHUNK] for i in range(0, len(mv), GZIP_CHUNK)]
+    return b"".join(_pool.map(lambda p: gzip.compress(bytes(p), compresslevel=level), parts))

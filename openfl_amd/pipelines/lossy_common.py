@@ -1,0 +1,76 @@
+"""Shared pieces of the KC / SKC / STC pipelines (GZIP, k-means, sparsify).
+
+Mirrors the reference classes (paths relative to /root/reference):
+  GZIPTransformer     kc_pipeline.py:117-156 (== skc :190-230 == stc :146-215)
+  _float_to_int       kc_pipeline.py:88-114
+The k-means / top-k / ternary numerics run on the GPU (openfl_amd.lossy);
+gzip and tiny (n < n_clusters) cases run on the host exactly as the
+reference does.
+"""
+import gzip
+
+import numpy as np
+import torch
+
+from openfl_amd import lossy
+from openfl_amd.codec import resolve_device
+from openfl_amd.pipelines.pipeline import Transformer
+
+
+def float_to_int(np_array):
+    """_float_to_int (kc_pipeline.py:88-114): sorted unique values -> int32 ranks."""
+    flat = np_array.reshape(-1)
+    uniq, idx = lossy.rank_map(flat)
+    int_array = idx.astype(np.int32).reshape(np_array.shape)
+    return int_array, {i: u for i, u in enumerate(uniq)}
+
+
+class GZIPTransformer(Transformer):
+    """float32 bytes -> gzip (lossless).  Large payloads become a multi-member
+    gzip stream compressed on host threads; gzip.decompress reads it."""
+
+    def __init__(self, level=9, threads=8):
+        self.lossy = False
+        self.level = level
+        self.threads = threads
+
+    def forward(self, data, **kwargs):
+        return lossy.gzip_compress(data.astype(np.float32).tobytes(), self.level, self.threads), {}
+
+    def backward(self, data, metadata, **kwargs):
+        return np.frombuffer(gzip.decompress(data), dtype=np.float32)
+
+
+def to_device(data, device):
+    flat = np.ascontiguousarray(np.asarray(data).reshape(-1), dtype=np.float32)
+    if not flat.flags.writeable:  # torch.from_numpy needs a writable buffer
+        flat = flat.copy()
+    if flat.size == 0:
+        return torch.empty(0, dtype=torch.float32, device=device)
+    return torch.from_numpy(flat).to(device)
+
+
+def kmeans_ranks(x_dev, n_cluster, value_dtype):
+    """k-means of a device vector -> (float32 rank tensor on device, int_to_float
+    map {rank: centre as value_dtype}) with the reference's rank semantics:
+    np.unique over the centres actually used (kc_pipeline.py:55-61)."""
+    seed = int(np.random.randint(0, 2 ** 31 - 1))  # sklearn draws from the global RNG too
+    centres, counts, _ = lossy.kmeans_fit(x_dev, n_cluster, n_init=n_cluster, seed=seed)
+    vals = centres.astype(value_dtype)
+    uniq = np.unique(vals[counts > 0])
+    rank_of_cluster = np.searchsorted(uniq, vals).astype(np.float32)
+    ranks = lossy.kmeans_label(x_dev, centres, rank_of_cluster)
+    return ranks, {i: u for i, u in enumerate(uniq)}
+
+
+def lut_backward(data, int2float_map, device):
+    """Reference lossy backward on a float32 array: sequential in-place
+    `data[data == key] = value` (kc_pipeline.py:79-83), on the GPU."""
+    arr = np.asarray(data)
+    if arr.size == 0:
+        return arr.astype(np.float32, copy=True)
+    out = lossy.lut_decode(to_device(arr, device), int2float_map)
+    return out.cpu().numpy().reshape(arr.shape)
+
+
+__all__ = ["GZIPTransformer", "float_to_int", "kmeans_ranks", "lut_backward", "resolve_device", "to_device"]
