@@ -1,0 +1,194 @@
+#!/usr/bin/env python3
+"""End-to-end loopback round (BASELINE config 5): 2 collaborators each send a
+ResNet-50-shaped fp32 update; per tensor: host ndarray -> Eden encode ->
+NamedTensor protobuf bytes -> parse -> Eden decode -> host ndarray.
+
+Modes (wall-clock, both collaborators, second of two rounds):
+  plugin   openfl_amd.pipelines.EdenPipeline per tensor (what TensorCodec calls):
+           H2D + encode + D2H per tensor, then H2D + decode + D2H per tensor
+  batched  openfl_amd.codec.EdenPlan over the whole state dict: one pinned H2D,
+           one encode launch sequence, one D2H of the planes arena; the
+           receiver does one H2D of all payloads, one decode, one D2H
+  cpu      the C oracle (oracle/eden_oracle.c, 1 thread) in the same flow
+           (the CPU pipeline timed beside it; test infrastructure)
+Prints one JSON line (also written to --out).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def state_dict(shapes, seed):
+    rng = np.random.default_rng(seed)
+    return [(n, (rng.standard_normal(s, dtype=np.float32) * np.float32(0.01))) for n, s in shapes]
+
+
+def run_plugin(sd, pipe, P):
+    wire = []
+    for name, arr in sd:
+        data, md = pipe.forward(arr)
+        wire.append(P.construct_named_tensor((name, "col", 1, False, ("trained",)), data, md,
+                                             False).SerializeToString())
+    out = []
+    for b in wire:
+        nt = P.NamedTensor()
+        nt.ParseFromString(b)
+        out.append(pipe.backward(nt.data_bytes, P.transformer_metadata_of(nt)))
+    return out, sum(len(b) for b in wire)
+
+
+def run_batched(sd, plan, P, torch, dev, host):
+    from openfl_amd.pipelines.eden_pipeline import eden_seed
+    # sender
+    xh, ph = host["x"], host["planes"]
+    for (name, arr), off in zip(sd, plan.elem_offsets):
+        xh[off:off + arr.size] = torch.from_numpy(arr.reshape(-1))
+    seeds = [eden_seed(arr) for _, arr in sd]
+    sd_dev = torch.tensor(seeds, dtype=torch.int32).to(dev, non_blocking=True)
+    x = host["xd"]
+    x.copy_(xh, non_blocking=True)
+    plan.encode(x, sd_dev, host["pd"], host["sd"], host["ws"])
+    ph.copy_(host["pd"], non_blocking=True)
+    sch = host["sd"].cpu().numpy()  # syncs
+    planes = ph.numpy()
+    wire = []
+    for t, (name, arr) in enumerate(sd):
+        po, pb, fs = plan.planes_offsets[t], plan.planes_nbytes[t], plan.first_slice[t]
+        md = {"int_list": list(arr.shape), "int_to_float": {0: float(seeds[t]), 1: float(arr.size)}}
+        for j, dim in enumerate(plan.dims[t]):
+            md["int_to_float"][2 + 2 * j] = float(sch[fs + j])
+            md["int_to_float"][3 + 2 * j] = float(dim)
+        wire.append(P.construct_named_tensor((name, "col", 1, False, ("trained",)), planes[po:po + pb].tobytes(),
+                                             [md], False).SerializeToString())
+    # receiver
+    rp = host["planes2"].numpy()
+    rs = np.zeros(plan.n_slices, np.float32)
+    rseeds = []
+    for t, b in enumerate(wire):
+        nt = P.NamedTensor()
+        nt.ParseFromString(b)
+        m = nt.transformer_metadata[0].int_to_float
+        po = plan.planes_offsets[t]
+        rp[po:po + len(nt.data_bytes)] = np.frombuffer(nt.data_bytes, np.uint8)
+        rseeds.append(int(m[0]))
+        fs = plan.first_slice[t]
+        for j in range(len(plan.dims[t])):
+            rs[fs + j] = m[2 + 2 * j]
+    host["pd"].copy_(host["planes2"], non_blocking=True)
+    sd2 = torch.tensor(rseeds, dtype=torch.int32).to(dev, non_blocking=True)
+    sc2 = torch.from_numpy(rs).to(dev, non_blocking=True)
+    plan.decode(host["pd"], sd2, sc2, host["yd"], host["ws"])
+    host["y"].copy_(host["yd"], non_blocking=True)
+    torch.cuda.synchronize()
+    y = host["y"].numpy()
+    out = [y[off:off + arr.size].reshape(arr.shape) for (_, arr), off in zip(sd, plan.elem_offsets)]
+    return out, sum(len(b) for b in wire)
+
+
+def run_cpu(sd, P):
+    from oracle import eden as O
+    from openfl_amd.pipelines.eden_pipeline import eden_seed
+    wire = []
+    for name, arr in sd:
+        seed = eden_seed(arr)
+        if arr.size > 100:
+            planes, scales, dims, tot = O.compress(arr, seed, 8)
+            md = {"int_list": list(arr.shape), "int_to_float": {0: float(seed), 1: float(tot)}}
+            for j, (s, d) in enumerate(zip(scales, dims)):
+                md["int_to_float"][2 + 2 * j] = s
+                md["int_to_float"][3 + 2 * j] = float(d)
+            data = planes.tobytes()
+        else:
+            data, md = arr.astype(np.float32).tobytes(), {"int_list": list(arr.shape)}
+        wire.append(P.construct_named_tensor((name, "col", 1, False, ("trained",)), data, [md], False)
+                    .SerializeToString())
+    out = []
+    for b in wire:
+        nt = P.NamedTensor()
+        nt.ParseFromString(b)
+        m = nt.transformer_metadata[0]
+        if len(m.int_to_float):
+            dims = [int(m.int_to_float[k]) for k in range(3, max(m.int_to_float) + 1, 2)]
+            sc = [m.int_to_float[k] for k in range(2, max(m.int_to_float) + 1, 2)]
+            y = O.decompress(nt.data_bytes, int(m.int_to_float[1]), sc, dims, int(m.int_to_float[0]), 8)
+            out.append(y.reshape(list(m.int_list)))
+        else:
+            out.append(np.frombuffer(nt.data_bytes, np.float32).reshape(list(m.int_list)))
+    return out, sum(len(b) for b in wire)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="resnet50_fp32")
+    ap.add_argument("--collaborators", type=int, default=2)
+    ap.add_argument("--modes", default="plugin,batched,cpu")
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    import torch
+    from openfl_amd import protocols as P
+    from openfl_amd.codec import EdenPlan
+    from openfl_amd.pipelines import EdenPipeline
+    from openfl_amd.workloads import WORKLOADS
+    dev = torch.device("cuda", 0)
+    shapes = WORKLOADS[args.workload]()
+    sds = [state_dict(shapes, 100 + c) for c in range(args.collaborators)]
+    in_bytes = sum(a.nbytes for sd in sds for _, a in sd)
+    res = {"workload": args.workload, "collaborators": args.collaborators, "input_bytes": in_bytes,
+           "tensors_per_collaborator": len(shapes)}
+
+    def rel_err(sd, out):
+        num = sum(float(np.sum((o.astype(np.float64) - a) ** 2)) for (_, a), o in zip(sd, out))
+        den = sum(float(np.sum(a.astype(np.float64) ** 2)) for _, a in sd)
+        return (num / den) ** 0.5
+
+    modes = args.modes.split(",")
+    if "plugin" in modes:
+        pipe = EdenPipeline(n_bits=8, dim_threshold=100, device="cuda:0")
+        for r in range(2):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            outs = [run_plugin(sd, pipe, P) for sd in sds]
+            dt = time.perf_counter() - t0
+        res["plugin"] = {"s": round(dt, 4), "GiB_s": round(in_bytes / dt / 2 ** 30, 3),
+                         "wire_bytes": sum(o[1] for o in outs), "rel_err": round(rel_err(sds[0], outs[0][0]), 6)}
+    if "batched" in modes:
+        numels = [a.size for _, a in sds[0]]
+        plan = EdenPlan(numels, 8)
+        host = {"x": torch.empty(plan.arena_numel, dtype=torch.float32).pin_memory(),
+                "y": torch.empty(plan.arena_numel, dtype=torch.float32).pin_memory(),
+                "planes": torch.empty(plan.planes_bytes, dtype=torch.uint8).pin_memory(),
+                "planes2": torch.empty(plan.planes_bytes, dtype=torch.uint8).pin_memory(),
+                "xd": torch.empty(plan.arena_numel, dtype=torch.float32, device=dev),
+                "yd": torch.empty(plan.arena_numel, dtype=torch.float32, device=dev),
+                "pd": torch.empty(plan.planes_bytes, dtype=torch.uint8, device=dev),
+                "sd": torch.empty(plan.n_slices, dtype=torch.float32, device=dev),
+                "ws": torch.empty(plan.ws_bytes, dtype=torch.uint8, device=dev)}
+        for r in range(2):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            outs = [run_batched(sd, plan, P, torch, dev, host) for sd in sds]
+            dt = time.perf_counter() - t0
+        res["batched"] = {"s": round(dt, 4), "GiB_s": round(in_bytes / dt / 2 ** 30, 3),
+                          "wire_bytes": sum(o[1] for o in outs), "rel_err": round(rel_err(sds[-1], outs[-1][0]), 6)}
+    if "cpu" in modes:
+        t0 = time.perf_counter()
+        outs = [run_cpu(sd, P) for sd in sds]
+        dt = time.perf_counter() - t0
+        res["cpu"] = {"s": round(dt, 3), "GiB_s": round(in_bytes / dt / 2 ** 30, 4), "cores": 1, "kind": "port",
+                      "wire_bytes": sum(o[1] for o in outs), "rel_err": round(rel_err(sds[0], outs[0][0]), 6)}
+    line = json.dumps(res)
+    print(line)
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(line + "\n")
+
+
+if __name__ == "__main__":
+    main()
