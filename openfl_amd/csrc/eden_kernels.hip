@@ -144,14 +144,21 @@ DEVI float sgn_elem(float v, uint32_t e, int p, uint32_t b) {
 // ---------------------------------------------------------------------------
 // Register-layout engine
 // ---------------------------------------------------------------------------
-struct Lay { int nb, r0, r1, r2, r3, r4; };
+// A layout: tile of 2^nb elements; element bit r_i lives in register bit i
+// (5 or 6 register bits: 32 or 64 elements per thread); the other element
+// bits are the thread index, lowest first.
+struct Lay { int nb, r0, r1, r2, r3, r4, r5 = -1; };
 
 template <Lay L> struct LT {
-    static constexpr int rb(int i) { return i == 0 ? L.r0 : i == 1 ? L.r1 : i == 2 ? L.r2 : i == 3 ? L.r3 : L.r4; }
-    static constexpr uint32_t rmask() { uint32_t m = 0; for (int i = 0; i < 5; ++i) m |= 1u << rb(i); return m; }
+    static constexpr int NR = L.r5 < 0 ? 5 : 6;
+    static constexpr int E = 1 << NR;
+    static constexpr int rb(int i) {
+        return i == 0 ? L.r0 : i == 1 ? L.r1 : i == 2 ? L.r2 : i == 3 ? L.r3 : i == 4 ? L.r4 : L.r5;
+    }
+    static constexpr uint32_t rmask() { uint32_t m = 0; for (int i = 0; i < NR; ++i) m |= 1u << rb(i); return m; }
     static constexpr uint32_t off(int r) {
         uint32_t o = 0;
-        for (int i = 0; i < 5; ++i) if ((r >> i) & 1) o |= 1u << rb(i);
+        for (int i = 0; i < NR; ++i) if ((r >> i) & 1) o |= 1u << rb(i);
         return o;
     }
     // deposit tid into the non-register bit positions, lowest first
@@ -169,20 +176,20 @@ template <Lay L> struct LT {
 // LDS address of tile element e: one pad word per 32 and per 1024 elements.
 // Additive over disjoint bit sets (pad(b | o) = pad(b) + pad(o)), so register
 // offsets become DS immediates, and conflict-free for every half-wave lane
-// pattern the layouts use: lanes varying index bits {0..4}, {5..9}, {2..6} or
-// {0,1,7,8,9} hit 32 distinct banks (bank = address mod 32 for b32 ops).
+// pattern the layouts use: lanes varying index bits {0..4}, {5..9}, {2..6},
+// {0,1,7,8,9} or {6..10} hit 32 distinct banks (bank = address mod 32).
 constexpr uint32_t cpad(uint32_t e) { return e + (e >> 5) + (e >> 10); }
 DEVI uint32_t pad(uint32_t e) { return e + (e >> 5) + (e >> 10); }
 constexpr size_t lds_floats(int nb) { return ((size_t)1 << nb) + ((size_t)1 << nb >> 5) + ((size_t)1 << nb >> 10); }
 
 // butterflies on every register bit whose element bit is in ACT
 template <Lay L, uint32_t ACT>
-DEVI void stages(float (&v)[32]) {
+DEVI void stages(float (&v)[LT<L>::E]) {
 #pragma unroll
-    for (int i = 0; i < 5; ++i) {
+    for (int i = 0; i < LT<L>::NR; ++i) {
         if ((ACT >> LT<L>::rb(i)) & 1u) {
 #pragma unroll
-            for (int r = 0; r < 32; ++r) {
+            for (int r = 0; r < LT<L>::E; ++r) {
                 if (!((r >> i) & 1)) {
                     const float a = v[r], b = v[r | (1 << i)];
                     v[r] = a + b;
@@ -193,15 +200,20 @@ DEVI void stages(float (&v)[32]) {
     }
 }
 
+// a value the compiler cannot hoist or CSE (keeps per-register addresses out of
+// loop-invariant code motion: they would pin dozens of VGPRs)
+DEVI uint32_t opaque(uint32_t v) { asm volatile("" : "+v"(v)); return v; }
+
 template <Lay A, Lay B>
-DEVI void exchange(float (&v)[32], float* s, uint32_t tid) {
-    const uint32_t ba = pad(LT<A>::base(tid));
+DEVI void exchange(float (&v)[LT<A>::E], float* s, uint32_t tid) {
+    static_assert(LT<A>::E == LT<B>::E, "layouts differ in register count");
+    const uint32_t ba = opaque(pad(LT<A>::base(tid)));
 #pragma unroll
-    for (int r = 0; r < 32; ++r) s[ba + cpad(LT<A>::off(r))] = v[r];
+    for (int r = 0; r < LT<A>::E; ++r) s[ba + cpad(LT<A>::off(r))] = v[r];
     __syncthreads();
-    const uint32_t bb = pad(LT<B>::base(tid));
+    const uint32_t bb = opaque(pad(LT<B>::base(tid)));
 #pragma unroll
-    for (int r = 0; r < 32; ++r) v[r] = s[bb + cpad(LT<B>::off(r))];
+    for (int r = 0; r < LT<B>::E; ++r) v[r] = s[bb + cpad(LT<B>::off(r))];
     __syncthreads();
 }
 
@@ -304,6 +316,82 @@ DEVI void unpack_centroids32(const uint32_t (&w)[8], const float* cen, float (&v
         for (int t = 0; t < 8; ++t) v[8 * g + t] = cen[(x >> (8 * t)) & 0xffu];
     }
 }
+// 64 contiguous values -> 8 plane words of 64 bits (bit t = element t); groups
+// [G0, G1) of 8 elements (callers split the range to interleave other work)
+template <int G0, int G1>
+DEVI float quant_pack64(const float (&v)[64], float ysc, float zm64, const QTab* q, uint64_t (&w)[8]) {
+    float dot = 0.f;
+#pragma unroll
+    for (int g = G0; g < G1; ++g) {
+        // volatile pins order the groups: no group's index math is hoisted
+        // ahead of the previous group (64 live indices would spill)
+        float vg[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            vg[t] = v[8 * g + t];
+            asm volatile("" : "+v"(vg[t]));
+        }
+        uint64_t x = 0;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const float y = vg[t] * ysc;
+            float c;
+            const int b = quant(y * zm64, q, c);
+            dot += c * y;
+            x |= (uint64_t)(uint32_t)b << (8 * t);
+        }
+        x = tr8x8(x);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w[i] |= ((x >> (8 * i)) & 0xffull) << (8 * g);
+        asm volatile("" ::: "memory");  // keep each group's LDS-table reads in the group
+    }
+    return dot;
+}
+DEVI void unpack_centroids64(const uint64_t (&w)[8], const float* cen, float (&v)[64]) {
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+        uint64_t x = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x |= ((w[i] >> (8 * g)) & 0xffull) << (8 * i);
+        x = tr8x8(x);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[8 * g + t] = cen[(x >> (8 * t)) & 0xffu];
+    }
+}
+DEVI void store_plane_word64(uint8_t* p, uint64_t w) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    if ((a & 7u) == 0) {
+        *reinterpret_cast<uint64_t*>(p) = w;
+    } else if ((a & 3u) == 0) {
+        reinterpret_cast<uint32_t*>(p)[0] = (uint32_t)w;
+        reinterpret_cast<uint32_t*>(p)[1] = (uint32_t)(w >> 32);
+    } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) p[q] = (uint8_t)(w >> (8 * q));
+    }
+}
+DEVI uint64_t load_plane_word64(const uint8_t* p) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    if ((a & 7u) == 0) return *reinterpret_cast<const uint64_t*>(p);
+    if ((a & 3u) == 0) {
+        return (uint64_t)reinterpret_cast<const uint32_t*>(p)[0] | ((uint64_t)reinterpret_cast<const uint32_t*>(p)[1] << 32);
+    }
+    uint64_t r = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) r |= (uint64_t)p[q] << (8 * q);
+    return r;
+}
+DEVI void store_planes64(uint8_t* plane0, uint32_t e, int64_t stride, int nbits, const uint64_t (&w)[8]) {
+    uint8_t* p = plane0 + (e >> 3);
+    for (int i = 0; i < nbits; ++i) store_plane_word64(p + (int64_t)i * stride, w[i]);
+}
+DEVI void load_planes64(const uint8_t* plane0, uint32_t e, int64_t stride, int nbits, uint64_t (&w)[8]) {
+    const uint8_t* p = plane0 + (e >> 3);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = 0;
+    for (int i = 0; i < nbits; ++i) w[i] = load_plane_word64(p + (int64_t)i * stride);
+}
+
 DEVI void store_plane_word(uint8_t* p, uint32_t w) {
     if ((reinterpret_cast<uintptr_t>(p) & 3u) == 0) {
         *reinterpret_cast<uint32_t*>(p) = w;
@@ -331,7 +419,6 @@ DEVI float pow2i(int e) { return __int_as_float((127 + e) << 23); }  // 2^e, |e|
 
 // Hide a value from the optimiser so per-register addresses are recomputed
 // (cheap ALU) instead of being kept live across a whole pass (32 VGPRs).
-DEVI uint32_t opaque(uint32_t v) { asm volatile("" : "+v"(v)); return v; }
 
 // ---------------------------------------------------------------------------
 // fp32 element I/O with valid-length bound (zero padding, :541-546); base is
@@ -424,10 +511,10 @@ template <> struct SmallSet<15> {
 // signs of the 32 register elements of layout L from an LDS byte table
 // (byte j, bit k = sign of element k*S + j), times mul
 template <Lay L>
-DEVI void apply_signs_tab(float (&v)[32], uint32_t base, const uint8_t* tab, int p, float mul) {
+DEVI void apply_signs_tab(float (&v)[LT<L>::E], uint32_t base, const uint8_t* tab, int p, float mul) {
     const uint32_t jm = (1u << (p - 3)) - 1u;
 #pragma unroll
-    for (int r = 0; r < 32; ++r) {
+    for (int r = 0; r < LT<L>::E; ++r) {
         const uint32_t e = base | LT<L>::off(r);
         v[r] = flip_unless(v[r] * mul, ((uint32_t)tab[e & jm] >> (e >> (p - 3))) & 1u);
     }
@@ -437,17 +524,17 @@ DEVI void apply_signs_tab(float (&v)[32], uint32_t base, const uint8_t* tab, int
 // nibble region (S = 2^(p-3) >= 2^15): j = (ebase mod S) + base + off(r), so
 // r2 = A*j + B is one add of the compile-time constant A*off(r) per element.
 template <Lay L>
-DEVI void apply_signs_direct(float (&v)[32], uint32_t ebase, uint32_t base, int p, uint32_t b, float mul) {
+DEVI void apply_signs_direct(float (&v)[LT<L>::E], uint32_t ebase, uint32_t base, int p, uint32_t b, float mul) {
     if (p >= 18) {
         const uint32_t jm = (1u << (p - 3)) - 1u;
         const uint32_t r2b = kLcgA * ((ebase & jm) + base) + b;
         const uint32_t sh = 4u * (ebase >> (p - 3)) + 3u;
 #pragma unroll
-        for (int r = 0; r < 32; ++r)
+        for (int r = 0; r < LT<L>::E; ++r)
             v[r] = flip_unless(v[r] * mul, (rd_mix(r2b + kLcgA * LT<L>::off(r)) >> sh) & 1u);
     } else {
 #pragma unroll
-        for (int r = 0; r < 32; ++r) v[r] = sgn_elem(v[r] * mul, ebase + (base | LT<L>::off(r)), p, b);
+        for (int r = 0; r < LT<L>::E; ++r) v[r] = sgn_elem(v[r] * mul, ebase + (base | LT<L>::off(r)), p, b);
     }
 }
 
@@ -661,145 +748,397 @@ __global__ __launch_bounds__(64) void k_dec_tiny(KArgs a) {
 }
 
 // ===========================================================================
-// Large slices (P >= 2^16): row passes (2^15 contiguous, NT = 1024)
+// Large slices (P >= 2^16): row passes over contiguous 2^15-element rows,
+// 512 threads x 64 registers (6 register bits; 2 exchanges per Hadamard)
+//   F1: L1 {0,1,11..14} -> L2 {2..6,10} -> L3 {5..10} (F1 does 7,8,9 there)
+//   F2: L3 {5..10} -> L4 {11..14,9,10} -> L5 {0..5} (64 contiguous: packing)
 // ===========================================================================
-using RS = SmallSet<15>;
+struct RowSet6 {
+    static constexpr Lay L1{15, 0, 1, 11, 12, 13, 14}, L2{15, 2, 3, 4, 5, 6, 10}, L3{15, 5, 6, 7, 8, 9, 10},
+                         L4{15, 11, 12, 13, 14, 9, 10}, L5{15, 0, 1, 2, 3, 4, 5};
+    static constexpr uint32_t F1a = bits_mask({0, 1, 11, 12, 13, 14}), F1b = bits_mask({2, 3, 4, 5, 6, 10}),
+                              F1c = bits_mask({7, 8, 9}), F2c = bits_mask({5, 6, 7, 8, 9, 10}),
+                              F2d = bits_mask({11, 12, 13, 14}), F2e = bits_mask({0, 1, 2, 3, 4});
+};
+using RS = RowSet6;
 constexpr int kRowLog = 15;
-constexpr int kRowNT = 1024;
+constexpr int kRowNT = 512;
 constexpr size_t kRowSmem = (sizeof(float) * lds_floats(kRowLog) + 15) & ~(size_t)15;
-constexpr size_t kRowSmemQ = kRowSmem + sizeof(QTab) + 4 * 16;
-constexpr size_t kRowSmemC = kRowSmem + sizeof(float) * 256;
+// LDS after the exchange buffer: [tile table][8 wave partials][QTab | centroids]
+constexpr int kTabCap = 1024;
+struct TileTab { int32_t ts[kTabCap + 1]; int32_t li[kTabCap]; int32_t pad_[3]; };
+constexpr size_t kRowTab = kRowSmem;
+constexpr size_t kRowRed = kRowTab + sizeof(TileTab);
+constexpr size_t kRowExtra = kRowRed + 64;
+constexpr size_t kRowSmemA = kRowExtra;
+constexpr size_t kRowSmemQ = kRowExtra + sizeof(QTab);
+constexpr size_t kRowSmemC = kRowExtra + sizeof(float) * 256;
+
+// block-uniform descriptor/scalar reads: loads issued after the loop's global
+// stores are vector loads, so pin their values to SGPRs explicitly (buffer
+// resources built from VGPRs turn into waterfall loops)
+// Reads through the constant address space are scalar loads (lgkmcnt): vector
+// loads would wait on the in-order vmcnt behind the tile prefetch.  Tables are
+// written by the host or earlier launches only.
+typedef const __attribute__((address_space(4))) uint32_t cu32;
+DEVI uint32_t sld(const void* p, int64_t i) { return ((cu32*)p)[i]; }
+DEVI SliceDesc udesc(const SliceDesc* d, int si) {
+    static_assert(sizeof(SliceDesc) == 72, "SliceDesc layout");
+    cu32* p = (cu32*)(d + si);
+    uint32_t w[18];
+#pragma unroll
+    for (int i = 0; i < 18; ++i) w[i] = p[i];
+    return __builtin_bit_cast(SliceDesc, w);
+}
+DEVI float sldf(const float* p, int64_t i) { return __builtin_bit_cast(float, sld(p, i)); }
+DEVI uint32_t uu(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Persistent row launches: one block per CU walks tiles t, t+G, t+2G, ...;
+// the next tile's input is in flight in registers while this one computes.
+struct TileWalk {
+    const KArgs& a;
+    TileTab* tab;
+    int count, total;
+    bool lds;
+    DEVI TileWalk(const KArgs& a_, TileTab* tab_, uint32_t tid) : a(a_), tab(tab_) {
+        count = a.count;
+        lds = count <= kTabCap;
+        if (lds) {
+            for (int i = (int)tid; i <= count; i += kRowNT) tab->ts[i] = a.tstart[i];
+            for (int i = (int)tid; i < count; i += kRowNT) tab->li[i] = a.list[i];
+        }
+        total = (int)sld(a.tstart, count);
+        __syncthreads();
+    }
+    // LDS and global searches stay separate: a generic (flat) pointer would make
+    // every probe wait for all outstanding global loads/stores (vmcnt(0))
+    template <typename P>
+    static DEVI int search(P ts, int count, int b) {
+        int lo = 0, hi = count - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (ts[mid] <= b) lo = mid; else hi = mid - 1;
+        }
+        return lo;
+    }
+    DEVI void at(int b, int& slice, uint32_t& tile) const {
+        if (lds) {
+            const int lo = search(tab->ts, count, b);
+            slice = (int)uu((uint32_t)tab->li[lo]);
+            tile = uu((uint32_t)(b - tab->ts[lo]));
+        } else {
+            int lo = 0, hi = count - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if ((int)sld(a.tstart, mid) <= b) lo = mid; else hi = mid - 1;
+            }
+            slice = (int)sld(a.list, lo);
+            tile = (uint32_t)(b - (int)sld(a.tstart, lo));
+        }
+    }
+};
+
+// Tile I/O through raw buffer resources: the tile base and extent live in
+// SGPRs, each lane keeps one byte offset (lane bits) and the register part is
+// a compile-time soffset/imm (lane and register bits are disjoint, so
+// base|off == base+off).  Accesses at or past num_records read 0 / are dropped
+// without touching memory; records are kept a multiple of the access width so
+// no access straddles the bound, and the <= 3 valid elements of a straddling
+// float4 are patched separately.  Nothing here branches on data that is in
+// flight: a prefetch must not meet a phi before the tile that consumes it.
+// (The clang builtins __builtin_amdgcn_raw_buffer_load_b128 / _b64 of this
+// toolchain lower to a 32-bit load; the LLVM intrinsics are bound directly.)
+typedef int rsrc_t __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+__device__ f32x4 raw_load_f32x4(rsrc_t r, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4f32");
+__device__ float raw_load_f32(rsrc_t r, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.f32");
+__device__ i32x2 raw_load_i32x2(rsrc_t r, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.v2i32");
+__device__ uint8_t raw_load_u8(rsrc_t r, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.i8");
+__device__ void raw_store_f32x4(f32x4 v, rsrc_t r, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.store.v4f32");
+__device__ void raw_store_f32(float v, rsrc_t r, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.store.f32");
+
+// word 3 = 0x00020000: 32-bit data format, as the gfx9 family expects
+DEVI rsrc_t mk_rsrc(const void* p, uint32_t bytes) {
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    rsrc_t r;
+    r.x = (int)(uint32_t)a;
+    r.y = (int)((uint32_t)(a >> 32) & 0xffffu);  // stride 0
+    r.z = (int)bytes;
+    r.w = 0x00020000;
+    return r;
+}
+DEVI uint32_t tile_valid(int64_t len) {
+    return len <= 0 ? 0u : (len >= (1 << kRowLog) ? (1u << kRowLog) : (uint32_t)len);
+}
+DEVI float4 bload4(rsrc_t r, uint32_t e, uint32_t k) {
+    const f32x4 q = raw_load_f32x4(r, (int)(e * 4u), (int)(k * 4u), 0);
+    return make_float4(q.x, q.y, q.z, q.w);
+}
+DEVI float bload1(rsrc_t r, uint32_t e, uint32_t k) { return raw_load_f32(r, (int)(e * 4u), (int)(k * 4u), 0); }
+DEVI void bstore1(rsrc_t r, uint32_t e, uint32_t k, float v) { raw_store_f32(v, r, (int)(e * 4u), (int)(k * 4u), 0); }
+DEVI void bstore4(rsrc_t r, uint32_t e, uint32_t k, const float* v) {
+    const f32x4 q = {v[0], v[1], v[2], v[3]};
+    raw_store_f32x4(q, r, (int)(e * 4u), (int)(k * 4u), 0);
+}
+
+// x tile (L1 layout, float4 per register quad); live = false reads nothing
+DEVI void fetch_x(const KArgs& a, const SliceDesc& D, uint32_t tile, bool live, uint32_t base1, float (&v)[64]) {
+    const uint32_t e0 = tile << kRowLog;
+    const uint32_t nv = live ? tile_valid(D.len - (int64_t)e0) : 0u;
+    const rsrc_t r = mk_rsrc(a.xin + D.x_off + e0, (nv & ~3u) * 4u);
+#pragma unroll
+    for (int k = 0; k < 64; k += 4) {
+        const float4 f = bload4(r, base1, LT<RS::L1>::off(k));
+        v[k] = f.x; v[k + 1] = f.y; v[k + 2] = f.z; v[k + 3] = f.w;
+    }
+}
+// the valid head of a float4 that straddles the slice's input length
+DEVI void fix_x(const KArgs& a, const SliceDesc& D, uint32_t tile, uint32_t base1, float (&v)[64]) {
+    const uint32_t e0 = tile << kRowLog;
+    const uint32_t nv = tile_valid(D.len - (int64_t)e0);
+    if (nv & 3u) {
+        const uint32_t eb = nv & ~3u;
+        const float* x = a.xin + D.x_off + e0 + eb;
+#pragma unroll
+        for (int k = 0; k < 64; k += 4)
+            if (base1 + LT<RS::L1>::off(k) == eb) {
+#pragma unroll
+                for (int q = 0; q < 3; ++q)
+                    if ((uint32_t)q < (nv & 3u)) v[k + q] = x[q];
+            }
+    }
+}
+DEVI void store_y(const KArgs& a, const SliceDesc& D, uint32_t tile, uint32_t base1, const float (&v)[64]) {
+    const uint32_t e0 = tile << kRowLog;
+    const uint32_t nv = tile_valid(D.ylen - (int64_t)e0);
+    const rsrc_t r = mk_rsrc(a.xout + D.y_off + e0, (nv & ~3u) * 4u);
+#pragma unroll
+    for (int k = 0; k < 64; k += 4) bstore4(r, base1, LT<RS::L1>::off(k), &v[k]);
+    if (nv & 3u) {
+        const uint32_t eb = nv & ~3u;
+        float* y = a.xout + D.y_off + e0 + eb;
+#pragma unroll
+        for (int k = 0; k < 64; k += 4)
+            if (base1 + LT<RS::L1>::off(k) == eb) {
+#pragma unroll
+                for (int q = 0; q < 3; ++q)
+                    if ((uint32_t)q < (nv & 3u)) y[q] = v[k + q];
+            }
+    }
+}
+// ws tiles are always whole (P is a multiple of the row)
+DEVI void fetch_ws(const KArgs& a, const SliceDesc& D, uint32_t tile, bool live, uint32_t base3, float (&v)[64]) {
+    const rsrc_t r = mk_rsrc(a.ws + D.ws_off + ((size_t)tile << kRowLog), live ? (4u << kRowLog) : 0u);
+#pragma unroll
+    for (int k = 0; k < 64; ++k) v[k] = bload1(r, base3, LT<RS::L3>::off(k));
+}
+template <int H>
+DEVI void fetch_ws_half(const KArgs& a, const SliceDesc& D, uint32_t tile, bool live, uint32_t base3, float (&v)[32]) {
+    const rsrc_t r = mk_rsrc(a.ws + D.ws_off + ((size_t)tile << kRowLog), live ? (4u << kRowLog) : 0u);
+#pragma unroll
+    for (int k = 0; k < 32; ++k) v[k] = bload1(r, base3, LT<RS::L3>::off(32 * H + k));
+}
+DEVI void store_ws(const KArgs& a, const SliceDesc& D, uint32_t tile, uint32_t base3, const float (&v)[64]) {
+    const rsrc_t r = mk_rsrc(a.ws + D.ws_off + ((size_t)tile << kRowLog), 4u << kRowLog);
+#pragma unroll
+    for (int k = 0; k < 64; ++k) bstore1(r, base3, LT<RS::L3>::off(k), v[k]);
+}
+// the tile's 8-byte word of every plane (planes >= nbits read as 0).  A8: the
+// launch's plane rows are 8-byte aligned; otherwise bytes.
+template <bool A8>
+DEVI void fetch_planes(const KArgs& a, const SliceDesc& D, uint32_t tile, bool live, uint32_t base5, uint64_t (&w)[8]) {
+    const uint8_t* p0 = a.pin + D.pl_off + ((size_t)tile << (kRowLog - 3));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const rsrc_t r = mk_rsrc(p0 + (int64_t)i * D.pl_stride, (live && i < a.nbits) ? (1u << (kRowLog - 3)) : 0u);
+        if (A8) {
+            const i32x2 q = raw_load_i32x2(r, (int)(base5 >> 3), 0, 0);
+            w[i] = (uint64_t)(uint32_t)q.x | ((uint64_t)(uint32_t)q.y << 32);
+        } else {
+            uint64_t x = 0;
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                x |= (uint64_t)raw_load_u8(r, (int)(base5 >> 3), c, 0) << (8 * c);
+            w[i] = x;
+        }
+    }
+}
 
 // encode pass A: x -> D1 -> F1 row stages -> ws ; partial sum of x^2
 __global__ __launch_bounds__(kRowNT) void k_enc_rowA(KArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float* s = reinterpret_cast<float*>(smem);
-    float* red = reinterpret_cast<float*>(smem + kRowSmem);
-    int si; uint32_t tile;
-    find_tile(a, si, tile);
-    const SliceDesc D = a.d[si];
+    float* red = reinterpret_cast<float*>(smem + kRowRed);
     const uint32_t tid = threadIdx.x;
-    const uint32_t b1 = seed_b(a.seeds[D.tensor]);
-    const uint32_t e0 = tile << kRowLog;
-    float v[32];
-    const uint32_t base1 = LT<RS::L1>::base(tid);
-    const float* x = a.xin + D.x_off + e0;
-    const int64_t len = D.len - (int64_t)e0;
+    const TileWalk tw(a, reinterpret_cast<TileTab*>(smem + kRowTab), tid);
+    int t = (int)blockIdx.x;
+    if (t >= tw.total) return;
+    const uint32_t base1 = LT<RS::L1>::base(tid), base3 = LT<RS::L3>::base(tid);
+    int si; uint32_t tile;
+    tw.at(t, si, tile);
+    float nx[64];
+    fetch_x(a, udesc(a.d, si), tile, true, base1, nx);
+    for (;;) {
+        float v[64];
 #pragma unroll
-    for (int r = 0; r < 32; r += 4) load4(x, base1 | LT<RS::L1>::off(r), len, &v[r]);
-    float ss = 0.f;
+        for (int r = 0; r < 64; ++r) v[r] = nx[r];
+        const SliceDesc D = udesc(a.d, si);
+        const int tn = t + (int)gridDim.x;
+        const bool more = tn < tw.total;
+        int sn; uint32_t tln;
+        tw.at(more ? tn : t, sn, tln);
+        fetch_x(a, udesc(a.d, sn), tln, more, base1, nx);
+        fix_x(a, D, tile, base1, v);
+        const uint32_t b1 = seed_b(sld(a.seeds, D.tensor));
+        float ss = 0.f;
 #pragma unroll
-    for (int r = 0; r < 32; ++r) ss += v[r] * v[r];
-    apply_signs_direct<RS::L1>(v, e0, base1, D.logp, b1, 1.0f);
-    stages<RS::L1, RS::F1a>(v);
-    exchange<RS::L1, RS::L2>(v, s, tid);
-    stages<RS::L2, RS::F1b>(v);
-    exchange<RS::L2, RS::L3>(v, s, tid);
-    stages<RS::L3, RS::F1c>(v);
-    float* w = a.ws + D.ws_off + e0;
-    const uint32_t base3 = LT<RS::L3>::base(tid);
-#pragma unroll
-    for (int r = 0; r < 32; ++r) w[base3 | LT<RS::L3>::off(r)] = v[r];
-    ss = block_sum<kRowNT>(ss, red);
-    if (tid == 0) a.part[D.part_off + tile] = ss;
+        for (int r = 0; r < 64; ++r) ss += v[r] * v[r];
+        apply_signs_direct<RS::L1>(v, tile << kRowLog, base1, D.logp, b1, 1.0f);
+        stages<RS::L1, RS::F1a>(v);
+        exchange<RS::L1, RS::L2>(v, s, tid);
+        stages<RS::L2, RS::F1b>(v);
+        exchange<RS::L2, RS::L3>(v, s, tid);
+        stages<RS::L3, RS::F1c>(v);
+        store_ws(a, D, tile, base3, v);
+        ss = block_sum<kRowNT>(ss, red);
+        if (tid == 0) a.part[D.part_off + tile] = ss;
+        if (!more) break;
+        t = tn; si = sn; tile = tln;
+    }
 }
 
 // encode pass C: ws -> F2 row stages -> y -> quantise, pack ; partial dot
 __global__ __launch_bounds__(kRowNT) void k_enc_rowC(KArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float* s = reinterpret_cast<float*>(smem);
-    QTab* qt = reinterpret_cast<QTab*>(smem + kRowSmem);
-    float* red = reinterpret_cast<float*>(qt + 1);
-    int si; uint32_t tile;
-    find_tile(a, si, tile);
-    const SliceDesc D = a.d[si];
+    float* red = reinterpret_cast<float*>(smem + kRowRed);
+    QTab* qt = reinterpret_cast<QTab*>(smem + kRowExtra);
     const uint32_t tid = threadIdx.x;
     load_qtable<kRowNT>(qt, a.nbits);
-    const uint32_t e0 = tile << kRowLog;
-    float v[32];
-    const float* w = a.ws + D.ws_off + e0;
-    const uint32_t base3 = LT<RS::L3>::base(tid);
+    const TileWalk tw(a, reinterpret_cast<TileTab*>(smem + kRowTab), tid);  // its barrier publishes qt
+    int t = (int)blockIdx.x;
+    if (t >= tw.total) return;
+    const uint32_t base3 = LT<RS::L3>::base(tid), base5 = LT<RS::L5>::base(tid);
+    int si; uint32_t tile;
+    tw.at(t, si, tile);
+    // stages + quantiser need ~220 VGPRs: only half of the next tile (32
+    // registers) is prefetched across them; the other half loads at the top
+    float na[32], nb[32];
+    fetch_ws_half<0>(a, udesc(a.d, si), tile, true, base3, na);
+    for (;;) {
+        float v[64];
 #pragma unroll
-    for (int r = 0; r < 32; ++r) v[r] = w[base3 | LT<RS::L3>::off(r)];
-    stages<RS::L3, RS::F2c>(v);
-    exchange<RS::L3, RS::L4>(v, s, tid);
-    stages<RS::L4, RS::F2d>(v);
-    exchange<RS::L4, RS::L5>(v, s, tid);  // its barriers also publish qt
-    stages<RS::L5, RS::F2e>(v);
-    const float nu = a.nu[si];
-    const bool pos = nu > 0.0f;
-    const float ysc = pow2i(-((D.logp + 1) / 2));
-    const float zm64 = 64.0f * (sqrtf((float)(1ll << D.logp)) / nu);
-    uint32_t wd[8];
-    float dot = quant_pack32(v, ysc, zm64, qt, wd);
-    if (!pos) {
-        dot = 0.f;
+        for (int r = 0; r < 32; ++r) v[r] = na[r];
+        const SliceDesc D = udesc(a.d, si);
+        fetch_ws_half<1>(a, D, tile, true, base3, nb);
+#pragma unroll
+        for (int r = 0; r < 32; ++r) v[32 + r] = nb[r];
+        const int tn = t + (int)gridDim.x;
+        const bool more = tn < tw.total;
+        int sn; uint32_t tln;
+        tw.at(more ? tn : t, sn, tln);
+        const SliceDesc Dn = udesc(a.d, sn);
+        fetch_ws_half<0>(a, Dn, tln, more, base3, na);
+        stages<RS::L3, RS::F2c>(v);
+        exchange<RS::L3, RS::L4>(v, s, tid);
+        stages<RS::L4, RS::F2d>(v);
+        exchange<RS::L4, RS::L5>(v, s, tid);
+        stages<RS::L5, RS::F2e>(v);
+        __builtin_amdgcn_sched_barrier(0);  // keep the quantiser out of the butterflies (VGPR cap)
+        const float nu = sldf(a.nu, si);
+        const float ysc = pow2i(-((D.logp + 1) / 2));
+        const float zm64 = 64.0f * (sqrtf((float)(1ll << D.logp)) / nu);
+        uint64_t wd[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) wd[i] = 0;
+        float dot = quant_pack64<0, 8>(v, ysc, zm64, qt, wd);
+        if (!(nu > 0.0f)) {
+            dot = 0.f;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) wd[i] = 0;
+        }
+        store_planes64(a.pout + D.pl_off, (tile << kRowLog) + base5, D.pl_stride, a.nbits, wd);
+        dot = block_sum<kRowNT>(dot, red);
+        if (tid == 0) a.part[D.part_off + tile] = dot;
+        if (!more) break;
+        t = tn; si = sn; tile = tln;
     }
-    store_planes(a.pout + D.pl_off, e0 + LT<RS::L5>::base(tid), D.pl_stride, a.nbits, wd);
-    dot = block_sum<kRowNT>(dot, red);
-    if (tid == 0) a.part[D.part_off + tile] = dot;
 }
 
 // decode pass A: planes -> C[bins] -> G1 row stages -> ws
+template <bool A8>
 __global__ __launch_bounds__(kRowNT) void k_dec_rowA(KArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float* s = reinterpret_cast<float*>(smem);
-    float* cen = reinterpret_cast<float*>(smem + kRowSmem);
-    int si; uint32_t tile;
-    find_tile(a, si, tile);
-    const SliceDesc D = a.d[si];
+    float* cen = reinterpret_cast<float*>(smem + kRowExtra);
     const uint32_t tid = threadIdx.x;
     if (tid < 256) cen[tid] = g_centroids[a.nbits - 1][tid];
-    const uint32_t e0 = tile << kRowLog;
-    float v[32];
-    {
-        uint32_t wd[8];
-        load_planes(a.pin + D.pl_off, e0 + LT<RS::L5>::base(tid), D.pl_stride, a.nbits, wd);
-        __syncthreads();
-        unpack_centroids32(wd, cen, v);
+    const TileWalk tw(a, reinterpret_cast<TileTab*>(smem + kRowTab), tid);  // its barrier publishes cen
+    int t = (int)blockIdx.x;
+    if (t >= tw.total) return;
+    const uint32_t base3 = LT<RS::L3>::base(tid), base5 = LT<RS::L5>::base(tid);
+    int si; uint32_t tile;
+    tw.at(t, si, tile);
+    uint64_t nw[8];
+    fetch_planes<A8>(a, udesc(a.d, si), tile, true, base5, nw);
+    for (;;) {
+        float v[64];
+        unpack_centroids64(nw, cen, v);
+        const SliceDesc D = udesc(a.d, si);
+        const int tn = t + (int)gridDim.x;
+        const bool more = tn < tw.total;
+        int sn; uint32_t tln;
+        tw.at(more ? tn : t, sn, tln);
+        fetch_planes<A8>(a, udesc(a.d, sn), tln, more, base5, nw);
+        stages<RS::L5, RS::F2e>(v);
+        exchange<RS::L5, RS::L4>(v, s, tid);
+        stages<RS::L4, RS::F2d>(v);
+        exchange<RS::L4, RS::L3>(v, s, tid);
+        stages<RS::L3, RS::F2c>(v);
+        store_ws(a, D, tile, base3, v);
+        if (!more) break;
+        t = tn; si = sn; tile = tln;
     }
-    stages<RS::L5, RS::F2e>(v);
-    exchange<RS::L5, RS::L4>(v, s, tid);
-    stages<RS::L4, RS::F2d>(v);
-    exchange<RS::L4, RS::L3>(v, s, tid);
-    stages<RS::L3, RS::F2c>(v);
-    float* w = a.ws + D.ws_off + e0;
-    const uint32_t base3 = LT<RS::L3>::base(tid);
-#pragma unroll
-    for (int r = 0; r < 32; ++r) w[base3 | LT<RS::L3>::off(r)] = v[r];
 }
 
 // decode pass C: ws -> G2 row stages -> D1, scale -> y
 __global__ __launch_bounds__(kRowNT) void k_dec_rowC(KArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float* s = reinterpret_cast<float*>(smem);
-    int si; uint32_t tile;
-    find_tile(a, si, tile);
-    const SliceDesc D = a.d[si];
     const uint32_t tid = threadIdx.x;
-    const uint32_t b1 = seed_b(a.seeds[D.tensor]);
-    const uint32_t e0 = tile << kRowLog;
-    float v[32];
-    const float* w = a.ws + D.ws_off + e0;
-    const uint32_t base3 = LT<RS::L3>::base(tid);
+    const TileWalk tw(a, reinterpret_cast<TileTab*>(smem + kRowTab), tid);
+    int t = (int)blockIdx.x;
+    if (t >= tw.total) return;
+    const uint32_t base1 = LT<RS::L1>::base(tid), base3 = LT<RS::L3>::base(tid);
+    int si; uint32_t tile;
+    tw.at(t, si, tile);
+    float nx[64];
+    fetch_ws(a, udesc(a.d, si), tile, true, base3, nx);
+    for (;;) {
+        float v[64];
 #pragma unroll
-    for (int r = 0; r < 32; ++r) v[r] = w[base3 | LT<RS::L3>::off(r)];
-    stages<RS::L3, RS::F1c>(v);
-    exchange<RS::L3, RS::L2>(v, s, tid);
-    stages<RS::L2, RS::F1b>(v);
-    exchange<RS::L2, RS::L1>(v, s, tid);
-    stages<RS::L1, RS::F1a>(v);
-    const uint32_t base1 = LT<RS::L1>::base(tid);
-    apply_signs_direct<RS::L1>(v, e0, base1, D.logp, b1, pow2i(-((D.logp + 1) / 2)));
-    const float sc = a.scales_in[D.scale_idx];
+        for (int r = 0; r < 64; ++r) v[r] = nx[r];
+        const SliceDesc D = udesc(a.d, si);
+        const int tn = t + (int)gridDim.x;
+        const bool more = tn < tw.total;
+        int sn; uint32_t tln;
+        tw.at(more ? tn : t, sn, tln);
+        fetch_ws(a, udesc(a.d, sn), tln, more, base3, nx);
+        const uint32_t b1 = seed_b(sld(a.seeds, D.tensor));
+        stages<RS::L3, RS::F1c>(v);
+        exchange<RS::L3, RS::L2>(v, s, tid);
+        stages<RS::L2, RS::F1b>(v);
+        exchange<RS::L2, RS::L1>(v, s, tid);
+        stages<RS::L1, RS::F1a>(v);
+        apply_signs_direct<RS::L1>(v, tile << kRowLog, base1, D.logp, b1, pow2i(-((D.logp + 1) / 2)));
+        const float sc = sldf(a.scales_in, D.scale_idx);
 #pragma unroll
-    for (int r = 0; r < 32; ++r) v[r] = sc * v[r];
-    float* y = a.xout + D.y_off + e0;
-    const int64_t len = D.ylen - (int64_t)e0;
-#pragma unroll
-    for (int r = 0; r < 32; r += 4) store4(y, base1 | LT<RS::L1>::off(r), len, &v[r]);
+        for (int r = 0; r < 64; ++r) v[r] = sc * v[r];
+        store_y(a, D, tile, base1, v);
+        if (!more) break;
+        t = tn; si = sn; tile = tln;
+    }
 }
 
 // ===========================================================================
@@ -994,6 +1333,7 @@ struct ofl_eden_plan {
     ofl::SliceDesc* d_slices = nullptr;
     int32_t* d_ints = nullptr;
     int device = -1;
+    int ncu = 256;              // persistent row launches: one block per CU
     bool uploaded = false;
     std::mutex mu;
 };
@@ -1046,10 +1386,11 @@ hipError_t set_all_attrs() {
     if ((e = set_small_attr<13>()) != hipSuccess) return e;
     if ((e = set_small_attr<14>()) != hipSuccess) return e;
     if ((e = set_small_attr<15>()) != hipSuccess) return e;
-    if ((e = set_lds((const void*)ofl::k_enc_rowA, ofl::kRowSmem + 64)) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_enc_rowA, ofl::kRowSmemA)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_enc_rowC, ofl::kRowSmemQ)) != hipSuccess) return e;
-    if ((e = set_lds((const void*)ofl::k_dec_rowA, ofl::kRowSmemC)) != hipSuccess) return e;
-    if ((e = set_lds((const void*)ofl::k_dec_rowC, ofl::kRowSmem)) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_dec_rowA<true>, ofl::kRowSmemC)) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_dec_rowA<false>, ofl::kRowSmemC)) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_dec_rowC, ofl::kRowSmemA)) != hipSuccess) return e;
     if ((e = set_col_attr<6>()) != hipSuccess) return e;
     if ((e = set_col_attr<7>()) != hipSuccess) return e;
     if ((e = set_col_attr<8>()) != hipSuccess) return e;
@@ -1104,14 +1445,19 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t st) {
 #undef SMALLCASE
             break;
         }
-        case K_ROWA:
-            e = enc ? launch(ofl::k_enc_rowA, l.blocks, ofl::kRowNT, ofl::kRowSmem + 64, st, a)
-                    : launch(ofl::k_dec_rowA, l.blocks, ofl::kRowNT, ofl::kRowSmemC, st, a);
+        case K_ROWA: {
+            const int64_t g = std::min<int64_t>(l.blocks, pl->ncu);
+            e = enc ? launch(ofl::k_enc_rowA, g, ofl::kRowNT, ofl::kRowSmemA, st, a)
+                    : (l.mid && (reinterpret_cast<uintptr_t>(base.pin) & 7u) == 0) ? launch(ofl::k_dec_rowA<true>, g, ofl::kRowNT, ofl::kRowSmemC, st, a)
+                           : launch(ofl::k_dec_rowA<false>, g, ofl::kRowNT, ofl::kRowSmemC, st, a);
             break;
-        case K_ROWC:
-            e = enc ? launch(ofl::k_enc_rowC, l.blocks, ofl::kRowNT, ofl::kRowSmemQ, st, a)
-                    : launch(ofl::k_dec_rowC, l.blocks, ofl::kRowNT, ofl::kRowSmem, st, a);
+        }
+        case K_ROWC: {
+            const int64_t g = std::min<int64_t>(l.blocks, pl->ncu);
+            e = enc ? launch(ofl::k_enc_rowC, g, ofl::kRowNT, ofl::kRowSmemQ, st, a)
+                    : launch(ofl::k_dec_rowC, g, ofl::kRowNT, ofl::kRowSmemA, st, a);
             break;
+        }
         case K_COL: {
             const size_t sm = col_smem(l.param, l.mid != 0);
 #define COLCASE(MM)                                                                                  \
@@ -1299,7 +1645,10 @@ int ofl_eden_plan_create(int ntensors, const int64_t* numel, const int64_t* elem
         pl->enc.insert(pl->enc.end(), colseq.begin(), colseq.end());
         pl->enc.push_back({K_ROWC, 0, 0, 0, lo_l, rp, nl, rows});
         pl->enc.push_back({K_FINAL, 0, 0, 0, lo_l, -1, nl, nl});
-        pl->dec.push_back({K_ROWA, 0, 0, 0, lo_l, rp, nl, rows});
+        // decode row A reads 8-byte plane words when every plane row is 8-byte aligned
+        int a8 = 1;
+        for (int32_t si : large) a8 &= (pl->slices[si].pl_off % 8 == 0) && (pl->slices[si].pl_stride % 8 == 0);
+        pl->dec.push_back({K_ROWA, 0, 0, a8, lo_l, rp, nl, rows});
         pl->dec.insert(pl->dec.end(), colseq.begin(), colseq.end());
         pl->dec.push_back({K_ROWC, 0, 0, 0, lo_l, rp, nl, rows});
     }
@@ -1337,6 +1686,8 @@ static int ensure_device(ofl_eden_plan_t pl) {
     std::lock_guard<std::mutex> g(pl->mu);
     if (pl->uploaded) return OFL_OK;
     HIP_TRY(hipGetDevice(&pl->device));
+    HIP_TRY(hipDeviceGetAttribute(&pl->ncu, hipDeviceAttributeMultiprocessorCount, pl->device));
+    if (pl->ncu < 1) pl->ncu = 1;
     if (!pl->slices.empty()) {
         HIP_TRY(hipMalloc(&pl->d_slices, sizeof(ofl::SliceDesc) * pl->slices.size()));
         HIP_TRY(hipMemcpy(pl->d_slices, pl->slices.data(), sizeof(ofl::SliceDesc) * pl->slices.size(), hipMemcpyHostToDevice));

@@ -108,8 +108,12 @@ def test_decode_matches_reference(case):
 # sizes hitting: tiny (P <= 2^10), small register kernels 2^11..2^14, the
 # large path with one column level (p = 15..22 -> M = 2..9) and two levels
 # (p = 23..25), multi-slice tensors and ragged tails.
+# 120_003 / (1 << 23) + 70_001: a large slice whose valid length ends inside a
+# float4 (row-pass tail patch) and, for the latter, a row tile with no valid
+# input at all; (1 << 21) + 7: plane rows not 8-byte aligned (byte-wise path).
 SIZES = [3, 64, 300, 1000, 2048, 3000, 4096, 8192, 12000, 16384, 16385, 1 << 15, 50_000, 1 << 17,
-         300_000, 1 << 19, 1 << 20, (1 << 21) + 7, 1 << 22, 1 << 23, (1 << 24) + 12345, 1 << 25]
+         120_003, 300_000, 1 << 19, 1 << 20, (1 << 21) + 7, 1 << 22, 1 << 23, (1 << 23) + 70_001,
+         (1 << 24) + 12345, 1 << 25]
 
 
 @pytest.mark.parametrize("n", SIZES)
@@ -199,6 +203,36 @@ def test_batch_equals_single():
         y1 = gpu_decode(p1, x.size, s1, d1, s, 8)
         off = plan.elem_offsets[t]
         np.testing.assert_array_equal(y[off:off + x.size], y1)
+
+
+def test_many_large_slices_one_launch():
+    """1100 large slices in one plan: more than the row kernels' LDS tile table
+    holds (1024), so the persistent walk takes the global-table path.  Every
+    tensor must equal its own single-tensor encode/decode."""
+    from openfl_amd.codec import EdenPlan
+    T = 1100
+    numels = [65536 + (t % 5) for t in range(T)]
+    plan = EdenPlan(numels, 8)
+    assert sum(len(d) for d in plan.dims) >= T
+    g = torch.Generator(device=DEV).manual_seed(3)
+    arena = torch.empty(plan.arena_numel, device=DEV).normal_(0, 0.01, generator=g)
+    seeds = [(7 * t + 1) % 65536 for t in range(T)]
+    c = _codec(8)
+    sd = torch.tensor(seeds, dtype=torch.int32, device=DEV)
+    planes, scales = c.encode_arena(plan, arena, sd)
+    y = c.decode_arena(plan, planes, scales, sd)
+    torch.cuda.synchronize()
+    xa = arena.cpu().numpy()
+    planes, scales, y = planes.cpu().numpy(), scales.cpu().numpy(), y.cpu().numpy()
+    for t in (0, 1, 511, 1022, 1023, 1024, 1025, T - 1):
+        off, n = plan.elem_offsets[t], numels[t]
+        x = xa[off:off + n]
+        p1, s1, d1 = gpu_encode(x, seeds[t], 8)
+        po, pb = plan.planes_offsets[t], plan.planes_nbytes[t]
+        np.testing.assert_array_equal(planes[po:po + pb], p1)
+        fs = plan.first_slice[t]
+        np.testing.assert_array_equal(scales[fs:fs + len(d1)], s1)
+        np.testing.assert_array_equal(y[off:off + n], gpu_decode(p1, n, s1, d1, seeds[t], 8))
 
 
 # --------------------------------------------------------- plugin surface ---
