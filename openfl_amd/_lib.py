@@ -89,11 +89,12 @@ def lib():
         with _lock:
             if _lib is None:
                 import torch  # noqa: F401  (HIP runtime first; see module doc)
-                if not os.path.exists(LIB_PATH):
+                path = os.environ.get("OFL_CODEC_LIB", LIB_PATH)  # dev: A/B a kernel variant
+                if not os.path.exists(path):
                     raise CodecError(
-                        f"{LIB_PATH} is missing: build it with `python -m openfl_amd.build` "
+                        f"{path} is missing: build it with `python -m openfl_amd.build` "
                         "(hipcc --offload-arch=gfx950); openfl_amd has no CPU fallback")
-                _lib = _bind(ctypes.CDLL(LIB_PATH))
+                _lib = _bind(ctypes.CDLL(path))
     return _lib
 
 

@@ -182,19 +182,33 @@ constexpr uint32_t cpad(uint32_t e) { return e + (e >> 5) + (e >> 10); }
 DEVI uint32_t pad(uint32_t e) { return e + (e >> 5) + (e >> 10); }
 constexpr size_t lds_floats(int nb) { return ((size_t)1 << nb) + ((size_t)1 << nb >> 5) + ((size_t)1 << nb >> 10); }
 
-// butterflies on every register bit whose element bit is in ACT
+// butterflies on every register bit whose element bit is in ACT.  Registers
+// (r, r+1) are treated as one 2-wide value so the butterflies issue as packed
+// fp32 adds (v_pk_add_f32: two butterflies per instruction; register bit 0
+// is the in-pair butterfly, a+b / a-b of the two halves).
+typedef float f2v __attribute__((ext_vector_type(2)));
 template <Lay L, uint32_t ACT>
 DEVI void stages(float (&v)[LT<L>::E]) {
 #pragma unroll
     for (int i = 0; i < LT<L>::NR; ++i) {
-        if ((ACT >> LT<L>::rb(i)) & 1u) {
+        if (!((ACT >> LT<L>::rb(i)) & 1u)) continue;
+        if (i == 0) {
 #pragma unroll
-            for (int r = 0; r < LT<L>::E; ++r) {
-                if (!((r >> i) & 1)) {
-                    const float a = v[r], b = v[r | (1 << i)];
-                    v[r] = a + b;
-                    v[r | (1 << i)] = a - b;
-                }
+            for (int r = 0; r < LT<L>::E; r += 2) {
+                const f2v a = {v[r], v[r]}, b = {v[r + 1], -v[r + 1]};
+                const f2v o = a + b;
+                v[r] = o.x;
+                v[r + 1] = o.y;
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < LT<L>::E; r += 2) {
+                if ((r >> i) & 1) continue;
+                const int q = r | (1 << i);
+                const f2v a = {v[r], v[r + 1]}, b = {v[q], v[q + 1]};
+                const f2v s = a + b, d = a - b;
+                v[r] = s.x; v[r + 1] = s.y;
+                v[q] = d.x; v[q + 1] = d.y;
             }
         }
     }
@@ -245,118 +259,149 @@ DEVI float block_sum(float v, float* red) {
 //   QEnt{lo = #B < (k-288)/64, 64*B[lo]}  (+inf when lo = 2^b - 1)
 // then bin = lo + (64 B[lo] < 64 z) exactly, and C[bin] from a 256-entry table.
 // ---------------------------------------------------------------------------
-struct QEnt { int lo; float b64; };
-struct QTab { QEnt grid[EDEN_GRID_CELLS]; float cen[256]; };
+// Bucketize table: one 16-byte entry per grid cell of width 1/64 holds the
+// only boundary inside the cell and the centroids on either side, so a bin and
+// its centroid cost one LDS read and one compare.
+struct QEnt { float b64; int lo; float clo; float chi; };
+struct QTab { QEnt grid[EDEN_GRID_CELLS]; };
 
 template <int NT>
 DEVI void load_qtable(QTab* q, int nbits) {
     const int nb = (1 << nbits) - 1;
+    const float* cen = g_centroids[nbits - 1];
     for (int k = threadIdx.x; k < EDEN_GRID_CELLS; k += NT) {
         const int lo = g_grid[nbits - 1][k];
-        q->grid[k] = QEnt{lo, lo < nb ? g_bounds[nbits - 1][lo] * 64.0f : __int_as_float(0x7f800000)};
+        const bool top = lo >= nb;
+        q->grid[k] = QEnt{top ? __int_as_float(0x7f800000) : g_bounds[nbits - 1][lo] * 64.0f, lo, cen[lo],
+                          top ? cen[lo] : cen[lo + 1]};
     }
-    for (int k = threadIdx.x; k < 256; k += NT) q->cen[k] = g_centroids[nbits - 1][k];
 }
 
-// bucketize + centroid (exact, one compare): returns bin, writes centroid
+// bucketize + centroid (exact, one compare): returns bin, writes centroid.
+// The clamp comes first so NaN lands in a valid cell (fmax(NaN, lo) = lo).
 DEVI int quant(float z64, const QTab* q, float& c) {
-    float f = floorf(z64);
-    f = fminf(fmaxf(f, -288.0f), 287.0f);
-    const int k = (int)f + EDEN_GRID_OFF;
+    const float zc = fminf(fmaxf(z64, -(float)EDEN_GRID_OFF), (float)(EDEN_GRID_OFF - 1));
+    const int k = (int)floorf(zc) + EDEN_GRID_OFF;
     const QEnt e = q->grid[k];
-    const int b = e.lo + (e.b64 < z64 ? 1 : 0);
-    c = q->cen[b];
-    return b;
+    const bool gt = e.b64 < z64;
+    c = gt ? e.chi : e.clo;
+    return e.lo + (gt ? 1 : 0);
 }
 
 // ---------------------------------------------------------------------------
-// 32 contiguous bins <-> nbits 32-bit plane words (8x8 bit transposes)
+// bins <-> bit planes.  A group is 8 contiguous elements, bins as bytes of a
+// 64-bit word (lo = elements 0..3, hi = 4..7).  tr8x8h transposes the 8x8 bit
+// matrix (afterwards byte i = plane-i bits of the group, bit t = element t);
+// the byte transposes then gather byte i of every group into plane word i.
 // ---------------------------------------------------------------------------
-DEVI uint64_t tr8x8(uint64_t x) {
-    uint64_t t;
-    t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;  x ^= t ^ (t << 7);
-    t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull; x ^= t ^ (t << 14);
-    t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull; x ^= t ^ (t << 28);
-    return x;
+DEVI void tr8x8h(uint32_t& lo, uint32_t& hi) {
+    uint32_t t;
+    t = (lo ^ (lo >> 7)) & 0x00AA00AAu;  lo ^= t ^ (t << 7);
+    t = (hi ^ (hi >> 7)) & 0x00AA00AAu;  hi ^= t ^ (t << 7);
+    t = (lo ^ (lo >> 14)) & 0x0000CCCCu; lo ^= t ^ (t << 14);
+    t = (hi ^ (hi >> 14)) & 0x0000CCCCu; hi ^= t ^ (t << 14);
+    t = (lo ^ (hi << 4)) & 0xF0F0F0F0u;  lo ^= t; hi ^= t >> 4;
+}
+// 4x4 byte transpose: o[i] byte j = r[j] byte i (8 v_perm_b32)
+DEVI void t4x4(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, uint32_t& o0, uint32_t& o1, uint32_t& o2,
+               uint32_t& o3) {
+    const uint32_t t0 = __builtin_amdgcn_perm(r1, r0, 0x05010400u), t1 = __builtin_amdgcn_perm(r1, r0, 0x07030602u);
+    const uint32_t t2 = __builtin_amdgcn_perm(r3, r2, 0x05010400u), t3 = __builtin_amdgcn_perm(r3, r2, 0x07030602u);
+    o0 = __builtin_amdgcn_perm(t2, t0, 0x05040100u);
+    o1 = __builtin_amdgcn_perm(t2, t0, 0x07060302u);
+    o2 = __builtin_amdgcn_perm(t3, t1, 0x05040100u);
+    o3 = __builtin_amdgcn_perm(t3, t1, 0x07060302u);
+}
+// 8x8 byte transpose of 64-bit rows given as lo/hi dwords: out row i byte g =
+// in row g byte i (an involution)
+DEVI void tr_bytes8(const uint32_t (&il)[8], const uint32_t (&ih)[8], uint32_t (&ol)[8], uint32_t (&oh)[8]) {
+    t4x4(il[0], il[1], il[2], il[3], ol[0], ol[1], ol[2], ol[3]);
+    t4x4(il[4], il[5], il[6], il[7], oh[0], oh[1], oh[2], oh[3]);
+    t4x4(ih[0], ih[1], ih[2], ih[3], ol[4], ol[5], ol[6], ol[7]);
+    t4x4(ih[4], ih[5], ih[6], ih[7], oh[4], oh[5], oh[6], oh[7]);
 }
 
-// quantise 32 contiguous values (registers r = element offset r) and build the
-// plane words: bit t of w[i] = bit i of bin(element t).  Returns <C[bins], y>.
+// quantise one group of 8 contiguous values -> (lo, hi) plane bytes; adds <C[bins], y>
+DEVI void quant_group(const float* vg, float ysc, float zm64, const QTab* q, uint32_t& lo, uint32_t& hi,
+                      float& dot) {
+    lo = 0;
+    hi = 0;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        const float y = vg[t] * ysc;
+        float c;
+        const uint32_t b = (uint32_t)quant(y * zm64, q, c);
+        dot += c * y;
+        if (t < 4) lo |= b << (8 * t); else hi |= b << (8 * (t - 4));
+    }
+    tr8x8h(lo, hi);
+}
+// volatile pins order the groups: no group's index math is hoisted ahead of
+// the previous group's (all 64 live indices would spill)
+template <int N>
+DEVI void pin_group(const float* v, float (&vg)[8]) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        vg[t] = v[t];
+        asm volatile("" : "+v"(vg[t]));
+    }
+}
+
+// 32 contiguous values -> 8 plane words of 32 bits (bit t = element t)
 DEVI float quant_pack32(const float (&v)[32], float ysc, float zm64, const QTab* q, uint32_t (&w)[8]) {
     float dot = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) w[i] = 0;
+    uint32_t xl[4], xh[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-        uint64_t x = 0;
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            const float y = v[8 * g + t] * ysc;
-            float c;
-            const int b = quant(y * zm64, q, c);
-            dot += c * y;
-            x |= (uint64_t)(uint32_t)b << (8 * t);
-        }
-        x = tr8x8(x);  // byte i = plane-i bits of elements 8g..8g+7
-#pragma unroll
-        for (int i = 0; i < 8; ++i) w[i] |= (uint32_t)((x >> (8 * i)) & 0xffu) << (8 * g);
-        asm volatile("" ::: "memory");  // keep each group's LDS-table reads in the group (VGPR cap 128)
+        float vg[8];
+        pin_group<8>(&v[8 * g], vg);
+        quant_group(vg, ysc, zm64, q, xl[g], xh[g], dot);
+        asm volatile("" : "+v"(xl[g]), "+v"(xh[g]), "+v"(dot) :: "memory");  // group done before the next
     }
+    t4x4(xl[0], xl[1], xl[2], xl[3], w[0], w[1], w[2], w[3]);
+    t4x4(xh[0], xh[1], xh[2], xh[3], w[4], w[5], w[6], w[7]);
     return dot;
+}
+// centroids of a group's plane bytes (lo, hi as produced by quant_group)
+DEVI void unpack_group(uint32_t lo, uint32_t hi, const float* cen, float* v) {
+    tr8x8h(lo, hi);  // involution: byte t = bin of element t
+#pragma unroll
+    for (int t = 0; t < 4; ++t) v[t] = cen[(lo >> (8 * t)) & 0xffu];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) v[4 + t] = cen[(hi >> (8 * t)) & 0xffu];
 }
 // plane words -> centroid values of 32 contiguous elements
 DEVI void unpack_centroids32(const uint32_t (&w)[8], const float* cen, float (&v)[32]) {
+    uint32_t xl[4], xh[4];
+    t4x4(w[0], w[1], w[2], w[3], xl[0], xl[1], xl[2], xl[3]);
+    t4x4(w[4], w[5], w[6], w[7], xh[0], xh[1], xh[2], xh[3]);
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-        uint64_t x = 0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) x |= (uint64_t)((w[i] >> (8 * g)) & 0xffu) << (8 * i);
-        x = tr8x8(x);  // involution: byte t = bin of element 8g+t
-#pragma unroll
-        for (int t = 0; t < 8; ++t) v[8 * g + t] = cen[(x >> (8 * t)) & 0xffu];
-    }
+    for (int g = 0; g < 4; ++g) unpack_group(xl[g], xh[g], cen, &v[8 * g]);
 }
-// 64 contiguous values -> 8 plane words of 64 bits (bit t = element t); groups
-// [G0, G1) of 8 elements (callers split the range to interleave other work)
-template <int G0, int G1>
+// 64 contiguous values -> 8 plane words of 64 bits (bit t = element t)
 DEVI float quant_pack64(const float (&v)[64], float ysc, float zm64, const QTab* q, uint64_t (&w)[8]) {
     float dot = 0.f;
+    uint32_t xl[8], xh[8];
 #pragma unroll
-    for (int g = G0; g < G1; ++g) {
-        // volatile pins order the groups: no group's index math is hoisted
-        // ahead of the previous group (64 live indices would spill)
+    for (int g = 0; g < 8; ++g) {
         float vg[8];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            vg[t] = v[8 * g + t];
-            asm volatile("" : "+v"(vg[t]));
-        }
-        uint64_t x = 0;
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            const float y = vg[t] * ysc;
-            float c;
-            const int b = quant(y * zm64, q, c);
-            dot += c * y;
-            x |= (uint64_t)(uint32_t)b << (8 * t);
-        }
-        x = tr8x8(x);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) w[i] |= ((x >> (8 * i)) & 0xffull) << (8 * g);
-        asm volatile("" ::: "memory");  // keep each group's LDS-table reads in the group
+        pin_group<8>(&v[8 * g], vg);
+        quant_group(vg, ysc, zm64, q, xl[g], xh[g], dot);
+        asm volatile("" : "+v"(xl[g]), "+v"(xh[g]), "+v"(dot) :: "memory");  // group done before the next
     }
+    uint32_t wl[8], wh[8];
+    tr_bytes8(xl, xh, wl, wh);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = (uint64_t)wl[i] | ((uint64_t)wh[i] << 32);
     return dot;
 }
 DEVI void unpack_centroids64(const uint64_t (&w)[8], const float* cen, float (&v)[64]) {
+    uint32_t il[8], ih[8], xl[8], xh[8];
 #pragma unroll
-    for (int g = 0; g < 8; ++g) {
-        uint64_t x = 0;
+    for (int i = 0; i < 8; ++i) { il[i] = (uint32_t)w[i]; ih[i] = (uint32_t)(w[i] >> 32); }
+    tr_bytes8(il, ih, xl, xh);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) x |= ((w[i] >> (8 * g)) & 0xffull) << (8 * i);
-        x = tr8x8(x);
-#pragma unroll
-        for (int t = 0; t < 8; ++t) v[8 * g + t] = cen[(x >> (8 * t)) & 0xffu];
-    }
+    for (int g = 0; g < 8; ++g) unpack_group(xl[g], xh[g], cen, &v[8 * g]);
 }
 DEVI void store_plane_word64(uint8_t* p, uint64_t w) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
@@ -933,12 +978,6 @@ DEVI void fetch_ws(const KArgs& a, const SliceDesc& D, uint32_t tile, bool live,
 #pragma unroll
     for (int k = 0; k < 64; ++k) v[k] = bload1(r, base3, LT<RS::L3>::off(k));
 }
-template <int H>
-DEVI void fetch_ws_half(const KArgs& a, const SliceDesc& D, uint32_t tile, bool live, uint32_t base3, float (&v)[32]) {
-    const rsrc_t r = mk_rsrc(a.ws + D.ws_off + ((size_t)tile << kRowLog), live ? (4u << kRowLog) : 0u);
-#pragma unroll
-    for (int k = 0; k < 32; ++k) v[k] = bload1(r, base3, LT<RS::L3>::off(32 * H + k));
-}
 DEVI void store_ws(const KArgs& a, const SliceDesc& D, uint32_t tile, uint32_t base3, const float (&v)[64]) {
     const rsrc_t r = mk_rsrc(a.ws + D.ws_off + ((size_t)tile << kRowLog), 4u << kRowLog);
 #pragma unroll
@@ -1022,24 +1061,19 @@ __global__ __launch_bounds__(kRowNT) void k_enc_rowC(KArgs a) {
     const uint32_t base3 = LT<RS::L3>::base(tid), base5 = LT<RS::L5>::base(tid);
     int si; uint32_t tile;
     tw.at(t, si, tile);
-    // stages + quantiser need ~220 VGPRs: only half of the next tile (32
-    // registers) is prefetched across them; the other half loads at the top
-    float na[32], nb[32];
-    fetch_ws_half<0>(a, udesc(a.d, si), tile, true, base3, na);
+    float nx[64];
+    fetch_ws(a, udesc(a.d, si), tile, true, base3, nx);
     for (;;) {
         float v[64];
 #pragma unroll
-        for (int r = 0; r < 32; ++r) v[r] = na[r];
+        for (int r = 0; r < 64; ++r) v[r] = nx[r];
         const SliceDesc D = udesc(a.d, si);
-        fetch_ws_half<1>(a, D, tile, true, base3, nb);
-#pragma unroll
-        for (int r = 0; r < 32; ++r) v[32 + r] = nb[r];
         const int tn = t + (int)gridDim.x;
         const bool more = tn < tw.total;
         int sn; uint32_t tln;
         tw.at(more ? tn : t, sn, tln);
         const SliceDesc Dn = udesc(a.d, sn);
-        fetch_ws_half<0>(a, Dn, tln, more, base3, na);
+        fetch_ws(a, Dn, tln, more, base3, nx);
         stages<RS::L3, RS::F2c>(v);
         exchange<RS::L3, RS::L4>(v, s, tid);
         stages<RS::L4, RS::F2d>(v);
@@ -1052,7 +1086,7 @@ __global__ __launch_bounds__(kRowNT) void k_enc_rowC(KArgs a) {
         uint64_t wd[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) wd[i] = 0;
-        float dot = quant_pack64<0, 8>(v, ysc, zm64, qt, wd);
+        float dot = quant_pack64(v, ysc, zm64, qt, wd);
         if (!(nu > 0.0f)) {
             dot = 0.f;
 #pragma unroll
