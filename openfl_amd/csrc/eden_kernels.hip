@@ -40,6 +40,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -127,11 +128,10 @@ DEVI uint32_t rd_mix(uint32_t r2) {
 DEVI uint32_t rd_word(uint32_t j, uint32_t b) { return rd_mix(kLcgA * j + b); }
 // the 8 sign bits of word j: bit k = 1 <=> nibble k >= 8 <=> element k*S+j is +1 (:440-447)
 DEVI uint32_t rd_byte(uint32_t j, uint32_t b) {
-    const uint32_t w = rd_word(j, b) >> 3;
-    uint32_t r = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) r |= ((w >> (4 * k)) & 1u) << k;
-    return r;
+    uint32_t x = (rd_word(j, b) >> 3) & 0x11111111u;  // sign bits at 4k
+    x = (x | (x >> 3)) & 0x03030303u;                  // -> bits 8m, 8m+1
+    x = (x | (x >> 6)) & 0x000F000Fu;                  // -> bits 16m .. 16m+3
+    return (x | (x >> 12)) & 0xFFu;                    // -> bits 0 .. 7
 }
 DEVI float flip_unless(float v, uint32_t plus) {  // plus = 1 -> +v, 0 -> -v
     return __uint_as_float(__float_as_uint(v) ^ ((plus ^ 1u) << 31));
@@ -840,6 +840,12 @@ DEVI uint32_t uu(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // Persistent row launches: one block per CU walks tiles t, t+G, t+2G, ...;
 // the next tile's input is in flight in registers while this one computes.
+// Persistent row launches: one block per CU walks tiles t, t+G, t+2G, ...
+// (G = gridDim.x); the next tile's input is in flight in registers while the
+// current one computes.  (Column passes stay one-tile-per-block: their tiles
+// read 128 B .. 4 KiB row segments that share DRAM pages with neighbouring
+// tiles, and hardware dispatch keeps the tiles in flight a contiguous window;
+// persistent column blocks drift apart and measured slower.)
 struct TileWalk {
     const KArgs& a;
     TileTab* tab;
@@ -1357,7 +1363,7 @@ struct ofl_eden_plan {
     int64_t planes_bytes = 0;
     int64_t ws_floats = 0;      // intermediates
     int64_t part_floats = 0;    // partials
-    int64_t nlarge = 0;
+    int64_t nlarge = 0;         // large slices (informational)
     std::vector<Launch> enc, dec;
     std::vector<int32_t> ints;  // launch lists and tile prefixes (host copy)
     // profiling: events around every launch of every call while enabled
@@ -1749,7 +1755,9 @@ int64_t ofl_eden_plan_workspace_bytes(ofl_eden_plan_t pl) {
     if (!pl) return -1;
     // intermediates | partials | norms, each 256-B aligned
     auto al = [](int64_t b) { return (b + 255) & ~255ll; };
-    return al(pl->ws_floats * 4) + al(pl->part_floats * 4) + al(pl->nlarge * 4) + 256;
+    // per-slice norms are indexed by slice id (all slices, not only large ones)
+    const int64_t nnu = (int64_t)pl->slices.size();
+    return al(pl->ws_floats * 4) + al(pl->part_floats * 4) + al(nnu * 4) + 256;
 }
 
 int ofl_eden_plan_tensor_info(ofl_eden_plan_t pl, int t, int64_t* planes_offset, int64_t* planes_bytes,

@@ -1,12 +1,12 @@
 #!/bin/bash
-# A/B kernel variants on the GPU box: runs bench.py once per library and prints
-# the per-kernel breakdown.  Usage: tools/ab_kernels.sh [lib.so ...]
-# (the default build first; each run is time-limited on its own)
+# A/B kernel variants on the GPU box: runs bench.py once per variant and prints
+# the per-kernel breakdown.  Variants: a library path (*.so, via OFL_CODEC_LIB)
+# or NAME=VALUE (an environment setting for that run).  The default build
+# runs first.  Usage: tools/ab_kernels.sh [lib.so | VAR=value ...]
 set -e
 mkdir -p gpurun_out
 run() {
-  local tag=$1 lib=$2
-  if [ -n "$lib" ]; then export OFL_CODEC_LIB=$lib; else unset OFL_CODEC_LIB; fi
+  local tag=$1
   timeout -k 10 240 python bench.py --steps 4 --warmup 1 --no-cpu-baseline > gpurun_out/ab_$tag.json 2> gpurun_out/ab_$tag.err
   python - "$tag" <<'PY'
 import json, sys
@@ -18,5 +18,11 @@ for k, v in d["roofline"]["kernels"].items():
         print(f"   {k:28s} {v['avg_us']:10.1f} us  {v['moved_GBps']:8.1f} GB/s")
 PY
 }
-run base ""
-for lib in "$@"; do run "$(basename $lib .so)" "$lib"; done
+run base
+for v in "$@"; do
+  if [[ "$v" == *.so ]]; then
+    OFL_CODEC_LIB=$v run "$(basename $v .so)"
+  else
+    env "$v" bash -c "$(declare -f run); run '${v//[^A-Za-z0-9_]/_}'"
+  fi
+done
