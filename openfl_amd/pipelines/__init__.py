@@ -6,11 +6,13 @@ The GPU pipelines (Eden, KC, SKC, STC) are imported lazily so that
 when used without a GPU).
 """
 from openfl_amd.pipelines.no_compression_pipeline import NoCompressionPipeline
+from openfl_amd.pipelines.random_shift_pipeline import RandomShiftPipeline, RandomShiftTransformer
 from openfl_amd.pipelines.pipeline import (Float32NumpyArrayToBytes, TransformationPipeline,
                                            Transformer)
 
 __all__ = ["EdenPipeline", "EdenTransformer", "Float32NumpyArrayToBytes", "KCPipeline", "NoCompressionPipeline",
-           "SKCPipeline", "STCPipeline", "TransformationPipeline", "Transformer"]
+           "RandomShiftPipeline", "RandomShiftTransformer", "SKCPipeline", "STCPipeline", "TransformationPipeline",
+           "Transformer"]
 
 _LAZY = {"EdenPipeline": "eden_pipeline", "EdenTransformer": "eden_pipeline", "Eden": "eden_pipeline",
          "KCPipeline": "kc_pipeline", "SKCPipeline": "skc_pipeline", "STCPipeline": "stc_pipeline"}

@@ -20,8 +20,11 @@ Reference functions exercised (citations are /root/reference-relative):
   openfl/pipelines/kc_pipeline.py:36-114     KmeansTransformer
   openfl/pipelines/stc_pipeline.py:30-143    SparsityTransformer / TernaryTransformer
   openfl/pipelines/skc_pipeline.py:33-187    SKC transformers
+  openfl/pipelines/random_shift_pipeline.py:12-77  RandomShiftTransformer / Pipeline
+  openfl/pipelines/no_compression_pipeline.py:10-15 NoCompressionPipeline
 
-Usage:  python tests/golden/make_golden.py   (writes tests/golden/*.npz, *.json)
+Usage:  python tests/golden/make_golden.py [--only plain]
+        (writes tests/golden/*.npz, *.json; --only plain rewrites plain_golden.json only)
 """
 import hashlib
 import importlib
@@ -45,7 +48,8 @@ def _load_reference():
         mod.__path__ = [os.path.join(REF, sub)]
         sys.modules[name] = mod
     mods = {}
-    for m in ("pipeline", "eden_pipeline", "kc_pipeline", "skc_pipeline", "stc_pipeline"):
+    for m in ("pipeline", "eden_pipeline", "kc_pipeline", "skc_pipeline", "stc_pipeline",
+              "random_shift_pipeline", "no_compression_pipeline"):
         mods[m] = importlib.import_module("openfl.pipelines." + m)
     return mods
 
@@ -243,8 +247,50 @@ def kc_fixtures(ref):
     return arrays, index
 
 
+def plain_fixtures(ref):
+    """Lossless pipelines: RandomShift (one np.random.uniform draw per call,
+    every shift in int_to_float) and NoCompression, in-process and with the
+    float32 wire values a receiver sees (MetadataProto.int_to_float)."""
+    out = {"random_shift": [], "no_compression": []}
+    for shape, seed in (((2, 3), 7), ((5,), 11), ((3, 4, 2), 2024)):
+        x = gen_input(int(np.prod(shape)), seed).reshape(shape)
+        np.random.seed(seed)
+        pipe = ref["random_shift_pipeline"].RandomShiftPipeline()
+        data, md = pipe.forward(x)
+        rec = {"shape": list(shape), "seed": seed, "x": x.reshape(-1).tolist(),
+               "data_hex": bytes(data).hex(),
+               "metadata": [{"int_list": list(m.get("int_list", [])),
+                             "int_to_float": [[int(k), float(v)] for k, v in m.get("int_to_float", {}).items()]}
+                            for m in md]}
+        y_mem = pipe.backward(data, [dict(m) for m in md])
+        rec["backward_inproc_hex"] = np.ascontiguousarray(y_mem).tobytes().hex()
+        rec["backward_inproc_dtype"] = str(y_mem.dtype)
+        wire = [{"int_list": list(m.get("int_list", [])),
+                 "int_to_float": {int(k): float(np.float32(v)) for k, v in m.get("int_to_float", {}).items()}}
+                for m in md]
+        y_wire = pipe.backward(data, wire)
+        rec["backward_wire_hex"] = np.ascontiguousarray(y_wire).tobytes().hex()
+        rec["backward_wire_dtype"] = str(y_wire.dtype)
+        out["random_shift"].append(rec)
+    for shape, dt in (((4, 3), "float32"), ((7,), "float64")):
+        x = gen_input(int(np.prod(shape)), 5).reshape(shape).astype(dt)
+        pipe = ref["no_compression_pipeline"].NoCompressionPipeline()
+        data, md = pipe.forward(x)
+        y = pipe.backward(data, [dict(m) for m in md])
+        out["no_compression"].append({"shape": list(shape), "dtype": dt, "x": x.reshape(-1).tolist(),
+                                      "data_hex": bytes(data).hex(),
+                                      "metadata": [{"int_list": list(m.get("int_list", []))} for m in md],
+                                      "backward_hex": y.tobytes().hex(), "backward_dtype": str(y.dtype)})
+    return out
+
+
 def main():
     ref = _load_reference()
+    with open(os.path.join(OUT, "plain_golden.json"), "w") as f:
+        json.dump(plain_fixtures(ref), f, indent=1)
+    if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "plain":
+        print("wrote plain_golden.json")
+        return
     arrays, index = eden_fixtures(ref)
     np.savez_compressed(os.path.join(OUT, "eden_golden.npz"), **arrays)
     with open(os.path.join(OUT, "eden_golden.json"), "w") as f:
