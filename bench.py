@@ -63,6 +63,48 @@ def cpu_baseline(shapes, x_host_fn, n_bits, sample_mib):
                       f"oracle/eden_oracle.c single-threaded; enc {t_enc:.2f} s + dec {t_dec:.2f} s"}
 
 
+def secondary(name, n_bits, steps, warmup, dev, wave_mib, streams):
+    """One more workload on this GPU (same step definition, inputs resident):
+    the north_star's 1 GiB set and BASELINE config 2 (ResNet-50) next to the
+    main line.  Device time from events around the timed steps."""
+    import torch
+    from openfl_amd.codec import EdenPlan
+    from openfl_amd.workloads import WORKLOADS, numel
+    numels = [numel(s) for _, s in WORKLOADS[name]()]
+    plan = EdenPlan(numels, n_bits, wave_mib=wave_mib, streams=streams)
+    x = torch.empty(max(plan.arena_numel, 1), dtype=torch.float32, device=dev)
+    gen = torch.Generator(device=dev)
+    for j, n in enumerate(numels):
+        gen.manual_seed(j)
+        off = plan.elem_offsets[j]
+        x[off:off + n].normal_(0.0, 0.01, generator=gen)
+    y = torch.empty_like(x)
+    planes = torch.empty(max(plan.planes_bytes, 1), dtype=torch.uint8, device=dev)
+    scales = torch.empty(max(plan.n_slices, 1), dtype=torch.float32, device=dev)
+    ws = torch.empty(max(plan.ws_bytes, 256), dtype=torch.uint8, device=dev)
+    seeds = torch.arange(len(numels), dtype=torch.int32, device=dev)
+    for _ in range(warmup):
+        plan.encode(x, seeds, planes, scales, ws)
+        plan.decode(planes, seeds, scales, y, ws)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(steps):
+        plan.encode(x, seeds, planes, scales, ws)
+        plan.decode(planes, seeds, scales, y, ws)
+    ev1.record()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    gpu_s = ev0.elapsed_time(ev1) / 1e3
+    alg = sum(l["bytes_alg"] for e in (True, False) for l in plan.launches(e))
+    return {"value": round(4 * sum(numels) * steps / wall / 2 ** 30, 2), "unit": "GiB/s",
+            "ms_per_step": round(1e3 * wall / steps, 4), "gpu_ms_per_step": round(1e3 * gpu_s / steps, 4),
+            "roofline_frac": round(alg * steps / gpu_s / 1e9 / PEAK_HBM_GBPS, 4),
+            "bytes": 4 * sum(numels), "tensors": len(numels), "slices": plan.n_slices, "waves": plan.n_waves,
+            "streams": plan.n_streams, "steps": steps}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -77,6 +119,14 @@ def main():
                     help="do not record per-launch HIP events in the timed region")
     ap.add_argument("--traffic-json", default=None,
                     help="rocprofv3 PMC-derived HBM bytes per step (tools/pmc_traffic.py output)")
+    ap.add_argument("--wave-mib", type=float, default=None,
+                    help="large-slice wave size (ofl_eden_plan_set_schedule; default: library's)")
+    ap.add_argument("--streams", type=int, default=None, help="1 or 2 (default: library's)")
+    ap.add_argument("--also", default="uniform_1gib,resnet50_fp32",
+                    help="secondary workloads timed after the main one (rank 0 line, 'also'); '' = none")
+    ap.add_argument("--also-steps", type=int, default=20)
+    ap.add_argument("--profile-steps", type=int, default=3,
+                    help="steps of the serialized per-kernel profile pass (two-stream schedules)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -97,7 +147,7 @@ def main():
     sizes = [numel(s) for _, s in shapes]
     mine = shard_indices(sizes, rank, world, args.scaling)
     numels = [sizes[i] for i in mine]
-    plan = EdenPlan(numels, args.n_bits)
+    plan = EdenPlan(numels, args.n_bits, wave_mib=args.wave_mib, streams=args.streams)
 
     # synthetic update: N(0, 0.01^2) fp32, seeded per (rank, tensor)
     x = torch.empty(max(plan.arena_numel, 1), dtype=torch.float32, device=dev)
@@ -122,7 +172,11 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    if not args.no_kernel_events:
+    # per-launch events inside the timed region only for a single-stream
+    # schedule: with two streams a launch's events also span the other
+    # stream's kernel it waits behind (a serialized profile pass follows)
+    two = plan.n_streams == 2
+    if not args.no_kernel_events and not two:
         plan.profile(True)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
@@ -143,19 +197,40 @@ def main():
     gpu_ms = ev0.elapsed_time(ev1)
     elapsed = max_over_ranks(elapsed, dev)
 
-    # per-kernel breakdown from the events recorded inside the timed region
+    # per-kernel breakdown: events of the timed region (one stream), or of a
+    # serialized profile pass over the same tensors (two streams)
     kernels = {}
+    kernels_source = None
     if not args.no_kernel_events:
+        pplan, pws = plan, ws
+        if two:
+            pplan = EdenPlan(numels, args.n_bits, wave_mib=args.wave_mib, streams=1)
+            pws = torch.empty(max(pplan.ws_bytes, 256), dtype=torch.uint8, device=dev)
+            pplan.encode(x, seeds, planes, scales, pws)
+            pplan.decode(planes, seeds, scales, y, pws)
+            torch.cuda.synchronize()
+            pplan.profile(True)
+            for _ in range(args.profile_steps):
+                pplan.encode(x, seeds, planes, scales, pws)
+                pplan.decode(planes, seeds, scales, y, pws)
+            torch.cuda.synchronize()
+            kernels_source = (f"serialized profile pass after the timed region: {args.profile_steps} steps of "
+                              f"the same tensors on one stream ({pplan.n_waves} waves); HIP events around "
+                              "every launch")
+        else:
+            kernels_source = "HIP events around every launch inside the timed region"
         for enc in (True, False):
-            ms, calls = plan.profile_collect(enc)
-            for info, m in zip(plan.launches(enc), ms):
+            ms, calls = pplan.profile_collect(enc)
+            for info, m in zip(pplan.launches(enc), ms):
                 k = kernels.setdefault(info["name"], {"ms": 0.0, "launches": 0, "bytes_moved": 0,
                                                       "bytes_alg": 0})
                 k["ms"] += float(m)
                 k["launches"] += calls
                 k["bytes_moved"] += info["bytes_moved"] * calls
                 k["bytes_alg"] += info["bytes_alg"] * calls
-        plan.profile(False)
+        pplan.profile(False)
+        if two:
+            del pplan, pws
 
     # quality check (not timed): relative L2 error of decode(encode(x))
     with torch.no_grad():
@@ -188,10 +263,16 @@ def main():
             "bytes_alg_per_launch": k["bytes_alg"] // k["launches"],
             "moved_GBps": round(k["bytes_moved"] / (k["ms"] / 1e3) / 1e9, 1),
             "moved_frac": round(k["bytes_moved"] / (k["ms"] / 1e3) / 1e9 / PEAK_HBM_GBPS, 4)}
+        roof["kernels_source"] = kernels_source
         roof["kernels"] = {n: {"avg_us": round(1e3 * v["ms"] / v["launches"], 2),
                                "share": round(v["ms"] / tot_ms, 3),
                                "moved_GBps": round(v["bytes_moved"] / max(v["ms"], 1e-9) / 1e6, 1)}
                            for n, v in sorted(kernels.items(), key=lambda kv: -kv[1]["ms"])}
+
+    also = {}
+    if world == 1 and args.also:
+        for name in [a for a in args.also.split(",") if a]:
+            also[name] = secondary(name, args.n_bits, args.also_steps, 3, dev, args.wave_mib, args.streams)
 
     out = None
     if rank == 0:
@@ -213,13 +294,15 @@ def main():
                     "resident in HBM; no checkpoint",
             "config": {"workload": args.workload, "tensors": len(numels), "numel_per_rank": sum(numels),
                        "bytes_per_rank": in_bytes_rank, "n_bits": args.n_bits, "slices": plan.n_slices,
-                       "planes_bytes_per_rank": plan.planes_bytes,
+                       "planes_bytes_per_rank": plan.planes_bytes, "waves": plan.n_waves,
+                       "streams": plan.n_streams, "wave_mib": plan.wave_mib,
                        "parallelism": (f"{world} independent replicas, one update set per GPU"
                                        if args.scaling == "weak" else f"LPT-sharded over {world} GPUs")},
             "gpu_ms_per_step": round(gpu_ms / args.steps, 3),
             "check_rel_l2": round(rel, 6),
             "roofline": roof,
             "cpu_baseline": cpu,
+            "also": also or None,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -76,6 +76,24 @@ int ofl_eden_plan_create(int ntensors, const int64_t* numel, const int64_t* elem
                          ofl_eden_plan_t* plan_out);
 void ofl_eden_plan_destroy(ofl_eden_plan_t plan);
 
+/* Large-slice schedule (no reference counterpart: how the gfx950 passes are
+ * ordered, never what they compute -- outputs are bit-identical for every
+ * schedule).  Slices with P > 2^15 run in "waves" of at most wave_bytes of
+ * fp32 intermediates (0: all large slices in one wave; a bigger slice is a
+ * wave of its own); each wave runs all of its passes back to back and the
+ * waves reuse `streams` workspace buffers, which bounds the workspace.
+ * streams = 2 alternates the waves between the caller's stream and a
+ * plan-owned side stream (forked from and joined back into the caller's
+ * stream inside every call) so one wave's launches fill the other's launch
+ * gaps and tails; there are then at least two waves (the large slices split
+ * in halves).  wave_bytes < 0 or streams == 0 keep the current value.  Only
+ * before the plan's first encode/decode; the workspace size changes with it.
+ * Default: 16 GiB waves, 2 streams (env OFL_EDEN_WAVE_MIB / OFL_EDEN_STREAMS
+ * override the default; DESIGN.md section 3.6 has the measurements). */
+int ofl_eden_plan_set_schedule(ofl_eden_plan_t plan, int64_t wave_bytes, int streams);
+int ofl_eden_plan_get_schedule(ofl_eden_plan_t plan, int64_t* wave_bytes, int* streams);
+int ofl_eden_plan_num_waves(ofl_eden_plan_t plan);
+
 /* Totals: slices (= length of the scales array), planes-arena bytes,
  * workspace bytes needed by encode and decode. */
 int64_t ofl_eden_plan_num_slices(ofl_eden_plan_t plan);
@@ -108,7 +126,7 @@ int ofl_eden_decode(ofl_eden_plan_t plan, const uint8_t* planes_arena, const uin
 
 /* ---- profiling (bench.py) --------------------------------------------------
  * While enabled, every encode/decode of the plan records a HIP event before
- * its first launch and after each launch on its stream.  collect() waits for
+ * and after each launch, on the launch's stream.  collect() waits for
  * the recorded calls of one direction, writes the summed per-launch
  * milliseconds (launch order) and the call count, and drops the records.
  * launch_info() names launch idx (kernel symbol as rocprofv3 shows it) with

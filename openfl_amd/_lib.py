@@ -18,7 +18,8 @@ OFL_OK = 0
 
 EXPORTS = (
     "ofl_version", "ofl_last_error", "ofl_eden_slice_plan", "ofl_eden_plan_create",
-    "ofl_eden_plan_destroy", "ofl_eden_plan_num_slices", "ofl_eden_plan_planes_bytes",
+    "ofl_eden_plan_destroy", "ofl_eden_plan_set_schedule", "ofl_eden_plan_num_waves",
+    "ofl_eden_plan_get_schedule", "ofl_eden_plan_num_slices", "ofl_eden_plan_planes_bytes",
     "ofl_eden_plan_workspace_bytes", "ofl_eden_plan_tensor_info", "ofl_eden_plan_tensor_dims",
     "ofl_eden_encode", "ofl_eden_decode", "ofl_eden_plan_profile", "ofl_eden_plan_num_launches",
     "ofl_eden_plan_launch_info", "ofl_eden_plan_profile_collect", "ofl_serial_sum_f32",
@@ -41,6 +42,12 @@ def _bind(L):
     L.ofl_eden_plan_create.restype = i32
     L.ofl_eden_plan_destroy.argtypes = [vp]
     L.ofl_eden_plan_destroy.restype = None
+    L.ofl_eden_plan_set_schedule.argtypes = [vp, i64, i32]
+    L.ofl_eden_plan_set_schedule.restype = i32
+    L.ofl_eden_plan_num_waves.argtypes = [vp]
+    L.ofl_eden_plan_num_waves.restype = i32
+    L.ofl_eden_plan_get_schedule.argtypes = [vp, vp, vp]
+    L.ofl_eden_plan_get_schedule.restype = i32
     for f in ("ofl_eden_plan_num_slices", "ofl_eden_plan_planes_bytes", "ofl_eden_plan_workspace_bytes"):
         getattr(L, f).argtypes = [vp]
         getattr(L, f).restype = i64

@@ -37,7 +37,9 @@ def slice_plan(n):
 class EdenPlan:
     """Layout + launch plan for one batch shape (list of numels, optional dims)."""
 
-    def __init__(self, numels, n_bits=8, dims=None, elem_offsets=None):
+    def __init__(self, numels, n_bits=8, dims=None, elem_offsets=None, wave_mib=None, streams=None):
+        """wave_mib / streams: large-slice schedule (ofl_eden_plan_set_schedule;
+        None keeps the library default).  Outputs do not depend on it."""
         L = _lib.lib()
         self.n_bits = int(n_bits)
         self.numels = [int(n) for n in numels]
@@ -64,6 +66,13 @@ class EdenPlan:
                                           self.n_bits, ctypes.byref(h)))
         self._h = h
         self._L = L
+        if wave_mib is not None or streams is not None:
+            _lib.check(L.ofl_eden_plan_set_schedule(h, -1 if wave_mib is None else int(float(wave_mib) * 2 ** 20),
+                                                    0 if streams is None else int(streams)))
+        self.n_waves = int(L.ofl_eden_plan_num_waves(h))
+        wb, ns = ctypes.c_int64(), ctypes.c_int()
+        _lib.check(L.ofl_eden_plan_get_schedule(h, ctypes.byref(wb), ctypes.byref(ns)))
+        self.wave_mib, self.n_streams = wb.value / 2 ** 20, ns.value
         self.n_slices = int(L.ofl_eden_plan_num_slices(h))
         self.planes_bytes = int(L.ofl_eden_plan_planes_bytes(h))
         self.ws_bytes = int(L.ofl_eden_plan_workspace_bytes(h))

@@ -78,7 +78,7 @@ struct KArgs {
     int32_t count;
     int32_t nbits;
     int32_t lo;             // column passes: first transformed bit
-    int32_t pad_;
+    int32_t do_nu;          // column passes: tile 0 of each slice writes the slice norm
     const float* xin;       // fp32 arena in (encode)
     float* xout;            // fp32 arena out (decode)
     float* ws;              // intermediate buffer base
@@ -1287,21 +1287,23 @@ __global__ __launch_bounds__(kColNT) void k_col(KArgs a) {
             for (int r = 0; r < 32; ++r) w[map(base1w | LT<CS::L1>::off(r))] = v[r];
         }
     }
+    // The slice norm nu = sqrt(sum of the row pass's partials of x^2)
+    // (|H D2 H D1 x| = |x|; eden_pipeline.py:515) for the final row pass: tile
+    // 0 of every slice in the slice's first column launch sums them in a fixed
+    // order (the same value whatever the launch grouping).
+    if (a.do_nu && tile == 0) {
+        __shared__ float nred[kColNT / 64];
+        const int64_t ntile = 1ll << (D.logp - kRowLog);
+        float ss = 0.f;
+        for (int64_t t = tid; t < ntile; t += kColNT) ss += a.part[D.part_off + t];
+        ss = block_sum<kColNT>(ss, nred);
+        if (tid == 0) a.nu[si] = sqrtf(ss);
+    }
 }
 
 // ===========================================================================
-// Per-slice reductions (large slices): norms before pass C, scales after.
+// Per-slice scales (large slices), after every final row pass.
 // ===========================================================================
-__global__ __launch_bounds__(256) void k_norms(KArgs a) {
-    __shared__ float red[4];
-    const int si = a.list[blockIdx.x];
-    const SliceDesc D = a.d[si];
-    const int64_t ntile = 1ll << (D.logp - kRowLog);
-    float ss = 0.f;
-    for (int64_t t = threadIdx.x; t < ntile; t += 256) ss += a.part[D.part_off + t];
-    ss = block_sum<256>(ss, red);
-    if (threadIdx.x == 0) a.nu[si] = sqrtf(ss);
-}
 
 __global__ __launch_bounds__(256) void k_finalize(KArgs a) {
     __shared__ float red[4];
@@ -1342,15 +1344,18 @@ struct Launch {
     int kind;        // see enum below
     int param;       // p (small) / M (column)
     int lo;          // column passes
-    int mid;         // column: fused middle pass
+    int mid;         // column: fused middle pass; decode row A: 8-byte plane words
     int list_off;    // into d_list
     int tstart_off;  // into d_tstart (multi-tile kernels), -1 otherwise
     int count;       // list entries
     int64_t blocks;  // grid size
-    int64_t bytes_moved;  // fp32/plane bytes this launch reads + writes in HBM (intermediates included)
-    int64_t bytes_alg;    // its share of the SURVEY 8(d) algorithmic bytes (x/y fp32 + planes only)
+    int nu = 0;      // column: tile 0 of each slice writes the slice norm
+    int stream = 0;  // 0: the caller's stream, 1: the plan's side stream
+    int join = 0;    // the caller's stream waits for the side stream before this launch
+    int64_t bytes_moved = 0;  // fp32/plane bytes this launch reads + writes (intermediates included)
+    int64_t bytes_alg = 0;    // its share of the SURVEY 8(d) algorithmic bytes (x/y fp32 + planes only)
 };
-enum Kind { K_TINY, K_SMALL, K_ROWA, K_ROWC, K_COL, K_NORMS, K_FINAL };
+enum Kind { K_TINY, K_SMALL, K_ROWA, K_ROWC, K_COL, K_FINAL };
 
 }  // namespace
 
@@ -1364,6 +1369,12 @@ struct ofl_eden_plan {
     int64_t ws_floats = 0;      // intermediates
     int64_t part_floats = 0;    // partials
     int64_t nlarge = 0;         // large slices (informational)
+    // slice ids per kernel class (fixed by the batch) and the schedule built
+    // from them (build_schedule)
+    std::vector<int32_t> tiny, small[5], large;
+    int64_t wave_bytes = 0;     // intermediate bytes per wave of large slices; 0: one wave
+    int nstreams = 1;           // 2: waves alternate between the caller's and a side stream
+    int nwaves = 0;
     std::vector<Launch> enc, dec;
     std::vector<int32_t> ints;  // launch lists and tile prefixes (host copy)
     // profiling: events around every launch of every call while enabled
@@ -1376,9 +1387,16 @@ struct ofl_eden_plan {
     int ncu = 256;              // persistent row launches: one block per CU
     bool uploaded = false;
     std::mutex mu;
+    hipStream_t side = nullptr;  // nstreams == 2 (created on first use)
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    std::mutex run_mu;          // serialises runs that use the side stream
 };
 
 namespace {
+
+// Default large-slice schedule (see build_schedule).
+constexpr int64_t kDefaultWaveMiB = 16384;
+constexpr int64_t kDefaultStreams = 2;
 
 int64_t low_po2(int64_t n) { int64_t p = 1; while (p * 2 <= n) p *= 2; return n ? p : 0; }
 int64_t high_po2(int64_t n) { int64_t p = 1; while (p < n) p *= 2; return n ? p : 0; }
@@ -1438,32 +1456,49 @@ hipError_t set_all_attrs() {
     return set_col_attr<10>();
 }
 
-int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t st) {
+int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller) {
     static std::once_flag attrs_once;
     static hipError_t attrs_err = hipSuccess;
     std::call_once(attrs_once, [] { attrs_err = set_all_attrs(); });
     if (attrs_err != hipSuccess) return fail(OFL_EHIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(attrs_err));
     const std::vector<Launch>& L = enc ? pl->enc : pl->dec;
+    // waves on the side stream fork from and join back into the caller's stream
+    const bool two = pl->side != nullptr;
+    std::unique_lock<std::mutex> lk(pl->run_mu, std::defer_lock);
+    if (two) {
+        lk.lock();
+        HIP_TRY(hipEventRecord(pl->ev_fork, caller));
+        HIP_TRY(hipStreamWaitEvent(pl->side, pl->ev_fork, 0));
+    }
+    const hipStream_t streams[2] = {caller, two ? pl->side : caller};
+    bool joined = !two;
     std::vector<hipEvent_t>* evs = nullptr;
-    if (pl->prof) {
+    if (pl->prof) {  // one event before and one after every launch, on its stream
         std::lock_guard<std::mutex> g(pl->mu);
         pl->prof_ev[enc].emplace_back();
         evs = &pl->prof_ev[enc].back();
-        for (size_t i = 0; i <= L.size(); ++i) {
+        for (size_t i = 0; i < 2 * L.size(); ++i) {
             hipEvent_t e;
             if (!pl->ev_pool.empty()) { e = pl->ev_pool.back(); pl->ev_pool.pop_back(); }
             else HIP_TRY(hipEventCreate(&e));
             evs->push_back(e);
         }
-        HIP_TRY(hipEventRecord((*evs)[0], st));
     }
     for (size_t li = 0; li < L.size(); ++li) {
         const Launch& l = L[li];
+        if (l.join && !joined) {
+            HIP_TRY(hipEventRecord(pl->ev_join, pl->side));
+            HIP_TRY(hipStreamWaitEvent(caller, pl->ev_join, 0));
+            joined = true;
+        }
+        const hipStream_t st = streams[l.stream];
         ofl::KArgs a = base;
         a.list = pl->d_ints + l.list_off;
         a.tstart = l.tstart_off >= 0 ? pl->d_ints + l.tstart_off : nullptr;
         a.count = l.count;
         a.lo = l.lo;
+        a.do_nu = l.nu;
+        if (evs) HIP_TRY(hipEventRecord((*evs)[2 * li], st));
         hipError_t e = hipSuccess;
         switch (l.kind) {
         case K_TINY:
@@ -1513,11 +1548,14 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t st) {
 #undef COLCASE
             break;
         }
-        case K_NORMS: e = launch(ofl::k_norms, l.blocks, 256, 0, st, a); break;
         case K_FINAL: e = launch(ofl::k_finalize, l.blocks, 256, 0, st, a); break;
         }
         if (e != hipSuccess) return fail(OFL_EHIP, std::string("kernel launch failed: ") + hipGetErrorString(e));
-        if (evs) HIP_TRY(hipEventRecord((*evs)[li + 1], st));
+        if (evs) HIP_TRY(hipEventRecord((*evs)[2 * li + 1], st));
+    }
+    if (!joined) {
+        HIP_TRY(hipEventRecord(pl->ev_join, pl->side));
+        HIP_TRY(hipStreamWaitEvent(caller, pl->ev_join, 0));
     }
     return OFL_OK;
 }
@@ -1530,9 +1568,144 @@ std::string launch_name(const Launch& l, bool enc) {
     case K_ROWA: return std::string("ofl::k_") + d + "_rowA";
     case K_ROWC: return std::string("ofl::k_") + d + "_rowC";
     case K_COL: return "ofl::k_col<" + std::to_string(l.param) + ", " + (l.mid ? "true" : "false") + ">";
-    case K_NORMS: return "ofl::k_norms";
     default: return "ofl::k_finalize";
     }
+}
+
+// Large slices run in waves of at most wave_bytes of intermediates (a bigger
+// slice is a wave of its own).  A wave runs row pass A, its column passes and
+// row pass C back to back, so its intermediates are re-read while they still
+// sit in the 256 MiB Infinity Cache; waves share nstreams workspace buffers
+// (wave w: buffer and stream w % nstreams).  The scales are finalised once,
+// after every wave.
+void build_schedule(ofl_eden_plan* pl) {
+    std::vector<int32_t>& ints = pl->ints;
+    ints.clear();
+    pl->enc.clear();
+    pl->dec.clear();
+    auto add_list = [&](const std::vector<int32_t>& l) {
+        const int o = (int)ints.size();
+        ints.insert(ints.end(), l.begin(), l.end());
+        return o;
+    };
+    auto add_prefix = [&](const std::vector<int32_t>& l, int log_tile, int64_t& total) {
+        const int o = (int)ints.size();
+        int64_t acc = 0;
+        for (int32_t si : l) { ints.push_back((int32_t)acc); acc += 1ll << (pl->slices[si].logp - log_tile); }
+        ints.push_back((int32_t)acc);
+        total = acc;
+        return o;
+    };
+    std::vector<Launch> common;
+    if (!pl->tiny.empty())
+        common.push_back({K_TINY, 0, 0, 0, add_list(pl->tiny), -1, (int)pl->tiny.size(), (int64_t)pl->tiny.size()});
+    for (int k = 0; k < 5; ++k)
+        if (!pl->small[k].empty())
+            common.push_back({K_SMALL, 11 + k, 0, 0, add_list(pl->small[k]), -1, (int)pl->small[k].size(),
+                              (int64_t)pl->small[k].size()});
+    pl->enc = common;
+    pl->dec = common;
+
+    const std::vector<int32_t>& large = pl->large;
+    std::vector<std::vector<int32_t>> waves;
+    int64_t cap = pl->wave_bytes > 0 ? pl->wave_bytes / 4 : INT64_MAX;
+    if (pl->nstreams == 2) {  // at least two waves, so both streams have work
+        int64_t tot = 0;
+        for (int32_t si : large) tot += 1ll << pl->slices[si].logp;
+        cap = std::min(cap, std::max<int64_t>(1, (tot + 1) / 2));
+    }
+    int64_t acc = 0, wmax = 0;
+    for (int32_t si : large) {
+        const int64_t P = 1ll << pl->slices[si].logp;
+        if (waves.empty() || acc + P > cap) { waves.emplace_back(); acc = 0; }
+        waves.back().push_back(si);
+        acc += P;
+        wmax = std::max(wmax, acc);
+    }
+    pl->nwaves = (int)waves.size();
+    const int nbuf = waves.size() > 1 ? pl->nstreams : 1;
+    pl->ws_floats = nbuf * wmax;
+    for (size_t w = 0; w < waves.size(); ++w) {
+        int64_t off = (int64_t)(w % nbuf) * wmax;
+        for (int32_t si : waves[w]) { pl->slices[si].ws_off = off; off += 1ll << pl->slices[si].logp; }
+    }
+    // decode row A reads 8-byte plane words when every plane row is 8-byte aligned
+    int a8 = 1;
+    for (int32_t si : large) a8 &= (pl->slices[si].pl_off % 8 == 0) && (pl->slices[si].pl_stride % 8 == 0);
+    for (size_t w = 0; w < waves.size(); ++w) {
+        const std::vector<int32_t>& wl = waves[w];
+        const int s = (int)(w % nbuf);
+        int64_t rows = 0;
+        const int lo_l = add_list(wl);
+        const int rp = add_prefix(wl, ofl::kRowLog, rows);
+        std::map<int, std::vector<int32_t>> byp;  // column launches grouped by p
+        for (int32_t si : wl) byp[pl->slices[si].logp].push_back(si);
+        std::vector<Launch> ce, cd;
+        for (auto& kv : byp) {
+            const int r = kv.first - ofl::kRowLog;
+            int64_t tiles = 0;
+            const int lo_c = add_list(kv.second);
+            const int tp = add_prefix(kv.second, ofl::kColLog, tiles);
+            const int cnt = (int)kv.second.size();
+            std::vector<Launch> seq;
+            if (r <= 10) {
+                seq.push_back({K_COL, r, ofl::kRowLog, 1, lo_c, tp, cnt, tiles});
+            } else {  // two column levels; the middle launch carries D2
+                const int m1 = r / 2, m2 = r - m1;
+                seq.push_back({K_COL, m1, ofl::kRowLog, 0, lo_c, tp, cnt, tiles});
+                seq.push_back({K_COL, m2, ofl::kRowLog + m1, 1, lo_c, tp, cnt, tiles});
+                seq.push_back({K_COL, m1, ofl::kRowLog, 0, lo_c, tp, cnt, tiles});
+            }
+            for (Launch& l : seq) l.stream = s;
+            cd.insert(cd.end(), seq.begin(), seq.end());
+            seq[0].nu = 1;  // encode: the first column launch writes the slice norms
+            ce.insert(ce.end(), seq.begin(), seq.end());
+        }
+        Launch ra{K_ROWA, 0, 0, 0, lo_l, rp, (int)wl.size(), rows};
+        Launch rc{K_ROWC, 0, 0, 0, lo_l, rp, (int)wl.size(), rows};
+        ra.stream = rc.stream = s;
+        pl->enc.push_back(ra);
+        pl->enc.insert(pl->enc.end(), ce.begin(), ce.end());
+        pl->enc.push_back(rc);
+        ra.mid = a8;
+        pl->dec.push_back(ra);
+        pl->dec.insert(pl->dec.end(), cd.begin(), cd.end());
+        pl->dec.push_back(rc);
+    }
+    if (!large.empty()) {  // scales need every wave's dot partials
+        Launch f{K_FINAL, 0, 0, 0, add_list(large), -1, (int)large.size(), (int64_t)large.size()};
+        f.join = 1;
+        pl->enc.push_back(f);
+    }
+    // per-launch byte accounting (bench / DESIGN.md roofline)
+    const int64_t n_bits = pl->nbits;
+    for (int dir = 0; dir < 2; ++dir) {
+        const bool enc = dir == 1;
+        for (Launch& l : enc ? pl->enc : pl->dec) {
+            int64_t mv = 0, al = 0;
+            for (int i = 0; i < l.count; ++i) {
+                const ofl::SliceDesc& D = pl->slices[ints[l.list_off + i]];
+                const int64_t P = 1ll << D.logp, pb = n_bits * P / 8;
+                switch (l.kind) {
+                case K_TINY: case K_SMALL:
+                    mv += enc ? 4 * D.len + pb : pb + 4 * D.ylen; al = mv; break;
+                case K_ROWA:
+                    mv += enc ? 4 * D.len + 4 * P : pb + 4 * P; al += enc ? 4 * D.len : pb; break;
+                case K_ROWC:
+                    mv += enc ? 4 * P + pb : 4 * P + 4 * D.ylen; al += enc ? pb : 4 * D.ylen; break;
+                case K_COL: mv += 8 * P; break;
+                default: mv += 4 * (P >> ofl::kRowLog); break;
+                }
+            }
+            l.bytes_moved = mv;
+            l.bytes_alg = al;
+        }
+    }
+}
+
+int64_t env_i64(const char* name, int64_t dflt) {
+    const char* s = getenv(name);
+    return (s && *s) ? strtoll(s, nullptr, 10) : dflt;
 }
 
 }  // namespace
@@ -1572,7 +1745,9 @@ int ofl_eden_plan_create(int ntensors, const int64_t* numel, const int64_t* elem
     pl->ntensors = ntensors;
     int64_t dims_pos = 0;
     // per-class slice lists
-    std::vector<int32_t> tiny, small[5], large;
+    std::vector<int32_t>& tiny = pl->tiny;
+    std::vector<int32_t>* small = pl->small;
+    std::vector<int32_t>& large = pl->large;
     for (int t = 0; t < ntensors; ++t) {
         const int64_t n = numel[t];
         std::vector<int64_t> Ps, Ls;  // padded sizes, valid input lengths
@@ -1626,9 +1801,7 @@ int ofl_eden_plan_create(int ntensors, const int64_t* numel, const int64_t* elem
             if (D.logp <= 10) tiny.push_back(si);
             else if (D.logp <= ofl::kRowLog) small[D.logp - 11].push_back(si);
             else {
-                D.ws_off = pl->ws_floats;
-                pl->ws_floats += P;
-                D.part_off = (int32_t)pl->part_floats;
+                D.part_off = (int32_t)pl->part_floats;  // ws_off: build_schedule
                 pl->part_floats += P >> ofl::kRowLog;
                 large.push_back(si);
             }
@@ -1638,83 +1811,10 @@ int ofl_eden_plan_create(int ntensors, const int64_t* numel, const int64_t* elem
         }
     }
     pl->nlarge = (int64_t)large.size();
-    // ---- launch lists ----
-    std::vector<int32_t>& ints = pl->ints;
-    auto add_list = [&](const std::vector<int32_t>& l) { int o = (int)ints.size(); ints.insert(ints.end(), l.begin(), l.end()); return o; };
-    auto add_prefix = [&](const std::vector<int32_t>& l, int log_tile, int64_t& total) {
-        int o = (int)ints.size();
-        int64_t acc = 0;
-        for (int32_t si : l) { ints.push_back((int32_t)acc); acc += 1ll << (pl->slices[si].logp - log_tile); }
-        ints.push_back((int32_t)acc);
-        total = acc;
-        return o;
-    };
-    std::vector<Launch> common;
-    if (!tiny.empty()) common.push_back({K_TINY, 0, 0, 0, add_list(tiny), -1, (int)tiny.size(), (int64_t)tiny.size()});
-    for (int k = 0; k < 5; ++k)
-        if (!small[k].empty())
-            common.push_back({K_SMALL, 11 + k, 0, 0, add_list(small[k]), -1, (int)small[k].size(), (int64_t)small[k].size()});
-    pl->enc = common;
-    pl->dec = common;
-    if (!large.empty()) {
-        int64_t rows = 0;
-        const int lo_l = add_list(large);
-        const int rp = add_prefix(large, ofl::kRowLog, rows);
-        // column launches grouped by p
-        std::map<int, std::vector<int32_t>> byp;
-        for (int32_t si : large) byp[pl->slices[si].logp].push_back(si);
-        std::vector<Launch> colseq;
-        for (auto& kv : byp) {
-            const int p = kv.first, r = p - ofl::kRowLog;
-            int64_t tiles = 0;
-            const int lo_c = add_list(kv.second);
-            const int tp = add_prefix(kv.second, ofl::kColLog, tiles);
-            const int cnt = (int)kv.second.size();
-            if (r <= 10) {
-                colseq.push_back({K_COL, r, ofl::kRowLog, 1, lo_c, tp, cnt, tiles});
-            } else {
-                const int m1 = r / 2, m2 = r - m1;
-                colseq.push_back({K_COL, m1, ofl::kRowLog, 0, lo_c, tp, cnt, tiles});
-                colseq.push_back({K_COL, m2, ofl::kRowLog + m1, 1, lo_c, tp, cnt, tiles});
-                colseq.push_back({K_COL, m1, ofl::kRowLog, 0, lo_c, tp, cnt, tiles});
-            }
-        }
-        const int nl = (int)large.size();
-        pl->enc.push_back({K_ROWA, 0, 0, 0, lo_l, rp, nl, rows});
-        pl->enc.push_back({K_NORMS, 0, 0, 0, lo_l, -1, nl, nl});
-        pl->enc.insert(pl->enc.end(), colseq.begin(), colseq.end());
-        pl->enc.push_back({K_ROWC, 0, 0, 0, lo_l, rp, nl, rows});
-        pl->enc.push_back({K_FINAL, 0, 0, 0, lo_l, -1, nl, nl});
-        // decode row A reads 8-byte plane words when every plane row is 8-byte aligned
-        int a8 = 1;
-        for (int32_t si : large) a8 &= (pl->slices[si].pl_off % 8 == 0) && (pl->slices[si].pl_stride % 8 == 0);
-        pl->dec.push_back({K_ROWA, 0, 0, a8, lo_l, rp, nl, rows});
-        pl->dec.insert(pl->dec.end(), colseq.begin(), colseq.end());
-        pl->dec.push_back({K_ROWC, 0, 0, 0, lo_l, rp, nl, rows});
-    }
-    // per-launch byte accounting (bench / DESIGN.md roofline)
-    for (int dir = 0; dir < 2; ++dir) {
-        const bool enc = dir == 1;
-        for (Launch& l : enc ? pl->enc : pl->dec) {
-            int64_t mv = 0, al = 0;
-            for (int i = 0; i < l.count; ++i) {
-                const ofl::SliceDesc& D = pl->slices[ints[l.list_off + i]];
-                const int64_t P = 1ll << D.logp, pb = (int64_t)n_bits * P / 8;
-                switch (l.kind) {
-                case K_TINY: case K_SMALL:
-                    mv += enc ? 4 * D.len + pb : pb + 4 * D.ylen; al = mv; break;
-                case K_ROWA:
-                    mv += enc ? 4 * D.len + 4 * P : pb + 4 * P; al += enc ? 4 * D.len : pb; break;
-                case K_ROWC:
-                    mv += enc ? 4 * P + pb : 4 * P + 4 * D.ylen; al += enc ? pb : 4 * D.ylen; break;
-                case K_COL: mv += 8 * P; break;
-                default: mv += 4 * (P >> ofl::kRowLog); break;
-                }
-            }
-            l.bytes_moved = mv;
-            l.bytes_alg = al;
-        }
-    }
+    // default schedule (tuning overrides: OFL_EDEN_WAVE_MIB, OFL_EDEN_STREAMS)
+    pl->wave_bytes = std::max<int64_t>(0, env_i64("OFL_EDEN_WAVE_MIB", kDefaultWaveMiB)) << 20;
+    pl->nstreams = (int)std::min<int64_t>(2, std::max<int64_t>(1, env_i64("OFL_EDEN_STREAMS", kDefaultStreams)));
+    build_schedule(pl);
     *plan_out = pl;
     return OFL_OK;
 }
@@ -1736,6 +1836,14 @@ static int ensure_device(ofl_eden_plan_t pl) {
         HIP_TRY(hipMalloc(&pl->d_ints, sizeof(int32_t) * pl->ints.size()));
         HIP_TRY(hipMemcpy(pl->d_ints, pl->ints.data(), sizeof(int32_t) * pl->ints.size(), hipMemcpyHostToDevice));
     }
+    bool side = false;
+    for (const Launch& l : pl->enc) side |= l.stream != 0;
+    for (const Launch& l : pl->dec) side |= l.stream != 0;
+    if (side) {
+        HIP_TRY(hipStreamCreateWithFlags(&pl->side, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&pl->ev_fork, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&pl->ev_join, hipEventDisableTiming));
+    }
     pl->uploaded = true;
     return OFL_OK;
 }
@@ -1746,8 +1854,31 @@ void ofl_eden_plan_destroy(ofl_eden_plan_t pl) {
     for (hipEvent_t e : pl->ev_pool) (void)hipEventDestroy(e);
     if (pl->d_slices) (void)hipFree(pl->d_slices);
     if (pl->d_ints) (void)hipFree(pl->d_ints);
+    if (pl->side) (void)hipStreamDestroy(pl->side);
+    if (pl->ev_fork) (void)hipEventDestroy(pl->ev_fork);
+    if (pl->ev_join) (void)hipEventDestroy(pl->ev_join);
     delete pl;
 }
+
+int ofl_eden_plan_set_schedule(ofl_eden_plan_t pl, int64_t wave_bytes, int streams) {
+    if (!pl) return fail(OFL_EINVAL, "null plan");
+    if (streams < 0 || streams > 2) return fail(OFL_EINVAL, "schedule: streams must be 1 or 2 (0 keeps)");
+    std::lock_guard<std::mutex> g(pl->mu);
+    if (pl->uploaded) return fail(OFL_EINVAL, "schedule must be set before the plan's first encode/decode");
+    if (wave_bytes >= 0) pl->wave_bytes = wave_bytes;
+    if (streams > 0) pl->nstreams = streams;
+    build_schedule(pl);
+    return OFL_OK;
+}
+
+int ofl_eden_plan_get_schedule(ofl_eden_plan_t pl, int64_t* wave_bytes, int* streams) {
+    if (!pl) return fail(OFL_EINVAL, "null plan");
+    if (wave_bytes) *wave_bytes = pl->wave_bytes;
+    if (streams) *streams = pl->nstreams;
+    return OFL_OK;
+}
+
+int ofl_eden_plan_num_waves(ofl_eden_plan_t pl) { return pl ? pl->nwaves : -1; }
 
 int64_t ofl_eden_plan_num_slices(ofl_eden_plan_t pl) { return pl ? (int64_t)pl->slices.size() : -1; }
 int64_t ofl_eden_plan_planes_bytes(ofl_eden_plan_t pl) { return pl ? pl->planes_bytes : -1; }
@@ -1855,10 +1986,10 @@ int ofl_eden_plan_profile_collect(ofl_eden_plan_t pl, int encode, double* ms_sum
     const int nl = (int)(encode ? pl->enc.size() : pl->dec.size());
     for (int i = 0; i < std::min(nl, max); ++i) ms_sum[i] = 0.0;
     for (auto& call : calls) {
-        HIP_TRY(hipEventSynchronize(call.back()));
         for (int i = 0; i < nl && i < max; ++i) {
             float ms = 0.f;
-            HIP_TRY(hipEventElapsedTime(&ms, call[i], call[i + 1]));
+            HIP_TRY(hipEventSynchronize(call[2 * i + 1]));
+            HIP_TRY(hipEventElapsedTime(&ms, call[2 * i], call[2 * i + 1]));
             ms_sum[i] += ms;
         }
         pl->ev_pool.insert(pl->ev_pool.end(), call.begin(), call.end());

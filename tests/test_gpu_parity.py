@@ -237,6 +237,42 @@ def test_many_large_slices_one_launch():
         np.testing.assert_array_equal(y[off:off + n], gpu_decode(p1, n, s1, d1, seeds[t], 8))
 
 
+def test_schedules_bit_identical():
+    """The large-slice schedule (waves, one or two streams) orders the passes
+    but never changes a value: planes, scales and decoded output are
+    bit-identical across schedules, including a slice bigger than the wave,
+    two column levels (2^26) and mixed small/tiny slices."""
+    from openfl_amd.codec import EdenPlan
+    numels = [(1 << 22) + 5, 1 << 16, 3000, (1 << 26) - 1000, 1 << 20, 77, (1 << 23) + (1 << 17), 1 << 22]
+    g = torch.Generator(device=DEV).manual_seed(21)
+    seeds = [(97 * t + 5) % 65536 for t in range(len(numels))]
+    c = _codec(8)
+    sd = torch.tensor(seeds, dtype=torch.int32, device=DEV)
+    ref = None
+    for wave_mib, streams in ((0, 1), (64, 1), (16, 2), (1, 2), (48, 1)):
+        plan = EdenPlan(numels, 8, wave_mib=wave_mib, streams=streams)
+        if ref is None:
+            arena = torch.empty(plan.arena_numel, device=DEV).normal_(0, 0.01, generator=g)
+        planes, scales = c.encode_arena(plan, arena, sd)
+        y = c.decode_arena(plan, planes, scales, sd)
+        torch.cuda.synchronize()
+        # the written ranges only (arena alignment gaps are never written)
+        out = (torch.cat([planes[o:o + b] for o, b in zip(plan.planes_offsets, plan.planes_nbytes)]),
+               scales[:plan.n_slices].clone(),
+               torch.cat([y[o:o + n] for o, n in zip(plan.elem_offsets, numels)]))
+        if ref is None:
+            ref = out
+            xs = torch.cat([arena[o:o + n] for o, n in zip(plan.elem_offsets, numels)])
+            rel = float(torch.linalg.vector_norm((out[2] - xs).double()) / torch.linalg.vector_norm(xs.double()))
+            assert 5.5e-3 < rel < 7.5e-3
+        else:
+            assert plan.n_waves > 1
+            for a, b in zip(out, ref):
+                assert torch.equal(a, b), (wave_mib, streams)
+    del arena, planes, y, ref
+    torch.cuda.empty_cache()
+
+
 # --------------------------------------------------------- plugin surface ---
 @pytest.mark.parametrize("rec", IDX["forward"], ids=lambda r: r["tag"])
 def test_pipeline_forward_backward_vs_reference(rec):

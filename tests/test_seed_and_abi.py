@@ -67,6 +67,34 @@ def test_host_plan_layout():
     assert p.ws_bytes >= 4 * 4096 * 1024  # large slice intermediates
 
 
+def test_wave_schedule_layout():
+    """Large slices in waves (ofl_eden_plan_set_schedule): wave count, launch
+    lists and the workspace (nstreams wave buffers instead of one slot per
+    slice).  Outputs are schedule-independent (tests/test_gpu_parity.py)."""
+    from openfl_amd import _lib
+    from openfl_amd.codec import EdenPlan
+    numels = [1 << 22] * 6 + [1000, 1 << 20]        # six 16 MiB slices, a small one, a 4 MiB slice
+    one = EdenPlan(numels, 8, wave_mib=0, streams=1)
+    assert one.n_waves == 1
+    assert one.ws_bytes >= 4 * (6 * (1 << 22) + (1 << 20))
+    w2 = EdenPlan(numels, 8, wave_mib=32, streams=2)
+    assert w2.n_waves == 4                            # [a b] [c d] [e f] [g]
+    assert 4 * 2 * (1 << 23) <= w2.ws_bytes < one.ws_bytes
+    for enc in (True, False):
+        names = [l["name"] for l in w2.launches(enc)]
+        d = "enc" if enc else "dec"
+        assert names.count(f"ofl::k_{d}_rowA") == 4 and names.count(f"ofl::k_{d}_rowC") == 4
+        assert names.count("ofl::k_finalize") == (1 if enc else 0)
+        # same algorithmic bytes whatever the schedule
+        assert sum(l["bytes_alg"] for l in w2.launches(enc)) == sum(l["bytes_alg"] for l in one.launches(enc))
+    w1 = EdenPlan(numels, 8, wave_mib=32, streams=1)
+    assert w1.n_waves == 4 and w1.ws_bytes < w2.ws_bytes
+    big = EdenPlan([1 << 25, 1 << 22], 8, wave_mib=16, streams=1)   # a slice above the wave size
+    assert big.n_waves == 2
+    with pytest.raises(_lib.CodecError, match="streams"):
+        EdenPlan(numels, 8, streams=3)
+
+
 def test_plan_errors():
     from openfl_amd import _lib
     from openfl_amd.codec import EdenPlan

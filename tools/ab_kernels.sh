@@ -7,7 +7,7 @@ set -e
 mkdir -p gpurun_out
 run() {
   local tag=$1
-  timeout -k 10 240 python bench.py --steps 4 --warmup 1 --no-cpu-baseline > gpurun_out/ab_$tag.json 2> gpurun_out/ab_$tag.err
+  timeout -k 10 240 python bench.py --steps 4 --warmup 1 --no-cpu-baseline --also "" ${AB_ARGS:-} > gpurun_out/ab_$tag.json 2> gpurun_out/ab_$tag.err
   python - "$tag" <<'PY'
 import json, sys
 tag = sys.argv[1]
@@ -23,6 +23,6 @@ for v in "$@"; do
   if [[ "$v" == *.so ]]; then
     OFL_CODEC_LIB=$v run "$(basename $v .so)"
   else
-    env "$v" bash -c "$(declare -f run); run '${v//[^A-Za-z0-9_]/_}'"
+    env $v bash -c "$(declare -f run); run '${v//[^A-Za-z0-9_]/_}'"
   fi
 done
