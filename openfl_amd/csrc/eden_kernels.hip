@@ -1302,6 +1302,132 @@ __global__ __launch_bounds__(kColNT) void k_col(KArgs a) {
 }
 
 // ===========================================================================
+// Column passes for M = 6..10 rows: 512 threads x 64 registers.  L1 keeps
+// rows r0..r5 in registers, L2 rows r(M-6)..r(M-1) with r5 last (register
+// index 5 in both layouts).  Lanes 0..31 sit on 32 consecutive columns in
+// both layouts, so the LDS exchange needs no padding to be conflict-free, and
+// it runs in two halves (r5 = 0, then 1) through a 2^14-float buffer: 68 KiB
+// of LDS per block, two blocks per CU (one loads while the other computes).
+// Tile I/O through a buffer resource over the slice's intermediate: the row
+// part of every register's address is a scalar offset.
+// ===========================================================================
+constexpr int kCol6NT = 512;
+constexpr int kHalfLog = kColLog - 1;
+constexpr size_t kCol6Half = sizeof(float) << kHalfLog;
+template <int M> struct Col6Set {
+    static_assert(M >= 6 && M <= 10, "Col6Set: 6 <= M <= 10");
+    static constexpr int K = kColLog - M;
+    static constexpr int row2(int i) { return (M - 6 + i) + ((M - 6 + i) >= 5 ? 1 : 0); }  // i < 5
+    static constexpr Lay L1{kColLog, K, K + 1, K + 2, K + 3, K + 4, K + 5};
+    static constexpr Lay L2{kColLog, K + row2(0), K + row2(1), K + row2(2), K + row2(3), K + row2(4), K + 5};
+    static constexpr uint32_t A1 = 63u << K;
+    static constexpr uint32_t A2 = M > 6 ? ((1u << (M - 6)) - 1u) << (K + 6) : 0u;
+    static constexpr int HB = K + 5;  // the half bit (row r5)
+};
+// drop tile bit HB from an index (additive over disjoint bit sets)
+template <int HB>
+DEVI constexpr uint32_t cidx(uint32_t e) { return (e & ((1u << HB) - 1u)) | ((e >> (HB + 1)) << HB); }
+
+template <Lay A, Lay B, int HB>
+DEVI void exchange_half(float (&v)[64], float* s, uint32_t tid) {
+    static_assert(LT<A>::rb(5) == HB && LT<B>::rb(5) == HB, "half bit must be register bit 5 of both layouts");
+    const uint32_t ba = opaque(cidx<HB>(LT<A>::base(tid)));
+    const uint32_t bb = opaque(cidx<HB>(LT<B>::base(tid)));
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int r = 32 * h; r < 32 * h + 32; ++r) s[ba + cidx<HB>(LT<A>::off(r))] = v[r];
+        __syncthreads();
+#pragma unroll
+        for (int r = 32 * h; r < 32 * h + 32; ++r) v[r] = s[bb + cidx<HB>(LT<B>::off(r))];
+        __syncthreads();
+    }
+}
+
+template <int M, bool MID>
+__global__ __launch_bounds__(kCol6NT, 4) void k_col6(KArgs a) {
+    using CS = Col6Set<M>;
+    constexpr int K = CS::K;
+    constexpr bool EXCH = M > 6;
+    constexpr Lay LC = EXCH ? CS::L2 : CS::L1;  // layout after the first Hadamard part
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float* s = reinterpret_cast<float*>(smem);
+    uint8_t* tab = smem + (EXCH ? kCol6Half : 0);
+    int si; uint32_t tile;
+    find_tile(a, si, tile);
+    const SliceDesc D = udesc(a.d, si);
+    const uint32_t tid = threadIdx.x;
+    const int lo = a.lo;
+    // tile -> slice bits: [K, lo) from tile low bits, [lo+M, p) from the rest
+    const uint32_t tl = tile & ((1u << (lo - K)) - 1u);
+    const uint32_t th = tile >> (lo - K);
+    const uint32_t tb = (tl << K) | (th << (lo + M));
+    auto map = [&](uint32_t t) -> uint32_t { return tb | (t & ((1u << K) - 1u)) | ((t >> K) << lo); };
+    const rsrc_t rw = mk_rsrc(a.ws + D.ws_off, (uint32_t)(4ull << D.logp));
+    constexpr uint32_t kTabMask = (1u << (kColLog - 3)) - 1u;
+    if constexpr (MID) {  // D2 sign bytes of the tile's 2^12 rand_diag words (see k_col)
+        const uint32_t b2 = seed_b(sld(a.seeds, D.tensor) + 1u);
+        for (uint32_t q = tid; q < (1u << (kColLog - 3)); q += kCol6NT)
+            tab[q] = (uint8_t)rd_byte(map(q) & ((1u << (D.logp - 3)) - 1u), b2);
+    }
+    float v[64];
+    const uint32_t base1 = LT<CS::L1>::base(tid);
+    {
+        const uint32_t vo = opaque(map(base1) * 4u);
+#pragma unroll
+        for (int r = 0; r < 64; ++r)
+            v[r] = raw_load_f32(rw, (int)vo, (int)uu((LT<CS::L1>::off(r) >> K) << lo) * 4, 0);
+    }
+    stages<CS::L1, CS::A1>(v);
+    if constexpr (EXCH) {
+        exchange_half<CS::L1, CS::L2, CS::HB>(v, s, tid);  // its barriers also publish tab
+        stages<CS::L2, CS::A2>(v);
+    } else if constexpr (MID) {
+        __syncthreads();
+    }
+    if constexpr (MID) {
+        const float m2 = pow2i(-(D.logp / 2));
+        // the tile's top 3 bits (the sign's nibble index) are register bits of
+        // LC, so each register's shift is a constant and its table offset an
+        // immediate
+        static_assert((LT<LC>::rmask() >> (kColLog - 3)) == 7u, "top 3 tile bits must be register bits");
+        const uint32_t bt = opaque(LT<LC>::base(tid) & kTabMask);
+#pragma unroll
+        for (int r = 0; r < 64; ++r) {
+            const uint32_t o = LT<LC>::off(r);
+            v[r] = flip_unless(v[r] * m2, ((uint32_t)tab[bt + (o & kTabMask)] >> (o >> (kColLog - 3))) & 1u);
+        }
+        if constexpr (EXCH) {
+            stages<CS::L2, CS::A2>(v);
+            exchange_half<CS::L2, CS::L1, CS::HB>(v, s, tid);
+        }
+        stages<CS::L1, CS::A1>(v);
+        const uint32_t vo = opaque(map(base1) * 4u);
+        int los = lo;
+        asm volatile("" : "+s"(los));  // recompute the row offsets: 64 SGPRs kept live would spill
+#pragma unroll
+        for (int r = 0; r < 64; ++r)
+            raw_store_f32(v[r], rw, (int)vo, (int)uu((LT<CS::L1>::off(r) >> K) << los) * 4, 0);
+    } else {
+        const uint32_t bcw = LT<LC>::base(tid);
+        const uint32_t vo = opaque(map(bcw) * 4u);
+        int los = lo;
+        asm volatile("" : "+s"(los));
+#pragma unroll
+        for (int r = 0; r < 64; ++r)
+            raw_store_f32(v[r], rw, (int)vo, (int)uu((LT<LC>::off(r) >> K) << los) * 4, 0);
+    }
+    if (a.do_nu && tile == 0) {  // slice norm, as in k_col
+        __shared__ float nred[kCol6NT / 64];
+        const int64_t ntile = 1ll << (D.logp - kRowLog);
+        float ss = 0.f;
+        for (int64_t t = tid; t < ntile; t += kCol6NT) ss += a.part[D.part_off + t];
+        ss = block_sum<kCol6NT>(ss, nred);
+        if (tid == 0) a.nu[si] = sqrtf(ss);
+    }
+}
+
+// ===========================================================================
 // Per-slice scales (large slices), after every final row pass.
 // ===========================================================================
 
@@ -1437,6 +1563,22 @@ hipError_t set_col_attr() {
     return e != hipSuccess ? e : set_lds((const void*)ofl::k_col<M, false>, col_smem(M, false));
 }
 
+size_t col6_smem(int M, bool mid) { return (M > 6 ? ofl::kCol6Half : 0) + (mid ? ofl::kColTab : 0); }
+
+template <int M>
+hipError_t set_col6_attr() {
+    hipError_t e = set_lds((const void*)ofl::k_col6<M, true>, col6_smem(M, true));
+    return e != hipSuccess ? e : set_lds((const void*)ofl::k_col6<M, false>, col6_smem(M, false));
+}
+
+// column passes with M >= 8 rows, or a middle pass with M >= 6, use k_col6
+// (measured: the 1024-thread k_col is ~4 % faster on the plain M = 7 pass);
+// OFL_EDEN_COL6=0 forces k_col everywhere (A/B)
+bool use_col6() {
+    static const bool on = [] { const char* s = getenv("OFL_EDEN_COL6"); return !(s && s[0] == '0'); }();
+    return on;
+}
+
 hipError_t set_all_attrs() {
     hipError_t e;
     if ((e = set_small_attr<11>()) != hipSuccess) return e;
@@ -1453,7 +1595,12 @@ hipError_t set_all_attrs() {
     if ((e = set_col_attr<7>()) != hipSuccess) return e;
     if ((e = set_col_attr<8>()) != hipSuccess) return e;
     if ((e = set_col_attr<9>()) != hipSuccess) return e;
-    return set_col_attr<10>();
+    if ((e = set_col_attr<10>()) != hipSuccess) return e;
+    if ((e = set_col6_attr<6>()) != hipSuccess) return e;
+    if ((e = set_col6_attr<7>()) != hipSuccess) return e;
+    if ((e = set_col6_attr<8>()) != hipSuccess) return e;
+    if ((e = set_col6_attr<9>()) != hipSuccess) return e;
+    return set_col6_attr<10>();
 }
 
 int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller) {
@@ -1534,6 +1681,20 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
             break;
         }
         case K_COL: {
+            if ((l.param >= 8 || (l.param >= 6 && l.mid)) && use_col6()) {
+                const size_t sm = col6_smem(l.param, l.mid != 0);
+#define COL6CASE(MM)                                                                                 \
+    case MM:                                                                                         \
+        e = l.mid ? launch(ofl::k_col6<MM, true>, l.blocks, ofl::kCol6NT, sm, st, a)                 \
+                  : launch(ofl::k_col6<MM, false>, l.blocks, ofl::kCol6NT, sm, st, a);               \
+        break;
+                switch (l.param) {
+                    COL6CASE(6) COL6CASE(7) COL6CASE(8) COL6CASE(9) COL6CASE(10)
+                default: return fail(OFL_EINVAL, "column pass height out of range");
+                }
+#undef COL6CASE
+                break;
+            }
             const size_t sm = col_smem(l.param, l.mid != 0);
 #define COLCASE(MM)                                                                                  \
     case MM:                                                                                         \
@@ -1567,7 +1728,10 @@ std::string launch_name(const Launch& l, bool enc) {
     case K_SMALL: return std::string("ofl::k_") + d + "_small<" + std::to_string(l.param) + ">";
     case K_ROWA: return std::string("ofl::k_") + d + "_rowA";
     case K_ROWC: return std::string("ofl::k_") + d + "_rowC";
-    case K_COL: return "ofl::k_col<" + std::to_string(l.param) + ", " + (l.mid ? "true" : "false") + ">";
+    case K_COL:
+        return std::string((l.param >= 8 || (l.param >= 6 && l.mid)) && use_col6() ? "ofl::k_col6<" : "ofl::k_col<") +
+               std::to_string(l.param) +
+               ", " + (l.mid ? "true" : "false") + ">";
     default: return "ofl::k_finalize";
     }
 }
