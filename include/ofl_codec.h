@@ -88,7 +88,7 @@ void ofl_eden_plan_destroy(ofl_eden_plan_t plan);
  * gaps and tails; there are then at least two waves (the large slices split
  * in halves).  wave_bytes < 0 or streams == 0 keep the current value.  Only
  * before the plan's first encode/decode; the workspace size changes with it.
- * Default: 16 GiB waves, 2 streams (env OFL_EDEN_WAVE_MIB / OFL_EDEN_STREAMS
+ * Default: 2 GiB waves, 2 streams (env OFL_EDEN_WAVE_MIB / OFL_EDEN_STREAMS
  * override the default; DESIGN.md section 3.6 has the measurements). */
 int ofl_eden_plan_set_schedule(ofl_eden_plan_t plan, int64_t wave_bytes, int streams);
 int ofl_eden_plan_get_schedule(ofl_eden_plan_t plan, int64_t* wave_bytes, int* streams);

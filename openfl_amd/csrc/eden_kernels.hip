@@ -1521,7 +1521,7 @@ struct ofl_eden_plan {
 namespace {
 
 // Default large-slice schedule (see build_schedule).
-constexpr int64_t kDefaultWaveMiB = 16384;
+constexpr int64_t kDefaultWaveMiB = 2048;
 constexpr int64_t kDefaultStreams = 2;
 
 int64_t low_po2(int64_t n) { int64_t p = 1; while (p * 2 <= n) p *= 2; return n ? p : 0; }
