@@ -161,6 +161,22 @@ size_t ofl_lossy_workspace_bytes(int64_t n);
 int ofl_kmeans1d_fit(const float* x, int64_t n, int k, int n_init, uint64_t seed, int max_exact,
                      double* centres, int64_t* counts, double* inertia, void* ws, size_t ws_bytes,
                      void* stream);
+/* Batched, device-resident 1-D k-means (KmeansTransformer.forward for many
+ * tensors at once, kc_pipeline.py:47-63 / skc_pipeline.py:127-131): tensor t
+ * is x_arena[offsets[t], offsets[t] + numels[t]) (host arrays; numels[t] >= k).
+ * Per tensor: min/max, 4096-bin histogram, weighted k-means++ (2 + ln k local
+ * trials, n_init restarts) + Lloyd on the histogram, then up to max_exact + 1
+ * exact Lloyd passes over the data until the float32 midpoints stop moving.
+ * ranks_out (device, same layout, may be NULL): float32 rank of each element's
+ * cluster among np.unique(used centres as value dtype: float64 if value_f64,
+ * else float32) -- the GZIPTransformer input.  Host outputs (any may be NULL):
+ * centres / counts / uniq [ntensors * k] (sorted), inertia / nuniq [ntensors].
+ * Deterministic (integer atomics, fixed-order reductions); one sync at the end. */
+size_t ofl_kmeans1d_batch_workspace_bytes(int ntensors, const int64_t* numels);
+int ofl_kmeans1d_batch(int ntensors, const float* x_arena, const int64_t* offsets, const int64_t* numels, int k,
+                       int n_init, uint64_t seed, int max_exact, int value_f64, float* ranks_out, double* centres,
+                       int64_t* counts, double* inertia, int32_t* nuniq, double* uniq, void* ws, size_t ws_bytes,
+                       void* stream);
 int ofl_kmeans1d_label(const float* x, int64_t n, const double* centres, int k,
                        const float* rank_of_cluster, float* out, void* stream);
 int ofl_sparsify_topk(const float* x, int64_t n, int64_t k, float* sparse_out, float* kept_min,
@@ -172,6 +188,13 @@ int ofl_ternary_ranks(const float* sparse, int64_t n, float rank_neg, float rank
                       float* out, void* stream);
 int ofl_lut_decode(const float* in, int64_t n, const float* keys, const float* vals, int nk, float* out,
                    void* stream);
+/* ofl_lut_decode for many tensors of one arena in one launch: tensor t has
+ * nk[t] <= max_nk <= 64 keys at keys[t * max_nk ...] (host arrays, copied
+ * before the call returns); ws: ofl_lut_decode_batch_workspace_bytes(). */
+size_t ofl_lut_decode_batch_workspace_bytes(int ntensors, int max_nk);
+int ofl_lut_decode_batch(int ntensors, const float* in_arena, const int64_t* offsets, const int64_t* numels,
+                         const int32_t* nk, const float* keys, const float* vals, int max_nk, float* out_arena,
+                         void* ws, size_t ws_bytes, void* stream);
 
 /* ---- host helpers ----------------------------------------------------------
  * Left-to-right serial sums in the array's own precision: the

@@ -24,7 +24,9 @@ EXPORTS = (
     "ofl_eden_encode", "ofl_eden_decode", "ofl_eden_plan_profile", "ofl_eden_plan_num_launches",
     "ofl_eden_plan_launch_info", "ofl_eden_plan_profile_collect", "ofl_serial_sum_f32",
     "ofl_serial_sum_f64", "ofl_lossy_last_error", "ofl_lossy_workspace_bytes", "ofl_kmeans1d_fit",
+    "ofl_kmeans1d_batch_workspace_bytes", "ofl_kmeans1d_batch",
     "ofl_kmeans1d_label", "ofl_sparsify_topk", "ofl_ternary_stats", "ofl_ternary_ranks", "ofl_lut_decode",
+    "ofl_lut_decode_batch_workspace_bytes", "ofl_lut_decode_batch",
 )
 
 
@@ -72,6 +74,11 @@ def _bind(L):
     L.ofl_lossy_workspace_bytes.restype = sz
     L.ofl_kmeans1d_fit.argtypes = [vp, i64, i32, i32, ctypes.c_uint64, i32, vp, vp, vp, vp, sz, vp]
     L.ofl_kmeans1d_fit.restype = i32
+    L.ofl_kmeans1d_batch_workspace_bytes.argtypes = [i32, vp]
+    L.ofl_kmeans1d_batch_workspace_bytes.restype = sz
+    L.ofl_kmeans1d_batch.argtypes = [i32, vp, vp, vp, i32, i32, ctypes.c_uint64, i32, i32, vp, vp, vp, vp, vp,
+                                     vp, vp, sz, vp]
+    L.ofl_kmeans1d_batch.restype = i32
     L.ofl_kmeans1d_label.argtypes = [vp, i64, vp, i32, vp, vp, vp]
     L.ofl_kmeans1d_label.restype = i32
     L.ofl_sparsify_topk.argtypes = [vp, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp]
@@ -82,6 +89,10 @@ def _bind(L):
     L.ofl_ternary_ranks.restype = i32
     L.ofl_lut_decode.argtypes = [vp, i64, vp, vp, i32, vp, vp]
     L.ofl_lut_decode.restype = i32
+    L.ofl_lut_decode_batch_workspace_bytes.argtypes = [i32, i32]
+    L.ofl_lut_decode_batch_workspace_bytes.restype = sz
+    L.ofl_lut_decode_batch.argtypes = [i32, vp, vp, vp, vp, vp, vp, i32, vp, vp, sz, vp]
+    L.ofl_lut_decode_batch.restype = i32
     L.ofl_serial_sum_f32.argtypes = [vp, i64]
     L.ofl_serial_sum_f32.restype = ctypes.c_float
     L.ofl_serial_sum_f64.argtypes = [vp, i64]

@@ -17,6 +17,7 @@
 #include <cstdint>
 #include <cstring>
 #include <limits>
+#include <mutex>
 #include <random>
 #include <string>
 #include <vector>
@@ -28,7 +29,6 @@
 namespace lossy {
 
 constexpr int kNT = 256;
-constexpr int kHistBins = 4096;   // k-means histogram resolution
 constexpr int kRadixBits = 11;    // radix-select digit
 constexpr int kRadix = 1 << kRadixBits;
 constexpr int kMaxK = 32;         // clusters supported
@@ -58,35 +58,6 @@ DEVI uint32_t fkey(float f) {
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
-// ---- min / max (NaN-free input assumed by callers; NaN propagates as max) --
-__global__ __launch_bounds__(kNT) void k_minmax(const float* x, int64_t n, uint32_t* out) {
-    float lo = INFINITY, hi = -INFINITY;
-    for (int64_t i = gtid(); i < n; i += gstride()) { const float v = x[i]; lo = fminf(lo, v); hi = fmaxf(hi, v); }
-    lo = wave_min(lo);
-    hi = wave_max(hi);
-    if ((threadIdx.x & 63) == 0) { atomicMin(&out[0], fkey(lo)); atomicMax(&out[1], fkey(hi)); }
-}
-
-// ---- value histogram: count + fp64 sum per bin over [lo, lo + nb/inv_w) ----
-__global__ __launch_bounds__(kNT) void k_hist(const float* x, int64_t n, float lo, float inv_w,
-                                              unsigned long long* cnt, double* sum) {
-    __shared__ unsigned int c[kHistBins];
-    __shared__ double s[kHistBins];
-    for (int b = threadIdx.x; b < kHistBins; b += kNT) { c[b] = 0; s[b] = 0.0; }
-    __syncthreads();
-    for (int64_t i = gtid(); i < n; i += gstride()) {
-        const float v = x[i];
-        int b = (int)((v - lo) * inv_w);
-        b = b < 0 ? 0 : (b >= kHistBins ? kHistBins - 1 : b);
-        atomicAdd(&c[b], 1u);
-        atomicAdd(&s[b], (double)v);
-    }
-    __syncthreads();
-    for (int b = threadIdx.x; b < kHistBins; b += kNT) {
-        if (c[b]) { atomicAdd(&cnt[b], (unsigned long long)c[b]); atomicAdd(&sum[b], s[b]); }
-    }
-}
-
 struct KmParams {
     float mids[kMaxK];       // sorted midpoints between consecutive sorted centres (k-1 used)
     float rank[kMaxK];       // label value to write per cluster (float32 rank)
@@ -97,28 +68,6 @@ DEVI int cluster_of(float v, const KmParams& p) {
 #pragma unroll
     for (int j = 0; j < kMaxK - 1; ++j) c += (j < p.k - 1 && p.mids[j] < v) ? 1 : 0;
     return c;
-}
-
-// ---- exact Lloyd statistics: per-cluster count, fp64 sum and sum of squares --
-__global__ __launch_bounds__(kNT) void k_km_accum(const float* x, int64_t n, KmParams p,
-                                                  unsigned long long* cnt, double* sum, double* sq) {
-    __shared__ unsigned int c[kMaxK];
-    __shared__ double s[kMaxK], q[kMaxK];
-    if (threadIdx.x < kMaxK) { c[threadIdx.x] = 0; s[threadIdx.x] = 0.0; q[threadIdx.x] = 0.0; }
-    __syncthreads();
-    for (int64_t i = gtid(); i < n; i += gstride()) {
-        const float v = x[i];
-        const int k = cluster_of(v, p);
-        atomicAdd(&c[k], 1u);
-        atomicAdd(&s[k], (double)v);
-        atomicAdd(&q[k], (double)v * (double)v);
-    }
-    __syncthreads();
-    if (threadIdx.x < p.k && c[threadIdx.x]) {
-        atomicAdd(&cnt[threadIdx.x], (unsigned long long)c[threadIdx.x]);
-        atomicAdd(&sum[threadIdx.x], s[threadIdx.x]);
-        atomicAdd(&sq[threadIdx.x], q[threadIdx.x]);
-    }
 }
 
 // ---- labels -> float32 ranks -------------------------------------------------
@@ -261,6 +210,592 @@ __global__ __launch_bounds__(kNT) void k_lut(const float* in, int64_t n, LutPara
     }
 }
 
+
+// ===========================================================================
+// Batched 1-D k-means (KmeansTransformer.forward, kc_pipeline.py:47-63 and
+// skc_pipeline.py:127-131, for many tensors of one fp32 arena) entirely on the
+// device and deterministic (integer atomics and fixed-order reductions only):
+//   k_bkm_minmax  per-tensor min / max                              (1 pass)
+//   k_bkm_hist    per-tensor 4096-bin histogram: counts + fixed-point
+//                 sums of the position inside the bin               (1 pass)
+//   k_bkm_seed    one workgroup per (tensor, restart): weighted k-means++ with
+//                 sklearn's 2 + ln(k) local trials, then Lloyd on the bin
+//                 means through prefix sums (O(1) cluster edges); n_init
+//                 restarts, lowest inertia
+//   k_bkm_acc     exact Lloyd statistics on the data: per block, count /
+//                 sum / sum of squares above every float32 midpoint (1 pass)
+//   k_bkm_update  one wave per tensor: fixed-order sum of the block
+//                 partials, new centres; stops when the float32 midpoints
+//                 do not move or at sklearn's tolerance (then one more
+//                 assignment pass); then counts, inertia, np.unique ranks
+//   k_bkm_label   float32 rank of each element's cluster         (1 pass)
+// A block covers kBkmChunk consecutive elements of one tensor.
+// ===========================================================================
+constexpr int kBkmChunk = 1 << 16;
+constexpr int kBkmBins = 4096;
+constexpr int kBkmMaxInit = 16;  // k-means++ restarts (n_init), one workgroup each
+
+struct BkmTensor { int64_t off; int64_t n; int32_t blk0; int32_t nblk; };
+struct BkmState {
+    uint32_t mm[2];          // ~key(min), key(max): both reduced by atomicMax from 0
+    int32_t converged;       // 0 running, 2 final assignment pass pending, 1 done
+    int32_t nuniq;
+    double cen[kMaxK];       // sorted centres
+    float mids[kMaxK];       // float32 midpoints of consecutive centres (+inf beyond k-1)
+    float rank[kMaxK];       // float32 rank of each cluster's value
+    double uniq[kMaxK];      // sorted distinct values of the used centres (value dtype)
+    long long cnt[kMaxK];
+    double inertia;
+    double cand[kBkmMaxInit][kMaxK];  // sorted centres of each restart
+    double cand_in[kBkmMaxInit];      // and its inertia on the histogram
+};
+struct BkmArgs {
+    const float* x;
+    float* out;
+    const BkmTensor* td;
+    int32_t ntensors;
+    int32_t k;
+    int32_t n_init;
+    int32_t value_f64;       // centre values as float64 (else rounded to float32)
+    int32_t final_pass;
+    int32_t pad_;
+    uint64_t seed;
+    BkmState* st;
+    uint32_t* hc;            // [T][4096] counts
+    unsigned long long* hs;  // [T][4096] sums of (position inside the bin) * 2^32
+    double* part;            // [blocks][3][kMaxK] cumulative partials
+};
+
+DEVI int bkm_tensor(const BkmArgs& a, int b) {
+    int lo = 0, hi = a.ntensors - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (a.td[mid].blk0 <= b) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+// this block's tensor and element range
+DEVI void bkm_range(const BkmArgs& a, int& t, int64_t& i0, int64_t& i1) {
+    t = bkm_tensor(a, (int)blockIdx.x);
+    const BkmTensor T = a.td[t];
+    i0 = (int64_t)(blockIdx.x - T.blk0) * kBkmChunk;
+    i1 = i0 + kBkmChunk < T.n ? i0 + kBkmChunk : T.n;
+}
+// f(v) for every element of p[i0, i1): 16-B loads over the aligned middle
+template <int NT = kNT, typename F>
+DEVI void bkm_visit(const float* p, int64_t i0, int64_t i1, F f) {
+    int64_t a4 = i0;
+    while (a4 < i1 && (reinterpret_cast<uintptr_t>(p + a4) & 15u)) ++a4;
+    for (int64_t j = i0 + threadIdx.x; j < a4; j += NT) f(p[j]);
+    const int64_t n4 = (i1 - a4) >> 2;
+    const float4* q = reinterpret_cast<const float4*>(p + a4);
+    for (int64_t j = threadIdx.x; j < n4; j += NT) {
+        const float4 v = q[j];
+        f(v.x); f(v.y); f(v.z); f(v.w);
+    }
+    for (int64_t j = a4 + 4 * n4 + threadIdx.x; j < i1; j += NT) f(p[j]);
+}
+
+__global__ __launch_bounds__(kNT) void k_bkm_minmax(BkmArgs a) {
+    __shared__ float rlo[kNT / 64], rhi[kNT / 64];
+    int t; int64_t i0, i1;
+    bkm_range(a, t, i0, i1);
+    float lo = INFINITY, hi = -INFINITY;
+    bkm_visit(a.x + a.td[t].off, i0, i1, [&](float v) { lo = fminf(lo, v); hi = fmaxf(hi, v); });
+    lo = wave_min(lo);
+    hi = wave_max(hi);
+    if ((threadIdx.x & 63) == 0) { rlo[threadIdx.x >> 6] = lo; rhi[threadIdx.x >> 6] = hi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 0; w < kNT / 64; ++w) { lo = fminf(lo, rlo[w]); hi = fmaxf(hi, rhi[w]); }
+        atomicMax(&a.st[t].mm[0], ~fkey(lo));
+        atomicMax(&a.st[t].mm[1], fkey(hi));
+    }
+}
+DEVI float bkm_unkey(uint32_t k) { return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k); }
+DEVI void bkm_bounds(const BkmState& S, float& lo, float& hi, float& inv_w) {
+    lo = bkm_unkey(~S.mm[0]);
+    hi = bkm_unkey(S.mm[1]);
+    inv_w = hi > lo ? (float)((double)kBkmBins / ((double)hi - (double)lo) * (1.0 - 1e-7)) : 0.0f;
+}
+
+__global__ __launch_bounds__(kNT) void k_bkm_hist(BkmArgs a) {
+    __shared__ uint32_t c[kBkmBins];
+    __shared__ unsigned long long sfx[kBkmBins];
+    for (int b = threadIdx.x; b < kBkmBins; b += kNT) { c[b] = 0; sfx[b] = 0; }
+    int t; int64_t i0, i1;
+    bkm_range(a, t, i0, i1);
+    float lo, hi, inv_w;
+    bkm_bounds(a.st[t], lo, hi, inv_w);
+    __syncthreads();
+    bkm_visit(a.x + a.td[t].off, i0, i1, [&](float v) {
+        const float f = (v - lo) * inv_w;
+        int b = (int)f;
+        b = b < 0 ? 0 : (b >= kBkmBins ? kBkmBins - 1 : b);
+        float fr = f - (float)b;
+        fr = fr < 0.f ? 0.f : (fr < 1.f ? fr : 0.99999994f);
+        atomicAdd(&c[b], 1u);
+        atomicAdd(&sfx[b], (unsigned long long)(fr * 4294967296.0f));
+    });
+    __syncthreads();
+    uint32_t* hc = a.hc + (int64_t)t * kBkmBins;
+    unsigned long long* hs = a.hs + (int64_t)t * kBkmBins;
+    for (int b = threadIdx.x; b < kBkmBins; b += kNT)
+        if (c[b]) { atomicAdd(&hc[b], c[b]); atomicAdd(&hs[b], sfx[b]); }
+}
+
+DEVI uint64_t bkm_rng(uint64_t& s) {  // xorshift64*
+    s ^= s >> 12; s ^= s << 25; s ^= s >> 27;
+    return s * 0x2545F4914F6CDD1Dull;
+}
+DEVI double bkm_uniform(uint64_t& s) { return (double)(bkm_rng(s) >> 11) * (1.0 / 9007199254740992.0); }
+// first i in [0, n) with P[i] > u for an inclusive prefix P (last index if none)
+template <typename T>
+DEVI int bkm_first_above(const T* P, int n, double u) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((double)P[mid] > u) hi = mid; else lo = mid + 1;
+    }
+    return lo;
+}
+// first i in [0, n] with pts[i] > m (pts ascending)
+DEVI int bkm_upper(const float* pts, int n, double m) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((double)pts[mid] > m) hi = mid; else lo = mid + 1;
+    }
+    return lo;
+}
+DEVI void bkm_set_centres(BkmState& S, const double* c, int k) {
+    for (int j = 0; j < kMaxK; ++j) S.cen[j] = j < k ? c[j] : c[k - 1];
+    for (int j = 0; j < kMaxK; ++j) S.mids[j] = j + 1 < k ? (float)((c[j] + c[j + 1]) / 2) : INFINITY;
+}
+
+// one workgroup per tensor: k-means of the weighted histogram points
+// inclusive wave scan of one double per lane; total = the whole wave's sum
+DEVI double wscan(double v, double& total) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double u = __shfl_up(v, o, 64);
+        if (lane >= o) v += u;
+    }
+    total = __shfl(v, 63, 64);
+    return v;
+}
+// block (256 threads) sum / inclusive scan of one double per thread; fixed order
+DEVI double bkm_bsum(double v, double* tmp) {
+    v = wave_sum(v);
+    if ((threadIdx.x & 63) == 0) tmp[threadIdx.x >> 6] = v;
+    __syncthreads();
+    const double s = (tmp[0] + tmp[1]) + (tmp[2] + tmp[3]);
+    __syncthreads();
+    return s;
+}
+DEVI double bkm_bscan(double v, double* tmp, double& total) {
+    double t;
+    v = wscan(v, t);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) tmp[w] = t;
+    __syncthreads();
+    double off = 0.0;
+    for (int j = 0; j < w; ++j) off += tmp[j];
+    total = (tmp[0] + tmp[1]) + (tmp[2] + tmp[3]);
+    __syncthreads();
+    return off + v;
+}
+
+// One workgroup per (tensor, restart): k-means of the 4096 histogram points (bin means,
+// weight = count; empty bins keep their centre with weight 0, so the points
+// stay sorted and the cluster edge of a midpoint m is found in O(1) from
+// (m - lo) * inv_w).  Weighted k-means++ with sklearn's local trials, then
+// Lloyd through prefix sums (lane j of wave 0 owns cluster j) to sklearn's
+// tolerance.  k_bkm_pick keeps the restart with the lowest histogram inertia.
+constexpr int kBkmSeedNT = 256;
+constexpr size_t kBkmSeedLds = 4 * sizeof(float) * kBkmBins + 2 * sizeof(double) * kBkmBins;  // 128 KiB
+__global__ __launch_bounds__(kBkmSeedNT) void k_bkm_seed(BkmArgs a) {
+    static_assert(kBkmSeedNT == 256, "bkm_bsum/bkm_bscan assume 4 waves");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    double* W = reinterpret_cast<double*>(smem);
+    double* S1 = W + kBkmBins;
+    float* pts = reinterpret_cast<float*>(S1 + kBkmBins);
+    float* wts = pts + kBkmBins;
+    float* d2 = wts + kBkmBins;
+    float* C = d2 + kBkmBins;
+    __shared__ double tmp[4];
+    __shared__ double cc[kMaxK];
+    const int t = blockIdx.x / a.n_init, run = blockIdx.x % a.n_init;
+    BkmState& S = a.st[t];
+    const int k = a.k;
+    auto emit = [&](double in) {  // this restart's result (thread 0)
+        for (int j = 0; j < k; ++j) S.cand[run][j] = cc[j];
+        S.cand_in[run] = in;
+    };
+    float lo, hi, inv_w;
+    bkm_bounds(S, lo, hi, inv_w);
+    if (!(hi > lo)) {  // constant (or non-finite: reported by the host) tensor
+        if (threadIdx.x == 0) {
+            for (int j = 0; j < k; ++j) cc[j] = lo;
+            emit(0.0);
+        }
+        return;
+    }
+    constexpr int PER = kBkmBins / kBkmSeedNT;  // 16 consecutive bins per thread
+    const int i0 = threadIdx.x * PER;
+    const uint32_t* hc = a.hc + (int64_t)t * kBkmBins;
+    const unsigned long long* hs = a.hs + (int64_t)t * kBkmBins;
+    const double width = 1.0 / (double)inv_w;
+    int occ = 0;
+    double w0 = 0.0, s0 = 0.0, q0 = 0.0;
+    for (int q = 0; q < PER; ++q) {
+        const int b = i0 + q;
+        const uint32_t cn = hc[b];
+        const double fr = cn ? (double)hs[b] / 4294967296.0 / (double)cn : 0.5;
+        const float p = (float)((double)lo + ((double)b + fr) * width);
+        pts[b] = p;
+        wts[b] = (float)cn;
+        occ += cn ? 1 : 0;
+        w0 += cn;
+        s0 += (double)cn * p;
+        q0 += (double)cn * p * p;
+    }
+    double tw, ts;
+    double ew = bkm_bscan(w0, tmp, tw) - w0;
+    double es = bkm_bscan(s0, tmp, ts) - s0;
+    for (int q = 0; q < PER; ++q) { ew += wts[i0 + q]; es += (double)wts[i0 + q] * pts[i0 + q]; W[i0 + q] = ew; S1[i0 + q] = es; }
+    const int nocc = (int)bkm_bsum((double)occ, tmp);
+    const double sq = bkm_bsum(q0, tmp);  // (also publishes pts / W / S1)
+    if (threadIdx.x == 0)  // rounding may break the order of neighbouring bin means
+        for (int i = 1; i < kBkmBins; ++i) if (pts[i] < pts[i - 1]) pts[i] = pts[i - 1];
+    __syncthreads();
+    if (nocc <= k) {  // no more occupied bins than clusters: they are the centres
+        if (threadIdx.x == 0) {
+            int j = 0;
+            for (int b = 0; b < kBkmBins && j < k; ++b) if (wts[b] > 0) cc[j++] = pts[b];
+            for (; j < k; ++j) cc[j] = cc[j - 1];
+            emit(0.0);
+        }
+        return;
+    }
+    const double wt = W[kBkmBins - 1];
+    const double mu = S1[kBkmBins - 1] / wt;
+    const double tol = 1e-4 * fmax(sq / wt - mu * mu, 0.0);  // sklearn's _tolerance
+    // first bin whose point lies above m (points sorted, each inside its bin)
+    auto edge = [&](double m) -> int {
+        int b = (int)floor((m - (double)lo) * (double)inv_w);
+        b = b < 0 ? 0 : (b > kBkmBins ? kBkmBins : b);
+        while (b > 0 && (double)pts[b - 1] > m) --b;
+        while (b < kBkmBins && (double)pts[b] <= m) ++b;
+        return b;
+    };
+    // every thread draws the same numbers
+    uint64_t rs = (a.seed ^ (0x9E3779B97F4A7C15ull * (uint64_t)(t + 1)) ^ (0xD1B54A32D192ED03ull * (uint64_t)(run + 1))) | 1ull;
+    for (int q = 0; q < 4; ++q) bkm_rng(rs);
+    const int trials = 2 + (int)log((double)k);  // sklearn's n_local_trials
+    {
+        // ---- weighted k-means++ ----
+        {
+            const int i = bkm_first_above(W, kBkmBins, bkm_uniform(rs) * wt);
+            const float c0 = pts[i];
+            if (threadIdx.x == 0) cc[0] = c0;
+            for (int q = 0; q < PER; ++q) { const float d = pts[i0 + q] - c0; d2[i0 + q] = d * d; }
+        }
+        for (int j = 1; j < k; ++j) {
+            double loc = 0.0;
+            for (int q = 0; q < PER; ++q) loc += (double)wts[i0 + q] * d2[i0 + q];
+            double pot;
+            double e = bkm_bscan(loc, tmp, pot) - loc;
+            for (int q = 0; q < PER; ++q) { e += (double)wts[i0 + q] * d2[i0 + q]; C[i0 + q] = (float)e; }
+            __syncthreads();
+            double bpot = INFINITY;
+            int bi = 0;
+            for (int tr = 0; tr < trials; ++tr) {
+                int ci = pot > 0.0 ? bkm_first_above(C, kBkmBins, bkm_uniform(rs) * pot)
+                                   : (int)(bkm_rng(rs) % (uint64_t)kBkmBins);
+                while (ci > 0 && wts[ci] == 0) --ci;  // (float rounding of C) never an empty bin
+                const float cv = pts[ci];
+                double np = 0.0;
+                for (int q = 0; q < PER; ++q) { const float d = pts[i0 + q] - cv; np += (double)wts[i0 + q] * fminf(d2[i0 + q], d * d); }
+                np = bkm_bsum(np, tmp);
+                if (np < bpot) { bpot = np; bi = ci; }
+            }
+            const float cv = pts[bi];
+            if (threadIdx.x == 0) cc[j] = cv;
+            for (int q = 0; q < PER; ++q) { const float d = pts[i0 + q] - cv; d2[i0 + q] = fminf(d2[i0 + q], d * d); }
+        }
+        __syncthreads();
+        // ---- Lloyd on the bin means, wave 0, lane j = cluster j ----
+        if (threadIdx.x == 0)
+            for (int i = 1; i < k; ++i) { const double v = cc[i]; int j = i - 1; while (j >= 0 && cc[j] > v) { cc[j + 1] = cc[j]; --j; } cc[j + 1] = v; }
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            const int lane = threadIdx.x;
+            double cj = lane < k ? cc[lane] : 0.0;
+            for (int it = 0; it < 300; ++it) {
+                const double cn = __shfl_down(cj, 1, 64);
+                const int end = lane + 1 < k ? edge((cj + cn) / 2) : kBkmBins;
+                int start = __shfl_up(end, 1, 64);
+                if (lane == 0) start = 0;
+                double nc = cj;
+                if (lane < k && end > start) {
+                    const double w = W[end - 1] - (start ? W[start - 1] : 0.0);
+                    const double sm = S1[end - 1] - (start ? S1[start - 1] : 0.0);
+                    if (w > 0) nc = sm / w;
+                }
+                const double shift = wave_sum(lane < k ? (nc - cj) * (nc - cj) : 0.0);
+                cj = nc;
+                // an empty cluster keeps its centre and may fall out of order
+                const double nx = __shfl_down(cj, 1, 64);
+                if (__any(lane + 1 < k && nx < cj)) {
+                    if (lane < k) cc[lane] = cj;
+                    if (lane == 0)
+                        for (int i = 1; i < k; ++i) { const double v = cc[i]; int j = i - 1; while (j >= 0 && cc[j] > v) { cc[j + 1] = cc[j]; --j; } cc[j + 1] = v; }
+                    if (lane < k) cj = cc[lane];
+                }
+                if (shift <= tol) break;
+            }
+            if (lane < k) cc[lane] = cj;
+        }
+        __syncthreads();
+        // ---- inertia of this run on the histogram ----
+        double in = 0.0;
+        for (int q = 0; q < PER; ++q) {
+            const double p = pts[i0 + q];
+            double bd = INFINITY;
+            for (int j = 0; j < k; ++j) { const double d = (p - cc[j]) * (p - cc[j]); bd = d < bd ? d : bd; }
+            in += (double)wts[i0 + q] * bd;
+        }
+        in = bkm_bsum(in, tmp);
+        if (threadIdx.x == 0) emit(in);
+    }
+}
+
+// the restart with the lowest histogram inertia (first on ties) seeds the exact passes
+__global__ __launch_bounds__(64) void k_bkm_pick(BkmArgs a) {
+    const int t = blockIdx.x * 64 + threadIdx.x;
+    if (t >= a.ntensors) return;
+    BkmState& S = a.st[t];
+    int b = 0;
+    for (int r = 1; r < a.n_init; ++r) if (S.cand_in[r] < S.cand_in[b]) b = r;
+    bkm_set_centres(S, S.cand[b], a.k);
+}
+
+// exact Lloyd statistics: per block, cumulative count / sum / sum of squares
+// above each of the KM1 midpoints (+ totals); float per thread, double across
+constexpr int kBkmAccNT = 1024;  // VALU-heavy per element: 16 waves per block
+template <int KM1>
+__global__ __launch_bounds__(kBkmAccNT) void k_bkm_acc(BkmArgs a) {
+    constexpr int NV = KM1 + 1;
+    __shared__ double red[kBkmAccNT / 64][3][NV];
+    int t; int64_t i0, i1;
+    bkm_range(a, t, i0, i1);
+    const BkmState& S = a.st[t];
+    if (S.converged == 1) return;
+    float m[KM1];
+#pragma unroll
+    for (int j = 0; j < KM1; ++j) m[j] = S.mids[j];
+    uint32_t n[NV];
+    float s[NV], q[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) { n[j] = 0; s[j] = 0.f; q[j] = 0.f; }
+    bkm_visit<kBkmAccNT>(a.x + a.td[t].off, i0, i1, [&](float v) {
+        const float vv = v * v;
+        n[0] += 1; s[0] += v; q[0] += vv;
+#pragma unroll
+        for (int j = 0; j < KM1; ++j) {
+            const bool g = v > m[j];
+            n[j + 1] += g ? 1u : 0u;
+            s[j + 1] += g ? v : 0.f;
+            q[j + 1] += g ? vv : 0.f;
+        }
+    });
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const double dn = wave_sum((double)n[j]), ds = wave_sum((double)s[j]), dq = wave_sum((double)q[j]);
+        if ((threadIdx.x & 63) == 0) { red[w][0][j] = dn; red[w][1][j] = ds; red[w][2][j] = dq; }
+    }
+    __syncthreads();
+    if (threadIdx.x < 3 * NV) {
+        const int r = threadIdx.x / NV, j = threadIdx.x % NV;
+        double acc = 0.0;
+        for (int ww = 0; ww < kBkmAccNT / 64; ++ww) acc += red[ww][r][j];
+        a.part[((int64_t)blockIdx.x * 3 + r) * kMaxK + j] = acc;
+    }
+}
+
+// one wave per tensor: new centres from the partials.  Lane l sums blocks
+// l, l+64, ... in order, then a fixed shuffle tree: deterministic.
+__global__ __launch_bounds__(64) void k_bkm_update(BkmArgs a) {
+    const int t = blockIdx.x;
+    BkmState& S = a.st[t];
+    if (S.converged == 1) return;
+    const BkmTensor T = a.td[t];
+    const int k = a.k;
+    __shared__ double g[3][kMaxK + 1];
+    for (int j = 0; j < k; ++j)
+        for (int r = 0; r < 3; ++r) {
+            double acc = 0.0;
+            for (int b = T.blk0 + (int)threadIdx.x; b < T.blk0 + T.nblk; b += 64)
+                acc += a.part[((int64_t)b * 3 + r) * kMaxK + j];
+            acc = wave_sum(acc);
+            if (threadIdx.x == 0) g[r][j] = acc;
+        }
+    if (threadIdx.x != 0) return;
+    double cg[kMaxK + 1], sg[kMaxK + 1], qg[kMaxK + 1];
+    for (int j = 0; j < k; ++j) { cg[j] = g[0][j]; sg[j] = g[1][j]; qg[j] = g[2][j]; }
+    cg[k] = 0.0; sg[k] = 0.0; qg[k] = 0.0;
+    // cluster j = (mid[j-1], mid[j]]: cumulative differences
+    double N[kMaxK], Sm[kMaxK], Q[kMaxK], nc[kMaxK];
+    for (int j = 0; j < k; ++j) {
+        N[j] = cg[j] - cg[j + 1];
+        Sm[j] = sg[j] - sg[j + 1];
+        Q[j] = qg[j] - qg[j + 1];
+        nc[j] = N[j] > 0 ? Sm[j] / N[j] : S.cen[j];
+    }
+    // sort the new centres with their statistics
+    for (int i = 1; i < k; ++i) {
+        const double v = nc[i], vn = N[i], vs = Sm[i], vq = Q[i];
+        int j = i - 1;
+        while (j >= 0 && nc[j] > v) { nc[j + 1] = nc[j]; N[j + 1] = N[j]; Sm[j + 1] = Sm[j]; Q[j + 1] = Q[j]; --j; }
+        nc[j + 1] = v; N[j + 1] = vn; Sm[j + 1] = vs; Q[j + 1] = vq;
+    }
+    bool same = true;
+    for (int j = 0; j + 1 < k; ++j) same = same && (float)((nc[j] + nc[j + 1]) / 2) == S.mids[j];
+    // sklearn's stopping rule: sum of squared centre shifts <= 1e-4 x the
+    // data variance; then one more assignment pass with the final centres
+    // (converged = 2) so that labels, counts and inertia belong to them
+    const double mean = sg[0] / cg[0];
+    const double tol = 1e-4 * fmax(qg[0] / cg[0] - mean * mean, 0.0);
+    double shift = 0.0;
+    for (int j = 0; j < k; ++j) shift += (nc[j] - S.cen[j]) * (nc[j] - S.cen[j]);
+    const bool pending = S.converged == 2;
+    if (!same && !pending && !a.final_pass) {
+        bkm_set_centres(S, nc, k);
+        if (shift <= tol) S.converged = 2;
+        return;
+    }
+    // final: counts and inertia of the assignment this pass was made with
+    double in = 0.0;
+    if (same && !pending) {  // strict convergence: centres = means of the unchanged clusters
+        for (int j = 0; j < k; ++j) if (N[j] > 0) in += Q[j] - Sm[j] * Sm[j] / N[j];
+        bkm_set_centres(S, nc, k);
+    } else {  // keep the centres the assignment was made with
+        for (int j = 0; j < k; ++j) {  // (statistics above are sorted by new centre: redo by cluster)
+            const double c = S.cen[j];
+            N[j] = cg[j] - cg[j + 1]; Sm[j] = sg[j] - sg[j + 1]; Q[j] = qg[j] - qg[j + 1];
+            in += Q[j] - 2 * c * Sm[j] + c * c * N[j];
+        }
+    }
+    S.inertia = in > 0 ? in : 0.0;
+    // np.unique over the used centres (value dtype) and each cluster's rank
+    double vals[kMaxK], uq[kMaxK];
+    int nu = 0;
+    for (int j = 0; j < k; ++j) {
+        vals[j] = a.value_f64 ? S.cen[j] : (double)(float)S.cen[j];
+        S.cnt[j] = (long long)(N[j] + 0.5);
+    }
+    for (int j = 0; j < k; ++j) {
+        if (S.cnt[j] <= 0) continue;
+        bool dup = false;
+        for (int i = 0; i < nu; ++i) dup = dup || uq[i] == vals[j];
+        if (!dup) uq[nu++] = vals[j];
+    }
+    for (int i = 1; i < nu; ++i) { const double v = uq[i]; int j = i - 1; while (j >= 0 && uq[j] > v) { uq[j + 1] = uq[j]; --j; } uq[j + 1] = v; }
+    for (int j = 0; j < k; ++j) {
+        int r = 0;
+        while (r < nu && uq[r] < vals[j]) ++r;
+        S.rank[j] = (float)r;
+    }
+    for (int i = 0; i < kMaxK; ++i) S.uniq[i] = i < nu ? uq[i] : 0.0;
+    S.nuniq = nu;
+    S.converged = 1;
+}
+
+template <int KM1>
+__global__ __launch_bounds__(kBkmAccNT) void k_bkm_label(BkmArgs a) {
+    int t; int64_t i0, i1;
+    bkm_range(a, t, i0, i1);
+    const BkmState& S = a.st[t];
+    float m[KM1], r[KM1 + 1];
+#pragma unroll
+    for (int j = 0; j < KM1; ++j) m[j] = S.mids[j];
+#pragma unroll
+    for (int j = 0; j <= KM1; ++j) r[j] = S.rank[j < a.k ? j : a.k - 1];
+    const float* x = a.x + a.td[t].off;
+    float* out = a.out + a.td[t].off;
+    auto rank_of = [&](float v) {
+        float o = r[0];
+#pragma unroll
+        for (int j = 0; j < KM1; ++j) o = v > m[j] ? r[j + 1] : o;
+        return o;
+    };
+    // x and out share the arena offset, so they are 16-B aligned together
+    int64_t a4 = i0;
+    while (a4 < i1 && (reinterpret_cast<uintptr_t>(x + a4) & 15u)) ++a4;
+    for (int64_t i = i0 + threadIdx.x; i < a4; i += kBkmAccNT) out[i] = rank_of(x[i]);
+    const int64_t n4 = (i1 - a4) >> 2;
+    const float4* x4 = reinterpret_cast<const float4*>(x + a4);
+    float4* o4 = reinterpret_cast<float4*>(out + a4);
+    for (int64_t i = threadIdx.x; i < n4; i += kBkmAccNT) {
+        const float4 v = x4[i];
+        o4[i] = make_float4(rank_of(v.x), rank_of(v.y), rank_of(v.z), rank_of(v.w));
+    }
+    for (int64_t i = a4 + 4 * n4 + threadIdx.x; i < i1; i += kBkmAccNT) out[i] = rank_of(x[i]);
+}
+
+
+// Batched reference backward (kc_pipeline.py:79-83 per tensor): tensor t's
+// float32 ranks -> values by the sequential in-place key->value replacement,
+// one launch for the whole arena (blocks as in the k-means passes).
+struct LutBatchArgs {
+    const float* in;
+    float* out;
+    const BkmTensor* td;
+    const int32_t* nk;     // [T]
+    const float* keys;     // [T][max_nk]
+    const float* vals;     // [T][max_nk]
+    int32_t ntensors;
+    int32_t max_nk;
+};
+__global__ __launch_bounds__(kNT) void k_lut_batch(LutBatchArgs a) {
+    __shared__ float ks[64], vs[64];
+    int lo = 0, hi = a.ntensors - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (a.td[mid].blk0 <= (int)blockIdx.x) lo = mid; else hi = mid - 1;
+    }
+    const int t = lo;
+    const BkmTensor T = a.td[t];
+    const int nk = a.nk[t];
+    if (threadIdx.x < nk) {
+        ks[threadIdx.x] = a.keys[(int64_t)t * a.max_nk + threadIdx.x];
+        vs[threadIdx.x] = a.vals[(int64_t)t * a.max_nk + threadIdx.x];
+    }
+    __syncthreads();
+    const int64_t i0 = (int64_t)(blockIdx.x - T.blk0) * kBkmChunk;
+    const int64_t i1 = i0 + kBkmChunk < T.n ? i0 + kBkmChunk : T.n;
+    const float* x = a.in + T.off;
+    float* y = a.out + T.off;
+    auto lut = [&](float v) {
+        for (int j = 0; j < nk; ++j) v = (v == ks[j]) ? vs[j] : v;
+        return v;
+    };
+    if (((reinterpret_cast<uintptr_t>(x + i0) | reinterpret_cast<uintptr_t>(y + i0)) & 15u) == 0) {
+        const int64_t n4 = (i1 - i0) >> 2;
+        const float4* x4 = reinterpret_cast<const float4*>(x + i0);
+        float4* y4 = reinterpret_cast<float4*>(y + i0);
+        for (int64_t i = threadIdx.x; i < n4; i += kNT) {
+            const float4 v = x4[i];
+            y4[i] = make_float4(lut(v.x), lut(v.y), lut(v.z), lut(v.w));
+        }
+        for (int64_t i = i0 + 4 * n4 + threadIdx.x; i < i1; i += kNT) y[i] = lut(x[i]);
+    } else {
+        for (int64_t i = i0 + threadIdx.x; i < i1; i += kNT) y[i] = lut(x[i]);
+    }
+}
 }  // namespace lossy
 
 // ===========================================================================
@@ -296,83 +831,6 @@ struct Scratch {
     }
 };
 
-double weighted_inertia(const std::vector<double>& c, const std::vector<double>& w, const std::vector<double>& m,
-                        const std::vector<double>& q) {
-    // sum over bins of sum_{x in bin} (x - c_nearest)^2 using count/sum/sumsq per bin
-    double tot = 0.0;
-    const int k = (int)c.size();
-    for (size_t b = 0; b < w.size(); ++b) {
-        if (w[b] == 0) continue;
-        const double mu = m[b] / w[b];
-        int best = 0; double bd = std::abs(mu - c[0]);
-        for (int j = 1; j < k; ++j) { double d = std::abs(mu - c[j]); if (d < bd) { bd = d; best = j; } }
-        tot += q[b] - 2 * c[best] * m[b] + w[b] * c[best] * c[best];
-    }
-    return tot;
-}
-
-// Lloyd on weighted 1-D points (bin means), from k-means++ seeding; returns centres
-std::vector<double> km_hist(const std::vector<double>& pts, const std::vector<double>& wts, int k, int n_init,
-                            uint64_t seed, int max_iter) {
-    std::mt19937_64 rng(seed);
-    std::vector<int> nz;
-    for (size_t i = 0; i < pts.size(); ++i) if (wts[i] > 0) nz.push_back((int)i);
-    std::vector<double> best;
-    double best_in = std::numeric_limits<double>::infinity();
-    const int trials = 2 + (int)std::log((double)k);  // sklearn's n_local_trials
-    for (int run = 0; run < n_init; ++run) {
-        std::vector<double> c;
-        // k-means++ (weighted)
-        std::discrete_distribution<int> pick0(wts.begin(), wts.end());
-        c.push_back(pts[pick0(rng)]);
-        std::vector<double> d2(pts.size());
-        for (size_t i = 0; i < pts.size(); ++i) d2[i] = (pts[i] - c[0]) * (pts[i] - c[0]);
-        while ((int)c.size() < k) {
-            double pot = 0.0;
-            std::vector<double> pw(pts.size());
-            for (size_t i = 0; i < pts.size(); ++i) { pw[i] = wts[i] * d2[i]; pot += pw[i]; }
-            if (!(pot > 0)) { c.push_back(pts[nz[rng() % nz.size()]]); continue; }
-            std::discrete_distribution<int> pk(pw.begin(), pw.end());
-            int bestc = -1; double bestpot = std::numeric_limits<double>::infinity();
-            for (int t = 0; t < trials; ++t) {
-                const int cand = pk(rng);
-                double np = 0.0;
-                for (size_t i = 0; i < pts.size(); ++i) {
-                    const double d = pts[i] - pts[cand];
-                    np += wts[i] * std::min(d2[i], d * d);
-                }
-                if (np < bestpot) { bestpot = np; bestc = cand; }
-            }
-            c.push_back(pts[bestc]);
-            for (size_t i = 0; i < pts.size(); ++i) { const double d = pts[i] - pts[bestc]; d2[i] = std::min(d2[i], d * d); }
-        }
-        std::sort(c.begin(), c.end());
-        // Lloyd
-        for (int it = 0; it < max_iter; ++it) {
-            std::vector<double> sw(k, 0.0), sx(k, 0.0);
-            for (size_t i = 0; i < pts.size(); ++i) {
-                if (wts[i] == 0) continue;
-                int j = 0;
-                while (j + 1 < k && (c[j] + c[j + 1]) / 2 < pts[i]) ++j;
-                sw[j] += wts[i]; sx[j] += wts[i] * pts[i];
-            }
-            double shift = 0.0;
-            for (int j = 0; j < k; ++j) if (sw[j] > 0) { const double nc = sx[j] / sw[j]; shift += (nc - c[j]) * (nc - c[j]); c[j] = nc; }
-            std::sort(c.begin(), c.end());
-            if (shift == 0.0) break;
-        }
-        double in = 0.0;
-        for (size_t i = 0; i < pts.size(); ++i) {
-            if (wts[i] == 0) continue;
-            double bd = std::numeric_limits<double>::infinity();
-            for (int j = 0; j < k; ++j) bd = std::min(bd, (pts[i] - c[j]) * (pts[i] - c[j]));
-            in += wts[i] * bd;
-        }
-        if (in < best_in) { best_in = in; best = c; }
-    }
-    return best;
-}
-
 lossy::KmParams km_params(const std::vector<double>& c) {
     lossy::KmParams p{};
     p.k = (int)c.size();
@@ -388,94 +846,175 @@ extern "C" {
 const char* ofl_lossy_last_error(void) { return g_lerr.c_str(); }
 
 size_t ofl_lossy_workspace_bytes(int64_t n) {
-    (void)n;
-    return 1 << 20;  // histograms, counters, per-block tie counts (<= 2048 blocks)
+    // histograms, counters, per-block tie counts (<= 2048 blocks); one-tensor k-means
+    return std::max<size_t>(1 << 20, ofl_kmeans1d_batch_workspace_bytes(1, &n));
 }
 
-// 1-D k-means of x (n fp32 on device): k-means++ (n_init restarts) + Lloyd on a
-// 4096-bin histogram, then exact Lloyd passes on the data until the
-// assignment is stable (or max_exact passes).  Outputs the sorted centres
-// (host doubles, k of them; empty clusters keep their histogram position),
-// per-cluster counts and the exact inertia.  Replaces sklearn KMeans.fit in
-// kc_pipeline.py:49-56 / skc_pipeline.py:127-131.
+// ---- batched 1-D k-means (device-resident; see the kernels above) ---------
+}  // extern "C"
+namespace {
+struct BkmLayout {
+    size_t td, st, hc, hs, part, total;
+    int64_t blocks;
+};
+BkmLayout bkm_layout(int T, const int64_t* numels) {
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    BkmLayout L{};
+    L.blocks = 0;
+    for (int t = 0; t < T; ++t) L.blocks += (numels[t] + lossy::kBkmChunk - 1) / lossy::kBkmChunk;
+    L.td = 0;
+    L.st = L.td + al(sizeof(lossy::BkmTensor) * T);
+    L.hc = L.st + al(sizeof(lossy::BkmState) * T);
+    L.hs = L.hc + al(sizeof(uint32_t) * lossy::kBkmBins * T);
+    L.part = L.hs + al(sizeof(unsigned long long) * lossy::kBkmBins * T);
+    L.total = L.part + al(sizeof(double) * 3 * lossy::kMaxK * (size_t)std::max<int64_t>(L.blocks, 1));
+    return L;
+}
+template <int KM1>
+void bkm_launch_acc(int64_t blocks, hipStream_t st, const lossy::BkmArgs& a) {
+    hipLaunchKernelGGL(lossy::k_bkm_acc<KM1>, dim3((unsigned)blocks), dim3(lossy::kBkmAccNT), 0, st, a);
+}
+template <int KM1>
+void bkm_launch_label(int64_t blocks, hipStream_t st, const lossy::BkmArgs& a) {
+    hipLaunchKernelGGL(lossy::k_bkm_label<KM1>, dim3((unsigned)blocks), dim3(lossy::kBkmAccNT), 0, st, a);
+}
+}  // namespace
+extern "C" {
+
+size_t ofl_kmeans1d_batch_workspace_bytes(int ntensors, const int64_t* numels) {
+    if (ntensors < 1 || !numels) return 256;
+    return bkm_layout(ntensors, numels).total + 256;
+}
+
+int ofl_kmeans1d_batch(int ntensors, const float* x_arena, const int64_t* offsets, const int64_t* numels, int k,
+                       int n_init, uint64_t seed, int max_exact, int value_f64, float* ranks_out, double* centres,
+                       int64_t* counts, double* inertia, int32_t* nuniq, double* uniq, void* ws, size_t ws_bytes,
+                       void* stream) {
+    if (ntensors < 1 || !x_arena || !offsets || !numels) return lfail(OFL_EINVAL, "kmeans: empty batch");
+    if (k < 1 || k > lossy::kMaxK) return lfail(OFL_EINVAL, "kmeans: need 1 <= k <= 32");
+    if (n_init < 1 || n_init > lossy::kBkmMaxInit || max_exact < 0)
+        return lfail(OFL_EINVAL, "kmeans: 1 <= n_init <= 16, max_exact >= 0");
+    for (int t = 0; t < ntensors; ++t)
+        if (numels[t] < k || numels[t] > (int64_t)lossy::kBkmChunk * 0x7fffffff)
+            return lfail(OFL_EINVAL, "kmeans: need n >= k for every tensor");
+    const BkmLayout L = bkm_layout(ntensors, numels);
+    if (!ws || ws_bytes < L.total) return lfail(OFL_ESPACE, "kmeans: workspace too small");
+    if (L.blocks > 0x7fffffff) return lfail(OFL_EINVAL, "kmeans: batch too large");
+    static std::once_flag once;
+    static hipError_t attr = hipSuccess;
+    std::call_once(once, [] {
+        attr = hipFuncSetAttribute((const void*)lossy::k_bkm_seed, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)lossy::kBkmSeedLds);
+    });
+    LHIP(attr);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    char* w = static_cast<char*>(ws);
+    std::vector<lossy::BkmTensor> td(ntensors);
+    int64_t blk = 0;
+    for (int t = 0; t < ntensors; ++t) {
+        const int64_t nb = (numels[t] + lossy::kBkmChunk - 1) / lossy::kBkmChunk;
+        td[t] = {offsets[t], numels[t], (int32_t)blk, (int32_t)nb};
+        blk += nb;
+    }
+    lossy::BkmArgs a{};
+    a.x = x_arena;
+    a.out = ranks_out;
+    a.td = reinterpret_cast<lossy::BkmTensor*>(w + L.td);
+    a.ntensors = ntensors;
+    a.k = k;
+    a.n_init = n_init;
+    a.value_f64 = value_f64 ? 1 : 0;
+    a.seed = seed;
+    a.st = reinterpret_cast<lossy::BkmState*>(w + L.st);
+    a.hc = reinterpret_cast<uint32_t*>(w + L.hc);
+    a.hs = reinterpret_cast<unsigned long long*>(w + L.hs);
+    a.part = reinterpret_cast<double*>(w + L.part);
+    LHIP(hipMemcpyAsync(w + L.td, td.data(), sizeof(lossy::BkmTensor) * ntensors, hipMemcpyHostToDevice, st));
+    LHIP(hipMemsetAsync(w + L.st, 0, L.part - L.st, st));  // states + histograms
+    const dim3 g((unsigned)L.blocks), b(lossy::kNT);
+    hipLaunchKernelGGL(lossy::k_bkm_minmax, g, b, 0, st, a);
+    hipLaunchKernelGGL(lossy::k_bkm_hist, g, b, 0, st, a);
+    hipLaunchKernelGGL(lossy::k_bkm_seed, dim3(ntensors * n_init), dim3(lossy::kBkmSeedNT), lossy::kBkmSeedLds, st, a);
+    hipLaunchKernelGGL(lossy::k_bkm_pick, dim3((ntensors + 63) / 64), dim3(64), 0, st, a);
+    for (int pass = 0; pass <= max_exact; ++pass) {
+        a.final_pass = pass == max_exact;
+        if (k <= 8) bkm_launch_acc<7>(L.blocks, st, a);
+        else if (k <= 16) bkm_launch_acc<15>(L.blocks, st, a);
+        else bkm_launch_acc<31>(L.blocks, st, a);
+        hipLaunchKernelGGL(lossy::k_bkm_update, dim3(ntensors), dim3(64), 0, st, a);
+    }
+    if (ranks_out) {
+        if (k <= 8) bkm_launch_label<7>(L.blocks, st, a);
+        else if (k <= 16) bkm_launch_label<15>(L.blocks, st, a);
+        else bkm_launch_label<31>(L.blocks, st, a);
+    }
+    LHIP(hipGetLastError());
+    std::vector<lossy::BkmState> sh(ntensors);
+    LHIP(hipMemcpyAsync(sh.data(), w + L.st, sizeof(lossy::BkmState) * ntensors, hipMemcpyDeviceToHost, st));
+    LHIP(hipStreamSynchronize(st));
+    for (int t = 0; t < ntensors; ++t) {
+        const float lo = unkey(~sh[t].mm[0]), hi = unkey(sh[t].mm[1]);
+        if (!std::isfinite(lo) || !std::isfinite(hi)) return lfail(OFL_EINVAL, "kmeans: non-finite input");
+        for (int j = 0; j < k; ++j) {
+            if (centres) centres[(int64_t)t * k + j] = sh[t].cen[j];
+            if (counts) counts[(int64_t)t * k + j] = sh[t].cnt[j];
+            if (uniq) uniq[(int64_t)t * k + j] = j < sh[t].nuniq ? sh[t].uniq[j] : 0.0;
+        }
+        if (inertia) inertia[t] = sh[t].inertia;
+        if (nuniq) nuniq[t] = sh[t].nuniq;
+    }
+    return OFL_OK;
+}
+
+size_t ofl_lut_decode_batch_workspace_bytes(int ntensors, int max_nk) {
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    return al(sizeof(lossy::BkmTensor) * std::max(ntensors, 1)) + al(4 * (size_t)std::max(ntensors, 1)) +
+           2 * al(4 * (size_t)std::max(ntensors, 1) * std::max(max_nk, 1)) + 256;
+}
+
+int ofl_lut_decode_batch(int ntensors, const float* in_arena, const int64_t* offsets, const int64_t* numels,
+                         const int32_t* nk, const float* keys, const float* vals, int max_nk, float* out_arena,
+                         void* ws, size_t ws_bytes, void* stream) {
+    if (ntensors < 1 || max_nk < 0 || max_nk > 64) return lfail(OFL_EINVAL, "lut: 1+ tensors, at most 64 keys");
+    if (ws_bytes < ofl_lut_decode_batch_workspace_bytes(ntensors, max_nk) || !ws)
+        return lfail(OFL_ESPACE, "lut: workspace too small");
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    char* w = static_cast<char*>(ws);
+    const size_t o_nk = al(sizeof(lossy::BkmTensor) * ntensors);
+    const size_t o_k = o_nk + al(4 * (size_t)ntensors);
+    const size_t o_v = o_k + al(4 * (size_t)ntensors * std::max(max_nk, 1));
+    std::vector<lossy::BkmTensor> td(ntensors);
+    int64_t blk = 0;
+    for (int t = 0; t < ntensors; ++t) {
+        if (nk[t] < 0 || nk[t] > max_nk) return lfail(OFL_EINVAL, "lut: key count out of range");
+        const int64_t nb = (numels[t] + lossy::kBkmChunk - 1) / lossy::kBkmChunk;
+        td[t] = {offsets[t], numels[t], (int32_t)blk, (int32_t)nb};
+        blk += nb;
+    }
+    if (blk == 0) return OFL_OK;
+    LHIP(hipMemcpyAsync(w, td.data(), sizeof(lossy::BkmTensor) * ntensors, hipMemcpyHostToDevice, st));
+    LHIP(hipMemcpyAsync(w + o_nk, nk, 4 * (size_t)ntensors, hipMemcpyHostToDevice, st));
+    if (max_nk) {
+        LHIP(hipMemcpyAsync(w + o_k, keys, 4 * (size_t)ntensors * max_nk, hipMemcpyHostToDevice, st));
+        LHIP(hipMemcpyAsync(w + o_v, vals, 4 * (size_t)ntensors * max_nk, hipMemcpyHostToDevice, st));
+    }
+    lossy::LutBatchArgs a{in_arena, out_arena, reinterpret_cast<lossy::BkmTensor*>(w),
+                          reinterpret_cast<int32_t*>(w + o_nk), reinterpret_cast<float*>(w + o_k),
+                          reinterpret_cast<float*>(w + o_v), ntensors, std::max(max_nk, 1)};
+    hipLaunchKernelGGL(lossy::k_lut_batch, dim3((unsigned)blk), dim3(lossy::kNT), 0, st, a);
+    LHIP(hipGetLastError());
+    return OFL_OK;
+}
+
+// single tensor, no labels: sorted centres, counts and inertia (replaces
+// sklearn KMeans.fit in kc_pipeline.py:49-56 / skc_pipeline.py:127-131)
 int ofl_kmeans1d_fit(const float* x, int64_t n, int k, int n_init, uint64_t seed, int max_exact,
                      double* centres, int64_t* counts, double* inertia, void* ws, size_t ws_bytes,
                      void* stream) {
-    if (k < 1 || k > lossy::kMaxK || n < k) return lfail(OFL_EINVAL, "kmeans: need 1 <= k <= 32 and n >= k");
-    hipStream_t st = static_cast<hipStream_t>(stream);
-    Scratch sc{static_cast<char*>(ws), ws_bytes};
-    uint32_t* mm = sc.take<uint32_t>(2);
-    unsigned long long* hc = sc.take<unsigned long long>(lossy::kHistBins);
-    double* hs = sc.take<double>(lossy::kHistBins);
-    unsigned long long* kc = sc.take<unsigned long long>(lossy::kMaxK);
-    double* ks = sc.take<double>(lossy::kMaxK);
-    double* kq = sc.take<double>(lossy::kMaxK);
-    if (!kq) return lfail(OFL_ESPACE, "kmeans: workspace too small");
-    const int g = grid_for(n);
-    const uint32_t init[2] = {0xffffffffu, 0u};
-    LHIP(hipMemcpyAsync(mm, init, 8, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(lossy::k_minmax, dim3(g), dim3(lossy::kNT), 0, st, x, n, mm);
-    uint32_t mmh[2];
-    LHIP(hipMemcpyAsync(mmh, mm, 8, hipMemcpyDeviceToHost, st));
-    LHIP(hipStreamSynchronize(st));
-    const float lo = unkey(mmh[0]), hi = unkey(mmh[1]);
-    if (!std::isfinite(lo) || !std::isfinite(hi)) return lfail(OFL_EINVAL, "kmeans: non-finite input");
-    std::vector<double> c;
-    if (hi > lo) {
-        const float inv_w = (float)(lossy::kHistBins / ((double)hi - (double)lo) * (1.0 - 1e-7));
-        LHIP(hipMemsetAsync(hc, 0, 8 * lossy::kHistBins, st));
-        LHIP(hipMemsetAsync(hs, 0, 8 * lossy::kHistBins, st));
-        hipLaunchKernelGGL(lossy::k_hist, dim3(g), dim3(lossy::kNT), 0, st, x, n, lo, inv_w, hc, hs);
-        std::vector<unsigned long long> hch(lossy::kHistBins);
-        std::vector<double> hsh(lossy::kHistBins);
-        LHIP(hipMemcpyAsync(hch.data(), hc, 8 * lossy::kHistBins, hipMemcpyDeviceToHost, st));
-        LHIP(hipMemcpyAsync(hsh.data(), hs, 8 * lossy::kHistBins, hipMemcpyDeviceToHost, st));
-        LHIP(hipStreamSynchronize(st));
-        std::vector<double> pts, wts;
-        for (int b = 0; b < lossy::kHistBins; ++b)
-            if (hch[b]) { pts.push_back(hsh[b] / (double)hch[b]); wts.push_back((double)hch[b]); }
-        int distinct = (int)pts.size();
-        if (distinct <= k) {  // fewer occupied bins than clusters: seed on them directly
-            c = pts;
-            while ((int)c.size() < k) c.push_back(c.back());
-        } else {
-            c = km_hist(pts, wts, k, n_init, seed, 300);
-        }
-    } else {
-        c.assign(k, (double)lo);
-    }
-    // exact Lloyd refinement on the full data
-    std::vector<unsigned long long> cnt(k);
-    std::vector<double> sum(k), sq(k);
-    for (int pass = 0; pass <= max_exact; ++pass) {
-        const lossy::KmParams p = km_params(c);
-        LHIP(hipMemsetAsync(kc, 0, 8 * lossy::kMaxK, st));
-        LHIP(hipMemsetAsync(ks, 0, 8 * lossy::kMaxK, st));
-        LHIP(hipMemsetAsync(kq, 0, 8 * lossy::kMaxK, st));
-        hipLaunchKernelGGL(lossy::k_km_accum, dim3(g), dim3(lossy::kNT), 0, st, x, n, p, kc, ks, kq);
-        LHIP(hipMemcpyAsync(cnt.data(), kc, 8 * k, hipMemcpyDeviceToHost, st));
-        LHIP(hipMemcpyAsync(sum.data(), ks, 8 * k, hipMemcpyDeviceToHost, st));
-        LHIP(hipMemcpyAsync(sq.data(), kq, 8 * k, hipMemcpyDeviceToHost, st));
-        LHIP(hipStreamSynchronize(st));
-        if (pass == max_exact) break;
-        std::vector<double> nc = c;
-        for (int j = 0; j < k; ++j) if (cnt[j]) nc[j] = sum[j] / (double)cnt[j];
-        std::sort(nc.begin(), nc.end());
-        // stable when the float32 midpoints (the assignment) do not change
-        const lossy::KmParams pn = km_params(nc);
-        bool same = true;
-        for (int j = 0; j + 1 < k; ++j) same = same && pn.mids[j] == p.mids[j];
-        c = nc;
-        if (same) { pass = max_exact - 1; }  // one more accumulate for final stats
-    }
-    double in = 0.0;
-    for (int j = 0; j < k; ++j) {
-        centres[j] = c[j];
-        if (counts) counts[j] = (int64_t)cnt[j];
-        in += sq[j] - 2 * c[j] * sum[j] + (double)cnt[j] * c[j] * c[j];
-    }
-    if (inertia) *inertia = std::max(0.0, in);
-    return OFL_OK;
+    const int64_t off = 0;
+    return ofl_kmeans1d_batch(1, x, &off, &n, k, n_init, seed, max_exact, 1, nullptr, centres, counts, inertia,
+                              nullptr, nullptr, ws, ws_bytes, stream);
 }
 
 // labels as float32 values: out[i] = rank_of_cluster[nearest sorted centre]

@@ -30,6 +30,16 @@ def _ws(device, n):
     return b
 
 
+def _ws_bytes(device, need):
+    bufs = getattr(_tls, "ws", None)
+    if bufs is None:
+        bufs = _tls.ws = {}
+    b = bufs.get(str(device))
+    if b is None or b.numel() < need:
+        b = bufs[str(device)] = torch.empty(need, dtype=torch.uint8, device=device)
+    return b
+
+
 def _stream(device):
     return torch.cuda.current_stream(device).cuda_stream
 
@@ -52,6 +62,35 @@ def kmeans_fit(x, k=6, n_init=6, seed=0, max_exact=8):
                                         c.ctypes.data, cnt.ctypes.data, ctypes.byref(inertia),
                                         ws.data_ptr(), ws.numel(), _stream(x.device)))
     return c, cnt, inertia.value
+
+
+def kmeans_batch(x_arena, offsets, numels, k=6, n_init=6, seed=0, max_exact=8, value_f64=False, ranks_out=None):
+    """Device k-means of many tensors of one float32 arena (ofl_kmeans1d_batch):
+    tensor t = x_arena[offsets[t]:offsets[t] + numels[t]].  Writes float32
+    ranks (np.unique order of the used centres, value dtype float64 if
+    value_f64) into ranks_out (a device arena like x_arena) when given.
+    -> (centres [T, k], counts [T, k], inertia [T], uniq: list of arrays)."""
+    _check_dev(x_arena)
+    L = _lib.lib()
+    T = len(numels)
+    off = np.ascontiguousarray(offsets, np.int64)
+    num = np.ascontiguousarray(numels, np.int64)
+    need = int(L.ofl_kmeans1d_batch_workspace_bytes(T, num.ctypes.data))
+    ws = _ws_bytes(x_arena.device, need)
+    c = np.zeros((T, k), np.float64)
+    cnt = np.zeros((T, k), np.int64)
+    inertia = np.zeros(T, np.float64)
+    nu = np.zeros(T, np.int32)
+    uq = np.zeros((T, k), np.float64)
+    if ranks_out is not None:
+        _check_dev(ranks_out)
+    _lib.check_lossy(L.ofl_kmeans1d_batch(T, x_arena.data_ptr(), off.ctypes.data, num.ctypes.data, k, n_init,
+                                          int(seed), max_exact, 1 if value_f64 else 0,
+                                          ranks_out.data_ptr() if ranks_out is not None else None,
+                                          c.ctypes.data, cnt.ctypes.data, inertia.ctypes.data, nu.ctypes.data,
+                                          uq.ctypes.data, ws.data_ptr(), ws.numel(), _stream(x_arena.device)))
+    dt = np.float64 if value_f64 else np.float32
+    return c, cnt, inertia, [uq[t, :nu[t]].astype(dt) for t in range(T)]
 
 
 def kmeans_label(x, centres, rank_of_cluster):
@@ -115,6 +154,31 @@ def lut_decode(ranks, int_to_float):
                                                vals.ctypes.data, keys.size, out.data_ptr(),
                                                _stream(ranks.device)))
     return out
+
+
+def lut_decode_batch(ranks_arena, offsets, numels, maps, out_arena):
+    """lut_decode for every tensor of an arena in one launch (maps[t]: the
+    tensor's int_to_float mapping, iteration order kept)."""
+    _check_dev(ranks_arena)
+    _check_dev(out_arena)
+    L = _lib.lib()
+    T = len(numels)
+    mk = max([len(m) for m in maps] + [1])
+    keys = np.zeros((T, mk), np.float32)
+    vals = np.zeros((T, mk), np.float32)
+    nk = np.zeros(T, np.int32)
+    for t, m in enumerate(maps):
+        nk[t] = len(m)
+        for j, (k, v) in enumerate(m.items()):
+            keys[t, j], vals[t, j] = float(k), float(v)
+    off = np.ascontiguousarray(offsets, np.int64)
+    num = np.ascontiguousarray(numels, np.int64)
+    ws = _ws_bytes(ranks_arena.device, int(L.ofl_lut_decode_batch_workspace_bytes(T, mk)))
+    _lib.check_lossy(L.ofl_lut_decode_batch(T, ranks_arena.data_ptr(), off.ctypes.data, num.ctypes.data,
+                                            nk.ctypes.data, keys.ctypes.data, vals.ctypes.data, mk,
+                                            out_arena.data_ptr(), ws.data_ptr(), ws.numel(),
+                                            _stream(ranks_arena.device)))
+    return out_arena
 
 
 def rank_map(values):

@@ -55,12 +55,10 @@ def kmeans_ranks(x_dev, n_cluster, value_dtype):
     map {rank: centre as value_dtype}) with the reference's rank semantics:
     np.unique over the centres actually used (kc_pipeline.py:55-61)."""
     seed = int(np.random.randint(0, 2 ** 31 - 1))  # sklearn draws from the global RNG too
-    centres, counts, _ = lossy.kmeans_fit(x_dev, n_cluster, n_init=n_cluster, seed=seed)
-    vals = centres.astype(value_dtype)
-    uniq = np.unique(vals[counts > 0])
-    rank_of_cluster = np.searchsorted(uniq, vals).astype(np.float32)
-    ranks = lossy.kmeans_label(x_dev, centres, rank_of_cluster)
-    return ranks, {i: u for i, u in enumerate(uniq)}
+    ranks = torch.empty_like(x_dev)
+    _, _, _, uniq = lossy.kmeans_batch(x_dev, [0], [x_dev.numel()], n_cluster, n_init=n_cluster, seed=seed,
+                                       value_f64=np.dtype(value_dtype) == np.float64, ranks_out=ranks)
+    return ranks, {i: u for i, u in enumerate(uniq[0])}
 
 
 def lut_backward(data, int2float_map, device):

@@ -147,6 +147,72 @@ def test_lut_sequential_semantics():
     np.testing.assert_array_equal(out, ref)   # element 0: 0 -> 2 -> 7
 
 
+def test_kmeans_batch_vs_sklearn_and_deterministic():
+    """Batched device k-means (ofl_kmeans1d_batch): every tensor's inertia
+    within 1 % of sklearn KMeans(6, n_init=6) on the same tensor, ranks = rank
+    of the nearest centre among np.unique(used centres), counts sum to n,
+    bit-identical across two runs; ragged sizes, a constant tensor and a
+    tensor with fewer distinct values than clusters included."""
+    from sklearn.cluster import KMeans
+    from openfl_amd import lossy
+    rng = np.random.default_rng(17)
+    xs = [rng.standard_normal(50_000).astype(np.float32) * np.float32(0.02),
+          (rng.standard_normal(70_001) ** 3).astype(np.float32),
+          np.full(1000, 0.25, np.float32),
+          np.repeat(np.float32([1.0, 2.0, 3.0]), 400),
+          rng.uniform(-1, 1, 6).astype(np.float32),
+          np.concatenate([rng.standard_normal(30_000) - 4, rng.standard_normal(30_000) + 4]).astype(np.float32)]
+    offs, acc = [], 0
+    for x in xs:
+        offs.append(acc)
+        acc += (x.size + 63) // 64 * 64 + 3          # ragged offsets: not 16-B aligned
+    arena = torch.zeros(acc, dtype=torch.float32, device=DEV)
+    for x, o in zip(xs, offs):
+        arena[o:o + x.size] = torch.from_numpy(x).to(DEV)
+    outs = []
+    for _ in range(2):
+        ranks = torch.full_like(arena, -1.0)
+        c, cnt, inertia, uniq = lossy.kmeans_batch(arena, offs, [x.size for x in xs], 6, n_init=6, seed=5,
+                                                   ranks_out=ranks)
+        outs.append((c, cnt, inertia, [u.copy() for u in uniq], ranks.cpu().numpy()))
+    for a, b in zip(outs[0][:3], outs[1][:3]):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(outs[0][4], outs[1][4])
+    c, cnt, inertia, uniq, rk = outs[0]
+    for t, (x, o) in enumerate(zip(xs, offs)):
+        assert cnt[t].sum() == x.size and np.all(np.diff(c[t]) >= 0)
+        cen32 = c[t].astype(np.float32)
+        assert np.array_equal(uniq[t], np.unique(cen32[cnt[t] > 0]))
+        r = rk[o:o + x.size].astype(np.int64)
+        used = cen32[cnt[t] > 0]
+        near = np.argmin(np.abs(x.astype(np.float64)[:, None] - used.astype(np.float64)[None, :]), axis=1)
+        assert np.mean(uniq[t][r] == used[near]) >= 0.9999
+        ours = _inertia(x, uniq[t])
+        if np.unique(x).size > 6:
+            np.random.seed(t)
+            ref = KMeans(n_clusters=6, n_init=6).fit(x.reshape(-1, 1)).inertia_
+            assert ours <= 1.01 * ref + 1e-9, (t, ours, ref)
+        else:
+            assert ours <= 1e-9
+
+
+def test_lut_decode_batch_equals_single():
+    from openfl_amd import lossy
+    rng = np.random.default_rng(4)
+    numels = [100_003, 7, 65_536, 200_000]
+    offs, acc = [], 0
+    for n in numels:
+        offs.append(acc)
+        acc += n + 5
+    ranks = torch.from_numpy(rng.integers(0, 6, acc).astype(np.float32)).to(DEV)
+    maps = [{0: 2.0, 1: 0.5, 2: 7.0, 3: -1.0}, {0: 1.5}, {i: float(i) * 0.1 - 0.2 for i in range(6)}, {}]
+    out = torch.full_like(ranks, -9.0)
+    lossy.lut_decode_batch(ranks, offs, numels, maps, out)
+    for o, n, m in zip(offs, numels, maps):
+        ref = lossy.lut_decode(ranks[o:o + n].contiguous(), m) if m else ranks[o:o + n]
+        assert torch.equal(out[o:o + n], ref)
+
+
 def test_kc_large_vs_sklearn():
     from sklearn.cluster import KMeans
     from openfl_amd.pipelines import KCPipeline
