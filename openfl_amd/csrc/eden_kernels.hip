@@ -321,17 +321,31 @@ DEVI void tr_bytes8(const uint32_t (&il)[8], const uint32_t (&ih)[8], uint32_t (
     t4x4(ih[4], ih[5], ih[6], ih[7], oh[4], oh[5], oh[6], oh[7]);
 }
 
-// quantise one group of 8 contiguous values -> (lo, hi) plane bytes; adds <C[bins], y>
-DEVI void quant_group(const float* vg, float ysc, float zm64, const QTab* q, uint32_t& lo, uint32_t& hi,
-                      float& dot) {
+// quantise one group of 8 contiguous values -> (lo, hi) plane bytes; adds
+// <C[bins], y> / ysc.  ysc is a power of two, so z = v * (ysc * zm64) and
+// (sum c * v) * ysc round exactly like (v * ysc) * zm64 and sum c * (v * ysc).
+// The 8 table reads are issued before any is consumed (LDS latency overlaps).
+DEVI void quant_group(const float* vg, float m64, const QTab* q, uint32_t& lo, uint32_t& hi, float& dotv) {
+    float z[8];
+    uint32_t addr[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        z[t] = vg[t] * m64;
+        const float zc = __builtin_amdgcn_fmed3f(z[t], -(float)EDEN_GRID_OFF, (float)(EDEN_GRID_OFF - 1));
+        addr[t] = (uint32_t)((int)floorf(zc) + EDEN_GRID_OFF);
+    }
+    QEnt e[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) e[t] = q->grid[addr[t]];
+    __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // the 8 DS reads first
+    __builtin_amdgcn_sched_group_barrier(0x002, 64, 0); // then the VALU
     lo = 0;
     hi = 0;
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
-        const float y = vg[t] * ysc;
-        float c;
-        const uint32_t b = (uint32_t)quant(y * zm64, q, c);
-        dot += c * y;
+        const bool gt = e[t].b64 < z[t];
+        dotv = fmaf(gt ? e[t].chi : e[t].clo, vg[t], dotv);
+        const uint32_t b = (uint32_t)e[t].lo + (gt ? 1u : 0u);
         if (t < 4) lo |= b << (8 * t); else hi |= b << (8 * (t - 4));
     }
     tr8x8h(lo, hi);
@@ -350,17 +364,18 @@ DEVI void pin_group(const float* v, float (&vg)[8]) {
 // 32 contiguous values -> 8 plane words of 32 bits (bit t = element t)
 DEVI float quant_pack32(const float (&v)[32], float ysc, float zm64, const QTab* q, uint32_t (&w)[8]) {
     float dot = 0.f;
+    const float m64 = ysc * zm64;
     uint32_t xl[4], xh[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
         float vg[8];
         pin_group<8>(&v[8 * g], vg);
-        quant_group(vg, ysc, zm64, q, xl[g], xh[g], dot);
+        quant_group(vg, m64, q, xl[g], xh[g], dot);
         asm volatile("" : "+v"(xl[g]), "+v"(xh[g]), "+v"(dot) :: "memory");  // group done before the next
     }
     t4x4(xl[0], xl[1], xl[2], xl[3], w[0], w[1], w[2], w[3]);
     t4x4(xh[0], xh[1], xh[2], xh[3], w[4], w[5], w[6], w[7]);
-    return dot;
+    return dot * ysc;
 }
 // centroids of a group's plane bytes (lo, hi as produced by quant_group)
 DEVI void unpack_group(uint32_t lo, uint32_t hi, const float* cen, float* v) {
@@ -381,19 +396,20 @@ DEVI void unpack_centroids32(const uint32_t (&w)[8], const float* cen, float (&v
 // 64 contiguous values -> 8 plane words of 64 bits (bit t = element t)
 DEVI float quant_pack64(const float (&v)[64], float ysc, float zm64, const QTab* q, uint64_t (&w)[8]) {
     float dot = 0.f;
+    const float m64 = ysc * zm64;
     uint32_t xl[8], xh[8];
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
         float vg[8];
         pin_group<8>(&v[8 * g], vg);
-        quant_group(vg, ysc, zm64, q, xl[g], xh[g], dot);
+        quant_group(vg, m64, q, xl[g], xh[g], dot);
         asm volatile("" : "+v"(xl[g]), "+v"(xh[g]), "+v"(dot) :: "memory");  // group done before the next
     }
     uint32_t wl[8], wh[8];
     tr_bytes8(xl, xh, wl, wh);
 #pragma unroll
     for (int i = 0; i < 8; ++i) w[i] = (uint64_t)wl[i] | ((uint64_t)wh[i] << 32);
-    return dot;
+    return dot * ysc;
 }
 DEVI void unpack_centroids64(const uint64_t (&w)[8], const float* cen, float (&v)[64]) {
     uint32_t il[8], ih[8], xl[8], xh[8];
@@ -1428,6 +1444,94 @@ __global__ __launch_bounds__(kCol6NT, 4) void k_col6(KArgs a) {
 }
 
 // ===========================================================================
+// Encode pass C with two blocks per CU (k_enc_rowC2).  The quantiser makes
+// k_enc_rowC latency-bound at one block per CU (LDS table reads, bank
+// conflicts, barriers); here the F2 row stages run through layouts that all
+// keep element bit 10 at register index 5:
+//   L3 {5..10} (F2c) -> L4 {11..14,9,10} (F2d) -> L5 {0..4,10} (F2e),
+// so both exchanges go in two halves through a padded 2^14-float buffer
+// (68 KiB; pad() keeps lanes 0..31 on distinct banks: they vary bits 0..4
+// in L3/L4 and bits 5..9 in L5).  With the 9 KiB quantiser table a block
+// takes 77 KiB: two blocks per CU, no register prefetch (the other block
+// hides the loads).  Each thread quantises two runs of 32 contiguous
+// elements (bit 10 = 0, 1) and stores one 32-bit word per plane per run.
+// ===========================================================================
+struct RowC2Set {
+    static constexpr Lay L3{15, 5, 6, 7, 8, 9, 10}, L4{15, 11, 12, 13, 14, 9, 10}, L5{15, 0, 1, 2, 3, 4, 10};
+    static constexpr uint32_t F2c = bits_mask({5, 6, 7, 8, 9, 10}), F2d = bits_mask({11, 12, 13, 14}),
+                              F2e = bits_mask({0, 1, 2, 3, 4});
+    static constexpr int HB = 10;
+};
+constexpr size_t kRowC2Ex = (sizeof(float) * lds_floats(kRowLog - 1) + 15) & ~(size_t)15;
+constexpr size_t kRowC2Smem = kRowC2Ex + sizeof(QTab) + 64;
+
+template <Lay A, Lay B, int HB>
+DEVI void exchange_half_pad(float (&v)[64], float* s, uint32_t tid) {
+    static_assert(LT<A>::rb(5) == HB && LT<B>::rb(5) == HB, "half bit must be register bit 5 of both layouts");
+    const uint32_t ba = opaque(pad(cidx<HB>(LT<A>::base(tid))));
+    const uint32_t bb = opaque(pad(cidx<HB>(LT<B>::base(tid))));
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int r = 32 * h; r < 32 * h + 32; ++r) s[ba + cpad(cidx<HB>(LT<A>::off(r)))] = v[r];
+        __syncthreads();
+#pragma unroll
+        for (int r = 32 * h; r < 32 * h + 32; ++r) v[r] = s[bb + cpad(cidx<HB>(LT<B>::off(r)))];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kRowNT, 4) void k_enc_rowC2(KArgs a) {
+    using R = RowC2Set;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float* s = reinterpret_cast<float*>(smem);
+    QTab* qt = reinterpret_cast<QTab*>(smem + kRowC2Ex);
+    float* red = reinterpret_cast<float*>(smem + kRowC2Ex + sizeof(QTab));
+    const uint32_t tid = threadIdx.x;
+    load_qtable<kRowNT>(qt, a.nbits);
+    __syncthreads();
+    const int total = (int)sld(a.tstart, a.count);
+    const uint32_t base3 = LT<R::L3>::base(tid), base5 = LT<R::L5>::base(tid);
+    for (int t = (int)blockIdx.x; t < total; t += (int)gridDim.x) {
+        int lo = 0, hi = a.count - 1;  // block-uniform search of the tile table (scalar loads)
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if ((int)sld(a.tstart, mid) <= t) lo = mid; else hi = mid - 1;
+        }
+        const int si = (int)sld(a.list, lo);
+        const uint32_t tile = (uint32_t)(t - (int)sld(a.tstart, lo));
+        const SliceDesc D = udesc(a.d, si);
+        float v[64];
+        fetch_ws(a, D, tile, true, base3, v);
+        stages<R::L3, R::F2c>(v);
+        exchange_half_pad<R::L3, R::L4, R::HB>(v, s, tid);
+        stages<R::L4, R::F2d>(v);
+        exchange_half_pad<R::L4, R::L5, R::HB>(v, s, tid);
+        stages<R::L5, R::F2e>(v);
+        __builtin_amdgcn_sched_barrier(0);
+        const float nu = sldf(a.nu, si);
+        const float ysc = pow2i(-((D.logp + 1) / 2));
+        const float zm64 = 64.0f * (sqrtf((float)(1ll << D.logp)) / nu);
+        const bool pos = nu > 0.0f;
+        float dot = 0.f;
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            uint32_t w[8];
+            dot += quant_pack32(*reinterpret_cast<const float(*)[32]>(&v[32 * g]), ysc, zm64, qt, w);
+            if (!pos) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) w[i] = 0;
+            }
+            store_planes(a.pout + D.pl_off, (tile << kRowLog) + base5 + ((uint32_t)g << R::HB), D.pl_stride,
+                         a.nbits, w);
+        }
+        if (!pos) dot = 0.f;
+        dot = block_sum<kRowNT>(dot, red);
+        if (tid == 0) a.part[D.part_off + tile] = dot;
+    }
+}
+
+// ===========================================================================
 // Per-slice scales (large slices), after every final row pass.
 // ===========================================================================
 
@@ -1571,6 +1675,12 @@ hipError_t set_col6_attr() {
     return e != hipSuccess ? e : set_lds((const void*)ofl::k_col6<M, false>, col6_smem(M, false));
 }
 
+// encode pass C uses k_enc_rowC2 (OFL_EDEN_ROWC2=0: k_enc_rowC, A/B)
+bool use_rowc2() {
+    static const bool on = [] { const char* s = getenv("OFL_EDEN_ROWC2"); return !(s && s[0] == '0'); }();
+    return on;
+}
+
 // column passes with M >= 8 rows, or a middle pass with M >= 6, use k_col6
 // (measured: the 1024-thread k_col is ~4 % faster on the plain M = 7 pass);
 // OFL_EDEN_COL6=0 forces k_col everywhere (A/B)
@@ -1588,6 +1698,7 @@ hipError_t set_all_attrs() {
     if ((e = set_small_attr<15>()) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_enc_rowA, ofl::kRowSmemA)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_enc_rowC, ofl::kRowSmemQ)) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_enc_rowC2, ofl::kRowC2Smem)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_dec_rowA<true>, ofl::kRowSmemC)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_dec_rowA<false>, ofl::kRowSmemC)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_dec_rowC, ofl::kRowSmemA)) != hipSuccess) return e;
@@ -1676,8 +1787,11 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
         }
         case K_ROWC: {
             const int64_t g = std::min<int64_t>(l.blocks, pl->ncu);
-            e = enc ? launch(ofl::k_enc_rowC, g, ofl::kRowNT, ofl::kRowSmemQ, st, a)
-                    : launch(ofl::k_dec_rowC, g, ofl::kRowNT, ofl::kRowSmemA, st, a);
+            if (enc && use_rowc2())
+                e = launch(ofl::k_enc_rowC2, std::min<int64_t>(l.blocks, 2 * pl->ncu), ofl::kRowNT, ofl::kRowC2Smem, st, a);
+            else
+                e = enc ? launch(ofl::k_enc_rowC, g, ofl::kRowNT, ofl::kRowSmemQ, st, a)
+                        : launch(ofl::k_dec_rowC, g, ofl::kRowNT, ofl::kRowSmemA, st, a);
             break;
         }
         case K_COL: {
@@ -1727,7 +1841,7 @@ std::string launch_name(const Launch& l, bool enc) {
     case K_TINY: return std::string("ofl::k_") + d + "_tiny";
     case K_SMALL: return std::string("ofl::k_") + d + "_small<" + std::to_string(l.param) + ">";
     case K_ROWA: return std::string("ofl::k_") + d + "_rowA";
-    case K_ROWC: return std::string("ofl::k_") + d + "_rowC";
+    case K_ROWC: return std::string("ofl::k_") + d + (enc && use_rowc2() ? "_rowC2" : "_rowC");
     case K_COL:
         return std::string((l.param >= 8 || (l.param >= 6 && l.mid)) && use_col6() ? "ofl::k_col6<" : "ofl::k_col<") +
                std::to_string(l.param) +
