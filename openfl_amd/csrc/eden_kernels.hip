@@ -1327,15 +1327,17 @@ __global__ __launch_bounds__(kColNT) void k_col(KArgs a) {
 // Tile I/O through a buffer resource over the slice's intermediate: the row
 // part of every register's address is a scalar offset.
 // ===========================================================================
-constexpr int kCol6NT = 512;
-constexpr int kHalfLog = kColLog - 1;
-constexpr size_t kCol6Half = sizeof(float) << kHalfLog;
-template <int M> struct Col6Set {
-    static_assert(M >= 6 && M <= 10, "Col6Set: 6 <= M <= 10");
-    static constexpr int K = kColLog - M;
+// TL = log2 of the tile: 15 (512 threads, 2 blocks per CU) or 16 (1024
+// threads, one block per CU, twice the columns per row segment).
+template <int TL> constexpr int col6_nt() { return 1 << (TL - 6); }
+template <int TL> constexpr size_t col6_half() { return sizeof(float) << (TL - 1); }
+template <int TL> constexpr size_t col6_tab() { return (size_t)1 << (TL - 3); }
+template <int M, int TL> struct Col6Set {
+    static_assert(M >= 6 && M <= 10 && (TL == 15 || TL == 16), "Col6Set: 6 <= M <= 10, TL 15 or 16");
+    static constexpr int K = TL - M;
     static constexpr int row2(int i) { return (M - 6 + i) + ((M - 6 + i) >= 5 ? 1 : 0); }  // i < 5
-    static constexpr Lay L1{kColLog, K, K + 1, K + 2, K + 3, K + 4, K + 5};
-    static constexpr Lay L2{kColLog, K + row2(0), K + row2(1), K + row2(2), K + row2(3), K + row2(4), K + 5};
+    static constexpr Lay L1{TL, K, K + 1, K + 2, K + 3, K + 4, K + 5};
+    static constexpr Lay L2{TL, K + row2(0), K + row2(1), K + row2(2), K + row2(3), K + row2(4), K + 5};
     static constexpr uint32_t A1 = 63u << K;
     static constexpr uint32_t A2 = M > 6 ? ((1u << (M - 6)) - 1u) << (K + 6) : 0u;
     static constexpr int HB = K + 5;  // the half bit (row r5)
@@ -1360,15 +1362,16 @@ DEVI void exchange_half(float (&v)[64], float* s, uint32_t tid) {
     }
 }
 
-template <int M, bool MID>
-__global__ __launch_bounds__(kCol6NT, 4) void k_col6(KArgs a) {
-    using CS = Col6Set<M>;
+template <int M, bool MID, int TL>
+__global__ __launch_bounds__(col6_nt<TL>(), 4) void k_col6(KArgs a) {
+    using CS = Col6Set<M, TL>;
+    constexpr int NT = col6_nt<TL>();
     constexpr int K = CS::K;
     constexpr bool EXCH = M > 6;
     constexpr Lay LC = EXCH ? CS::L2 : CS::L1;  // layout after the first Hadamard part
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float* s = reinterpret_cast<float*>(smem);
-    uint8_t* tab = smem + (EXCH ? kCol6Half : 0);
+    uint8_t* tab = smem + (EXCH ? col6_half<TL>() : 0);
     int si; uint32_t tile;
     find_tile(a, si, tile);
     const SliceDesc D = udesc(a.d, si);
@@ -1380,10 +1383,10 @@ __global__ __launch_bounds__(kCol6NT, 4) void k_col6(KArgs a) {
     const uint32_t tb = (tl << K) | (th << (lo + M));
     auto map = [&](uint32_t t) -> uint32_t { return tb | (t & ((1u << K) - 1u)) | ((t >> K) << lo); };
     const rsrc_t rw = mk_rsrc(a.ws + D.ws_off, (uint32_t)(4ull << D.logp));
-    constexpr uint32_t kTabMask = (1u << (kColLog - 3)) - 1u;
+    constexpr uint32_t kTabMask = (1u << (TL - 3)) - 1u;
     if constexpr (MID) {  // D2 sign bytes of the tile's 2^12 rand_diag words (see k_col)
         const uint32_t b2 = seed_b(sld(a.seeds, D.tensor) + 1u);
-        for (uint32_t q = tid; q < (1u << (kColLog - 3)); q += kCol6NT)
+        for (uint32_t q = tid; q < (1u << (TL - 3)); q += NT)
             tab[q] = (uint8_t)rd_byte(map(q) & ((1u << (D.logp - 3)) - 1u), b2);
     }
     float v[64];
@@ -1406,12 +1409,12 @@ __global__ __launch_bounds__(kCol6NT, 4) void k_col6(KArgs a) {
         // the tile's top 3 bits (the sign's nibble index) are register bits of
         // LC, so each register's shift is a constant and its table offset an
         // immediate
-        static_assert((LT<LC>::rmask() >> (kColLog - 3)) == 7u, "top 3 tile bits must be register bits");
+        static_assert((LT<LC>::rmask() >> (TL - 3)) == 7u, "top 3 tile bits must be register bits");
         const uint32_t bt = opaque(LT<LC>::base(tid) & kTabMask);
 #pragma unroll
         for (int r = 0; r < 64; ++r) {
             const uint32_t o = LT<LC>::off(r);
-            v[r] = flip_unless(v[r] * m2, ((uint32_t)tab[bt + (o & kTabMask)] >> (o >> (kColLog - 3))) & 1u);
+            v[r] = flip_unless(v[r] * m2, ((uint32_t)tab[bt + (o & kTabMask)] >> (o >> (TL - 3))) & 1u);
         }
         if constexpr (EXCH) {
             stages<CS::L2, CS::A2>(v);
@@ -1434,11 +1437,11 @@ __global__ __launch_bounds__(kCol6NT, 4) void k_col6(KArgs a) {
             raw_store_f32(v[r], rw, (int)vo, (int)uu((LT<LC>::off(r) >> K) << los) * 4, 0);
     }
     if (a.do_nu && tile == 0) {  // slice norm, as in k_col
-        __shared__ float nred[kCol6NT / 64];
+        __shared__ float nred[NT / 64];
         const int64_t ntile = 1ll << (D.logp - kRowLog);
         float ss = 0.f;
-        for (int64_t t = tid; t < ntile; t += kCol6NT) ss += a.part[D.part_off + t];
-        ss = block_sum<kCol6NT>(ss, nred);
+        for (int64_t t = tid; t < ntile; t += NT) ss += a.part[D.part_off + t];
+        ss = block_sum<NT>(ss, nred);
         if (tid == 0) a.nu[si] = sqrtf(ss);
     }
 }
@@ -1582,6 +1585,7 @@ struct Launch {
     int nu = 0;      // column: tile 0 of each slice writes the slice norm
     int stream = 0;  // 0: the caller's stream, 1: the plan's side stream
     int join = 0;    // the caller's stream waits for the side stream before this launch
+    int tl = 15;     // column: log2 of the tile (16: k_col6 with 1024 threads)
     int64_t bytes_moved = 0;  // fp32/plane bytes this launch reads + writes (intermediates included)
     int64_t bytes_alg = 0;    // its share of the SURVEY 8(d) algorithmic bytes (x/y fp32 + planes only)
 };
@@ -1667,12 +1671,23 @@ hipError_t set_col_attr() {
     return e != hipSuccess ? e : set_lds((const void*)ofl::k_col<M, false>, col_smem(M, false));
 }
 
-size_t col6_smem(int M, bool mid) { return (M > 6 ? ofl::kCol6Half : 0) + (mid ? ofl::kColTab : 0); }
+size_t col6_smem(int M, bool mid, int tl) {
+    return tl == 16 ? (M > 6 ? ofl::col6_half<16>() : 0) + (mid ? ofl::col6_tab<16>() : 0)
+                    : (M > 6 ? ofl::col6_half<15>() : 0) + (mid ? ofl::col6_tab<15>() : 0);
+}
 
-template <int M>
+template <int M, int TL>
 hipError_t set_col6_attr() {
-    hipError_t e = set_lds((const void*)ofl::k_col6<M, true>, col6_smem(M, true));
-    return e != hipSuccess ? e : set_lds((const void*)ofl::k_col6<M, false>, col6_smem(M, false));
+    hipError_t e = set_lds((const void*)ofl::k_col6<M, true, TL>, col6_smem(M, true, TL));
+    return e != hipSuccess ? e : set_lds((const void*)ofl::k_col6<M, false, TL>, col6_smem(M, false, TL));
+}
+
+// 2^16-element tiles for the 2^24 / 2^25 middle column passes: off by default
+// (measured slower than two 2^15-tile blocks per CU: 457 vs 432 us, 357 vs
+// 307 us per launch); OFL_EDEN_COL16=1 selects them (A/B)
+bool use_col16() {
+    static const bool on = [] { const char* s = getenv("OFL_EDEN_COL16"); return s && s[0] == '1'; }();
+    return on;
 }
 
 // encode pass C uses k_enc_rowC2 (OFL_EDEN_ROWC2=0: k_enc_rowC, A/B)
@@ -1707,11 +1722,13 @@ hipError_t set_all_attrs() {
     if ((e = set_col_attr<8>()) != hipSuccess) return e;
     if ((e = set_col_attr<9>()) != hipSuccess) return e;
     if ((e = set_col_attr<10>()) != hipSuccess) return e;
-    if ((e = set_col6_attr<6>()) != hipSuccess) return e;
-    if ((e = set_col6_attr<7>()) != hipSuccess) return e;
-    if ((e = set_col6_attr<8>()) != hipSuccess) return e;
-    if ((e = set_col6_attr<9>()) != hipSuccess) return e;
-    return set_col6_attr<10>();
+    if ((e = set_col6_attr<6, 15>()) != hipSuccess) return e;
+    if ((e = set_col6_attr<7, 15>()) != hipSuccess) return e;
+    if ((e = set_col6_attr<8, 15>()) != hipSuccess) return e;
+    if ((e = set_col6_attr<9, 15>()) != hipSuccess) return e;
+    if ((e = set_col6_attr<10, 15>()) != hipSuccess) return e;
+    if ((e = set_col6_attr<9, 16>()) != hipSuccess) return e;
+    return set_col6_attr<10, 16>();
 }
 
 int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller) {
@@ -1795,12 +1812,20 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
             break;
         }
         case K_COL: {
+            if (l.tl == 16) {  // 2^16-element tiles (M = 9, 10)
+                const size_t sm = col6_smem(l.param, l.mid != 0, 16);
+                e = l.param == 9 ? (l.mid ? launch(ofl::k_col6<9, true, 16>, l.blocks, 1024, sm, st, a)
+                                          : launch(ofl::k_col6<9, false, 16>, l.blocks, 1024, sm, st, a))
+                                 : (l.mid ? launch(ofl::k_col6<10, true, 16>, l.blocks, 1024, sm, st, a)
+                                          : launch(ofl::k_col6<10, false, 16>, l.blocks, 1024, sm, st, a));
+                break;
+            }
             if ((l.param >= 8 || (l.param >= 6 && l.mid)) && use_col6()) {
-                const size_t sm = col6_smem(l.param, l.mid != 0);
+                const size_t sm = col6_smem(l.param, l.mid != 0, 15);
 #define COL6CASE(MM)                                                                                 \
     case MM:                                                                                         \
-        e = l.mid ? launch(ofl::k_col6<MM, true>, l.blocks, ofl::kCol6NT, sm, st, a)                 \
-                  : launch(ofl::k_col6<MM, false>, l.blocks, ofl::kCol6NT, sm, st, a);               \
+        e = l.mid ? launch(ofl::k_col6<MM, true, 15>, l.blocks, 512, sm, st, a)                      \
+                  : launch(ofl::k_col6<MM, false, 15>, l.blocks, 512, sm, st, a);                    \
         break;
                 switch (l.param) {
                     COL6CASE(6) COL6CASE(7) COL6CASE(8) COL6CASE(9) COL6CASE(10)
@@ -1843,9 +1868,10 @@ std::string launch_name(const Launch& l, bool enc) {
     case K_ROWA: return std::string("ofl::k_") + d + "_rowA";
     case K_ROWC: return std::string("ofl::k_") + d + (enc && use_rowc2() ? "_rowC2" : "_rowC");
     case K_COL:
+        if (l.tl == 16) return "ofl::k_col6<" + std::to_string(l.param) + ", " + (l.mid ? "true" : "false") + ", 16>";
         return std::string((l.param >= 8 || (l.param >= 6 && l.mid)) && use_col6() ? "ofl::k_col6<" : "ofl::k_col<") +
-               std::to_string(l.param) +
-               ", " + (l.mid ? "true" : "false") + ">";
+               std::to_string(l.param) + ", " + (l.mid ? "true" : "false") +
+               ((l.param >= 8 || (l.param >= 6 && l.mid)) && use_col6() ? ", 15>" : ">");
     default: return "ofl::k_finalize";
     }
 }
@@ -1927,7 +1953,15 @@ void build_schedule(ofl_eden_plan* pl) {
             const int cnt = (int)kv.second.size();
             std::vector<Launch> seq;
             if (r <= 10) {
-                seq.push_back({K_COL, r, ofl::kRowLog, 1, lo_c, tp, cnt, tiles});
+                if ((r == 9 || r == 10) && use_col16()) {  // 2^16-element tiles: 2x longer row segments
+                    int64_t t16 = 0;
+                    const int tp16 = add_prefix(kv.second, 16, t16);
+                    Launch l{K_COL, r, ofl::kRowLog, 1, lo_c, tp16, cnt, t16};
+                    l.tl = 16;
+                    seq.push_back(l);
+                } else {
+                    seq.push_back({K_COL, r, ofl::kRowLog, 1, lo_c, tp, cnt, tiles});
+                }
             } else {  // two column levels; the middle launch carries D2
                 const int m1 = r / 2, m2 = r - m1;
                 seq.push_back({K_COL, m1, ofl::kRowLog, 0, lo_c, tp, cnt, tiles});

@@ -83,7 +83,8 @@ def test_wave_schedule_layout():
     for enc in (True, False):
         names = [l["name"] for l in w2.launches(enc)]
         d = "enc" if enc else "dec"
-        assert names.count(f"ofl::k_{d}_rowA") == 4 and names.count(f"ofl::k_{d}_rowC") == 4
+        assert names.count(f"ofl::k_{d}_rowA") == 4
+        assert sum(n.startswith(f"ofl::k_{d}_rowC") for n in names) == 4
         assert names.count("ofl::k_finalize") == (1 if enc else 0)
         # same algorithmic bytes whatever the schedule
         assert sum(l["bytes_alg"] for l in w2.launches(enc)) == sum(l["bytes_alg"] for l in one.launches(enc))
