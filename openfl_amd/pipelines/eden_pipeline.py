@@ -24,6 +24,7 @@ Deliberate differences (DESIGN.md "Reference quirks"):
   * device="cpu" (the reference default) selects the current GPU.
 """
 import threading
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 import torch
@@ -48,14 +49,26 @@ def _serial_sum(flat):
     return sum(flat)
 
 
-def eden_seed(data, mode="reference"):
-    """Seed of EdenTransformer.forward (:771-772); draws ONE np.random value."""
-    flat = data.reshape(-1)
-    if mode == "fast":
-        flat = flat[:_FAST_SEED_PREFIX]
-    s = _serial_sum(flat)
-    seed = (hash(s * 13 + 7) + np.random.randint(1, 2 ** 16)) % (2 ** 16)
+def eden_seed(data, mode="reference", total=None):
+    """Seed of EdenTransformer.forward (:771-772); draws ONE np.random value.
+    total: the precomputed serial sum (forward_batch computes them in parallel)."""
+    if total is None:
+        flat = data.reshape(-1)
+        if mode == "fast":
+            flat = flat[:_FAST_SEED_PREFIX]
+        total = _serial_sum(flat)
+    seed = (hash(total * 13 + 7) + np.random.randint(1, 2 ** 16)) % (2 ** 16)
     return int(float(seed))
+
+
+_pool = None
+
+
+def _threads():
+    global _pool
+    if _pool is None:
+        _pool = ThreadPoolExecutor(max_workers=8)
+    return _pool
 
 
 class Eden:
@@ -76,6 +89,12 @@ class Eden:
         if st is None:
             st = self._tls.stream = torch.cuda.Stream(device=self.device)
         return st
+
+    def _staging(self):
+        sg = getattr(self._tls, "staging", None)
+        if sg is None:
+            sg = self._tls.staging = _Staging()
+        return sg
 
     def compress(self, vec, seed):
         """(planes uint8 ndarray, scales list[float], dims list[int], total_dim) (:555-611)."""
@@ -118,6 +137,102 @@ class Eden:
         return out
 
 
+class _Staging:
+    """Pinned host buffers of one batch shape (grown on demand)."""
+
+    def __init__(self):
+        self.bufs = {}
+
+    def get(self, name, n, dtype):
+        b = self.bufs.get(name)
+        if b is None or b.numel() < n or b.dtype != dtype:
+            b = torch.empty(max(int(n), 1), dtype=dtype).pin_memory()
+            self.bufs[name] = b
+        return b
+
+
+def _batch_encode(eden, arrays, seeds):
+    """Eden-encode many host arrays with one plan: pinned staging, one H2D, one
+    launch sequence, one D2H of the planes arena.  -> [(planes bytes, scales,
+    dims)] per array, the per-tensor Eden.compress results."""
+    codec = eden.codec
+    flats = [np.ascontiguousarray(np.asarray(a).reshape(-1), dtype=np.float32) for a in arrays]
+    plan = codec.plan([f.size for f in flats])
+    st = eden._stream()
+    stg = eden._staging()
+    xh = stg.get("x", plan.arena_numel, torch.float32)
+    ph = stg.get("planes", plan.planes_bytes, torch.uint8)
+    sh = stg.get("scales", plan.n_slices, torch.float32)
+    xn = xh.numpy()
+
+    def fill(i):
+        off = plan.elem_offsets[i]
+        xn[off:off + flats[i].size] = flats[i]
+    list(_threads().map(fill, range(len(flats))))
+    with torch.cuda.stream(st):
+        x = torch.empty(max(plan.arena_numel, 1), dtype=torch.float32, device=eden.device)
+        x.copy_(xh[:max(plan.arena_numel, 1)], non_blocking=True)
+        sd = torch.tensor(seeds, dtype=torch.int32).pin_memory().to(eden.device, non_blocking=True)
+        planes, scales = codec.encode_arena(plan, x, sd, stream=st)
+        ph[:max(plan.planes_bytes, 1)].copy_(planes[:max(plan.planes_bytes, 1)], non_blocking=True)
+        sh[:max(plan.n_slices, 1)].copy_(scales[:max(plan.n_slices, 1)], non_blocking=True)
+    st.synchronize()
+    pn, sn = ph.numpy(), sh.numpy()
+    out = []
+    for t in range(len(flats)):
+        po, pb, fs = plan.planes_offsets[t], plan.planes_nbytes[t], plan.first_slice[t]
+        dims = plan.dims[t]
+        out.append((pn[po:po + pb].tobytes(), [float(v) for v in sn[fs:fs + len(dims)]], list(dims)))
+    return out
+
+
+def _batch_decode(eden, items):
+    """Eden-decode many payloads (planes bytes, int_to_float metadata) with one
+    plan.  -> fresh float32 arrays (flat, total_dim elements each)."""
+    codec = eden.codec
+    totals, dims, scales, seeds = [], [], [], []
+    for data, md in items:
+        keys = list(md.keys())
+        totals.append(int(md[1]))
+        dims.append([int(md[k + 1]) for k in range(2, max(keys) + 1, 2)])
+        scales.append([md[k] for k in range(2, max(keys) + 1, 2)])
+        seeds.append(int(md[0]))
+        if totals[-1] > sum(dims[-1]):
+            raise ValueError(f"Eden metadata: total_dim {totals[-1]} exceeds the slices ({sum(dims[-1])})")
+    plan = codec.plan(totals, dims=dims)
+    st = eden._stream()
+    stg = eden._staging()
+    ph = stg.get("planes_in", plan.planes_bytes, torch.uint8)
+    yh = stg.get("y", plan.arena_numel, torch.float32)
+    pn = ph.numpy()
+    sc = np.asarray([v for s_ in scales for v in s_] or [0.0], np.float32)
+
+    def fill(t):
+        data = items[t][0]
+        po, pb = plan.planes_offsets[t], plan.planes_nbytes[t]
+        buf = np.frombuffer(data, dtype=np.uint8)
+        if buf.size < pb:
+            raise ValueError(f"Eden payload has {buf.size} bytes, expected {pb}")
+        pn[po:po + pb] = buf[:pb]
+    list(_threads().map(fill, range(len(items))))
+    with torch.cuda.stream(st):
+        planes = torch.empty(max(plan.planes_bytes, 1), dtype=torch.uint8, device=eden.device)
+        planes.copy_(ph[:max(plan.planes_bytes, 1)], non_blocking=True)
+        scd = torch.from_numpy(sc).pin_memory().to(eden.device, non_blocking=True)
+        sdd = torch.tensor(seeds, dtype=torch.int32).pin_memory().to(eden.device, non_blocking=True)
+        y = codec.decode_arena(plan, planes, scd, sdd, stream=st)
+        yh[:max(plan.arena_numel, 1)].copy_(y[:max(plan.arena_numel, 1)], non_blocking=True)
+    st.synchronize()
+    yn = yh.numpy()
+    outs = [None] * len(items)
+
+    def take(t):
+        off = plan.elem_offsets[t]
+        outs[t] = yn[off:off + totals[t]].copy()
+    list(_threads().map(take, range(len(items))))
+    return outs
+
+
 class EdenTransformer(Transformer):
     """Eden quantising transformer (:723-818)."""
 
@@ -152,6 +267,46 @@ class EdenTransformer(Transformer):
             out = self.no_comp.backward(data, metadata)
         return out.astype(np.float32)
 
+    # -- many tensors per call (same results as forward/backward in order) --
+    def forward_batch(self, arrays):
+        """[forward(a) for a in arrays], with the Eden tensors coded in one
+        batch: the seeds' serial sums run in parallel host threads, then the
+        np.random draws happen in tensor order exactly as per-tensor calls do."""
+        arrays = [np.asarray(a) for a in arrays]
+
+        def total(a):
+            flat = a.reshape(-1)
+            return _serial_sum(flat[:_FAST_SEED_PREFIX] if self.seed_mode == "fast" else flat)
+        totals = list(_threads().map(total, arrays))
+        seeds = [eden_seed(a, self.seed_mode, t) for a, t in zip(arrays, totals)]
+        big = [i for i, a in enumerate(arrays) if a.size > self.dim_threshold]
+        enc = _batch_encode(self.eden, [arrays[i] for i in big], [seeds[i] for i in big]) if big else []
+        out = [None] * len(arrays)
+        for i, (planes, scales, dims) in zip(big, enc):
+            md = {"int_list": list(arrays[i].shape), "int_to_float": {0: float(seeds[i]), 1: float(arrays[i].size)}}
+            k = 2
+            for sc, d in zip(scales, dims):
+                md["int_to_float"][k] = sc
+                md["int_to_float"][k + 1] = float(d)
+                k += 2
+            out[i] = (planes, md)
+        for i, a in enumerate(arrays):
+            if out[i] is None:
+                out[i] = self.no_comp.forward(a)
+        return out
+
+    def backward_batch(self, items):
+        """[backward(data, md) for data, md in items], the Eden ones decoded in one batch."""
+        big = [i for i, (_, md) in enumerate(items) if np.prod(md["int_list"]) > self.dim_threshold]
+        dec = _batch_decode(self.eden, [(items[i][0], items[i][1]["int_to_float"]) for i in big]) if big else []
+        out = [None] * len(items)
+        for i, y in zip(big, dec):
+            out[i] = y.reshape(list(items[i][1]["int_list"]))
+        for i, (data, md) in enumerate(items):
+            if out[i] is None:
+                out[i] = self.no_comp.backward(data, md).astype(np.float32)
+        return out
+
 
 class EdenPipeline(TransformationPipeline):
     """plan.yaml: template openfl_amd.pipelines.EdenPipeline, settings n_bits /
@@ -170,3 +325,15 @@ class EdenPipeline(TransformationPipeline):
             data, metadata = transformer.forward(data=data, **kwargs)
             transformer_metadata.append(metadata)
         return data, transformer_metadata
+
+    def forward_batch(self, arrays):
+        """Batch form of forward for a whole model update (the aggregator's
+        end-of-round loop, a model snapshot): [(bytes, [metadata]), ...],
+        identical to [forward(a) for a in arrays] (same bytes, metadata and
+        np.random draws); one H2D / launch sequence / D2H for all tensors."""
+        return [(b, [md]) for b, md in self.transformers[0].forward_batch(arrays)]
+
+    def backward_batch(self, items):
+        """[backward(data, metadata_list) for ...] in one batch; like backward,
+        pops each item's metadata list (pipeline.py:161-163)."""
+        return self.transformers[0].backward_batch([(data, mds.pop()) for data, mds in items])

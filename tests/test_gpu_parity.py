@@ -302,6 +302,31 @@ def test_pipeline_forward_backward_vs_reference(rec):
     assert_decode_close(out.reshape(-1), ARR["fwy_" + rec["tag"]].reshape(-1))
 
 
+def test_pipeline_batch_equals_per_tensor():
+    """forward_batch / backward_batch == per-tensor forward / backward: same
+    bytes, metadata, np.random draws and decoded arrays (mixed sizes incl.
+    raw small tensors, a tensor at the threshold and float64 input)."""
+    from openfl_amd.pipelines import EdenPipeline
+    rng = np.random.default_rng(8)
+    arrays = [rng.standard_normal((64, 3, 7, 7)).astype(np.float32), rng.standard_normal(100).astype(np.float32),
+              rng.standard_normal(5).astype(np.float32), rng.standard_normal((1000, 300)).astype(np.float32),
+              rng.standard_normal(70_001), rng.standard_normal((2048, 2048)).astype(np.float32) * 0.01]
+    pipe = EdenPipeline(n_bits=8, device=DEV)
+    np.random.seed(123)
+    ref = [pipe.forward(a) for a in arrays]
+    after = np.random.randint(0, 2 ** 31)
+    np.random.seed(123)
+    got = pipe.forward_batch(arrays)
+    assert np.random.randint(0, 2 ** 31) == after
+    for (b1, m1), (b2, m2) in zip(ref, got):
+        assert b1 == b2 and m1 == m2
+    ys_ref = [pipe.backward(b, [dict(m[0])]) for b, m in ref]
+    ys = pipe.backward_batch([(b, [dict(m[0])]) for b, m in got])
+    for a, b in zip(ys_ref, ys):
+        assert a.dtype == b.dtype == np.float32 and a.shape == b.shape
+        np.testing.assert_array_equal(a, b)
+
+
 def test_pipeline_float32_metadata_roundtrip():
     """Metadata as it arrives off the wire: float32 values (base.proto:22)."""
     from openfl_amd.pipelines import EdenPipeline
