@@ -182,10 +182,28 @@ int ofl_kmeans1d_label(const float* x, int64_t n, const double* centres, int k,
 int ofl_sparsify_topk(const float* x, int64_t n, int64_t k, float* sparse_out, float* kept_min,
                       int64_t* n_pos, int64_t* n_neg, int64_t* n_zero, double* abs_sum, int* shifted,
                       void* ws, size_t ws_bytes, void* stream);
+/* ofl_sparsify_topk for many tensors of one arena (tensor t at offsets[t],
+ * numels[t] elements, keep ks[t] with 1 <= ks[t] <= numels[t]; host arrays).
+ * Radix select on the device (3 digit passes + tie pass + select pass, no
+ * host round trips); sparse_arena (device, same layout) gets the dense
+ * float32 sparse output.  Host outputs [ntensors] (any may be NULL) as in
+ * ofl_sparsify_topk.  Deterministic; one sync at the end.
+ * ws: ofl_sparsify_topk_batch_workspace_bytes(). */
+size_t ofl_sparsify_topk_batch_workspace_bytes(int ntensors, const int64_t* numels);
+int ofl_sparsify_topk_batch(int ntensors, const float* x_arena, const int64_t* offsets, const int64_t* numels,
+                            const int64_t* ks, float* sparse_arena, float* kept_min, int64_t* n_pos, int64_t* n_neg,
+                            int64_t* n_zero, double* abs_sum, int32_t* shifted, void* ws, size_t ws_bytes,
+                            void* stream);
 int ofl_ternary_stats(const float* x, int64_t n, int64_t* n_pos, int64_t* n_neg, double* abs_sum, void* ws,
                       size_t ws_bytes, void* stream);
 int ofl_ternary_ranks(const float* sparse, int64_t n, float rank_neg, float rank_zero, float rank_pos,
                       float* out, void* stream);
+/* ofl_ternary_ranks for many tensors of one arena: ranks3[3 t .. 3 t + 2] =
+ * (rank_neg, rank_zero, rank_pos) of tensor t (host, copied before return).
+ * ws: ofl_ternary_ranks_batch_workspace_bytes(). */
+size_t ofl_ternary_ranks_batch_workspace_bytes(int ntensors);
+int ofl_ternary_ranks_batch(int ntensors, const float* sparse_arena, const int64_t* offsets, const int64_t* numels,
+                            const float* ranks3, float* out_arena, void* ws, size_t ws_bytes, void* stream);
 int ofl_lut_decode(const float* in, int64_t n, const float* keys, const float* vals, int nk, float* out,
                    void* stream);
 /* ofl_lut_decode for many tensors of one arena in one launch: tensor t has

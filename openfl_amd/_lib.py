@@ -27,6 +27,8 @@ EXPORTS = (
     "ofl_kmeans1d_batch_workspace_bytes", "ofl_kmeans1d_batch",
     "ofl_kmeans1d_label", "ofl_sparsify_topk", "ofl_ternary_stats", "ofl_ternary_ranks", "ofl_lut_decode",
     "ofl_lut_decode_batch_workspace_bytes", "ofl_lut_decode_batch",
+    "ofl_sparsify_topk_batch_workspace_bytes", "ofl_sparsify_topk_batch",
+    "ofl_ternary_ranks_batch_workspace_bytes", "ofl_ternary_ranks_batch",
 )
 
 
@@ -93,6 +95,14 @@ def _bind(L):
     L.ofl_lut_decode_batch_workspace_bytes.restype = sz
     L.ofl_lut_decode_batch.argtypes = [i32, vp, vp, vp, vp, vp, vp, i32, vp, vp, sz, vp]
     L.ofl_lut_decode_batch.restype = i32
+    L.ofl_sparsify_topk_batch_workspace_bytes.argtypes = [i32, vp]
+    L.ofl_sparsify_topk_batch_workspace_bytes.restype = sz
+    L.ofl_sparsify_topk_batch.argtypes = [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp]
+    L.ofl_sparsify_topk_batch.restype = i32
+    L.ofl_ternary_ranks_batch_workspace_bytes.argtypes = [i32]
+    L.ofl_ternary_ranks_batch_workspace_bytes.restype = sz
+    L.ofl_ternary_ranks_batch.argtypes = [i32, vp, vp, vp, vp, vp, vp, sz, vp]
+    L.ofl_ternary_ranks_batch.restype = i32
     L.ofl_serial_sum_f32.argtypes = [vp, i64]
     L.ofl_serial_sum_f32.restype = ctypes.c_float
     L.ofl_serial_sum_f64.argtypes = [vp, i64]

@@ -75,42 +75,7 @@ __global__ __launch_bounds__(kNT) void k_km_label(const float* x, int64_t n, KmP
     for (int64_t i = gtid(); i < n; i += gstride()) out[i] = p.rank[cluster_of(x[i], p)];
 }
 
-// ---- radix select on |x| bits (float32 magnitudes order like their bits) ----
-// digit d of the 31 magnitude bits: pass 0 -> bits [20,31), 1 -> [9,20), 2 -> [0,9)
-__global__ __launch_bounds__(kNT) void k_abs_radix(const float* x, int64_t n, uint32_t prefix,
-                                                   uint32_t prefix_mask, int shift, uint32_t digit_mask,
-                                                   uint32_t* hist) {
-    __shared__ uint32_t h[kRadix];
-    for (int b = threadIdx.x; b < kRadix; b += kNT) h[b] = 0;
-    __syncthreads();
-    for (int64_t i = gtid(); i < n; i += gstride()) {
-        const uint32_t m = __float_as_uint(x[i]) & 0x7fffffffu;
-        if ((m & prefix_mask) == prefix) atomicAdd(&h[(m >> shift) & digit_mask], 1u);
-    }
-    __syncthreads();
-    for (int b = threadIdx.x; b < kRadix; b += kNT) if (h[b]) atomicAdd(&hist[b], h[b]);
-}
-
-// per-block count of elements with |x| bits == T (tie rank by index)
-__global__ __launch_bounds__(kNT) void k_tie_count(const float* x, int64_t n, int64_t per_block, uint32_t T,
-                                                   uint32_t* block_ties) {
-    const int64_t b0 = (int64_t)blockIdx.x * per_block, b1 = std::min<int64_t>(n, b0 + per_block);
-    uint32_t c = 0;
-    for (int64_t i = b0 + threadIdx.x; i < b1; i += kNT) c += ((__float_as_uint(x[i]) & 0x7fffffffu) == T) ? 1u : 0u;
-    c = wave_sum(c);
-    if ((threadIdx.x & 63) == 0) atomicAdd(&block_ties[blockIdx.x], c);
-}
-
-// kept-element flag for element i of block b (ties kept lowest index first):
-// |x| > T, or |x| == T and its index rank among ties < tie_keep.  The in-block
-// tie rank needs an ordered scan: each block walks its range in kNT-chunks.
-struct SelParams {
-    uint32_t T;
-    int64_t tie_keep;     // how many |x| == T elements are kept (lowest index)
-    int64_t per_block;
-    float shift;          // 1e-7 or 0 added to kept values (skc_pipeline.py:92-93)
-};
-
+// 256-thread exclusive scan of one uint32 per thread (block total in `total`)
 DEVI uint32_t block_excl_scan(uint32_t v, uint32_t* tmp, uint32_t& total) {
     // 256 threads: wave-level inclusive scan, then wave offsets
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -128,50 +93,6 @@ DEVI uint32_t block_excl_scan(uint32_t v, uint32_t* tmp, uint32_t& total) {
     for (int j = 0; j < kNT / 64; ++j) { if (j < w) off += tmp[j]; total += tmp[j]; }
     __syncthreads();
     return off + inc - v;
-}
-
-// stats of the kept set after the shift: min kept value (pre-shift), counts of
-// kept values that end up > 0, < 0, == 0, and fp64 sum of |kept + shift|
-__global__ __launch_bounds__(kNT) void k_select(const float* x, int64_t n, SelParams sp, const uint64_t* tie_base,
-                                                float* sparse_out, float* kmin, unsigned long long* counts,
-                                                double* abs_sum) {
-    __shared__ uint32_t tmp[kNT / 64];
-    const int64_t b0 = (int64_t)blockIdx.x * sp.per_block, b1 = std::min<int64_t>(n, b0 + sp.per_block);
-    int64_t ties = (int64_t)tie_base[blockIdx.x];
-    float mn = INFINITY;
-    uint32_t cpos = 0, cneg = 0, czero = 0;
-    double as = 0.0;
-    for (int64_t base = b0; base < b1; base += kNT) {
-        const int64_t i = base + threadIdx.x;
-        const bool in = i < b1;
-        const float v = in ? x[i] : 0.0f;
-        const uint32_t m = __float_as_uint(v) & 0x7fffffffu;
-        const uint32_t tie = (in && m == sp.T) ? 1u : 0u;
-        uint32_t tot;
-        const uint32_t rank = block_excl_scan(tie, tmp, tot);
-        const bool keep = in && (m > sp.T || (tie && ties + (int64_t)rank < sp.tie_keep));
-        ties += tot;
-        float outv = 0.0f;
-        if (keep) {
-            mn = fminf(mn, v);
-            outv = v + sp.shift;  // float32 add (NEP 50: python float is weak)
-            cpos += outv > 0.0f;
-            cneg += outv < 0.0f;
-            czero += outv == 0.0f;
-            as += fabs((double)outv);
-        }
-        if (sparse_out && in) sparse_out[i] = outv;
-    }
-    mn = wave_min(mn);
-    cpos = wave_sum(cpos); cneg = wave_sum(cneg); czero = wave_sum(czero);
-    as = wave_sum(as);
-    if ((threadIdx.x & 63) == 0) {
-        atomicMin(reinterpret_cast<uint32_t*>(kmin), fkey(mn));
-        atomicAdd(&counts[0], (unsigned long long)cpos);
-        atomicAdd(&counts[1], (unsigned long long)cneg);
-        atomicAdd(&counts[2], (unsigned long long)czero);
-        atomicAdd(abs_sum, as);
-    }
 }
 
 // ternary ranks of the sparse array (stc_pipeline.py:105-130): value > 0 ->
@@ -796,6 +717,336 @@ __global__ __launch_bounds__(kNT) void k_lut_batch(LutBatchArgs a) {
         for (int64_t i = i0 + threadIdx.x; i < i1; i += kNT) y[i] = lut(x[i]);
     }
 }
+// ===========================================================================
+// Batched exact top-k by magnitude (SparsityTransformer._topk_func,
+// skc_pipeline.py:72-94 / stc_pipeline.py:53-91, for many tensors of one
+// fp32 arena), device-resident and deterministic.  |x| bit patterns order like
+// the magnitudes, so the k-th largest is found by a 3-digit radix select over
+// the 31 magnitude bits (11 + 11 + 9):
+//   k_btk_hist   per-tensor digit histogram of the elements matching the
+//                prefix found so far                                 (1 pass)
+//   k_btk_digit  one wave per tensor: the digit holding the need-th largest,
+//                prefix/need update, histogram cleared for the next pass
+// then T = the k-th largest |x| bits and `need` = ties at T kept (lowest index
+// first, the reference's argsort order for ties being unspecified):
+//   k_btk_ties   per block: ties at T, min kept-for-sure value (|x| > T), min
+//                tie value, in-block tie rank of the first negative tie (1 pass)
+//   k_btk_scan   one wave per tensor: exclusive prefix of the tie counts and
+//                the exact minimum of the kept set -> the +1e-7 shift (:92-93)
+//   k_btk_select dense sparse output (kept + shift, else 0) and per-block
+//                kept-set statistics (1 pass: read x, write sparse)
+//   k_btk_final  one wave per tensor: fixed-order sums of the statistics
+// Blocks cover kBkmChunk consecutive elements of one tensor, as in k-means.
+// ===========================================================================
+struct BtkState {
+    int64_t k;            // kept count (ceil(n p))
+    int64_t need;         // rank from the top within the current prefix; after pass 3: ties kept
+    uint32_t prefix, pmask;
+    float kmin;           // min kept value (before the shift)
+    float shift;          // 1e-7 or 0
+    int64_t n_pos, n_neg, n_zero;
+    double abs_sum;       // fp64 sum of |kept + shift|
+};
+struct BtkBlock {
+    uint32_t ties;        // |x| bits == T in this block
+    int32_t neg_rank;     // in-block tie rank of the first negative tie, -1 if none
+    float smin;           // min value with |x| > T
+    float tmin;           // min value with |x| == T
+    uint64_t tie_base;    // ties in the tensor's earlier blocks
+    uint32_t cpos, cneg, czero, pad_;
+    double asum;
+};
+struct BtkArgs {
+    const float* x;
+    float* out;
+    const BkmTensor* td;
+    int32_t ntensors;
+    int32_t pass;
+    BtkState* st;
+    uint32_t* hist;       // [T][kRadix]
+    BtkBlock* blk;        // [blocks]
+};
+
+DEVI int tensor_of(const BkmTensor* td, int nt, int b) {
+    int lo = 0, hi = nt - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (td[mid].blk0 <= b) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+// f(v, i) for every element of p[i0, i1) (i = index inside the tensor)
+template <typename F>
+DEVI void btk_visit(const float* p, int64_t i0, int64_t i1, F f) {
+    int64_t a4 = i0;
+    while (a4 < i1 && (reinterpret_cast<uintptr_t>(p + a4) & 15u)) ++a4;
+    for (int64_t j = i0 + threadIdx.x; j < a4; j += kNT) f(p[j], j);
+    const int64_t n4 = (i1 - a4) >> 2;
+    const float4* q = reinterpret_cast<const float4*>(p + a4);
+    for (int64_t j = threadIdx.x; j < n4; j += kNT) {
+        const float4 v = q[j];
+        const int64_t i = a4 + 4 * j;
+        f(v.x, i); f(v.y, i + 1); f(v.z, i + 2); f(v.w, i + 3);
+    }
+    for (int64_t j = a4 + 4 * n4 + threadIdx.x; j < i1; j += kNT) f(p[j], j);
+}
+DEVI int btk_shift(int pass) { return pass == 0 ? 20 : (pass == 1 ? 9 : 0); }
+DEVI int btk_width(int pass) { return pass == 2 ? 9 : 11; }
+
+__global__ __launch_bounds__(kNT) void k_btk_hist(BtkArgs a) {
+    __shared__ uint32_t h[kRadix];
+    for (int b = threadIdx.x; b < kRadix; b += kNT) h[b] = 0;
+    const int t = tensor_of(a.td, a.ntensors, (int)blockIdx.x);
+    const BkmTensor T = a.td[t];
+    const int64_t i0 = (int64_t)(blockIdx.x - T.blk0) * kBkmChunk;
+    const int64_t i1 = i0 + kBkmChunk < T.n ? i0 + kBkmChunk : T.n;
+    const uint32_t prefix = a.st[t].prefix, pmask = a.st[t].pmask;
+    const int sh = btk_shift(a.pass);
+    const uint32_t dm = (1u << btk_width(a.pass)) - 1u;
+    __syncthreads();
+    btk_visit(a.x + T.off, i0, i1, [&](float v, int64_t) {
+        const uint32_t m = __float_as_uint(v) & 0x7fffffffu;
+        if ((m & pmask) == prefix) atomicAdd(&h[(m >> sh) & dm], 1u);
+    });
+    __syncthreads();
+    uint32_t* g = a.hist + (int64_t)t * kRadix;
+    for (int b = threadIdx.x; b <= (int)dm; b += kNT) if (h[b]) atomicAdd(&g[b], h[b]);
+}
+
+__global__ __launch_bounds__(64) void k_btk_digit(BtkArgs a) {
+    const int t = blockIdx.x, lane = threadIdx.x;
+    BtkState& S = a.st[t];
+    uint32_t* h = a.hist + (int64_t)t * kRadix;
+    const int width = btk_width(a.pass), sh = btk_shift(a.pass);
+    const int per = (1 << width) / 64;
+    const int64_t need = S.need;
+    int64_t s = 0;
+    for (int j = 0; j < per; ++j) s += h[lane * per + j];
+    // suffix sums from the top bin: S_l = sum over lanes >= l
+    int64_t suf = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t u = __shfl_down(suf, o, 64);
+        if (lane + o < 64) suf += u;
+    }
+    const unsigned long long hit = __ballot(suf >= need);
+    const int L = hit ? 63 - __clzll((long long)hit) : 0;   // the need-th largest lies in lane L's bins
+    if (lane == L) {
+        int64_t acc = suf - s;  // elements in bins above lane L's range
+        int d = lane * per;
+        for (int b = lane * per + per - 1; b > lane * per; --b) {
+            if (acc + (int64_t)h[b] >= need) { d = b; break; }
+            acc += h[b];
+        }
+        S.prefix |= (uint32_t)d << sh;
+        S.pmask |= (uint32_t)((1 << width) - 1) << sh;
+        S.need = need - acc;
+    }
+    for (int j = 0; j < per; ++j) h[lane * per + j] = 0;
+}
+
+// 256-thread block reductions through a 4-entry LDS array
+template <typename V, typename Op>
+DEVI V btk_breduce(V v, V* tmp, Op op) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = op(v, __shfl_xor(v, o, 64));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) tmp[threadIdx.x >> 6] = v;
+    __syncthreads();
+    V r = tmp[0];
+#pragma unroll
+    for (int w = 1; w < kNT / 64; ++w) r = op(r, tmp[w]);
+    return r;
+}
+
+__global__ __launch_bounds__(kNT) void k_btk_ties(BtkArgs a) {
+    __shared__ uint32_t tu[kNT / 64];
+    __shared__ float tf[kNT / 64];
+    __shared__ int64_t ti[kNT / 64];
+    const int t = tensor_of(a.td, a.ntensors, (int)blockIdx.x);
+    const BkmTensor T = a.td[t];
+    const int64_t i0 = (int64_t)(blockIdx.x - T.blk0) * kBkmChunk;
+    const int64_t i1 = i0 + kBkmChunk < T.n ? i0 + kBkmChunk : T.n;
+    const uint32_t Tb = a.st[t].prefix;
+    const float* p = a.x + T.off;
+    uint32_t c = 0;
+    float smin = INFINITY, tmin = INFINITY;
+    int64_t neg = INT64_MAX;
+    btk_visit(p, i0, i1, [&](float v, int64_t i) {
+        const uint32_t m = __float_as_uint(v) & 0x7fffffffu;
+        if (m > Tb) smin = fminf(smin, v);
+        if (m == Tb) {
+            ++c;
+            tmin = fminf(tmin, v);
+            if (v < 0.0f && i < neg) neg = i;
+        }
+    });
+    c = btk_breduce(c, tu, [](uint32_t x, uint32_t y) { return x + y; });
+    smin = btk_breduce(smin, tf, [](float x, float y) { return fminf(x, y); });
+    tmin = btk_breduce(tmin, tf, [](float x, float y) { return fminf(x, y); });
+    neg = btk_breduce(neg, ti, [](int64_t x, int64_t y) { return x < y ? x : y; });
+    int32_t rank = -1;
+    if (neg != INT64_MAX) {  // rare: a negative tie -> its rank among the block's ties
+        uint32_t r = 0;
+        for (int64_t i = i0 + threadIdx.x; i < neg; i += kNT) r += (__float_as_uint(p[i]) & 0x7fffffffu) == Tb;
+        rank = (int32_t)btk_breduce(r, tu, [](uint32_t x, uint32_t y) { return x + y; });
+    }
+    if (threadIdx.x == 0) {
+        BtkBlock& B = a.blk[blockIdx.x];
+        B.ties = c;
+        B.neg_rank = rank;
+        B.smin = smin;
+        B.tmin = tmin;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_btk_scan(BtkArgs a) {
+    const int t = blockIdx.x, lane = threadIdx.x;
+    const BkmTensor T = a.td[t];
+    BtkState& S = a.st[t];
+    const int64_t need = S.need;
+    uint64_t carry = 0;
+    float smin = INFINITY, tmin = INFINITY;
+    int negkept = 0;
+    for (int b0 = 0; b0 < T.nblk; b0 += 64) {
+        const int b = b0 + lane;
+        BtkBlock* B = a.blk + T.blk0 + b;
+        const uint64_t c = b < T.nblk ? B->ties : 0;
+        uint64_t inc = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t u = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += u;
+        }
+        if (b < T.nblk) {
+            const uint64_t base = carry + inc - c;
+            B->tie_base = base;
+            smin = fminf(smin, B->smin);
+            tmin = fminf(tmin, B->tmin);
+            if (B->neg_rank >= 0 && (int64_t)base + B->neg_rank < need) negkept = 1;
+        }
+        carry += __shfl(inc, 63, 64);
+    }
+    smin = wave_min(smin);
+    tmin = wave_min(tmin);
+    negkept = __any(negkept);
+    if (lane == 0) {
+        float kmin = smin;
+        const float Tf = __uint_as_float(S.prefix);
+        if (need > 0) kmin = fminf(kmin, (int64_t)carry <= need ? tmin : (negkept ? -Tf : Tf));
+        S.kmin = kmin;
+        // reference: `if min(topk_mag) - 0 < 10e-8: topk_mag = topk_mag + 10e-8`
+        S.shift = ((double)kmin < 10e-8) ? (float)10e-8 : 0.0f;
+    }
+}
+
+__global__ __launch_bounds__(kNT) void k_btk_select(BtkArgs a) {
+    __shared__ uint32_t tu[kNT / 64];
+    __shared__ double td[kNT / 64];
+    const int t = tensor_of(a.td, a.ntensors, (int)blockIdx.x);
+    const BkmTensor T = a.td[t];
+    const int64_t i0 = (int64_t)(blockIdx.x - T.blk0) * kBkmChunk;
+    const int64_t i1 = i0 + kBkmChunk < T.n ? i0 + kBkmChunk : T.n;
+    const uint32_t Tb = a.st[t].prefix;
+    const int64_t need = a.st[t].need;
+    const float shift = a.st[t].shift;
+    BtkBlock& B = a.blk[blockIdx.x];
+    const int64_t base = (int64_t)B.tie_base, nt = B.ties;
+    const float* p = a.x + T.off;
+    float* o = a.out + T.off;
+    uint32_t cpos = 0, cneg = 0, czero = 0;
+    double as = 0.0;
+    auto kept = [&](float v) {
+        const float w = v + shift;  // float32 add (NEP 50: python float is weak)
+        cpos += w > 0.0f;
+        cneg += w < 0.0f;
+        czero += w == 0.0f;
+        as += fabs((double)w);
+        return w;
+    };
+    if (nt == 0 || base >= need || base + nt <= need) {
+        // the block's ties are all dropped or all kept: no ordering needed
+        const bool keep_ties = nt > 0 && base + nt <= need;
+        auto f = [&](float v) {
+            const uint32_t m = __float_as_uint(v) & 0x7fffffffu;
+            return (m > Tb || (keep_ties && m == Tb)) ? kept(v) : 0.0f;
+        };
+        if (((reinterpret_cast<uintptr_t>(p + i0) | reinterpret_cast<uintptr_t>(o + i0)) & 15u) == 0) {
+            const int64_t n4 = (i1 - i0) >> 2;
+            const float4* x4 = reinterpret_cast<const float4*>(p + i0);
+            float4* y4 = reinterpret_cast<float4*>(o + i0);
+            for (int64_t j = threadIdx.x; j < n4; j += kNT) {
+                const float4 v = x4[j];
+                y4[j] = make_float4(f(v.x), f(v.y), f(v.z), f(v.w));
+            }
+            for (int64_t j = i0 + 4 * n4 + threadIdx.x; j < i1; j += kNT) o[j] = f(p[j]);
+        } else {
+            for (int64_t j = i0 + threadIdx.x; j < i1; j += kNT) o[j] = f(p[j]);
+        }
+    } else {
+        // the boundary block: in-order tie ranks, kNT elements at a time
+        int64_t ties = base;
+        for (int64_t c0 = i0; c0 < i1; c0 += kNT) {
+            const int64_t i = c0 + threadIdx.x;
+            const bool in = i < i1;
+            const float v = in ? p[i] : 0.0f;
+            const uint32_t m = __float_as_uint(v) & 0x7fffffffu;
+            const uint32_t tie = (in && m == Tb) ? 1u : 0u;
+            uint32_t tot;
+            const uint32_t r = block_excl_scan(tie, tu, tot);
+            const bool keep = in && (m > Tb || (tie && ties + (int64_t)r < need));
+            ties += tot;
+            if (in) o[i] = keep ? kept(v) : 0.0f;
+        }
+    }
+    cpos = btk_breduce(cpos, tu, [](uint32_t x, uint32_t y) { return x + y; });
+    cneg = btk_breduce(cneg, tu, [](uint32_t x, uint32_t y) { return x + y; });
+    czero = btk_breduce(czero, tu, [](uint32_t x, uint32_t y) { return x + y; });
+    as = btk_breduce(as, td, [](double x, double y) { return x + y; });
+    if (threadIdx.x == 0) { B.cpos = cpos; B.cneg = cneg; B.czero = czero; B.asum = as; }
+}
+
+__global__ __launch_bounds__(64) void k_btk_final(BtkArgs a) {
+    const int t = blockIdx.x, lane = threadIdx.x;
+    const BkmTensor T = a.td[t];
+    uint64_t p = 0, n = 0, z = 0;
+    double s = 0.0;
+    for (int b = lane; b < T.nblk; b += 64) {
+        const BtkBlock& B = a.blk[T.blk0 + b];
+        p += B.cpos; n += B.cneg; z += B.czero; s += B.asum;
+    }
+    p = wave_sum(p); n = wave_sum(n); z = wave_sum(z); s = wave_sum(s);
+    if (lane == 0) {
+        BtkState& S = a.st[t];
+        S.n_pos = (int64_t)p; S.n_neg = (int64_t)n; S.n_zero = (int64_t)z; S.abs_sum = s;
+    }
+}
+
+// ternary ranks of a sparse arena, per-tensor (rank_neg, rank_zero, rank_pos)
+// (stc_pipeline.py:105-130 then _float_to_int)
+__global__ __launch_bounds__(kNT) void k_ternary_batch(const float* in, float* out, const BkmTensor* td, int nt,
+                                                       const float* ranks3) {
+    const int t = tensor_of(td, nt, (int)blockIdx.x);
+    const BkmTensor T = td[t];
+    const int64_t i0 = (int64_t)(blockIdx.x - T.blk0) * kBkmChunk;
+    const int64_t i1 = i0 + kBkmChunk < T.n ? i0 + kBkmChunk : T.n;
+    const float rn = ranks3[3 * t], rz = ranks3[3 * t + 1], rp = ranks3[3 * t + 2];
+    const float* x = in + T.off;
+    float* y = out + T.off;
+    auto f = [&](float v) { return v > 0.0f ? rp : (v < 0.0f ? rn : rz); };
+    if (((reinterpret_cast<uintptr_t>(x + i0) | reinterpret_cast<uintptr_t>(y + i0)) & 15u) == 0) {
+        const int64_t n4 = (i1 - i0) >> 2;
+        const float4* x4 = reinterpret_cast<const float4*>(x + i0);
+        float4* y4 = reinterpret_cast<float4*>(y + i0);
+        for (int64_t i = threadIdx.x; i < n4; i += kNT) {
+            const float4 v = x4[i];
+            y4[i] = make_float4(f(v.x), f(v.y), f(v.z), f(v.w));
+        }
+        for (int64_t i = i0 + 4 * n4 + threadIdx.x; i < i1; i += kNT) y[i] = f(x[i]);
+    } else {
+        for (int64_t i = i0 + threadIdx.x; i < i1; i += kNT) y[i] = f(x[i]);
+    }
+}
 }  // namespace lossy
 
 // ===========================================================================
@@ -846,8 +1097,9 @@ extern "C" {
 const char* ofl_lossy_last_error(void) { return g_lerr.c_str(); }
 
 size_t ofl_lossy_workspace_bytes(int64_t n) {
-    // histograms, counters, per-block tie counts (<= 2048 blocks); one-tensor k-means
-    return std::max<size_t>(1 << 20, ofl_kmeans1d_batch_workspace_bytes(1, &n));
+    // one-tensor k-means or top-k
+    return std::max<size_t>({(size_t)1 << 20, ofl_kmeans1d_batch_workspace_bytes(1, &n),
+                             ofl_sparsify_topk_batch_workspace_bytes(1, &n)});
 }
 
 // ---- batched 1-D k-means (device-resident; see the kernels above) ---------
@@ -1030,84 +1282,135 @@ int ofl_kmeans1d_label(const float* x, int64_t n, const double* centres, int k, 
     return OFL_OK;
 }
 
-// top-k by magnitude (skc/stc SparsityTransformer._topk_func, skc_pipeline.py:72-94):
-// exact k-th largest |x| by 3-pass radix select; ties at the threshold are
-// kept lowest index first.  Writes the dense float32 sparse array (kept values
-// + shift, zeros elsewhere; shift = 1e-7 iff min(kept) < 1e-7, :92-93) and
-// returns the kept-set statistics used by the ternary / k-means stages.
+// ---- batched top-k by magnitude (kernels k_btk_*) -------------------------
+}  // extern "C"
+namespace {
+struct BtkLayout {
+    size_t td, st, hist, blk, total;
+    int64_t blocks;
+};
+BtkLayout btk_layout(int T, const int64_t* numels) {
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    BtkLayout L{};
+    for (int t = 0; t < T; ++t) L.blocks += (numels[t] + lossy::kBkmChunk - 1) / lossy::kBkmChunk;
+    L.td = 0;
+    L.st = L.td + al(sizeof(lossy::BkmTensor) * T);
+    L.hist = L.st + al(sizeof(lossy::BtkState) * T);
+    L.blk = L.hist + al(sizeof(uint32_t) * lossy::kRadix * T);
+    L.total = L.blk + al(sizeof(lossy::BtkBlock) * (size_t)std::max<int64_t>(L.blocks, 1));
+    return L;
+}
+}  // namespace
+extern "C" {
+
+size_t ofl_sparsify_topk_batch_workspace_bytes(int ntensors, const int64_t* numels) {
+    if (ntensors < 1 || !numels) return 256;
+    return btk_layout(ntensors, numels).total + 256;
+}
+
+int ofl_sparsify_topk_batch(int ntensors, const float* x_arena, const int64_t* offsets, const int64_t* numels,
+                            const int64_t* ks, float* sparse_arena, float* kept_min, int64_t* n_pos, int64_t* n_neg,
+                            int64_t* n_zero, double* abs_sum, int32_t* shifted, void* ws, size_t ws_bytes,
+                            void* stream) {
+    if (ntensors < 1 || !x_arena || !sparse_arena || !offsets || !numels || !ks)
+        return lfail(OFL_EINVAL, "sparsify: empty batch");
+    for (int t = 0; t < ntensors; ++t)
+        if (ks[t] < 1 || ks[t] > numels[t] || numels[t] > (int64_t)lossy::kBkmChunk * 0x7fffffff)
+            return lfail(OFL_EINVAL, "sparsify: need 1 <= k <= n");
+    const BtkLayout L = btk_layout(ntensors, numels);
+    if (!ws || ws_bytes < L.total) return lfail(OFL_ESPACE, "sparsify: workspace too small");
+    if (L.blocks > 0x7fffffff) return lfail(OFL_EINVAL, "sparsify: batch too large");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    char* w = static_cast<char*>(ws);
+    std::vector<lossy::BkmTensor> td(ntensors);
+    std::vector<lossy::BtkState> sh(ntensors);
+    int64_t blk = 0;
+    for (int t = 0; t < ntensors; ++t) {
+        const int64_t nb = (numels[t] + lossy::kBkmChunk - 1) / lossy::kBkmChunk;
+        td[t] = {offsets[t], numels[t], (int32_t)blk, (int32_t)nb};
+        blk += nb;
+        sh[t] = lossy::BtkState{};
+        sh[t].k = sh[t].need = ks[t];
+    }
+    lossy::BtkArgs a{};
+    a.x = x_arena;
+    a.out = sparse_arena;
+    a.td = reinterpret_cast<lossy::BkmTensor*>(w + L.td);
+    a.ntensors = ntensors;
+    a.st = reinterpret_cast<lossy::BtkState*>(w + L.st);
+    a.hist = reinterpret_cast<uint32_t*>(w + L.hist);
+    a.blk = reinterpret_cast<lossy::BtkBlock*>(w + L.blk);
+    LHIP(hipMemcpyAsync(w + L.td, td.data(), sizeof(lossy::BkmTensor) * ntensors, hipMemcpyHostToDevice, st));
+    LHIP(hipMemcpyAsync(w + L.st, sh.data(), sizeof(lossy::BtkState) * ntensors, hipMemcpyHostToDevice, st));
+    LHIP(hipMemsetAsync(w + L.hist, 0, L.blk - L.hist, st));
+    const dim3 g((unsigned)L.blocks), b(lossy::kNT);
+    for (int pass = 0; pass < 3; ++pass) {
+        a.pass = pass;
+        hipLaunchKernelGGL(lossy::k_btk_hist, g, b, 0, st, a);
+        hipLaunchKernelGGL(lossy::k_btk_digit, dim3(ntensors), dim3(64), 0, st, a);
+    }
+    hipLaunchKernelGGL(lossy::k_btk_ties, g, b, 0, st, a);
+    hipLaunchKernelGGL(lossy::k_btk_scan, dim3(ntensors), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(lossy::k_btk_select, g, b, 0, st, a);
+    hipLaunchKernelGGL(lossy::k_btk_final, dim3(ntensors), dim3(64), 0, st, a);
+    LHIP(hipGetLastError());
+    LHIP(hipMemcpyAsync(sh.data(), w + L.st, sizeof(lossy::BtkState) * ntensors, hipMemcpyDeviceToHost, st));
+    LHIP(hipStreamSynchronize(st));
+    for (int t = 0; t < ntensors; ++t) {
+        if (kept_min) kept_min[t] = sh[t].kmin;
+        if (shifted) shifted[t] = sh[t].shift != 0.0f;
+        if (n_pos) n_pos[t] = sh[t].n_pos;
+        if (n_neg) n_neg[t] = sh[t].n_neg;
+        if (n_zero) n_zero[t] = sh[t].n_zero;
+        if (abs_sum) abs_sum[t] = sh[t].abs_sum;
+    }
+    return OFL_OK;
+}
+
+// top-k by magnitude of one tensor (skc/stc SparsityTransformer._topk_func,
+// skc_pipeline.py:72-94): the batched path with T = 1.  Exact k-th largest
+// |x|; ties at the threshold kept lowest index first; dense float32 sparse
+// array (kept values + shift, zeros elsewhere; shift = 1e-7 iff min(kept) <
+// 1e-7, :92-93) and the kept-set statistics of the ternary / k-means stages.
 int ofl_sparsify_topk(const float* x, int64_t n, int64_t k, float* sparse_out, float* kept_min,
                       int64_t* n_pos, int64_t* n_neg, int64_t* n_zero, double* abs_sum, int* shifted,
                       void* ws, size_t ws_bytes, void* stream) {
-    if (k < 1 || k > n) return lfail(OFL_EINVAL, "sparsify: need 1 <= k <= n");
+    const int64_t off = 0;
+    int32_t sh = 0;
+    const int rc = ofl_sparsify_topk_batch(1, x, &off, &n, &k, sparse_out, kept_min, n_pos, n_neg, n_zero, abs_sum,
+                                           &sh, ws, ws_bytes, stream);
+    if (rc == OFL_OK && shifted) *shifted = sh;
+    return rc;
+}
+
+size_t ofl_ternary_ranks_batch_workspace_bytes(int ntensors) {
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    return al(sizeof(lossy::BkmTensor) * std::max(ntensors, 1)) + al(12 * (size_t)std::max(ntensors, 1)) + 256;
+}
+
+int ofl_ternary_ranks_batch(int ntensors, const float* sparse_arena, const int64_t* offsets, const int64_t* numels,
+                            const float* ranks3, float* out_arena, void* ws, size_t ws_bytes, void* stream) {
+    if (ntensors < 1 || !offsets || !numels || !ranks3) return lfail(OFL_EINVAL, "ternary: empty batch");
+    if (!ws || ws_bytes < ofl_ternary_ranks_batch_workspace_bytes(ntensors))
+        return lfail(OFL_ESPACE, "ternary: workspace too small");
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     hipStream_t st = static_cast<hipStream_t>(stream);
-    Scratch sc{static_cast<char*>(ws), ws_bytes};
-    uint32_t* hist = sc.take<uint32_t>(lossy::kRadix);
-    const int g = grid_for(n);
-    const int64_t per_block = (n + g - 1) / g;
-    uint32_t* bt = sc.take<uint32_t>(g);
-    uint64_t* tb = sc.take<uint64_t>(g);
-    uint32_t* kmin = sc.take<uint32_t>(1);
-    unsigned long long* cnts = sc.take<unsigned long long>(3);
-    double* as = sc.take<double>(1);
-    if (!as) return lfail(OFL_ESPACE, "sparsify: workspace too small");
-    // radix select: the k-th largest magnitude (31 bits: 11 + 11 + 9)
-    uint32_t prefix = 0, pmask = 0;
-    int64_t need = k;  // rank from the top within the current prefix
-    const int shifts[3] = {20, 9, 0};
-    const int widths[3] = {11, 11, 9};
-    std::vector<uint32_t> h(lossy::kRadix);
-    for (int pass = 0; pass < 3; ++pass) {
-        LHIP(hipMemsetAsync(hist, 0, 4 * lossy::kRadix, st));
-        hipLaunchKernelGGL(lossy::k_abs_radix, dim3(g), dim3(lossy::kNT), 0, st, x, n, prefix, pmask, shifts[pass],
-                           (uint32_t)((1 << widths[pass]) - 1), hist);
-        LHIP(hipMemcpyAsync(h.data(), hist, 4 * lossy::kRadix, hipMemcpyDeviceToHost, st));
-        LHIP(hipStreamSynchronize(st));
-        const int nb = 1 << widths[pass];
-        int d = nb - 1;
-        for (; d > 0; --d) { if ((int64_t)h[d] >= need) break; need -= h[d]; }
-        prefix |= (uint32_t)d << shifts[pass];
-        pmask |= (uint32_t)(nb - 1) << shifts[pass];
+    char* w = static_cast<char*>(ws);
+    const size_t o_r = al(sizeof(lossy::BkmTensor) * ntensors);
+    std::vector<lossy::BkmTensor> td(ntensors);
+    int64_t blk = 0;
+    for (int t = 0; t < ntensors; ++t) {
+        const int64_t nb = (numels[t] + lossy::kBkmChunk - 1) / lossy::kBkmChunk;
+        td[t] = {offsets[t], numels[t], (int32_t)blk, (int32_t)nb};
+        blk += nb;
     }
-    const uint32_t T = prefix;  // exact bits of the k-th largest |x|; `need` ties at T are kept
-    // per-block tie counts -> exclusive prefix (host)
-    LHIP(hipMemsetAsync(bt, 0, 4 * g, st));
-    hipLaunchKernelGGL(lossy::k_tie_count, dim3(g), dim3(lossy::kNT), 0, st, x, n, per_block, T, bt);
-    std::vector<uint32_t> bth(g);
-    LHIP(hipMemcpyAsync(bth.data(), bt, 4 * g, hipMemcpyDeviceToHost, st));
-    LHIP(hipStreamSynchronize(st));
-    std::vector<uint64_t> tbh(g);
-    uint64_t acc = 0;
-    for (int b = 0; b < g; ++b) { tbh[b] = acc; acc += bth[b]; }
-    LHIP(hipMemcpyAsync(tb, tbh.data(), 8 * g, hipMemcpyHostToDevice, st));
-    lossy::SelParams sp{T, need, per_block, 0.0f};
-    // pass 1: kept min (decides the shift); pass 2: with the shift, write + stats
-    for (int pass = 0; pass < 2; ++pass) {
-        const uint32_t kinit = 0xffffffffu;
-        LHIP(hipMemcpyAsync(kmin, &kinit, 4, hipMemcpyHostToDevice, st));
-        LHIP(hipMemsetAsync(cnts, 0, 24, st));
-        LHIP(hipMemsetAsync(as, 0, 8, st));
-        hipLaunchKernelGGL(lossy::k_select, dim3(g), dim3(lossy::kNT), 0, st, x, n, sp, tb,
-                           pass == 1 ? sparse_out : nullptr, reinterpret_cast<float*>(kmin), cnts, as);
-        uint32_t km;
-        unsigned long long ch[3];
-        double ash;
-        LHIP(hipMemcpyAsync(&km, kmin, 4, hipMemcpyDeviceToHost, st));
-        LHIP(hipMemcpyAsync(ch, cnts, 24, hipMemcpyDeviceToHost, st));
-        LHIP(hipMemcpyAsync(&ash, as, 8, hipMemcpyDeviceToHost, st));
-        LHIP(hipStreamSynchronize(st));
-        const float mn = unkey(km);
-        if (pass == 0) {
-            // reference: `if min(topk_mag) - 0 < 10e-8: topk_mag = topk_mag + 10e-8`
-            sp.shift = ((double)mn < 10e-8) ? (float)10e-8 : 0.0f;
-            if (kept_min) *kept_min = mn;
-            if (shifted) *shifted = sp.shift != 0.0f;
-        } else {
-            if (n_pos) *n_pos = (int64_t)ch[0];
-            if (n_neg) *n_neg = (int64_t)ch[1];
-            if (n_zero) *n_zero = (int64_t)ch[2];
-            if (abs_sum) *abs_sum = ash;
-        }
-    }
+    if (blk == 0) return OFL_OK;
+    if (blk > 0x7fffffff) return lfail(OFL_EINVAL, "ternary: batch too large");
+    LHIP(hipMemcpyAsync(w, td.data(), sizeof(lossy::BkmTensor) * ntensors, hipMemcpyHostToDevice, st));
+    LHIP(hipMemcpyAsync(w + o_r, ranks3, 12 * (size_t)ntensors, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(lossy::k_ternary_batch, dim3((unsigned)blk), dim3(lossy::kNT), 0, st, sparse_arena, out_arena,
+                       reinterpret_cast<lossy::BkmTensor*>(w), ntensors, reinterpret_cast<float*>(w + o_r));
+    LHIP(hipGetLastError());
     return OFL_OK;
 }
 

@@ -123,6 +123,49 @@ def sparsify_topk(x, k):
                  "abs_sum": asum.value, "shifted": bool(shifted.value), "k": int(k)}
 
 
+def sparsify_topk_batch(x_arena, offsets, numels, ks, sparse_out):
+    """sparsify_topk for every tensor of a float32 arena in one device pass
+    sequence (ofl_sparsify_topk_batch): tensor t = x_arena[offsets[t]:
+    offsets[t] + numels[t]], keep ks[t]; sparse_out (device, same layout)
+    gets the dense sparse arrays.  -> dict of per-tensor numpy stats."""
+    _check_dev(x_arena)
+    _check_dev(sparse_out)
+    L = _lib.lib()
+    T = len(numels)
+    off = np.ascontiguousarray(offsets, np.int64)
+    num = np.ascontiguousarray(numels, np.int64)
+    kk = np.ascontiguousarray(ks, np.int64)
+    ws = _ws_bytes(x_arena.device, int(L.ofl_sparsify_topk_batch_workspace_bytes(T, num.ctypes.data)))
+    kmin = np.zeros(T, np.float32)
+    npos, nneg, nzero = np.zeros(T, np.int64), np.zeros(T, np.int64), np.zeros(T, np.int64)
+    asum = np.zeros(T, np.float64)
+    shifted = np.zeros(T, np.int32)
+    _lib.check_lossy(L.ofl_sparsify_topk_batch(T, x_arena.data_ptr(), off.ctypes.data, num.ctypes.data,
+                                               kk.ctypes.data, sparse_out.data_ptr(), kmin.ctypes.data,
+                                               npos.ctypes.data, nneg.ctypes.data, nzero.ctypes.data,
+                                               asum.ctypes.data, shifted.ctypes.data, ws.data_ptr(), ws.numel(),
+                                               _stream(x_arena.device)))
+    return {"kept_min": kmin, "n_pos": npos, "n_neg": nneg, "n_zero": nzero, "abs_sum": asum,
+            "shifted": shifted.astype(bool), "k": kk}
+
+
+def ternary_ranks_batch(sparse_arena, offsets, numels, ranks3, out_arena):
+    """ternary_ranks for every tensor of an arena (ranks3[t] = (rank_neg,
+    rank_zero, rank_pos) of tensor t) in one launch."""
+    _check_dev(sparse_arena)
+    _check_dev(out_arena)
+    L = _lib.lib()
+    T = len(numels)
+    off = np.ascontiguousarray(offsets, np.int64)
+    num = np.ascontiguousarray(numels, np.int64)
+    r3 = np.ascontiguousarray(ranks3, np.float32).reshape(T, 3)
+    ws = _ws_bytes(sparse_arena.device, int(L.ofl_ternary_ranks_batch_workspace_bytes(T)))
+    _lib.check_lossy(L.ofl_ternary_ranks_batch(T, sparse_arena.data_ptr(), off.ctypes.data, num.ctypes.data,
+                                               r3.ctypes.data, out_arena.data_ptr(), ws.data_ptr(), ws.numel(),
+                                               _stream(sparse_arena.device)))
+    return out_arena
+
+
 def ternary_stats(x):
     """(n_pos, n_neg, fp64 sum |x|) of a float32 device vector."""
     _check_dev(x)

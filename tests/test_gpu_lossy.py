@@ -226,3 +226,86 @@ def test_kc_large_vs_sklearn():
     y = pipe.backward(payload, mds)
     assert y.shape == x.shape
     assert np.linalg.norm(y - x) / np.linalg.norm(x) < 0.3
+
+
+def _topk_ref(x, k):
+    """numpy restatement of SparsityTransformer._topk_func (skc_pipeline.py:
+    72-94) with ties at the k-th magnitude kept lowest index first."""
+    order = np.argsort(-np.abs(x), kind="stable")[:k]
+    kept = np.zeros(x.size, bool)
+    kept[order] = True
+    shift = np.float32(1e-7) if np.min(x[kept]) < 1e-7 else np.float32(0)
+    sp = np.where(kept, x + shift, np.float32(0)).astype(np.float32)
+    v = sp[kept]
+    return sp, {"n_pos": int(np.sum(v > 0)), "n_neg": int(np.sum(v < 0)), "n_zero": int(np.sum(v == 0)),
+                "abs_sum": float(np.sum(np.abs(v.astype(np.float64)))), "shifted": bool(shift),
+                "kept_min": np.min(x[kept])}
+
+
+def test_sparsify_topk_batch_vs_numpy():
+    """Batched device top-k (ofl_sparsify_topk_batch) against the numpy
+    restatement: ragged / unaligned offsets, ties straddling 64 Ki-element
+    blocks (partial keep inside one block), negative and positive ties at the
+    threshold, an all-zero tensor, k = 1 and k = n.  Bit-exact sparse arrays,
+    exact counts; fp64 |sum| to 1e-12; deterministic across runs."""
+    from openfl_amd import lossy
+    rng = np.random.default_rng(23)
+    xs, ks = [], []
+    a = rng.standard_normal(300_000).astype(np.float32)
+    a[rng.choice(a.size, 5000, replace=False)] = np.float32(2.5) * rng.choice([-1, 1], 5000).astype(np.float32)
+    xs.append(a); ks.append(int(np.sum(np.abs(a) > 2.5)) + 2600)       # partial keep of the 5000 ties
+    b = np.zeros(200_000, np.float32)
+    b[1::3] = -0.5                                                       # negative ties only
+    b[70_000] = 9.0
+    xs.append(b); ks.append(30_000)
+    c = np.zeros(1000, np.float32)
+    xs.append(c); ks.append(10)                                          # all zeros: T = 0
+    d = rng.standard_normal(4097).astype(np.float32)
+    xs.append(d); ks.append(1)
+    e = np.abs(rng.standard_normal(5000)).astype(np.float32) + np.float32(1.0)
+    xs.append(e); ks.append(5000)                                        # k = n, no shift
+    f = rng.standard_normal(1 << 20).astype(np.float32)
+    xs.append(f); ks.append(int(np.ceil(f.size * 0.1)))
+    offs, acc = [], 0
+    for x in xs:
+        offs.append(acc)
+        acc += x.size + 3                                                # unaligned
+    arena = torch.zeros(acc, dtype=torch.float32, device=DEV)
+    for x, o in zip(xs, offs):
+        arena[o:o + x.size] = torch.from_numpy(x).to(DEV)
+    res = []
+    for _ in range(2):
+        out = torch.full_like(arena, 7.0)
+        st = lossy.sparsify_topk_batch(arena, offs, [x.size for x in xs], ks, out)
+        res.append((out.cpu().numpy(), st))
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    out, st = res[0]
+    for t, (x, o, k) in enumerate(zip(xs, offs, ks)):
+        sp, ref = _topk_ref(x, k)
+        np.testing.assert_array_equal(out[o:o + x.size], sp, err_msg=str(t))
+        for key in ("n_pos", "n_neg", "n_zero", "shifted"):
+            assert st[key][t] == ref[key], (t, key)
+        assert st["kept_min"][t] == ref["kept_min"], t
+        assert abs(st["abs_sum"][t] - ref["abs_sum"]) <= 1e-12 * max(ref["abs_sum"], 1e-30), t
+        assert res[1][1]["abs_sum"][t] == st["abs_sum"][t]
+    # per-tensor entry point = batch of one
+    sp1, st1 = lossy.sparsify_topk(torch.from_numpy(xs[0]).to(DEV), ks[0])
+    np.testing.assert_array_equal(sp1.cpu().numpy(), out[offs[0]:offs[0] + xs[0].size])
+
+
+def test_ternary_ranks_batch_equals_single():
+    from openfl_amd import lossy
+    rng = np.random.default_rng(8)
+    numels = [70_001, 5, 131_072]
+    offs, acc = [], 0
+    for n in numels:
+        offs.append(acc)
+        acc += n + 1
+    x = rng.standard_normal(acc).astype(np.float32)
+    x[rng.random(acc) < 0.5] = 0
+    xd = torch.from_numpy(x).to(DEV)
+    r3 = [(0.0, 1.0, 2.0), (0.0, 0.0, 1.0), (1.0, 0.0, 2.0)]
+    out = torch.full_like(xd, -1.0)
+    lossy.ternary_ranks_batch(xd, offs, numels, r3, out)
+    for o, n, r in zip(offs, numels, r3):
+        assert torch.equal(out[o:o + n], lossy.ternary_ranks(xd[o:o + n].contiguous(), *r))

@@ -48,6 +48,8 @@ class Arena:
             self.x[o:o + x.numel()] = x
         self.ranks = torch.empty_like(self.x)
         self.y = torch.empty_like(self.x)
+        self.sparse = torch.empty_like(self.x)
+        self.ks = [int(np.ceil(n * 0.1)) for n in self.numels]   # p_sparsity 0.1
 
     def view(self, a, t):
         return a[self.offsets[t]:self.offsets[t] + self.numels[t]]
@@ -75,8 +77,37 @@ def kc_plugin_step(xs):
         lossy.lut_decode(ranks, m)
 
 
-def stc_step(xs):
-    """STCPipeline.forward device part (top-k, ternary ranks) + LUT decode."""
+def stc_step(ar):
+    """STCPipeline.forward device part for the whole set (batched top-k, ternary
+    ranks) + batched LUT decode; the ternary maps are O(1) host work per tensor."""
+    from openfl_amd import lossy
+    from openfl_amd.pipelines.stc_pipeline import ternary_map
+    st = lossy.sparsify_topk_batch(ar.x, ar.offsets, ar.numels, ar.ks, ar.sparse)
+    maps, r3 = [], []
+    for t, n in enumerate(ar.numels):
+        m, r = ternary_map(n, st["n_pos"][t], st["n_neg"][t], st["abs_sum"][t])
+        maps.append(m)
+        r3.append(r)
+    lossy.ternary_ranks_batch(ar.sparse, ar.offsets, ar.numels, r3, ar.ranks)
+    lossy.lut_decode_batch(ar.ranks, ar.offsets, ar.numels, maps, ar.y)
+    return ar.y
+
+
+def skc_step(ar):
+    """SKCPipeline.forward device part for the whole set (batched top-k, batched
+    k-means of the sparse vectors with float64 centre values) + LUT decode."""
+    from openfl_amd import lossy
+    lossy.sparsify_topk_batch(ar.x, ar.offsets, ar.numels, ar.ks, ar.sparse)
+    _, _, _, uniq = lossy.kmeans_batch(ar.sparse, ar.offsets, ar.numels, 6, n_init=6,
+                                       seed=int(np.random.randint(0, 2 ** 31 - 1)), value_f64=True,
+                                       ranks_out=ar.ranks)
+    maps = [{i: u for i, u in enumerate(uniq[t])} for t in range(len(ar.numels))]
+    lossy.lut_decode_batch(ar.ranks, ar.offsets, ar.numels, maps, ar.y)
+    return ar.y
+
+
+def stc_plugin_step(xs):
+    """STC per tensor (SparsityTransformer / TernaryTransformer plugin calls)."""
     from openfl_amd import lossy
     from openfl_amd.pipelines.stc_pipeline import ternary_map
     for x in xs:
@@ -86,8 +117,8 @@ def stc_step(xs):
         lossy.lut_decode(lossy.ternary_ranks(sparse, rn, rz, rp), m)
 
 
-def skc_step(xs):
-    """SKCPipeline.forward device part (top-k, k-means of the sparse vector) + LUT decode."""
+def skc_plugin_step(xs):
+    """SKC per tensor (SparsityTransformer / KmeansTransformer plugin calls)."""
     from openfl_amd import lossy
     from openfl_amd.pipelines.lossy_common import kmeans_ranks
     for x in xs:
@@ -153,8 +184,9 @@ def main():
 
     ar = Arena(xs)
     res = {}
-    for name, fn, arg in (("kc", kc_step, ar), ("kc_plugin", kc_plugin_step, xs), ("stc", stc_step, xs),
-                          ("skc", skc_step, xs)):
+    for name, fn, arg in (("kc", kc_step, ar), ("kc_plugin", kc_plugin_step, xs), ("stc", stc_step, ar),
+                          ("stc_plugin", stc_plugin_step, xs), ("skc", skc_step, ar),
+                          ("skc_plugin", skc_plugin_step, xs)):
         if name.split("_")[0] not in only:
             continue
         t = timed(fn, arg, args.steps, args.warmup)
