@@ -721,11 +721,13 @@ __global__ __launch_bounds__(1 << (P_LOG - 5)) void k_dec_small(KArgs a) {
 }
 
 // ===========================================================================
-// Tiny slices (P <= 2^10): one 64-thread workgroup per slice, LDS-resident.
+// Tiny slices (P <= 2^10): one 256-thread workgroup per slice, LDS-resident
+// (latency-bound: more threads per slice shorten every stage).
 // ===========================================================================
+constexpr int kTinyNT = 256;
 DEVI void fwht_lds_generic(float* s, int P) {
     for (int h = 1; h < P; h <<= 1) {
-        for (int q = threadIdx.x; q < (P >> 1); q += 64) {
+        for (int q = threadIdx.x; q < (P >> 1); q += kTinyNT) {
             const int i = ((q & ~(h - 1)) << 1) | (q & (h - 1));
             const float a = s[i], b = s[i + h];
             s[i] = a + b;
@@ -735,45 +737,45 @@ DEVI void fwht_lds_generic(float* s, int P) {
     }
 }
 
-__global__ __launch_bounds__(64) void k_enc_tiny(KArgs a) {
+__global__ __launch_bounds__(kTinyNT) void k_enc_tiny(KArgs a) {
     __shared__ float s[1024];
     __shared__ unsigned char bins[1024];
     __shared__ QTab qt[1];
-    __shared__ float red[1];
+    __shared__ float red[kTinyNT / 64];
     const SliceDesc D = a.d[a.list[blockIdx.x]];
     const int p = D.logp, P = 1 << p;
     const uint32_t seed = a.seeds[D.tensor];
     const uint32_t b1 = seed_b(seed), b2 = seed_b(seed + 1u);
-    load_qtable<64>(qt, a.nbits);
+    load_qtable<kTinyNT>(qt, a.nbits);
     const float* x = a.xin + D.x_off;
-    for (int e = threadIdx.x; e < P; e += 64) s[e] = sgn_elem(e < D.len ? x[e] : 0.0f, e, p, b1);
+    for (int e = threadIdx.x; e < P; e += kTinyNT) s[e] = sgn_elem(e < D.len ? x[e] : 0.0f, e, p, b1);
     __syncthreads();
     fwht_lds_generic(s, P);
     const float m2 = pow2i(-(p / 2));
-    for (int e = threadIdx.x; e < P; e += 64) s[e] = sgn_elem(s[e] * m2, e, p, b2);
+    for (int e = threadIdx.x; e < P; e += kTinyNT) s[e] = sgn_elem(s[e] * m2, e, p, b2);
     __syncthreads();
     fwht_lds_generic(s, P);
     const float ysc = pow2i(-((p + 1) / 2));
     float ss = 0.f;
-    for (int e = threadIdx.x; e < P; e += 64) { const float y = s[e] * ysc; s[e] = y; ss += y * y; }
-    ss = block_sum<64>(ss, red);
+    for (int e = threadIdx.x; e < P; e += kTinyNT) { const float y = s[e] * ysc; s[e] = y; ss += y * y; }
+    ss = block_sum<kTinyNT>(ss, red);
     const float nu = sqrtf(ss);
     const bool pos = nu > 0.0f;
     const float zm64 = 64.0f * (sqrtf((float)P) / nu);
     float dot = 0.f;
-    for (int e = threadIdx.x; e < P; e += 64) {
+    for (int e = threadIdx.x; e < P; e += kTinyNT) {
         float c;
         const int b = pos ? quant(s[e] * zm64, qt, c) : 0;
         if (pos) dot += c * s[e];
         bins[e] = (unsigned char)b;
     }
-    dot = block_sum<64>(dot, red);
+    dot = block_sum<kTinyNT>(dot, red);
     float scale = pos ? (nu * nu) / dot : 0.0f;
     const bool zero = !pos || isnan(scale);
     if (zero) scale = 0.0f;
     __syncthreads();
     uint8_t* pl = a.pout + D.pl_off;
-    for (int q = threadIdx.x; q < (P >> 3) * a.nbits; q += 64) {
+    for (int q = threadIdx.x; q < (P >> 3) * a.nbits; q += kTinyNT) {
         const int i = q / (P >> 3), j = q % (P >> 3);
         uint32_t by = 0;
         if (!zero)
@@ -783,14 +785,14 @@ __global__ __launch_bounds__(64) void k_enc_tiny(KArgs a) {
     if (threadIdx.x == 0) a.scales[D.scale_idx] = scale;
 }
 
-__global__ __launch_bounds__(64) void k_dec_tiny(KArgs a) {
+__global__ __launch_bounds__(kTinyNT) void k_dec_tiny(KArgs a) {
     __shared__ float s[1024];
     const SliceDesc D = a.d[a.list[blockIdx.x]];
     const int p = D.logp, P = 1 << p;
     const uint32_t seed = a.seeds[D.tensor];
     const uint32_t b1 = seed_b(seed), b2 = seed_b(seed + 1u);
     const uint8_t* pl = a.pin + D.pl_off;
-    for (int e = threadIdx.x; e < P; e += 64) {
+    for (int e = threadIdx.x; e < P; e += kTinyNT) {
         int b = 0;
         for (int i = 0; i < a.nbits; ++i) b |= ((pl[(int64_t)i * D.pl_stride + (e >> 3)] >> (e & 7)) & 1) << i;
         s[e] = g_centroids[a.nbits - 1][b];
@@ -798,13 +800,13 @@ __global__ __launch_bounds__(64) void k_dec_tiny(KArgs a) {
     __syncthreads();
     fwht_lds_generic(s, P);
     const float m2 = pow2i(-(p / 2));
-    for (int e = threadIdx.x; e < P; e += 64) s[e] = sgn_elem(s[e] * m2, e, p, b2);
+    for (int e = threadIdx.x; e < P; e += kTinyNT) s[e] = sgn_elem(s[e] * m2, e, p, b2);
     __syncthreads();
     fwht_lds_generic(s, P);
     const float m1 = pow2i(-((p + 1) / 2));
     const float sc = a.scales_in[D.scale_idx];
     float* y = a.xout + D.y_off;
-    for (int e = threadIdx.x; e < P; e += 64)
+    for (int e = threadIdx.x; e < P; e += kTinyNT)
         if (e < D.ylen) y[e] = sc * sgn_elem(s[e] * m1, e, p, b1);
 }
 
@@ -1777,7 +1779,8 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
         hipError_t e = hipSuccess;
         switch (l.kind) {
         case K_TINY:
-            e = enc ? launch(ofl::k_enc_tiny, l.blocks, 64, 0, st, a) : launch(ofl::k_dec_tiny, l.blocks, 64, 0, st, a);
+            e = enc ? launch(ofl::k_enc_tiny, l.blocks, ofl::kTinyNT, 0, st, a)
+                    : launch(ofl::k_dec_tiny, l.blocks, ofl::kTinyNT, 0, st, a);
             break;
         case K_SMALL: {
             const int p = l.param;
@@ -1907,9 +1910,6 @@ void build_schedule(ofl_eden_plan* pl) {
         if (!pl->small[k].empty())
             common.push_back({K_SMALL, 11 + k, 0, 0, add_list(pl->small[k]), -1, (int)pl->small[k].size(),
                               (int64_t)pl->small[k].size()});
-    pl->enc = common;
-    pl->dec = common;
-
     const std::vector<int32_t>& large = pl->large;
     std::vector<std::vector<int32_t>> waves;
     int64_t cap = pl->wave_bytes > 0 ? pl->wave_bytes / 4 : INT64_MAX;
@@ -1928,6 +1928,16 @@ void build_schedule(ofl_eden_plan* pl) {
     }
     pl->nwaves = (int)waves.size();
     const int nbuf = waves.size() > 1 ? pl->nstreams : 1;
+    // the tiny / small slices are independent of the waves: they go on the
+    // stream with fewer large-slice elements, so they overlap the other's waves
+    if (nbuf == 2) {
+        int64_t load[2] = {0, 0};
+        for (size_t w = 0; w < waves.size(); ++w)
+            for (int32_t si : waves[w]) load[w % 2] += 1ll << pl->slices[si].logp;
+        for (Launch& l : common) l.stream = load[1] < load[0] ? 1 : 0;
+    }
+    pl->enc = common;
+    pl->dec = common;
     pl->ws_floats = nbuf * wmax;
     for (size_t w = 0; w < waves.size(); ++w) {
         int64_t off = (int64_t)(w % nbuf) * wmax;
