@@ -214,6 +214,45 @@ int ofl_lut_decode_batch(int ntensors, const float* in_arena, const int64_t* off
                          const int32_t* nk, const float* keys, const float* vals, int max_nk, float* out_arena,
                          void* ws, size_t ws_bytes, void* stream);
 
+/* ---- aggregator end of round (csrc/agg_kernels.hip) -------------------------
+ * Aggregator._prepare_trained (aggregator.py:780-865) runs, per tensor,
+ * WeightedAverage (weighted_average.py:12-14, np.average(tensors, weights,
+ * axis=0)), TensorCodec.generate_delta (tensor_codec.py:150-180: new - base),
+ * compress + decompress, and apply_delta (tensor_codec.py:182-211: base +
+ * delta).  These entry points do the arithmetic on flat device arenas
+ * (all tensors of a model update), bit-exact with NumPy: float64 products and
+ * an in-order float64 sum over collaborators, division by wsum (the float64
+ * sum of the weights, computed by the caller with NumPy), float64 subtraction
+ * of the float32 base.  Errors: ofl_agg_last_error().
+ *
+ * ofl_wavg_delta  xs: host array of ncollab device pointers (n floats each),
+ *                 weights: host [ncollab].  base may be NULL (delta = average).
+ *                 Outputs (device, any may be NULL): agg_out float64 average
+ *                 (required as running sums when ncollab > 16), delta64_out
+ *                 float64 delta, delta32_out the delta rounded to float32 (the
+ *                 codec input, Eden.compress :579).
+ * ofl_wavg_delta_ranges  the float64 delta at listed element ranges (host
+ *                 starts/counts; single[r] != 0: a single-element tensor,
+ *                 pairwise order as below), packed into out (device) -- the
+ *                 values the Eden seed's serial sums read.  Synchronous.
+ * ofl_wavg_delta_points  recompute listed elements (host idx) the way NumPy
+ *                 reduces a single-element tensor's (C, 1) stack: pairwise
+ *                 sum of the C products (1 <= ncollab <= 2048);
+ *                 call after ofl_wavg_delta for the 1-element tensors.
+ * ofl_apply_delta out = base + delta in float32 (out may alias either input). */
+const char* ofl_agg_last_error(void);
+int ofl_wavg_delta(int ncollab, const float* const* xs, const double* weights, double wsum, const float* base,
+                   int64_t n, double* agg_out, double* delta64_out, float* delta32_out, void* stream);
+size_t ofl_wavg_ranges_workspace_bytes(int ncollab, int nranges);
+int ofl_wavg_delta_ranges(int ncollab, const float* const* xs, const double* weights, double wsum,
+                          const float* base, int nranges, const int64_t* starts, const int64_t* counts,
+                          const int32_t* single, double* out, void* ws, size_t ws_bytes, void* stream);
+size_t ofl_wavg_points_workspace_bytes(int ncollab, int npoints);
+int ofl_wavg_delta_points(int ncollab, const float* const* xs, const double* weights, double wsum, const float* base,
+                          int npoints, const int64_t* idx, double* agg_out, double* delta64_out, float* delta32_out,
+                          void* ws, size_t ws_bytes, void* stream);
+int ofl_apply_delta(const float* base, const float* delta, int64_t n, float* out, void* stream);
+
 /* ---- host helpers ----------------------------------------------------------
  * Left-to-right serial sums in the array's own precision: the
  * `sum(data.flatten())` term of the reference seed formula

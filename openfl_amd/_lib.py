@@ -29,6 +29,8 @@ EXPORTS = (
     "ofl_lut_decode_batch_workspace_bytes", "ofl_lut_decode_batch",
     "ofl_sparsify_topk_batch_workspace_bytes", "ofl_sparsify_topk_batch",
     "ofl_ternary_ranks_batch_workspace_bytes", "ofl_ternary_ranks_batch",
+    "ofl_agg_last_error", "ofl_wavg_delta", "ofl_wavg_ranges_workspace_bytes", "ofl_wavg_delta_ranges",
+    "ofl_wavg_points_workspace_bytes", "ofl_wavg_delta_points", "ofl_apply_delta",
 )
 
 
@@ -103,6 +105,19 @@ def _bind(L):
     L.ofl_ternary_ranks_batch_workspace_bytes.restype = sz
     L.ofl_ternary_ranks_batch.argtypes = [i32, vp, vp, vp, vp, vp, vp, sz, vp]
     L.ofl_ternary_ranks_batch.restype = i32
+    L.ofl_agg_last_error.restype = ctypes.c_char_p
+    L.ofl_wavg_delta.argtypes = [i32, vp, vp, ctypes.c_double, vp, i64, vp, vp, vp, vp]
+    L.ofl_wavg_delta.restype = i32
+    L.ofl_wavg_ranges_workspace_bytes.argtypes = [i32, i32]
+    L.ofl_wavg_ranges_workspace_bytes.restype = sz
+    L.ofl_wavg_delta_ranges.argtypes = [i32, vp, vp, ctypes.c_double, vp, i32, vp, vp, vp, vp, vp, sz, vp]
+    L.ofl_wavg_delta_ranges.restype = i32
+    L.ofl_wavg_points_workspace_bytes.argtypes = [i32, i32]
+    L.ofl_wavg_points_workspace_bytes.restype = sz
+    L.ofl_wavg_delta_points.argtypes = [i32, vp, vp, ctypes.c_double, vp, i32, vp, vp, vp, vp, vp, sz, vp]
+    L.ofl_wavg_delta_points.restype = i32
+    L.ofl_apply_delta.argtypes = [vp, vp, i64, vp, vp]
+    L.ofl_apply_delta.restype = i32
     L.ofl_serial_sum_f32.argtypes = [vp, i64]
     L.ofl_serial_sum_f32.restype = ctypes.c_float
     L.ofl_serial_sum_f64.argtypes = [vp, i64]
@@ -129,6 +144,12 @@ def lib():
 def check_lossy(rc):
     if rc != OFL_OK:
         raise CodecError(lib().ofl_lossy_last_error().decode() or f"libofl_codec error {rc}")
+    return rc
+
+
+def check_agg(rc):
+    if rc != OFL_OK:
+        raise CodecError(lib().ofl_agg_last_error().decode() or f"libofl_codec error {rc}")
     return rc
 
 

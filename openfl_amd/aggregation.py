@@ -1,0 +1,265 @@
+"""The aggregator's end-of-round tensor work on the device.
+
+Reference (paths relative to /root/reference/openfl):
+  interface/aggregation_functions/weighted_average.py:12-58
+      WeightedAverage.call -> np.average(tensors, weights=weights, axis=0)
+  component/aggregator/aggregator.py:780-865  _prepare_trained, per tensor:
+      agg = WeightedAverage(local tensors)            (float64)
+      delta = TensorCodec.generate_delta(agg, base)   (agg - base, float64)
+      payload, md = TensorCodec.compress(delta)       (the compression pipeline)
+      dec = TensorCodec.decompress(payload, md)       (float32)
+      model = TensorCodec.apply_delta(dec, base)      (base + dec, float32)
+  pipelines/tensor_codec.py:150-211  generate_delta / apply_delta
+
+RoundEnd does that for every tensor of a model update in one device pass
+sequence over flat arenas (csrc/agg_kernels.hip + the Eden plan): average +
+delta in one kernel (float64 arithmetic in NumPy's order, delta rounded to
+float32 as Eden.compress does), the seeds' serial sums from the delta's values
+(fast mode: a 4096-element prefix per tensor, reference mode: all of it), one
+Eden encode and decode of all the big tensors, and apply_delta in place.  The
+payloads, metadata, np.random draws and new model are identical to calling
+the reference's functions tensor by tensor with an openfl_amd EdenPipeline
+(tests/test_gpu_aggregation.py).  No CPU fallback: without the library or a
+GPU every call raises CodecError.
+"""
+import numpy as np
+import torch
+
+from openfl_amd import _lib
+from openfl_amd.codec import EdenPlan, resolve_device
+from openfl_amd.pipelines.eden_pipeline import _FAST_SEED_PREFIX, _serial_sum, eden_seed
+
+_ALIGN = 64
+
+
+def _stream(device):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _f64_weights(weights, n):
+    w = np.asarray(weights)
+    if w.ndim != 1 or w.size != n:
+        raise _lib.CodecError("one weight per collaborator tensor")
+    if np.result_type(np.float32, w.dtype) != np.float64:
+        raise _lib.CodecError("weights must promote float32 tensors to float64 (np.average result dtype)")
+    return np.ascontiguousarray(w, np.float64)
+
+
+def weight_sum(weights, ndim):
+    """np.average's denominator for tensors of `ndim` dimensions: NumPy's own
+    float64 sum of the broadcast weights (weighted_average.py:14)."""
+    w = np.asarray(weights)
+    stack = np.zeros((w.size,) + (1,) * ndim, np.float32)
+    scl = np.average(stack, weights=w, axis=0, returned=True)[1]
+    return float(np.asarray(scl).reshape(-1)[0])
+
+
+def _wavg_launch(xs, w64, wsum, base, n, agg=None, delta64=None, delta32=None, device=None):
+    ptrs = np.asarray([x.data_ptr() for x in xs], np.uint64)
+    _lib.check_agg(_lib.lib().ofl_wavg_delta(
+        len(xs), ptrs.ctypes.data, w64.ctypes.data, wsum, base.data_ptr() if base is not None else None, int(n),
+        agg.data_ptr() if agg is not None else None, delta64.data_ptr() if delta64 is not None else None,
+        delta32.data_ptr() if delta32 is not None else None, _stream(device)))
+
+
+def _points_launch(xs, w64, wsum, base, idx, agg, delta32, device, ws):
+    ptrs = np.asarray([x.data_ptr() for x in xs], np.uint64)
+    ix = np.ascontiguousarray(idx, np.int64)
+    L = _lib.lib()
+    need = int(L.ofl_wavg_points_workspace_bytes(len(xs), ix.size))
+    buf = ws(need)
+    _lib.check_agg(L.ofl_wavg_delta_points(
+        len(xs), ptrs.ctypes.data, w64.ctypes.data, wsum, base.data_ptr() if base is not None else None, ix.size,
+        ix.ctypes.data, agg.data_ptr() if agg is not None else None, None,
+        delta32.data_ptr() if delta32 is not None else None, buf.data_ptr(), buf.numel(), _stream(device)))
+
+
+class _Scratch:
+    def __init__(self, device):
+        self.device = device
+        self.buf = None
+
+    def __call__(self, nbytes):
+        if self.buf is None or self.buf.numel() < nbytes:
+            self.buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=self.device)
+        return self.buf
+
+
+def weighted_average(tensors, weights, device=None):
+    """np.average(tensors, weights=weights, axis=0) on the GPU
+    (weighted_average.py:12-14): float32 tensors, float64 result, bit-exact."""
+    dev = resolve_device(device)
+    arrs = [np.asarray(t) for t in tensors]
+    if not arrs:
+        raise _lib.CodecError("weighted_average: no tensors")
+    shape = arrs[0].shape
+    if any(a.shape != shape or a.dtype != np.float32 for a in arrs):
+        raise _lib.CodecError("weighted_average: float32 tensors of one shape")
+    w64 = _f64_weights(weights, len(arrs))
+    wsum = weight_sum(w64, len(shape))
+    if wsum == 0.0:
+        raise ZeroDivisionError("Weights sum to zero, can't be normalized")
+    n = int(np.prod(shape, dtype=np.int64))
+    with torch.cuda.device(dev):
+        xs = [torch.from_numpy(np.ascontiguousarray(a).reshape(-1)).to(dev) for a in arrs]
+        agg = torch.empty(max(n, 1), dtype=torch.float64, device=dev)
+        if n == 1:
+            _points_launch(xs, w64, wsum, None, [0], agg, None, dev, _Scratch(dev))
+        elif n:
+            _wavg_launch(xs, w64, wsum, None, n, agg=agg, device=dev)
+        return agg[:n].cpu().numpy().reshape(shape)
+
+
+class WeightedAverage:
+    """AggregationFunction plugin (weighted_average.py:17-58): call(local_tensors, ...)
+    -> np.average of the LocalTensor tensors by their weights, on the GPU."""
+
+    def __init__(self, device=None):
+        self.device = device
+
+    def call(self, local_tensors, *_):
+        tensors, weights = zip(*[(x.tensor, x.weight) for x in local_tensors])
+        return weighted_average(tensors, weights, self.device)
+
+    def __call__(self, local_tensors, *args):
+        return self.call(local_tensors, *args)
+
+
+class RoundEnd:
+    """Aggregator._prepare_trained for a whole model update (aggregator.py:780-865).
+
+    pipeline: an openfl_amd EdenPipeline (its n_bits, dim_threshold and
+    seed_mode apply); shapes: the model's tensor shapes in the aggregator's
+    order.  Tensors live in flat float32 arenas, tensor i at offsets[i]
+    (64-element aligned); arena() / pack() / view() make and read them.
+    """
+
+    def __init__(self, pipeline, shapes, device=None):
+        tr = pipeline.transformers[0]
+        self.transformer = tr
+        self.device = resolve_device(device) if device is not None else tr.eden.device
+        self.dim_threshold = tr.dim_threshold
+        self.seed_mode = tr.seed_mode
+        self.n_bits = tr.eden.nbits
+        self.shapes = [tuple(int(d) for d in s) for s in shapes]
+        self.numels = [int(np.prod(s, dtype=np.int64)) for s in self.shapes]
+        self.offsets, acc = [], 0
+        for n in self.numels:
+            self.offsets.append(acc)
+            acc += (n + _ALIGN - 1) // _ALIGN * _ALIGN
+        self.arena_numel = max(acc, 1)
+        self.big = [i for i, n in enumerate(self.numels) if n > self.dim_threshold]
+        self.single = [i for i, n in enumerate(self.numels) if n == 1]
+        self.plan = EdenPlan([self.numels[i] for i in self.big], self.n_bits,
+                             elem_offsets=[self.offsets[i] for i in self.big]) if self.big else None
+        self._ws = _Scratch(self.device)
+        self._codec_ws = None
+
+    # -- arenas --
+    def arena(self):
+        return torch.zeros(self.arena_numel, dtype=torch.float32, device=self.device)
+
+    def pack(self, arrays):
+        a = self.arena()
+        for i, x in enumerate(arrays):
+            x = np.asarray(x, np.float32).reshape(-1)
+            if x.size != self.numels[i]:
+                raise _lib.CodecError(f"tensor {i}: {x.size} elements, expected {self.numels[i]}")
+            a[self.offsets[i]:self.offsets[i] + x.size] = torch.from_numpy(x).to(self.device)
+        return a
+
+    def view(self, arena, i):
+        return arena[self.offsets[i]:self.offsets[i] + self.numels[i]].view(self.shapes[i])
+
+    def _wsum(self, w64):
+        sums = {weight_sum(w64, d) for d in {len(s) for s in self.shapes}}
+        if len(sums) != 1:
+            raise _lib.CodecError("weight sums differ between tensor ranks")
+        s = sums.pop()
+        if s == 0.0:
+            raise ZeroDivisionError("Weights sum to zero, can't be normalized")
+        return s
+
+    def run(self, collab_arenas, weights, base_arena=None, agg_out=None, payloads=True, out=None):
+        """collab_arenas: one float32 device arena per collaborator (this
+        layout); weights: per collaborator; base_arena: the previous model
+        (None: no base, the delta is the average).  Writes the new model
+        into `out` (default: a new arena; may be base_arena) and, if given,
+        the float64 average into agg_out (arena_numel elements).
+        -> (new model arena, [(payload bytes, [metadata])] per tensor or None,
+        seeds)."""
+        dev = self.device
+        xs = list(collab_arenas)
+        for x in xs + ([base_arena] if base_arena is not None else []):
+            if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and x.numel() >= self.arena_numel):
+                raise _lib.CodecError("arenas must be contiguous float32 device tensors of arena_numel elements")
+        if agg_out is not None and not (agg_out.dtype == torch.float64 and agg_out.numel() >= self.arena_numel):
+            raise _lib.CodecError("agg_out must be float64 with arena_numel elements")
+        w64 = _f64_weights(weights, len(xs))
+        wsum = self._wsum(w64)
+        L = _lib.lib()
+        with torch.cuda.device(dev):
+            delta = torch.empty(self.arena_numel, dtype=torch.float32, device=dev)
+            if agg_out is None and len(xs) > 16:  # running sums between chained launches
+                agg_out = torch.empty(self.arena_numel, dtype=torch.float64, device=dev)
+            # 1. average + delta (float64), delta rounded to float32
+            _wavg_launch(xs, w64, wsum, base_arena, self.arena_numel, agg=agg_out, delta32=delta, device=dev)
+            if self.single:
+                _points_launch(xs, w64, wsum, base_arena, [self.offsets[i] for i in self.single], agg_out, delta,
+                               dev, self._ws)
+            # 2. seeds: serial sums of the float64 delta, one np.random draw per tensor in order
+            fast = self.seed_mode == "fast"
+            counts = [min(n, _FAST_SEED_PREFIX) if fast else n for n in self.numels]
+            single = np.asarray([1 if n == 1 else 0 for n in self.numels], np.int32)
+            tot = sum(counts)
+            packed = torch.empty(max(tot, 1), dtype=torch.float64, device=dev)
+            ptrs = np.asarray([x.data_ptr() for x in xs], np.uint64)
+            st_ = np.asarray(self.offsets, np.int64)
+            ct_ = np.asarray(counts, np.int64)
+            buf = self._ws(int(L.ofl_wavg_ranges_workspace_bytes(len(xs), len(counts))))
+            _lib.check_agg(L.ofl_wavg_delta_ranges(
+                len(xs), ptrs.ctypes.data, w64.ctypes.data, wsum,
+                base_arena.data_ptr() if base_arena is not None else None, len(counts), st_.ctypes.data,
+                ct_.ctypes.data, single.ctypes.data, packed.data_ptr(), buf.data_ptr(), buf.numel(), _stream(dev)))
+            ph = packed[:tot].cpu().numpy()
+            seeds, o = [], 0
+            for c in counts:
+                seeds.append(eden_seed(None, self.seed_mode, _serial_sum(ph[o:o + c]) if c else np.float64(0.0)))
+                o += c
+            # 3. encode, (payloads), decode in place, apply
+            result = [None] * len(self.numels) if payloads else None
+            if self.plan is not None:
+                p = self.plan
+                sd = torch.tensor([seeds[i] for i in self.big], dtype=torch.int32).to(dev)
+                planes = torch.empty(max(p.planes_bytes, 1), dtype=torch.uint8, device=dev)
+                scales = torch.empty(max(p.n_slices, 1), dtype=torch.float32, device=dev)
+                if self._codec_ws is None or self._codec_ws.numel() < p.ws_bytes:
+                    self._codec_ws = torch.empty(max(p.ws_bytes, 256), dtype=torch.uint8, device=dev)
+                p.encode(delta, sd, planes, scales, self._codec_ws)
+                if payloads:
+                    pn = planes[:p.planes_bytes].cpu().numpy()
+                    sn = scales[:p.n_slices].cpu().numpy()
+                    for t, i in enumerate(self.big):
+                        po, pb, fs = p.planes_offsets[t], p.planes_nbytes[t], p.first_slice[t]
+                        md = {0: float(seeds[i]), 1: float(self.numels[i])}
+                        for k, (s, d) in enumerate(zip(sn[fs:fs + len(p.dims[t])], p.dims[t])):
+                            md[2 + 2 * k] = float(s)
+                            md[3 + 2 * k] = float(d)
+                        result[i] = (pn[po:po + pb].tobytes(), [{"int_list": list(self.shapes[i]), "int_to_float": md}])
+                p.decode(planes, sd, scales, delta, self._codec_ws)
+            if payloads:
+                small = [i for i in range(len(self.numels)) if result[i] is None]
+                if small:  # float32 bytes of the delta (Float32NumpyArrayToBytes), one D2H
+                    dh = torch.cat([delta[self.offsets[i]:self.offsets[i] + self.numels[i]] for i in small]).cpu().numpy()
+                    o = 0
+                    for i in small:
+                        result[i] = (dh[o:o + self.numels[i]].tobytes(), [{"int_list": list(self.shapes[i])}])
+                        o += self.numels[i]
+            if out is None:
+                out = torch.empty(self.arena_numel, dtype=torch.float32, device=dev)
+            if base_arena is not None:
+                _lib.check_agg(L.ofl_apply_delta(base_arena.data_ptr(), delta.data_ptr(), self.arena_numel,
+                                                 out.data_ptr(), _stream(dev)))
+            else:
+                out.copy_(delta)
+        return out, result, seeds

@@ -1,0 +1,117 @@
+"""GPU: aggregator end-of-round arithmetic (csrc/agg_kernels.hip) and the fused
+RoundEnd against the reference's per-tensor sequence (aggregator.py:780-865:
+np.average -> generate_delta -> compress -> decompress -> apply_delta) run
+with the same pipeline on the host side of the API.  Everything is compared
+bit for bit: float64 averages, payload bytes, metadata, seeds, new model."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.mark.parametrize("C", [1, 2, 3, 9, 20])
+@pytest.mark.parametrize("shape", [(1000,), (7, 13), (2,), (1,), (), (3, 1, 5)])
+def test_weighted_average_bit_exact(C, shape):
+    from openfl_amd.aggregation import WeightedAverage, weighted_average
+    from openfl_amd.tensor_codec import LocalTensor
+    rng = np.random.default_rng(C * 100 + len(shape))
+    xs = [np.asarray(rng.standard_normal(shape) * 10.0 ** rng.integers(-3, 3)).astype(np.float32) for _ in range(C)]
+    w = list(rng.random(C) * 5)
+    ref = np.average(xs, weights=w, axis=0)
+    got = weighted_average(xs, w, DEV)
+    assert got.dtype == np.float64 and got.shape == ref.shape
+    np.testing.assert_array_equal(got, ref)
+    lt = [LocalTensor(f"c{i}", x, wi) for i, (x, wi) in enumerate(zip(xs, w))]
+    np.testing.assert_array_equal(WeightedAverage(DEV).call(lt), ref)
+
+
+def test_weighted_average_errors():
+    from openfl_amd import _lib
+    from openfl_amd.aggregation import weighted_average
+    x = np.ones(4, np.float32)
+    with pytest.raises(ZeroDivisionError):
+        weighted_average([x, x], [0.0, 0.0], DEV)
+    with pytest.raises(_lib.CodecError):
+        weighted_average([x, x.astype(np.float64)], [1.0, 1.0], DEV)
+
+
+def _reference_round(pipe, shapes, collabs, w, base):
+    """_prepare_trained per tensor with the host API (np.average, TensorCodec)."""
+    from openfl_amd.tensor_codec import TensorCodec, TensorKey
+    tc = TensorCodec(pipe)
+    payloads, models, aggs = [], [], []
+    for i, s in enumerate(shapes):
+        agg = np.average([c[i] for c in collabs], weights=w, axis=0)
+        aggs.append(agg)
+        key = TensorKey(f"t{i}", "aggregator_x", 0, False, ("aggregated",))
+        if base is not None:
+            dk, delta = tc.generate_delta(key, agg, base[i])
+        else:
+            dk, delta = key, agg
+        ck, payload, md = tc.compress(dk, delta)
+        payloads.append((payload, [dict(m) for m in md]))
+        _, dec = tc.decompress(ck, payload, md)
+        if base is not None:
+            _, new = tc.apply_delta(dk, dec, base[i])
+        else:
+            new = dec
+        models.append(np.asarray(new, np.float32))
+    return payloads, models, aggs
+
+
+@pytest.mark.parametrize("seed_mode", ["fast", "reference"])
+@pytest.mark.parametrize("with_base", [True, False])
+def test_round_end_matches_per_tensor(seed_mode, with_base):
+    from openfl_amd.aggregation import RoundEnd
+    from openfl_amd.pipelines import EdenPipeline
+    rng = np.random.default_rng(7)
+    shapes = [(64, 3, 3, 3), (64,), (1,), (300, 200), (5000,), (2, 2), (1 << 18,), (100,), (101,)]
+    C = 3
+    collabs = [[(rng.standard_normal(s) * 0.01).astype(np.float32) for s in shapes] for _ in range(C)]
+    base = [(rng.standard_normal(s) * 0.1).astype(np.float32) for s in shapes] if with_base else None
+    w = [0.2, 0.5, 0.3]
+    pipe = EdenPipeline(n_bits=8, device=DEV, seed_mode=seed_mode)
+    np.random.seed(11)
+    ref_pay, ref_models, ref_aggs = _reference_round(pipe, shapes, collabs, w, base)
+    after_ref = np.random.randint(0, 2 ** 31)
+
+    re = RoundEnd(pipe, shapes, DEV)
+    arenas = [re.pack(c) for c in collabs]
+    base_a = re.pack(base) if with_base else None
+    agg = torch.empty(re.arena_numel, dtype=torch.float64, device=DEV)
+    np.random.seed(11)
+    new, pay, seeds = re.run(arenas, w, base_a, agg_out=agg)
+    assert np.random.randint(0, 2 ** 31) == after_ref          # one draw per tensor, in order
+    for i, s in enumerate(shapes):
+        np.testing.assert_array_equal(re.view(agg, i).cpu().numpy(), ref_aggs[i], err_msg=str(i))
+        assert pay[i][0] == ref_pay[i][0], i
+        assert pay[i][1] == ref_pay[i][1], i
+        np.testing.assert_array_equal(re.view(new, i).cpu().numpy(), ref_models[i].reshape(s), err_msg=str(i))
+    # payloads decode with the plain pipeline
+    y = pipe.backward(pay[3][0], [dict(m) for m in pay[3][1]])
+    assert y.shape == shapes[3]
+
+
+def test_round_end_many_collaborators_chained():
+    """> 16 collaborators: the running float64 sums are chained through agg_out."""
+    from openfl_amd.aggregation import RoundEnd
+    from openfl_amd.pipelines import EdenPipeline
+    rng = np.random.default_rng(3)
+    shapes = [(4096,), (1,), (70_000,)]
+    C = 37
+    collabs = [[rng.standard_normal(s).astype(np.float32) for s in shapes] for _ in range(C)]
+    base = [rng.standard_normal(s).astype(np.float32) for s in shapes]
+    w = list(rng.random(C))
+    pipe = EdenPipeline(n_bits=4, device=DEV, seed_mode="fast")
+    np.random.seed(5)
+    ref_pay, ref_models, ref_aggs = _reference_round(pipe, shapes, collabs, w, base)
+    re = RoundEnd(pipe, shapes, DEV)
+    agg = torch.empty(re.arena_numel, dtype=torch.float64, device=DEV)
+    np.random.seed(5)
+    new, pay, _ = re.run([re.pack(c) for c in collabs], w, re.pack(base), agg_out=agg)
+    for i in range(len(shapes)):
+        np.testing.assert_array_equal(re.view(agg, i).cpu().numpy(), ref_aggs[i])
+        assert pay[i] == ref_pay[i]
+        np.testing.assert_array_equal(re.view(new, i).cpu().numpy(), ref_models[i])
