@@ -123,6 +123,12 @@ int ofl_eden_encode(ofl_eden_plan_t plan, const float* x_arena, const uint32_t* 
 int ofl_eden_decode(ofl_eden_plan_t plan, const uint8_t* planes_arena, const uint32_t* seeds,
                     const float* scales, float* y_arena, void* ws, size_t ws_bytes,
                     void* stream);
+/* decode fused with TensorCodec.apply_delta (tensor_codec.py:182-211):
+ * y = base + decoded, two float32 roundings as in NumPy (decoded delta first,
+ * then the add).  base_arena has the plan's layout; y_arena may alias it. */
+int ofl_eden_decode_add(ofl_eden_plan_t plan, const uint8_t* planes_arena, const uint32_t* seeds,
+                        const float* scales, const float* base_arena, float* y_arena, void* ws,
+                        size_t ws_bytes, void* stream);
 
 /* ---- profiling (bench.py) --------------------------------------------------
  * While enabled, every encode/decode of the plan records a HIP event before
@@ -235,11 +241,17 @@ int ofl_lut_decode_batch(int ntensors, const float* in_arena, const int64_t* off
  *                 starts/counts; single[r] != 0: a single-element tensor,
  *                 pairwise order as below), packed into out (device) -- the
  *                 values the Eden seed's serial sums read.  Synchronous.
+ * ofl_wavg_delta_range_sums  the same ranges, each summed left to right in
+ *                 float64 on the device (Python's sum() of the seed formula,
+ *                 eden_pipeline.py:771); sums: host [nranges].  Synchronous.
  * ofl_wavg_delta_points  recompute listed elements (host idx) the way NumPy
  *                 reduces a single-element tensor's (C, 1) stack: pairwise
  *                 sum of the C products (1 <= ncollab <= 2048);
  *                 call after ofl_wavg_delta for the 1-element tensors.
- * ofl_apply_delta out = base + delta in float32 (out may alias either input). */
+ * ofl_apply_delta out = base + delta in float32 (out may alias either input).
+ * ofl_apply_delta_ranges  the same on listed ranges; starts [nranges] and dst
+ *                 [nranges + 1] (exclusive prefix of the range lengths, dst[n]
+ *                 = total) are DEVICE arrays, so nothing synchronises. */
 const char* ofl_agg_last_error(void);
 int ofl_wavg_delta(int ncollab, const float* const* xs, const double* weights, double wsum, const float* base,
                    int64_t n, double* agg_out, double* delta64_out, float* delta32_out, void* stream);
@@ -247,11 +259,17 @@ size_t ofl_wavg_ranges_workspace_bytes(int ncollab, int nranges);
 int ofl_wavg_delta_ranges(int ncollab, const float* const* xs, const double* weights, double wsum,
                           const float* base, int nranges, const int64_t* starts, const int64_t* counts,
                           const int32_t* single, double* out, void* ws, size_t ws_bytes, void* stream);
+size_t ofl_wavg_range_sums_workspace_bytes(int ncollab, int nranges, int64_t total);
+int ofl_wavg_delta_range_sums(int ncollab, const float* const* xs, const double* weights, double wsum,
+                              const float* base, int nranges, const int64_t* starts, const int64_t* counts,
+                              const int32_t* single, double* sums, void* ws, size_t ws_bytes, void* stream);
 size_t ofl_wavg_points_workspace_bytes(int ncollab, int npoints);
 int ofl_wavg_delta_points(int ncollab, const float* const* xs, const double* weights, double wsum, const float* base,
                           int npoints, const int64_t* idx, double* agg_out, double* delta64_out, float* delta32_out,
                           void* ws, size_t ws_bytes, void* stream);
 int ofl_apply_delta(const float* base, const float* delta, int64_t n, float* out, void* stream);
+int ofl_apply_delta_ranges(const float* base, const float* delta, float* out, int nranges, const int64_t* starts,
+                           const int64_t* dst, int64_t total, void* stream);
 
 /* ---- host helpers ----------------------------------------------------------
  * Left-to-right serial sums in the array's own precision: the

@@ -21,7 +21,7 @@ EXPORTS = (
     "ofl_eden_plan_destroy", "ofl_eden_plan_set_schedule", "ofl_eden_plan_num_waves",
     "ofl_eden_plan_get_schedule", "ofl_eden_plan_num_slices", "ofl_eden_plan_planes_bytes",
     "ofl_eden_plan_workspace_bytes", "ofl_eden_plan_tensor_info", "ofl_eden_plan_tensor_dims",
-    "ofl_eden_encode", "ofl_eden_decode", "ofl_eden_plan_profile", "ofl_eden_plan_num_launches",
+    "ofl_eden_encode", "ofl_eden_decode", "ofl_eden_decode_add", "ofl_eden_plan_profile", "ofl_eden_plan_num_launches",
     "ofl_eden_plan_launch_info", "ofl_eden_plan_profile_collect", "ofl_serial_sum_f32",
     "ofl_serial_sum_f64", "ofl_lossy_last_error", "ofl_lossy_workspace_bytes", "ofl_kmeans1d_fit",
     "ofl_kmeans1d_batch_workspace_bytes", "ofl_kmeans1d_batch",
@@ -30,7 +30,9 @@ EXPORTS = (
     "ofl_sparsify_topk_batch_workspace_bytes", "ofl_sparsify_topk_batch",
     "ofl_ternary_ranks_batch_workspace_bytes", "ofl_ternary_ranks_batch",
     "ofl_agg_last_error", "ofl_wavg_delta", "ofl_wavg_ranges_workspace_bytes", "ofl_wavg_delta_ranges",
+    "ofl_wavg_range_sums_workspace_bytes", "ofl_wavg_delta_range_sums",
     "ofl_wavg_points_workspace_bytes", "ofl_wavg_delta_points", "ofl_apply_delta",
+    "ofl_apply_delta_ranges",
 )
 
 
@@ -65,6 +67,8 @@ def _bind(L):
     L.ofl_eden_encode.restype = i32
     L.ofl_eden_decode.argtypes = [vp, vp, vp, vp, vp, vp, sz, vp]
     L.ofl_eden_decode.restype = i32
+    L.ofl_eden_decode_add.argtypes = [vp, vp, vp, vp, vp, vp, vp, sz, vp]
+    L.ofl_eden_decode_add.restype = i32
     L.ofl_eden_plan_profile.argtypes = [vp, i32]
     L.ofl_eden_plan_profile.restype = i32
     L.ofl_eden_plan_num_launches.argtypes = [vp, i32]
@@ -112,12 +116,18 @@ def _bind(L):
     L.ofl_wavg_ranges_workspace_bytes.restype = sz
     L.ofl_wavg_delta_ranges.argtypes = [i32, vp, vp, ctypes.c_double, vp, i32, vp, vp, vp, vp, vp, sz, vp]
     L.ofl_wavg_delta_ranges.restype = i32
+    L.ofl_wavg_range_sums_workspace_bytes.argtypes = [i32, i32, i64]
+    L.ofl_wavg_range_sums_workspace_bytes.restype = sz
+    L.ofl_wavg_delta_range_sums.argtypes = [i32, vp, vp, ctypes.c_double, vp, i32, vp, vp, vp, vp, vp, sz, vp]
+    L.ofl_wavg_delta_range_sums.restype = i32
     L.ofl_wavg_points_workspace_bytes.argtypes = [i32, i32]
     L.ofl_wavg_points_workspace_bytes.restype = sz
     L.ofl_wavg_delta_points.argtypes = [i32, vp, vp, ctypes.c_double, vp, i32, vp, vp, vp, vp, vp, sz, vp]
     L.ofl_wavg_delta_points.restype = i32
     L.ofl_apply_delta.argtypes = [vp, vp, i64, vp, vp]
     L.ofl_apply_delta.restype = i32
+    L.ofl_apply_delta_ranges.argtypes = [vp, vp, vp, i32, vp, vp, i64, vp]
+    L.ofl_apply_delta_ranges.restype = i32
     L.ofl_serial_sum_f32.argtypes = [vp, i64]
     L.ofl_serial_sum_f32.restype = ctypes.c_float
     L.ofl_serial_sum_f64.argtypes = [vp, i64]

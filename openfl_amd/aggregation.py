@@ -15,7 +15,8 @@ RoundEnd does that for every tensor of a model update in one device pass
 sequence over flat arenas (csrc/agg_kernels.hip + the Eden plan): average +
 delta in one kernel (float64 arithmetic in NumPy's order, delta rounded to
 float32 as Eden.compress does), the seeds' serial sums from the delta's values
-(fast mode: a 4096-element prefix per tensor, reference mode: all of it), one
+summed on the device (fast mode: a 4096-element prefix per tensor, reference
+mode: all of it, one thread per tensor in Python's left-to-right order), one
 Eden encode and decode of all the big tensors, and apply_delta in place.  The
 payloads, metadata, np.random draws and new model are identical to calling
 the reference's functions tensor by tensor with an openfl_amd EdenPipeline
@@ -27,7 +28,7 @@ import torch
 
 from openfl_amd import _lib
 from openfl_amd.codec import EdenPlan, resolve_device
-from openfl_amd.pipelines.eden_pipeline import _FAST_SEED_PREFIX, _serial_sum, eden_seed
+from openfl_amd.pipelines.eden_pipeline import _FAST_SEED_PREFIX, eden_seeds
 
 _ALIGN = 64
 
@@ -154,6 +155,14 @@ class RoundEnd:
                              elem_offsets=[self.offsets[i] for i in self.big]) if self.big else None
         self._ws = _Scratch(self.device)
         self._codec_ws = None
+        # tensors the codec does not touch (small, <= dim_threshold): their
+        # apply_delta runs on these ranges (device tables)
+        rest = [i for i in range(len(self.numels)) if i not in set(self.big) and self.numels[i] > 0]
+        self._rest_n = len(rest)
+        self._rest_total = sum(self.numels[i] for i in rest)
+        dst = np.cumsum([0] + [self.numels[i] for i in rest]).astype(np.int64)
+        self._rest_start = torch.tensor([self.offsets[i] for i in rest] or [0], dtype=torch.int64).to(self.device)
+        self._rest_dst = torch.from_numpy(dst).to(self.device)
 
     # -- arenas --
     def arena(self):
@@ -212,20 +221,16 @@ class RoundEnd:
             counts = [min(n, _FAST_SEED_PREFIX) if fast else n for n in self.numels]
             single = np.asarray([1 if n == 1 else 0 for n in self.numels], np.int32)
             tot = sum(counts)
-            packed = torch.empty(max(tot, 1), dtype=torch.float64, device=dev)
             ptrs = np.asarray([x.data_ptr() for x in xs], np.uint64)
             st_ = np.asarray(self.offsets, np.int64)
             ct_ = np.asarray(counts, np.int64)
-            buf = self._ws(int(L.ofl_wavg_ranges_workspace_bytes(len(xs), len(counts))))
-            _lib.check_agg(L.ofl_wavg_delta_ranges(
+            sums = np.zeros(len(counts), np.float64)
+            buf = self._ws(int(L.ofl_wavg_range_sums_workspace_bytes(len(xs), len(counts), tot)))
+            _lib.check_agg(L.ofl_wavg_delta_range_sums(
                 len(xs), ptrs.ctypes.data, w64.ctypes.data, wsum,
                 base_arena.data_ptr() if base_arena is not None else None, len(counts), st_.ctypes.data,
-                ct_.ctypes.data, single.ctypes.data, packed.data_ptr(), buf.data_ptr(), buf.numel(), _stream(dev)))
-            ph = packed[:tot].cpu().numpy()
-            seeds, o = [], 0
-            for c in counts:
-                seeds.append(eden_seed(None, self.seed_mode, _serial_sum(ph[o:o + c]) if c else np.float64(0.0)))
-                o += c
+                ct_.ctypes.data, single.ctypes.data, sums.ctypes.data, buf.data_ptr(), buf.numel(), _stream(dev)))
+            seeds = eden_seeds(list(sums))
             # 3. encode, (payloads), decode in place, apply
             result = [None] * len(self.numels) if payloads else None
             if self.plan is not None:
@@ -246,7 +251,12 @@ class RoundEnd:
                             md[2 + 2 * k] = float(s)
                             md[3 + 2 * k] = float(d)
                         result[i] = (pn[po:po + pb].tobytes(), [{"int_list": list(self.shapes[i]), "int_to_float": md}])
-                p.decode(planes, sd, scales, delta, self._codec_ws)
+                if base_arena is not None:  # decode + apply_delta fused: out = base + decoded
+                    if out is None:
+                        out = torch.empty(self.arena_numel, dtype=torch.float32, device=dev)
+                    p.decode(planes, sd, scales, out, self._codec_ws, base=base_arena)
+                else:
+                    p.decode(planes, sd, scales, delta, self._codec_ws)
             if payloads:
                 small = [i for i in range(len(self.numels)) if result[i] is None]
                 if small:  # float32 bytes of the delta (Float32NumpyArrayToBytes), one D2H
@@ -258,8 +268,13 @@ class RoundEnd:
             if out is None:
                 out = torch.empty(self.arena_numel, dtype=torch.float32, device=dev)
             if base_arena is not None:
-                _lib.check_agg(L.ofl_apply_delta(base_arena.data_ptr(), delta.data_ptr(), self.arena_numel,
-                                                 out.data_ptr(), _stream(dev)))
+                if self.plan is not None:
+                    _lib.check_agg(L.ofl_apply_delta_ranges(
+                        base_arena.data_ptr(), delta.data_ptr(), out.data_ptr(), self._rest_n,
+                        self._rest_start.data_ptr(), self._rest_dst.data_ptr(), self._rest_total, _stream(dev)))
+                else:
+                    _lib.check_agg(L.ofl_apply_delta(base_arena.data_ptr(), delta.data_ptr(), self.arena_numel,
+                                                     out.data_ptr(), _stream(dev)))
             else:
                 out.copy_(delta)
         return out, result, seeds

@@ -108,17 +108,21 @@ class EdenPlan:
                                            ws.data_ptr() if ws is not None else None,
                                            ws.numel() if ws is not None else 0, st.cuda_stream))
 
-    def decode(self, planes, seeds, scales, y_arena, ws, stream=None):
-        """planes u8 + scales f32 -> y_arena fp32 (numel[t] elements of each tensor)."""
+    def decode(self, planes, seeds, scales, y_arena, ws, stream=None, base=None):
+        """planes u8 + scales f32 -> y_arena fp32 (numel[t] elements of each
+        tensor); with base (an arena of this layout): y = base + decoded
+        (TensorCodec.apply_delta fused, ofl_eden_decode_add)."""
         self._check(y_arena, torch.float32, self.arena_numel)
         self._check(planes, torch.uint8, self.planes_bytes)
         self._check(scales, torch.float32, self.n_slices)
         self._check(seeds, torch.int32, len(self.numels))
+        if base is not None:
+            self._check(base, torch.float32, self.arena_numel)
         st = stream if stream is not None else torch.cuda.current_stream(y_arena.device)
-        _lib.check(self._L.ofl_eden_decode(self._h, planes.data_ptr(), seeds.data_ptr(),
-                                           scales.data_ptr(), y_arena.data_ptr(),
-                                           ws.data_ptr() if ws is not None else None,
-                                           ws.numel() if ws is not None else 0, st.cuda_stream))
+        _lib.check(self._L.ofl_eden_decode_add(self._h, planes.data_ptr(), seeds.data_ptr(),
+                                               scales.data_ptr(), base.data_ptr() if base is not None else None,
+                                               y_arena.data_ptr(), ws.data_ptr() if ws is not None else None,
+                                               ws.numel() if ws is not None else 0, st.cuda_stream))
 
     # -- profiling (HIP events between launches; see ofl_codec.h) --
     def profile(self, enable=True):

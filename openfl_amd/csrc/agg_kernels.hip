@@ -203,6 +203,35 @@ __global__ __launch_bounds__(kNT) void k_wavg_ranges(RangeArgs r, double* out) {
     }
 }
 
+// serial float64 sum of each packed range, left to right like Python's sum()
+// over NumPy scalars: one 256-thread block per range stages 2048 values at a
+// time in LDS, then one lane runs the dependent add chain from LDS (loads
+// issued eight ahead of the adds)
+__global__ __launch_bounds__(256) void k_range_sums(const double* packed, const int64_t* dst, double* sums) {
+    __shared__ double v[2048];
+    const int r = blockIdx.x;
+    const int64_t j0 = dst[r], j1 = dst[r + 1];
+    double s = 0.0;
+    for (int64_t c0 = j0; c0 < j1; c0 += 2048) {
+        const int m = (int)(j1 - c0 < 2048 ? j1 - c0 : 2048);
+        __syncthreads();
+        for (int k = threadIdx.x; k < m; k += 256) v[k] = packed[c0 + k];
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int k = 0;
+            for (; k + 8 <= m; k += 8) {
+                double t[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) t[q] = v[k + q];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) s = s + t[q];
+            }
+            for (; k < m; ++k) s = s + v[k];
+        }
+    }
+    if (threadIdx.x == 0) sums[r] = s;
+}
+
 // apply_delta: out = base + delta (float32)
 __global__ __launch_bounds__(kNT) void k_apply(const float* base, const float* delta, int64_t n, float* out) {
     const int64_t stride = (int64_t)gridDim.x * kNT;
@@ -216,6 +245,22 @@ __global__ __launch_bounds__(kNT) void k_apply(const float* base, const float* d
         o4[i] = make_float4(b.x + d.x, b.y + d.y, b.z + d.z, b.w + d.w);
     }
     for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += stride) out[i] = base[i] + delta[i];
+}
+
+// apply_delta on listed ranges (device tables): the tensors the codec does
+// not touch when the decode itself adds the base (ofl_eden_decode_add)
+__global__ __launch_bounds__(kNT) void k_apply_ranges(const float* base, const float* delta, float* out,
+                                                      const int64_t* start, const int64_t* dst, int nr) {
+    const int64_t total = dst[nr];
+    for (int64_t j = (int64_t)blockIdx.x * kNT + threadIdx.x; j < total; j += (int64_t)gridDim.x * kNT) {
+        int lo = 0, hi = nr - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (dst[mid] <= j) lo = mid; else hi = mid - 1;
+        }
+        const int64_t i = start[lo] + (j - dst[lo]);
+        out[i] = base[i] + delta[i];
+    }
 }
 
 }  // namespace agg
@@ -333,6 +378,36 @@ int ofl_wavg_delta_ranges(int ncollab, const float* const* xs, const double* wei
     return OFL_OK;
 }
 
+size_t ofl_wavg_range_sums_workspace_bytes(int ncollab, int nranges, int64_t total) {
+    return ofl_wavg_ranges_workspace_bytes(ncollab, nranges) + 8 * (size_t)(std::max<int64_t>(total, 1) + nranges) + 512;
+}
+
+int ofl_wavg_delta_range_sums(int ncollab, const float* const* xs, const double* weights, double wsum,
+                              const float* base, int nranges, const int64_t* starts, const int64_t* counts,
+                              const int32_t* single, double* sums, void* ws, size_t ws_bytes, void* stream) {
+    if (nranges < 1) return OFL_OK;
+    if (!sums || !counts) return afail(OFL_EINVAL, "wavg range sums: null output");
+    int64_t total = 0;
+    for (int i = 0; i < nranges; ++i) total += counts[i] > 0 ? counts[i] : 0;
+    if (!ws || ws_bytes < ofl_wavg_range_sums_workspace_bytes(ncollab, nranges, total))
+        return afail(OFL_ESPACE, "wavg range sums: workspace too small");
+    const size_t head = (ofl_wavg_ranges_workspace_bytes(ncollab, nranges) + 255) & ~(size_t)255;
+    char* w = static_cast<char*>(ws);
+    double* packed = reinterpret_cast<double*>(w + head);
+    double* dsums = packed + std::max<int64_t>(total, 1);
+    const int rc = ofl_wavg_delta_ranges(ncollab, xs, weights, wsum, base, nranges, starts, counts, single, packed,
+                                         ws, head, stream);
+    if (rc != OFL_OK) return rc;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    // the range table the ranges call staged: dst prefix after the pointers, weights and starts
+    const int64_t* dst = reinterpret_cast<const int64_t*>(w + 16 * (size_t)ncollab + 8 * (size_t)nranges);
+    hipLaunchKernelGGL(agg::k_range_sums, dim3(nranges), dim3(256), 0, st, packed, dst, dsums);
+    AHIP(hipGetLastError());
+    AHIP(hipMemcpyAsync(sums, dsums, 8 * (size_t)nranges, hipMemcpyDeviceToHost, st));
+    AHIP(hipStreamSynchronize(st));
+    return OFL_OK;
+}
+
 size_t ofl_wavg_points_workspace_bytes(int ncollab, int npoints) {
     return 16 * (size_t)std::max(ncollab, 1) + 8 * (size_t)std::max(npoints, 1) + 512;
 }
@@ -374,6 +449,16 @@ int ofl_apply_delta(const float* base, const float* delta, int64_t n, float* out
     if (n == 0) return OFL_OK;
     hipLaunchKernelGGL(agg::k_apply, dim3(grid_for(n, 16)), dim3(agg::kNT), 0, static_cast<hipStream_t>(stream), base,
                        delta, n, out);
+    AHIP(hipGetLastError());
+    return OFL_OK;
+}
+
+int ofl_apply_delta_ranges(const float* base, const float* delta, float* out, int nranges, const int64_t* starts,
+                           const int64_t* dst, int64_t total, void* stream) {
+    if (nranges < 1 || total <= 0) return OFL_OK;
+    if (!base || !delta || !out || !starts || !dst) return afail(OFL_EINVAL, "apply_delta_ranges: bad arguments");
+    hipLaunchKernelGGL(agg::k_apply_ranges, dim3(grid_for(total, 1)), dim3(agg::kNT), 0,
+                       static_cast<hipStream_t>(stream), base, delta, out, starts, dst, nranges);
     AHIP(hipGetLastError());
     return OFL_OK;
 }

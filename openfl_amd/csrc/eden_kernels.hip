@@ -89,6 +89,7 @@ struct KArgs {
     const float* scales_in; // decode: in
     float* part;            // partial sums
     float* nu;              // per-slice norms (large)
+    const float* yadd;      // decode: nullable, y = yadd + decoded (apply_delta, float32 add)
 };
 
 // Eden tables in global memory (copied to LDS per workgroup)
@@ -503,6 +504,13 @@ DEVI void store4(float* base, uint32_t i, int64_t len, const float* v) {
     }
 }
 
+// y = base + decoded as two rounded float32 operations (apply_delta,
+// tensor_codec.py:211: the decoded delta is a float32 array first)
+DEVI float add_rn(float b, float d) {
+#pragma clang fp contract(off)
+    return b + d;
+}
+
 // block-uniform slice lookup for multi-tile launches (tile b of the launch)
 DEVI void find_tile_at(const KArgs& a, int b, int& slice, uint32_t& tile) {
     int lo = 0, hi = a.count - 1;
@@ -716,6 +724,16 @@ __global__ __launch_bounds__(1 << (P_LOG - 5)) void k_dec_small(KArgs a) {
 #pragma unroll
     for (int r = 0; r < 32; ++r) v[r] = sc * v[r];
     float* y = a.xout + D.y_off;
+    if (a.yadd) {
+        const float* yb = a.yadd + D.y_off;
+#pragma unroll
+        for (int r = 0; r < 32; r += 4) {
+            float b[4];
+            load4(yb, base | LT<S::L1>::off(r), D.ylen, b);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[r + q] = add_rn(b[q], v[r + q]);
+        }
+    }
 #pragma unroll
     for (int r = 0; r < 32; r += 4) store4(y, base | LT<S::L1>::off(r), D.ylen, &v[r]);
 }
@@ -806,8 +824,12 @@ __global__ __launch_bounds__(kTinyNT) void k_dec_tiny(KArgs a) {
     const float m1 = pow2i(-((p + 1) / 2));
     const float sc = a.scales_in[D.scale_idx];
     float* y = a.xout + D.y_off;
+    const float* yb = a.yadd ? a.yadd + D.y_off : nullptr;
     for (int e = threadIdx.x; e < P; e += kTinyNT)
-        if (e < D.ylen) y[e] = sc * sgn_elem(s[e] * m1, e, p, b1);
+        if (e < D.ylen) {
+            const float d = sc * sgn_elem(s[e] * m1, e, p, b1);
+            y[e] = yb ? add_rn(yb[e], d) : d;
+        }
 }
 
 // ===========================================================================
@@ -982,17 +1004,28 @@ DEVI void store_y(const KArgs& a, const SliceDesc& D, uint32_t tile, uint32_t ba
     const uint32_t e0 = tile << kRowLog;
     const uint32_t nv = tile_valid(D.ylen - (int64_t)e0);
     const rsrc_t r = mk_rsrc(a.xout + D.y_off + e0, (nv & ~3u) * 4u);
+    if (a.yadd) {  // apply_delta fused: y = base + decoded
+        const rsrc_t rb = mk_rsrc(a.yadd + D.y_off + e0, (nv & ~3u) * 4u);
 #pragma unroll
-    for (int k = 0; k < 64; k += 4) bstore4(r, base1, LT<RS::L1>::off(k), &v[k]);
+        for (int k = 0; k < 64; k += 4) {
+            const float4 b = bload4(rb, base1, LT<RS::L1>::off(k));
+            const float o[4] = {add_rn(b.x, v[k]), add_rn(b.y, v[k + 1]), add_rn(b.z, v[k + 2]), add_rn(b.w, v[k + 3])};
+            bstore4(r, base1, LT<RS::L1>::off(k), o);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 64; k += 4) bstore4(r, base1, LT<RS::L1>::off(k), &v[k]);
+    }
     if (nv & 3u) {
         const uint32_t eb = nv & ~3u;
         float* y = a.xout + D.y_off + e0 + eb;
+        const float* yb = a.yadd ? a.yadd + D.y_off + e0 + eb : nullptr;
 #pragma unroll
         for (int k = 0; k < 64; k += 4)
             if (base1 + LT<RS::L1>::off(k) == eb) {
 #pragma unroll
                 for (int q = 0; q < 3; ++q)
-                    if ((uint32_t)q < (nv & 3u)) y[q] = v[k + q];
+                    if ((uint32_t)q < (nv & 3u)) y[q] = yb ? add_rn(yb[q], v[k + q]) : v[k + q];
             }
     }
 }
@@ -2259,12 +2292,18 @@ int ofl_eden_encode(ofl_eden_plan_t pl, const float* x_arena, const uint32_t* se
 
 int ofl_eden_decode(ofl_eden_plan_t pl, const uint8_t* planes_arena, const uint32_t* seeds, const float* scales,
                     float* y_arena, void* ws, size_t ws_bytes, void* stream) {
+    return ofl_eden_decode_add(pl, planes_arena, seeds, scales, nullptr, y_arena, ws, ws_bytes, stream);
+}
+
+int ofl_eden_decode_add(ofl_eden_plan_t pl, const uint8_t* planes_arena, const uint32_t* seeds, const float* scales,
+                        const float* base_arena, float* y_arena, void* ws, size_t ws_bytes, void* stream) {
     if (!pl) return fail(OFL_EINVAL, "null plan");
     ofl::KArgs a;
     int rc = prep_args(pl, a, ws, ws_bytes);
     if (rc) return rc;
     a.pin = planes_arena;
     a.xout = y_arena;
+    a.yadd = base_arena;
     a.seeds = seeds;
     a.scales_in = scales;
     return run(pl, false, a, static_cast<hipStream_t>(stream));

@@ -61,6 +61,15 @@ def eden_seed(data, mode="reference", total=None):
     return int(float(seed))
 
 
+def eden_seeds(totals):
+    """eden_seed for many tensors in order from their serial sums: one
+    np.random.randint(1, 2**16, size=T) call -- the legacy generator yields the
+    same values and end state as T single calls (MT19937 32-bit bounded draws
+    are unbuffered), without T Python-level calls."""
+    draws = np.random.randint(1, 2 ** 16, size=len(totals)) if len(totals) else []
+    return [int(float((hash(t * 13 + 7) + int(r)) % (2 ** 16))) for t, r in zip(totals, draws)]
+
+
 _pool = None
 
 
@@ -278,7 +287,7 @@ class EdenTransformer(Transformer):
             flat = a.reshape(-1)
             return _serial_sum(flat[:_FAST_SEED_PREFIX] if self.seed_mode == "fast" else flat)
         totals = list(_threads().map(total, arrays))
-        seeds = [eden_seed(a, self.seed_mode, t) for a, t in zip(arrays, totals)]
+        seeds = eden_seeds(totals)
         big = [i for i, a in enumerate(arrays) if a.size > self.dim_threshold]
         enc = _batch_encode(self.eden, [arrays[i] for i in big], [seeds[i] for i in big]) if big else []
         out = [None] * len(arrays)

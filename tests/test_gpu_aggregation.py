@@ -89,6 +89,11 @@ def test_round_end_matches_per_tensor(seed_mode, with_base):
         assert pay[i][0] == ref_pay[i][0], i
         assert pay[i][1] == ref_pay[i][1], i
         np.testing.assert_array_equal(re.view(new, i).cpu().numpy(), ref_models[i].reshape(s), err_msg=str(i))
+    if with_base:  # in-place model update (out aliases the base arena)
+        np.random.seed(11)
+        inplace = base_a.clone()
+        re.run(arenas, w, inplace, payloads=False, out=inplace)
+        assert torch.equal(inplace, new)
     # payloads decode with the plain pipeline
     y = pipe.backward(pay[3][0], [dict(m) for m in pay[3][1]])
     assert y.shape == shapes[3]

@@ -109,3 +109,18 @@ def test_plan_from_metadata_dims():
     from openfl_amd.codec import EdenPlan
     p = EdenPlan([7], n_bits=3, dims=[[8, 8, 8]])
     assert p.dims == [[8, 8, 8]] and p.planes_bytes == 3 * 24 // 8
+
+
+def test_batched_seed_draws_match_single_calls():
+    """eden_seeds: one vectorised np.random draw = T single draws (values and
+    the generator's state afterwards)."""
+    from openfl_amd.pipelines.eden_pipeline import eden_seed, eden_seeds
+    rng = np.random.default_rng(9)
+    totals = [np.float32(v) for v in rng.standard_normal(500)] + [np.float64(0.0), np.float64(-3.25)]
+    for s in (0, 1, 12345):
+        np.random.seed(s)
+        one = [eden_seed(None, "reference", t) for t in totals]
+        after = np.random.randint(0, 2 ** 31)
+        np.random.seed(s)
+        assert eden_seeds(totals) == one
+        assert np.random.randint(0, 2 ** 31) == after
