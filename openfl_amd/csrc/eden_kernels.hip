@@ -1259,7 +1259,7 @@ template <int M> struct ColSet {
 constexpr size_t kColTab = 4096;
 
 template <int M, bool MID>
-__global__ __launch_bounds__(kColNT) void k_col(KArgs a) {
+DEVI void col_body(const KArgs& a, int b) {
     using CS = ColSet<M>;
     constexpr int K = CS::K;
     constexpr bool TAB = MID && M >= 3;
@@ -1267,7 +1267,7 @@ __global__ __launch_bounds__(kColNT) void k_col(KArgs a) {
     float* s = reinterpret_cast<float*>(smem);
     uint8_t* tab = smem + (M > 5 ? kColSmem : 0);
     int si; uint32_t tile;
-    find_tile(a, si, tile);
+    find_tile_at(a, b, si, tile);
     const SliceDesc D = a.d[si];
     const uint32_t tid = threadIdx.x;
     const int lo = a.lo;
@@ -1349,6 +1349,35 @@ __global__ __launch_bounds__(kColNT) void k_col(KArgs a) {
         for (int64_t t = tid; t < ntile; t += kColNT) ss += a.part[D.part_off + t];
         ss = block_sum<kColNT>(ss, nred);
         if (tid == 0) a.nu[si] = sqrtf(ss);
+    }
+}
+template <int M, bool MID>
+__global__ __launch_bounds__(kColNT) void k_col(KArgs a) {
+    col_body<M, MID>(a, (int)blockIdx.x);
+}
+
+// Several single-level middle passes (heights M = 1..5) in one launch: a
+// wave's slices of different sizes share the grid instead of running one
+// short launch per height.  a.list -> table of kColGroup ints per group
+// {M, list, tstart (both relative to the table), count, first block};
+// a.count = groups.
+constexpr int kColGroup = 5;
+__global__ __launch_bounds__(kColNT) void k_col_multi(KArgs a) {
+    const int b = (int)blockIdx.x;
+    int g = 0;
+    while (g + 1 < a.count && a.list[kColGroup * (g + 1) + 4] <= b) ++g;
+    const int32_t* G = a.list + kColGroup * g;
+    KArgs a2 = a;
+    a2.list = a.list + G[1];
+    a2.tstart = a.list + G[2];
+    a2.count = G[3];
+    const int lb = b - G[4];
+    switch (G[0]) {
+    case 1: col_body<1, true>(a2, lb); break;
+    case 2: col_body<2, true>(a2, lb); break;
+    case 3: col_body<3, true>(a2, lb); break;
+    case 4: col_body<4, true>(a2, lb); break;
+    default: col_body<5, true>(a2, lb); break;
     }
 }
 
@@ -1624,7 +1653,7 @@ struct Launch {
     int64_t bytes_moved = 0;  // fp32/plane bytes this launch reads + writes (intermediates included)
     int64_t bytes_alg = 0;    // its share of the SURVEY 8(d) algorithmic bytes (x/y fp32 + planes only)
 };
-enum Kind { K_TINY, K_SMALL, K_ROWA, K_ROWC, K_COL, K_FINAL };
+enum Kind { K_TINY, K_SMALL, K_ROWA, K_ROWC, K_COL, K_FINAL, K_COLM };
 
 }  // namespace
 
@@ -1736,6 +1765,11 @@ bool use_rowc2() {
 // OFL_EDEN_COL6=0 forces k_col everywhere (A/B)
 bool use_col6() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_COL6"); return !(s && s[0] == '0'); }();
+    return on;
+}
+// one k_col_multi launch per wave for the single-level heights 1..5
+bool use_colmulti() {
+    static const bool on = [] { const char* s = getenv("OFL_EDEN_COLMULTI"); return !(s && s[0] == '0'); }();
     return on;
 }
 
@@ -1885,6 +1919,7 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
             break;
         }
         case K_FINAL: e = launch(ofl::k_finalize, l.blocks, 256, 0, st, a); break;
+        case K_COLM: e = launch(ofl::k_col_multi, l.blocks, ofl::kColNT, ofl::kColTab, st, a); break;
         }
         if (e != hipSuccess) return fail(OFL_EHIP, std::string("kernel launch failed: ") + hipGetErrorString(e));
         if (evs) HIP_TRY(hipEventRecord((*evs)[2 * li + 1], st));
@@ -1908,6 +1943,7 @@ std::string launch_name(const Launch& l, bool enc) {
         return std::string((l.param >= 8 || (l.param >= 6 && l.mid)) && use_col6() ? "ofl::k_col6<" : "ofl::k_col<") +
                std::to_string(l.param) + ", " + (l.mid ? "true" : "false") +
                ((l.param >= 8 || (l.param >= 6 && l.mid)) && use_col6() ? ", 15>" : ">");
+    case K_COLM: return "ofl::k_col_multi";
     default: return "ofl::k_finalize";
     }
 }
@@ -1988,8 +2024,39 @@ void build_schedule(ofl_eden_plan* pl) {
         std::map<int, std::vector<int32_t>> byp;  // column launches grouped by p
         for (int32_t si : wl) byp[pl->slices[si].logp].push_back(si);
         std::vector<Launch> ce, cd;
+        std::vector<std::pair<int, const std::vector<int32_t>*>> mg;  // heights 1..5 -> one k_col_multi
+        if (use_colmulti()) {
+            for (auto& kv : byp)
+                if (kv.first - ofl::kRowLog >= 1 && kv.first - ofl::kRowLog <= 5) mg.push_back({kv.first - ofl::kRowLog, &kv.second});
+            if (mg.size() < 2) mg.clear();
+        }
+        if (!mg.empty()) {
+            const int gt = (int)ints.size();
+            ints.resize(ints.size() + ofl::kColGroup * mg.size());
+            int64_t blk = 0, mv = 0;
+            for (size_t g = 0; g < mg.size(); ++g) {
+                int64_t tiles = 0;
+                const int lo_c = add_list(*mg[g].second);
+                const int tp = add_prefix(*mg[g].second, ofl::kColLog, tiles);
+                int32_t* G = &ints[gt + ofl::kColGroup * g];
+                G[0] = mg[g].first;
+                G[1] = lo_c - gt;
+                G[2] = tp - gt;
+                G[3] = (int32_t)mg[g].second->size();
+                G[4] = (int32_t)blk;
+                blk += tiles;
+                for (int32_t si : *mg[g].second) mv += 8ll << pl->slices[si].logp;
+            }
+            Launch l{K_COLM, 0, ofl::kRowLog, 1, gt, -1, (int)mg.size(), blk};
+            l.stream = s;
+            l.bytes_moved = mv;
+            cd.push_back(l);
+            l.nu = 1;  // encode: every group is a slice's first (only) column launch
+            ce.push_back(l);
+        }
         for (auto& kv : byp) {
             const int r = kv.first - ofl::kRowLog;
+            if (!mg.empty() && r >= 1 && r <= 5) continue;  // in the k_col_multi launch
             int64_t tiles = 0;
             const int lo_c = add_list(kv.second);
             const int tp = add_prefix(kv.second, ofl::kColLog, tiles);
@@ -2037,6 +2104,7 @@ void build_schedule(ofl_eden_plan* pl) {
     for (int dir = 0; dir < 2; ++dir) {
         const bool enc = dir == 1;
         for (Launch& l : enc ? pl->enc : pl->dec) {
+            if (l.kind == K_COLM) continue;  // counted when built (its list is a group table)
             int64_t mv = 0, al = 0;
             for (int i = 0; i < l.count; ++i) {
                 const ofl::SliceDesc& D = pl->slices[ints[l.list_off + i]];

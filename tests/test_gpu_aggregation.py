@@ -93,7 +93,8 @@ def test_round_end_matches_per_tensor(seed_mode, with_base):
         np.random.seed(11)
         inplace = base_a.clone()
         re.run(arenas, w, inplace, payloads=False, out=inplace)
-        assert torch.equal(inplace, new)
+        for i in range(len(shapes)):  # tensors only: the alignment gaps are not written
+            assert torch.equal(re.view(inplace, i), re.view(new, i)), i
     # payloads decode with the plain pipeline
     y = pipe.backward(pay[3][0], [dict(m) for m in pay[3][1]])
     assert y.shape == shapes[3]
