@@ -58,6 +58,40 @@ DEVI uint32_t fkey(float f) {
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
+// LDS histogram increment with wave aggregation for concentrated data: the
+// lanes that share the first active lane's bin add once (popcount / wave
+// sum), the others add directly.  Sparse or low-entropy inputs (top-k zeros,
+// exponent digits) otherwise serialise up to 64 same-address LDS atomics.
+DEVI void lds_count(uint32_t* h, int b) {
+    const int bl = __builtin_amdgcn_readfirstlane(b);
+    const unsigned long long m = __ballot(b == bl);
+    if (__popcll(m) >= 8) {
+        if (b == bl) {
+            if ((int)(threadIdx.x & 63) == __builtin_ffsll((long long)m) - 1) atomicAdd(&h[bl], (uint32_t)__popcll(m));
+        } else {
+            atomicAdd(&h[b], 1u);
+        }
+    } else {
+        atomicAdd(&h[b], 1u);
+    }
+}
+DEVI void lds_add64(unsigned long long* h, int b, unsigned long long v) {
+    const int bl = __builtin_amdgcn_readfirstlane(b);
+    const unsigned long long m = __ballot(b == bl);
+    if (__popcll(m) >= 8) {
+        unsigned long long s = b == bl ? v : 0ull;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+        if (b == bl) {
+            if ((int)(threadIdx.x & 63) == __builtin_ffsll((long long)m) - 1) atomicAdd(&h[bl], s);
+        } else {
+            atomicAdd(&h[b], v);
+        }
+    } else {
+        atomicAdd(&h[b], v);
+    }
+}
+
 struct KmParams {
     float mids[kMaxK];       // sorted midpoints between consecutive sorted centres (k-1 used)
     float rank[kMaxK];       // label value to write per cluster (float32 rank)
@@ -240,10 +274,15 @@ DEVI void bkm_bounds(const BkmState& S, float& lo, float& hi, float& inv_w) {
     inv_w = hi > lo ? (float)((double)kBkmBins / ((double)hi - (double)lo) * (1.0 - 1e-7)) : 0.0f;
 }
 
+// one 64-bit LDS atomic per element: count in bits [47, 64) (a block has at
+// most 2^16 elements), the position inside the bin as 2^30 fixed point in
+// bits [0, 47) (at most 2^16 * 2^30 = 2^46 per block); flushed as a count
+// and a 2^32 fixed-point sum
+constexpr int kBkmCntShift = 47;
 __global__ __launch_bounds__(kNT) void k_bkm_hist(BkmArgs a) {
-    __shared__ uint32_t c[kBkmBins];
-    __shared__ unsigned long long sfx[kBkmBins];
-    for (int b = threadIdx.x; b < kBkmBins; b += kNT) { c[b] = 0; sfx[b] = 0; }
+    static_assert(kBkmChunk <= (1 << 16), "packed histogram counts");
+    __shared__ unsigned long long h[kBkmBins];
+    for (int b = threadIdx.x; b < kBkmBins; b += kNT) h[b] = 0;
     int t; int64_t i0, i1;
     bkm_range(a, t, i0, i1);
     float lo, hi, inv_w;
@@ -255,14 +294,18 @@ __global__ __launch_bounds__(kNT) void k_bkm_hist(BkmArgs a) {
         b = b < 0 ? 0 : (b >= kBkmBins ? kBkmBins - 1 : b);
         float fr = f - (float)b;
         fr = fr < 0.f ? 0.f : (fr < 1.f ? fr : 0.99999994f);
-        atomicAdd(&c[b], 1u);
-        atomicAdd(&sfx[b], (unsigned long long)(fr * 4294967296.0f));
+        lds_add64(h, b, (1ull << kBkmCntShift) | (unsigned long long)(fr * 1073741824.0f));
     });
     __syncthreads();
     uint32_t* hc = a.hc + (int64_t)t * kBkmBins;
     unsigned long long* hs = a.hs + (int64_t)t * kBkmBins;
-    for (int b = threadIdx.x; b < kBkmBins; b += kNT)
-        if (c[b]) { atomicAdd(&hc[b], c[b]); atomicAdd(&hs[b], sfx[b]); }
+    for (int b = threadIdx.x; b < kBkmBins; b += kNT) {
+        const unsigned long long v = h[b];
+        if (v) {
+            atomicAdd(&hc[b], (uint32_t)(v >> kBkmCntShift));
+            atomicAdd(&hs[b], (v & ((1ull << kBkmCntShift) - 1)) << 2);
+        }
+    }
 }
 
 DEVI uint64_t bkm_rng(uint64_t& s) {  // xorshift64*
@@ -806,7 +849,7 @@ __global__ __launch_bounds__(kNT) void k_btk_hist(BtkArgs a) {
     __syncthreads();
     btk_visit(a.x + T.off, i0, i1, [&](float v, int64_t) {
         const uint32_t m = __float_as_uint(v) & 0x7fffffffu;
-        if ((m & pmask) == prefix) atomicAdd(&h[(m >> sh) & dm], 1u);
+        if ((m & pmask) == prefix) lds_count(h, (int)((m >> sh) & dm));  // ballots see the candidates only
     });
     __syncthreads();
     uint32_t* g = a.hist + (int64_t)t * kRadix;

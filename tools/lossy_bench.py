@@ -166,7 +166,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cpu-sample", type=int, default=1 << 20, help="elements of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--only", default="", help="comma list of kc,stc,skc (default all)")
+    ap.add_argument("--only", default="", help="comma list of kc,kc_plugin,stc,stc_plugin,skc,skc_plugin (default all)")
     args = ap.parse_args()
 
     import torch
@@ -180,14 +180,14 @@ def main():
         xs.append(torch.empty(numel(s), dtype=torch.float32, device=dev).normal_(0.0, 0.01, generator=g))
     nbytes = 4 * sum(x.numel() for x in xs)
     np.random.seed(0)
-    only = set(a for a in args.only.split(",") if a) or {"kc", "stc", "skc"}
+    only = set(a for a in args.only.split(",") if a) or {"kc", "kc_plugin", "stc", "stc_plugin", "skc", "skc_plugin"}
 
     ar = Arena(xs)
     res = {}
     for name, fn, arg in (("kc", kc_step, ar), ("kc_plugin", kc_plugin_step, xs), ("stc", stc_step, ar),
                           ("stc_plugin", stc_plugin_step, xs), ("skc", skc_step, ar),
                           ("skc_plugin", skc_plugin_step, xs)):
-        if name.split("_")[0] not in only:
+        if name not in only:
             continue
         t = timed(fn, arg, args.steps, args.warmup)
         res[name] = {"value": round(nbytes / t / 2 ** 30, 3), "ms_per_step": round(1e3 * t, 3)}
