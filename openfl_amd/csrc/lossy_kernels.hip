@@ -371,6 +371,23 @@ DEVI double bkm_bscan(double v, double* tmp, double& total) {
     return off + v;
 }
 
+// exclusive running max over the block's threads in thread order (256 threads)
+DEVI float bkm_bscan_max_excl(float v, double* tmp) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const float u = __shfl_up(v, o, 64);
+        if (lane >= o) v = fmaxf(v, u);
+    }
+    float ex = __shfl_up(v, 1, 64);
+    if (lane == 0) ex = -INFINITY;
+    if (lane == 63) tmp[w] = v;
+    __syncthreads();
+    for (int j = 0; j < w; ++j) ex = fmaxf(ex, (float)tmp[j]);
+    __syncthreads();
+    return ex;
+}
+
 // One workgroup per (tensor, restart): k-means of the 4096 histogram points (bin means,
 // weight = count; empty bins keep their centre with weight 0, so the points
 // stay sorted and the cluster edge of a midpoint m is found in O(1) from
@@ -431,8 +448,12 @@ __global__ __launch_bounds__(kBkmSeedNT) void k_bkm_seed(BkmArgs a) {
     for (int q = 0; q < PER; ++q) { ew += wts[i0 + q]; es += (double)wts[i0 + q] * pts[i0 + q]; W[i0 + q] = ew; S1[i0 + q] = es; }
     const int nocc = (int)bkm_bsum((double)occ, tmp);
     const double sq = bkm_bsum(q0, tmp);  // (also publishes pts / W / S1)
-    if (threadIdx.x == 0)  // rounding may break the order of neighbouring bin means
-        for (int i = 1; i < kBkmBins; ++i) if (pts[i] < pts[i - 1]) pts[i] = pts[i - 1];
+    {  // rounding may break the order of neighbouring bin means: running max (block scan)
+        float mx = -INFINITY;
+        for (int q = 0; q < PER; ++q) mx = fmaxf(mx, pts[i0 + q]);
+        float r = bkm_bscan_max_excl(mx, tmp);
+        for (int q = 0; q < PER; ++q) { r = fmaxf(r, pts[i0 + q]); pts[i0 + q] = r; }
+    }
     __syncthreads();
     if (nocc <= k) {  // no more occupied bins than clusters: they are the centres
         if (threadIdx.x == 0) {
