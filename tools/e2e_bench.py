@@ -49,15 +49,24 @@ def run_plugin(sd, pipe, P):
 def run_batched(sd, pipe, P):
     """EdenPipeline.forward_batch / backward_batch: the whole state dict per
     call (pinned staging, one H2D / launch sequence / D2H each way)."""
+    t = [time.perf_counter()]
     enc = pipe.forward_batch([a for _, a in sd])
+    t.append(time.perf_counter())
     wire = [P.construct_named_tensor((name, "col", 1, False, ("trained",)), data, md, False).SerializeToString()
             for (name, _), (data, md) in zip(sd, enc)]
+    t.append(time.perf_counter())
     items = []
     for b in wire:
         nt = P.NamedTensor()
         nt.ParseFromString(b)
         items.append((nt.data_bytes, P.transformer_metadata_of(nt)))
-    return pipe.backward_batch(items), sum(len(b) for b in wire)
+    t.append(time.perf_counter())
+    out = pipe.backward_batch(items)
+    t.append(time.perf_counter())
+    run_batched.phases = {k: round(1e3 * (b - a), 2) for k, a, b in
+                          zip(("forward_batch_ms", "protobuf_build_ms", "protobuf_parse_ms", "backward_batch_ms"),
+                              t[:-1], t[1:])}
+    return out, sum(len(b) for b in wire)
 
 
 def run_cpu(sd, P):
@@ -135,7 +144,8 @@ def main():
                 dt = time.perf_counter() - t0
             key = "batched" if mode == "reference" else "batched_fast_seed"
             res[key] = {"s": round(dt, 4), "GiB_s": round(in_bytes / dt / 2 ** 30, 3),
-                        "wire_bytes": sum(o[1] for o in outs), "rel_err": round(rel_err(sds[-1], outs[-1][0]), 6)}
+                        "wire_bytes": sum(o[1] for o in outs), "rel_err": round(rel_err(sds[-1], outs[-1][0]), 6),
+                        "last_collaborator_phases": dict(run_batched.phases)}
     if "cpu" in modes:
         t0 = time.perf_counter()
         outs = [run_cpu(sd, P) for sd in sds]
