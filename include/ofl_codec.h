@@ -271,6 +271,24 @@ int ofl_apply_delta(const float* base, const float* delta, int64_t n, float* out
 int ofl_apply_delta_ranges(const float* base, const float* delta, float* out, int nranges, const int64_t* starts,
                            const int64_t* dst, int64_t total, void* stream);
 
+/* ---- gzip of rank arrays (csrc/deflate_kernels.hip) -------------------------
+ * GZIPTransformer.forward (kc_pipeline.py:128-156, skc_pipeline.py:201-230,
+ * stc_pipeline.py:185-215) compresses the float32 ranks with gzip.compress;
+ * gzip.decompress reads any valid stream, so this produces one on the GPU: a
+ * multi-member gzip stream (4096 float32 values per member, one
+ * dynamic-Huffman deflate block each: copies of each value's previous
+ * occurrence, literals at first occurrences), CRC-32 and ISIZE per member.
+ * x: DEVICE float32 [n], every value an integer 0..31 (the ranks the lossy
+ * pipelines write; anything else -> OFL_EINVAL, nothing written).  out: HOST
+ * buffer of out_cap >= ofl_gzip_ranks_bound(n) bytes; *out_len = stream
+ * length.  ws: device, ofl_gzip_ranks_workspace_bytes(n).  Synchronous.
+ * Errors: ofl_gzip_last_error(). */
+const char* ofl_gzip_last_error(void);
+size_t ofl_gzip_ranks_workspace_bytes(int64_t n);
+size_t ofl_gzip_ranks_bound(int64_t n);
+int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size_t* out_len, void* ws,
+                   size_t ws_bytes, void* stream);
+
 /* ---- host helpers ----------------------------------------------------------
  * Left-to-right serial sums in the array's own precision: the
  * `sum(data.flatten())` term of the reference seed formula

@@ -33,6 +33,7 @@ EXPORTS = (
     "ofl_wavg_range_sums_workspace_bytes", "ofl_wavg_delta_range_sums",
     "ofl_wavg_points_workspace_bytes", "ofl_wavg_delta_points", "ofl_apply_delta",
     "ofl_apply_delta_ranges",
+    "ofl_gzip_last_error", "ofl_gzip_ranks_workspace_bytes", "ofl_gzip_ranks_bound", "ofl_gzip_ranks",
 )
 
 
@@ -128,6 +129,13 @@ def _bind(L):
     L.ofl_apply_delta.restype = i32
     L.ofl_apply_delta_ranges.argtypes = [vp, vp, vp, i32, vp, vp, i64, vp]
     L.ofl_apply_delta_ranges.restype = i32
+    L.ofl_gzip_last_error.restype = ctypes.c_char_p
+    L.ofl_gzip_ranks_workspace_bytes.argtypes = [i64]
+    L.ofl_gzip_ranks_workspace_bytes.restype = sz
+    L.ofl_gzip_ranks_bound.argtypes = [i64]
+    L.ofl_gzip_ranks_bound.restype = sz
+    L.ofl_gzip_ranks.argtypes = [vp, i64, vp, sz, vp, vp, sz, vp]
+    L.ofl_gzip_ranks.restype = i32
     L.ofl_serial_sum_f32.argtypes = [vp, i64]
     L.ofl_serial_sum_f32.restype = ctypes.c_float
     L.ofl_serial_sum_f64.argtypes = [vp, i64]
@@ -154,6 +162,12 @@ def lib():
 def check_lossy(rc):
     if rc != OFL_OK:
         raise CodecError(lib().ofl_lossy_last_error().decode() or f"libofl_codec error {rc}")
+    return rc
+
+
+def check_gzip(rc):
+    if rc != OFL_OK:
+        raise CodecError(lib().ofl_gzip_last_error().decode() or f"libofl_codec error {rc}")
     return rc
 
 

@@ -1,0 +1,499 @@
+// deflate_kernels.hip -- gzip on the GPU for the lossy pipelines' rank arrays
+// (SURVEY §8(f) row 3).  Reference: GZIPTransformer.forward
+// (kc_pipeline.py:128-156, skc_pipeline.py:201-230, stc_pipeline.py:185-215):
+// gzip.compress(float32 ranks bytes), decoded by gzip.decompress.  Any valid
+// gzip stream decodes to the same bytes, so the wire stays compatible: the
+// output here is a multi-member gzip stream (RFC 1952), one member per 4096
+// float32 ranks (16 KiB of input), each member one dynamic-Huffman deflate
+// block (RFC 1951), which Python's gzip.decompress reads.
+//
+// The ranks are small integers stored as float32 (0.0, 1.0, ... < 32), i.e.
+// tokens of 4 bytes from a tiny alphabet.  Each token is coded as a copy of
+// its previous occurrence in the member (length 4, distance 4 x gap; found by
+// per-thread scans + a block prefix max) or, at a first occurrence, as its 4
+// literal bytes.  Per member: token classes and symbol histograms in LDS,
+// Huffman code lengths (limited to 15 / 7 bits by flattening the
+// frequencies), canonical codes, the code-length RLE header, a block scan of
+// the tokens' bit costs, bits OR-ed into an LDS buffer, CRC-32 from per-thread
+// table CRCs combined with GF(2) shift matrices, then one coalesced copy out.
+// Deterministic (bit positions come from scans; OR is order-free).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "ofl_codec.h"
+
+#define DEVI __device__ __forceinline__
+
+namespace gz {
+
+constexpr int kTok = 4096;                 // float32 tokens per gzip member
+constexpr int kNT = 256;
+constexpr int kPer = kTok / kNT;           // 16 consecutive tokens per thread
+constexpr int kTypes = 32;                 // token values 0..31
+constexpr int kMaxGap = 8192;              // distance 4 x gap <= 32768
+constexpr int kOutWords = 8192;            // 32 KiB bit buffer >= worst-case member
+constexpr int kOutBytes = 4 * kOutWords;
+constexpr int kLit = 286, kDist = 30, kCL = 19;
+constexpr int kBatch = 4096;               // members per launch (host loop)
+
+__constant__ uint16_t c_dbase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129,
+                                     193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+__constant__ uint8_t c_dext[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+__constant__ uint8_t c_clord[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+__constant__ uint32_t c_adv[17][32];       // raw CRC advance by 2^k zero bytes: GF(2) matrix columns
+
+// Huffman scratch (thread 0), overlaid on the token tables once they are consumed
+struct HScratch {
+    uint32_t w[2 * kLit];
+    int16_t parent[2 * kLit];
+    int16_t sym[kLit];
+    uint8_t dead[2 * kLit];
+    uint16_t rle_sym[kLit + kDist];
+    uint16_t rle_ext[kLit + kDist];
+};
+struct Smem {
+    uint32_t out[kOutWords];
+    uint32_t crct[256];
+    union {
+        int16_t last[kNT][kTypes];         // per thread: last index of each type in its segment; then exclusive prefix max
+        HScratch h;
+    } u;
+    int16_t ptot[8][kTypes];
+    uint32_t hl[kLit], hd[kDist], hc[kCL];
+    uint8_t ll[kLit], ld[kDist], lc[kCL];
+    uint16_t kl[kLit], kd[kDist], kc[kCL];  // bit-reversed canonical codes
+    uint32_t scan[kNT / 64];
+    uint32_t crc_r[kNT], crc_n[kNT];
+    uint32_t hdr_bits, total_bits, nrle;
+    int bad;
+};
+static_assert(sizeof(HScratch) <= sizeof(int16_t) * kNT * kTypes, "Huffman scratch fits the token tables");
+
+DEVI void put_bits(uint32_t* out, uint32_t pos, uint32_t val, int nb) {
+    if (nb == 0) return;
+    const uint32_t w = pos >> 5, sh = pos & 31u;
+    atomicOr(&out[w], val << sh);
+    if (sh + (uint32_t)nb > 32u) atomicOr(&out[w + 1], val >> (32u - sh));
+}
+DEVI uint32_t rev_bits(uint32_t c, int n) { return __brev(c) >> (32 - n); }
+DEVI int dist_code(uint32_t d) {
+    int c = 29;
+    while (c > 0 && c_dbase[c] > d) --c;
+    return c;
+}
+DEVI uint32_t crc_adv(uint32_t v, uint32_t len) {
+    for (int k = 0; k < 17; ++k)
+        if ((len >> k) & 1u) {
+            uint32_t r = 0;
+            for (int i = 0; i < 32; ++i) r ^= ((v >> i) & 1u) ? c_adv[k][i] : 0u;
+            v = r;
+        }
+    return v;
+}
+
+// Huffman code lengths of freq[0..n) limited to maxlen (thread 0): two
+// smallest live nodes merged until one is left; if too deep, halve the
+// frequencies (keeping them >= 1) and rebuild
+// complete: a lone symbol gets a partner (zlib accepts an incomplete code only
+// for distances)
+DEVI void huff_lengths(const uint32_t* freq, int n, int maxlen, uint8_t* len, HScratch& h, bool complete) {
+    int m = 0;
+    for (int s = 0; s < n; ++s) { len[s] = 0; if (freq[s]) { h.sym[m] = (int16_t)s; h.w[m] = freq[s]; ++m; } }
+    if (m == 0) return;
+    if (m == 1) {
+        len[h.sym[0]] = 1;
+        if (complete) len[h.sym[0] == 0 ? 1 : 0] = 1;
+        return;
+    }
+    for (;;) {
+        for (int i = 0; i < 2 * m; ++i) { h.dead[i] = 0; h.parent[i] = -1; }
+        int nodes = m;
+        for (int it = 0; it < m - 1; ++it) {
+            int a = -1, b = -1;
+            for (int i = 0; i < nodes; ++i) {
+                if (h.dead[i]) continue;
+                if (a < 0 || h.w[i] < h.w[a]) { b = a; a = i; }
+                else if (b < 0 || h.w[i] < h.w[b]) b = i;
+            }
+            h.w[nodes] = h.w[a] + h.w[b];
+            h.dead[a] = h.dead[b] = 1;
+            h.parent[a] = h.parent[b] = (int16_t)nodes;
+            ++nodes;
+        }
+        int deepest = 0;
+        for (int i = 0; i < m; ++i) {
+            int d = 0;
+            for (int j = i; h.parent[j] >= 0; j = h.parent[j]) ++d;
+            len[h.sym[i]] = (uint8_t)d;
+            deepest = d > deepest ? d : deepest;
+        }
+        if (deepest <= maxlen) return;
+        for (int i = 0; i < m; ++i) h.w[i] = (h.w[i] >> 1) | 1u;
+    }
+}
+// canonical codes (RFC 1951 3.2.2), stored bit-reversed for LSB-first output
+DEVI void huff_codes(const uint8_t* len, int n, uint16_t* code) {
+    uint32_t cnt[16] = {0}, next[16];
+    for (int s = 0; s < n; ++s) cnt[len[s]]++;
+    cnt[0] = 0;
+    uint32_t c = 0;
+    for (int b = 1; b < 16; ++b) { c = (c + cnt[b - 1]) << 1; next[b] = c; }
+    for (int s = 0; s < n; ++s) code[s] = len[s] ? (uint16_t)rev_bits(next[len[s]]++, len[s]) : 0;
+}
+
+struct GzArgs {
+    const float* x;
+    int64_t n;
+    int64_t chunk0;      // first member of this launch
+    uint8_t* slots;      // [members][kOutBytes]
+    uint32_t* sizes;     // [members]
+    int* bad;            // set if a value is not a rank 0..31
+};
+
+__global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    Smem& S = *reinterpret_cast<Smem*>(smem_raw);
+    const int tid = threadIdx.x;
+    const int64_t c = a.chunk0 + blockIdx.x;
+    const int64_t e0 = c * kTok;
+    const int ntok = (int)std::min<int64_t>(kTok, a.n - e0);
+    for (int i = tid; i < kOutWords; i += kNT) S.out[i] = 0;
+    for (int i = tid; i < 256; i += kNT) {
+        uint32_t r = (uint32_t)i;
+        for (int k = 0; k < 8; ++k) r = (r & 1u) ? (r >> 1) ^ 0xEDB88320u : r >> 1;
+        S.crct[i] = r;
+    }
+    for (int i = tid; i < kLit; i += kNT) S.hl[i] = 0;
+    if (tid < kDist) S.hd[tid] = 0;
+    if (tid < kCL) S.hc[tid] = 0;
+    if (tid == 0) S.bad = 0;
+    for (int t = 0; t < kTypes; ++t) S.u.last[tid][t] = -1;
+    __syncthreads();
+
+    // ---- tokens, validity, local previous occurrences, raw CRC ----
+    const int i0 = tid * kPer;
+    const int nv = std::max(0, std::min(kPer, ntok - i0));
+    int tok[kPer];
+    int prev[kPer];
+    uint32_t crc = 0;
+    bool bad = false;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        tok[q] = 0;
+        prev[q] = -1;
+        if (q < nv) {
+            const float v = a.x[e0 + i0 + q];
+            const int t = (int)v;
+            const uint32_t bits = __float_as_uint(v);
+            if (!(t >= 0 && t < kTypes && bits == __float_as_uint((float)t))) bad = true;
+            const int tt = (t >= 0 && t < kTypes) ? t : 0;
+            tok[q] = tt;
+            prev[q] = S.u.last[tid][tt];
+            S.u.last[tid][tt] = (int16_t)(i0 + q);
+            for (int b = 0; b < 4; ++b) crc = S.crct[(crc ^ (bits >> (8 * b))) & 0xffu] ^ (crc >> 8);
+        }
+    }
+    if (bad) atomicOr(&S.bad, 1);
+    S.crc_r[tid] = crc;
+    S.crc_n[tid] = 4u * (uint32_t)nv;
+    __syncthreads();
+    if (S.bad) {  // block-uniform
+        if (tid == 0) { atomicOr(a.bad, 1); a.sizes[blockIdx.x] = 0; }
+        return;
+    }
+    // exclusive prefix max of the per-thread last indices, per type (in place):
+    // thread (type t, part p) walks rows 32p..32p+31, then parts are combined
+    {
+        const int t = tid & 31, p = tid >> 5;
+        int run = -1;
+        for (int r = 32 * p; r < 32 * p + 32; ++r) {
+            const int v = S.u.last[r][t];
+            S.u.last[r][t] = (int16_t)run;
+            run = v > run ? v : run;
+        }
+        S.ptot[p][t] = (int16_t)run;
+        __syncthreads();
+        int off = -1;
+        for (int pp = 0; pp < p; ++pp) off = S.ptot[pp][t] > off ? S.ptot[pp][t] : off;
+        for (int r = 32 * p; r < 32 * p + 32; ++r) if (off > S.u.last[r][t]) S.u.last[r][t] = (int16_t)off;
+        __syncthreads();
+    }
+    // ---- classify: copy of the previous occurrence (length 4) or 4 literals ----
+    int dcode[kPer];
+    uint32_t dext[kPer];
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        dcode[q] = -1;
+        dext[q] = 0;
+        if (q < nv) {
+            int pv = prev[q] >= 0 ? prev[q] : S.u.last[tid][tok[q]];
+            const int gap = i0 + q - pv;
+            if (pv >= 0 && gap <= kMaxGap) {
+                const uint32_t d = 4u * (uint32_t)gap;
+                const int dc = dist_code(d);
+                dcode[q] = dc;
+                dext[q] = d - c_dbase[dc];
+                atomicAdd(&S.hl[258], 1u);
+                atomicAdd(&S.hd[dc], 1u);
+            } else {
+                const uint32_t bits = __float_as_uint((float)tok[q]);
+                for (int b = 0; b < 4; ++b) atomicAdd(&S.hl[(bits >> (8 * b)) & 0xffu], 1u);
+            }
+        }
+    }
+    // CRC of the member: tree of (raw crc, byte count) pairs
+    for (int st = 1; st < kNT; st <<= 1) {
+        __syncthreads();
+        if ((tid & (2 * st - 1)) == 0) {
+            S.crc_r[tid] = crc_adv(S.crc_r[tid], S.crc_n[tid + st]) ^ S.crc_r[tid + st];
+            S.crc_n[tid] += S.crc_n[tid + st];
+        }
+    }
+    __syncthreads();
+    // ---- thread 0: codes and the headers ----
+    if (tid == 0) {
+        HScratch& h = S.u.h;
+        S.hl[256] = 1;  // end of block
+        huff_lengths(S.hl, kLit, 15, S.ll, h, true);
+        bool anyd = false;
+        for (int i = 0; i < kDist; ++i) anyd = anyd || S.hd[i];
+        if (!anyd) S.hd[0] = 1;  // one (unused) distance code
+        huff_lengths(S.hd, kDist, 15, S.ld, h, false);
+        int nlit = kLit;
+        while (nlit > 257 && S.ll[nlit - 1] == 0) --nlit;
+        int ndist = kDist;
+        while (ndist > 1 && S.ld[ndist - 1] == 0) --ndist;
+        // run-length code of the concatenated code lengths
+        const int N = nlit + ndist;
+        int nr = 0;
+        for (int i = 0; i < N;) {
+            const uint8_t cur = i < nlit ? S.ll[i] : S.ld[i - nlit];
+            int run = 1;
+            while (i + run < N && (i + run < nlit ? S.ll[i + run] : S.ld[i + run - nlit]) == cur) ++run;
+            int left = run;
+            if (cur == 0) {
+                while (left >= 11) { const int r = left < 138 ? left : 138; h.rle_sym[nr] = 18; h.rle_ext[nr++] = (uint16_t)(r - 11); left -= r; }
+                if (left >= 3) { h.rle_sym[nr] = 17; h.rle_ext[nr++] = (uint16_t)(left - 3); left = 0; }
+                while (left > 0) { h.rle_sym[nr] = 0; h.rle_ext[nr++] = 0; --left; }
+            } else {
+                h.rle_sym[nr] = cur; h.rle_ext[nr++] = 0; --left;
+                while (left >= 3) { const int r = left < 6 ? left : 6; h.rle_sym[nr] = 16; h.rle_ext[nr++] = (uint16_t)(r - 3); left -= r; }
+                while (left > 0) { h.rle_sym[nr] = cur; h.rle_ext[nr++] = 0; --left; }
+            }
+            i += run;
+        }
+        for (int i = 0; i < nr; ++i) S.hc[h.rle_sym[i]]++;
+        huff_lengths(S.hc, kCL, 7, S.lc, h, true);
+        huff_codes(S.ll, kLit, S.kl);
+        huff_codes(S.ld, kDist, S.kd);
+        huff_codes(S.lc, kCL, S.kc);
+        int ncl = kCL;
+        while (ncl > 4 && S.lc[c_clord[ncl - 1]] == 0) --ncl;
+        uint32_t pos = 0;
+        const uint8_t hdr[10] = {0x1f, 0x8b, 0x08, 0x00, 0, 0, 0, 0, 0x00, 0xff};
+        for (int i = 0; i < 10; ++i) { put_bits(S.out, pos, hdr[i], 8); pos += 8; }
+        put_bits(S.out, pos, 1u, 1); pos += 1;          // BFINAL
+        put_bits(S.out, pos, 2u, 2); pos += 2;          // BTYPE = dynamic
+        put_bits(S.out, pos, (uint32_t)(nlit - 257), 5); pos += 5;
+        put_bits(S.out, pos, (uint32_t)(ndist - 1), 5); pos += 5;
+        put_bits(S.out, pos, (uint32_t)(ncl - 4), 4); pos += 4;
+        for (int i = 0; i < ncl; ++i) { put_bits(S.out, pos, S.lc[c_clord[i]], 3); pos += 3; }
+        for (int i = 0; i < nr; ++i) {
+            const int sy = h.rle_sym[i];
+            put_bits(S.out, pos, S.kc[sy], S.lc[sy]); pos += S.lc[sy];
+            const int eb = sy == 16 ? 2 : (sy == 17 ? 3 : (sy == 18 ? 7 : 0));
+            put_bits(S.out, pos, h.rle_ext[i], eb); pos += eb;
+        }
+        S.hdr_bits = pos;
+    }
+    __syncthreads();
+    // ---- token bits: block scan of the costs, then OR into the buffer ----
+    uint32_t cost[kPer];
+    uint32_t mine = 0;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        cost[q] = 0;
+        if (q < nv) {
+            if (dcode[q] >= 0) {
+                cost[q] = S.ll[258] + S.ld[dcode[q]] + c_dext[dcode[q]];
+            } else {
+                const uint32_t bits = __float_as_uint((float)tok[q]);
+                for (int b = 0; b < 4; ++b) cost[q] += S.ll[(bits >> (8 * b)) & 0xffu];
+            }
+        }
+        mine += cost[q];
+    }
+    const int lane = tid & 63, w = tid >> 6;
+    uint32_t inc = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
+    }
+    if (lane == 63) S.scan[w] = inc;
+    __syncthreads();
+    uint32_t pos = S.hdr_bits + inc - mine;
+    for (int j = 0; j < w; ++j) pos += S.scan[j];
+    if (tid == kNT - 1) S.total_bits = pos + mine;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        if (q < nv) {
+            if (dcode[q] >= 0) {
+                put_bits(S.out, pos, S.kl[258], S.ll[258]); pos += S.ll[258];
+                put_bits(S.out, pos, S.kd[dcode[q]], S.ld[dcode[q]]); pos += S.ld[dcode[q]];
+                put_bits(S.out, pos, dext[q], c_dext[dcode[q]]); pos += c_dext[dcode[q]];
+            } else {
+                const uint32_t bits = __float_as_uint((float)tok[q]);
+                for (int b = 0; b < 4; ++b) {
+                    const uint32_t by = (bits >> (8 * b)) & 0xffu;
+                    put_bits(S.out, pos, S.kl[by], S.ll[by]); pos += S.ll[by];
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // ---- end of block, byte padding, CRC-32 and ISIZE ----
+    if (tid == 0) {
+        uint32_t p = S.total_bits;
+        put_bits(S.out, p, S.kl[256], S.ll[256]); p += S.ll[256];
+        p = (p + 7u) & ~7u;
+        const uint32_t crc32 = crc_adv(0xffffffffu, S.crc_n[0]) ^ S.crc_r[0] ^ 0xffffffffu;
+        put_bits(S.out, p, crc32, 32); p += 32;
+        put_bits(S.out, p, S.crc_n[0], 32); p += 32;
+        S.total_bits = p;
+        a.sizes[blockIdx.x] = p >> 3;
+    }
+    __syncthreads();
+    const uint32_t nbytes = S.total_bits >> 3;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(a.slots + (int64_t)blockIdx.x * kOutBytes);
+    for (uint32_t i = tid; i < (nbytes + 3u) / 4u; i += kNT) dst[i] = S.out[i];
+}
+
+// exclusive scan of the member sizes (one block) -> offsets, total at [n]
+__global__ __launch_bounds__(1024) void k_gzip_scan(const uint32_t* sizes, int n, uint64_t* off) {
+    __shared__ uint64_t part[1024 / 64];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int per = (n + 1023) / 1024;
+    const int b0 = tid * per, b1 = std::min(n, b0 + per);
+    uint64_t s = 0;
+    for (int i = b0; i < b1; ++i) s += sizes[i];
+    uint64_t inc = s;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
+    }
+    if (lane == 63) part[w] = inc;
+    __syncthreads();
+    uint64_t base = inc - s;
+    for (int j = 0; j < w; ++j) base += part[j];
+    for (int i = b0; i < b1; ++i) { off[i] = base; base += sizes[i]; }
+    if (tid == 1023) off[n] = base;
+}
+
+// members -> one contiguous stream
+__global__ __launch_bounds__(256) void k_gzip_pack(const uint8_t* slots, const uint32_t* sizes, const uint64_t* off,
+                                                   uint8_t* packed) {
+    const uint8_t* src = slots + (int64_t)blockIdx.x * kOutBytes;
+    uint8_t* dst = packed + off[blockIdx.x];
+    for (uint32_t i = threadIdx.x; i < sizes[blockIdx.x]; i += 256) dst[i] = src[i];
+}
+
+}  // namespace gz
+
+namespace {
+thread_local std::string g_gzerr;
+int gzfail(int code, const std::string& m) { g_gzerr = m; return code; }
+#define GZHIP(x)                                                                                        \
+    do {                                                                                                \
+        hipError_t e_ = (x);                                                                            \
+        if (e_ != hipSuccess) return gzfail(OFL_EHIP, std::string(#x " failed: ") + hipGetErrorString(e_)); \
+    } while (0)
+
+// raw CRC-32 advance matrices for 2^k zero bytes
+void crc_matrices(uint32_t (&m)[17][32]) {
+    uint32_t tab[256];
+    for (uint32_t i = 0; i < 256; ++i) {
+        uint32_t r = i;
+        for (int k = 0; k < 8; ++k) r = (r & 1u) ? (r >> 1) ^ 0xEDB88320u : r >> 1;
+        tab[i] = r;
+    }
+    for (int i = 0; i < 32; ++i) { const uint32_t v = 1u << i; m[0][i] = tab[v & 0xffu] ^ (v >> 8); }
+    auto apply = [](const uint32_t* M, uint32_t v) {
+        uint32_t r = 0;
+        for (int i = 0; i < 32; ++i) if ((v >> i) & 1u) r ^= M[i];
+        return r;
+    };
+    for (int k = 1; k < 17; ++k)
+        for (int i = 0; i < 32; ++i) m[k][i] = apply(m[k - 1], apply(m[k - 1], 1u << i));
+}
+}  // namespace
+
+extern "C" {
+
+const char* ofl_gzip_last_error(void) { return g_gzerr.c_str(); }
+
+size_t ofl_gzip_ranks_workspace_bytes(int64_t n) {
+    const int64_t members = std::max<int64_t>(1, std::min<int64_t>((n + gz::kTok - 1) / gz::kTok, gz::kBatch));
+    return 2 * (size_t)members * gz::kOutBytes + 4 * (size_t)members + 8 * (size_t)(members + 1) + 1024;
+}
+
+size_t ofl_gzip_ranks_bound(int64_t n) {
+    const int64_t members = std::max<int64_t>(1, (n + gz::kTok - 1) / gz::kTok);
+    return (size_t)members * gz::kOutBytes;
+}
+
+int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size_t* out_len, void* ws,
+                   size_t ws_bytes, void* stream) {
+    if (n < 1 || !x || !out || !out_len) return gzfail(OFL_EINVAL, "gzip ranks: empty input");
+    if (!ws || ws_bytes < ofl_gzip_ranks_workspace_bytes(n)) return gzfail(OFL_ESPACE, "gzip ranks: workspace too small");
+    static std::once_flag once;
+    static hipError_t init = hipSuccess;
+    std::call_once(once, [] {
+        uint32_t m[17][32];
+        crc_matrices(m);
+        init = hipMemcpyToSymbol(HIP_SYMBOL(gz::c_adv), m, sizeof(m));
+        if (init == hipSuccess)
+            init = hipFuncSetAttribute((const void*)gz::k_gzip_members, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)sizeof(gz::Smem));
+    });
+    GZHIP(init);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const int64_t members = (n + gz::kTok - 1) / gz::kTok;
+    const int64_t batch = std::min<int64_t>(members, gz::kBatch);
+    char* w = static_cast<char*>(ws);
+    uint8_t* slots = reinterpret_cast<uint8_t*>(w);
+    uint8_t* packed = slots + (size_t)batch * gz::kOutBytes;
+    uint32_t* sizes = reinterpret_cast<uint32_t*>(packed + (size_t)batch * gz::kOutBytes);
+    uint64_t* off = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(sizes) + ((4 * (size_t)batch + 7) & ~(size_t)7));
+    int* bad = reinterpret_cast<int*>(off + batch + 1);
+    GZHIP(hipMemsetAsync(bad, 0, sizeof(int), st));
+    size_t total = 0;
+    for (int64_t c0 = 0; c0 < members; c0 += batch) {
+        const int nb = (int)std::min<int64_t>(batch, members - c0);
+        gz::GzArgs a{x, n, c0, slots, sizes, bad};
+        hipLaunchKernelGGL(gz::k_gzip_members, dim3(nb), dim3(gz::kNT), sizeof(gz::Smem), st, a);
+        hipLaunchKernelGGL(gz::k_gzip_scan, dim3(1), dim3(1024), 0, st, sizes, nb, off);
+        hipLaunchKernelGGL(gz::k_gzip_pack, dim3(nb), dim3(256), 0, st, slots, sizes, off, packed);
+        GZHIP(hipGetLastError());
+        uint64_t tot = 0;
+        int badh = 0;
+        GZHIP(hipMemcpyAsync(&tot, off + nb, 8, hipMemcpyDeviceToHost, st));
+        GZHIP(hipMemcpyAsync(&badh, bad, sizeof(int), hipMemcpyDeviceToHost, st));
+        GZHIP(hipStreamSynchronize(st));
+        if (badh) return gzfail(OFL_EINVAL, "gzip ranks: values must be float32 integers 0..31");
+        if (total + tot > out_cap) return gzfail(OFL_ESPACE, "gzip ranks: output buffer too small");
+        GZHIP(hipMemcpyAsync(out + total, packed, tot, hipMemcpyDeviceToHost, st));
+        GZHIP(hipStreamSynchronize(st));
+        total += tot;
+    }
+    *out_len = total;
+    return OFL_OK;
+}
+
+}  // extern "C"

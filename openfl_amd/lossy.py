@@ -224,6 +224,26 @@ def lut_decode_batch(ranks_arena, offsets, numels, maps, out_arena):
     return out_arena
 
 
+def gzip_ranks(x):
+    """gzip.compress of a float32 device array of ranks (integers 0..31), on
+    the GPU (ofl_gzip_ranks): a multi-member gzip stream that gzip.decompress
+    reads back to x's bytes.  Raises CodecError for other values."""
+    _check_dev(x)
+    L = _lib.lib()
+    n = x.numel()
+    if n == 0:
+        return gzip.compress(b"", compresslevel=9)
+    ws = _ws_bytes(x.device, int(L.ofl_gzip_ranks_workspace_bytes(n)))
+    cap = int(L.ofl_gzip_ranks_bound(n))
+    out = getattr(_tls, "gz_out", None)
+    if out is None or out.numel() < cap:
+        out = _tls.gz_out = torch.empty(cap, dtype=torch.uint8).pin_memory()
+    ln = ctypes.c_size_t()
+    _lib.check_gzip(L.ofl_gzip_ranks(x.data_ptr(), n, out.data_ptr(), cap, ctypes.byref(ln), ws.data_ptr(),
+                                     ws.numel(), _stream(x.device)))
+    return out[:ln.value].numpy().tobytes()
+
+
 def rank_map(values):
     """_float_to_int (kc_pipeline.py:88-114): sorted unique values -> ranks.
     Returns (unique sorted values, rank index per input value)."""

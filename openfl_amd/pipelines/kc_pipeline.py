@@ -47,10 +47,10 @@ class KCPipeline(TransformationPipeline):
     """plan.yaml: template openfl_amd.pipelines.KCPipeline, settings n_clusters
     (p_sparsity accepted and ignored, like the reference :160-181)."""
 
-    def __init__(self, p_sparsity=0.01, n_clusters=6, device="cpu", gzip_level=9, **kwargs):
+    def __init__(self, p_sparsity=0.01, n_clusters=6, device="cpu", gzip_level=9, gzip_backend="host", **kwargs):
         self.p = p_sparsity
         self.n_cluster = n_clusters
-        super().__init__(transformers=[KmeansTransformer(n_clusters, device), GZIPTransformer(gzip_level)],
+        super().__init__(transformers=[KmeansTransformer(n_clusters, device), GZIPTransformer(gzip_level, backend=gzip_backend)],
                          **kwargs)
 
     def forward(self, data, **kwargs):
@@ -60,5 +60,5 @@ class KCPipeline(TransformationPipeline):
         ranks, m = km._ranks(data)
         if ranks is None:
             return super().forward(data, **kwargs)
-        payload, gz_md = gz.forward(ranks.cpu().numpy())
+        payload, gz_md = gz.forward_device(ranks)
         return payload, [{"int_list": list(data.shape), "int_to_float": m}, gz_md]

@@ -26,16 +26,33 @@ def float_to_int(np_array):
 
 
 class GZIPTransformer(Transformer):
-    """float32 bytes -> gzip (lossless).  Large payloads become a multi-member
-    gzip stream compressed on host threads; gzip.decompress reads it."""
+    """float32 bytes -> gzip (lossless).  backend="host": gzip.compress at
+    `level` (large payloads as a multi-member stream compressed on host
+    threads); backend="device": the GPU gzip of rank arrays
+    (lossy.gzip_ranks, csrc/deflate_kernels.hip).  Either way
+    gzip.decompress reads the stream back to the same bytes."""
 
-    def __init__(self, level=9, threads=8):
+    def __init__(self, level=9, threads=8, backend="host"):
+        if backend not in ("host", "device"):
+            raise ValueError("gzip backend must be 'host' or 'device'")
         self.lossy = False
         self.level = level
         self.threads = threads
+        self.backend = backend
 
     def forward(self, data, **kwargs):
         return lossy.gzip_compress(data.astype(np.float32).tobytes(), self.level, self.threads), {}
+
+    def forward_device(self, ranks_dev):
+        """forward of a float32 device array of ranks: on the GPU with the
+        device backend (values outside 0..31 go through the host gzip)."""
+        if self.backend == "device":
+            try:
+                return lossy.gzip_ranks(ranks_dev), {}
+            except lossy._lib.CodecError as e:
+                if "values must be" not in str(e):
+                    raise
+        return self.forward(ranks_dev.cpu().numpy())
 
     def backward(self, data, metadata, **kwargs):
         return np.frombuffer(gzip.decompress(data), dtype=np.float32)

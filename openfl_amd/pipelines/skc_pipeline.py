@@ -37,11 +37,11 @@ class SKCPipeline(TransformationPipeline):
     """plan.yaml: template openfl_amd.pipelines.SKCPipeline, settings
     p_sparsity, n_clusters (:233-262)."""
 
-    def __init__(self, p_sparsity=0.1, n_clusters=6, device="cpu", gzip_level=9, **kwargs):
+    def __init__(self, p_sparsity=0.1, n_clusters=6, device="cpu", gzip_level=9, gzip_backend="host", **kwargs):
         self.p = p_sparsity
         self.n_cluster = n_clusters
         super().__init__(transformers=[SparsityTransformer(self.p, device), KmeansTransformer(n_clusters, device),
-                                       GZIPTransformer(gzip_level)], **kwargs)
+                                       GZIPTransformer(gzip_level, backend=gzip_backend)], **kwargs)
 
     def forward(self, data, **kwargs):
         sp, km, gz = self.transformers
@@ -49,7 +49,7 @@ class SKCPipeline(TransformationPipeline):
         if sparse.numel() >= km.n_cluster:
             # the reference clusters the float64 sparse vector: float64 centres
             ranks, m = kmeans_ranks(sparse, km.n_cluster, np.float64)
-            payload, gz_md = gz.forward(ranks.cpu().numpy())
+            payload, gz_md = gz.forward_device(ranks)
             return payload, [{"int_list": list(data.shape)}, {"int_to_float": m}, gz_md]
         return super().forward(data, **kwargs)
 

@@ -192,6 +192,29 @@ def main():
         t = timed(fn, arg, args.steps, args.warmup)
         res[name] = {"value": round(nbytes / t / 2 ** 30, 3), "ms_per_step": round(1e3 * t, 3)}
 
+    # GZIPTransformer on the KC ranks: GPU gzip of the whole set vs host gzip -9
+    if "gzip" in only or not args.only:
+        from openfl_amd import lossy
+        import gzip as _gz
+        kc_step(ar)
+        torch.cuda.synchronize()
+        z = lossy.gzip_ranks(ar.ranks)
+        reps = 3
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            z = lossy.gzip_ranks(ar.ranks)
+        t_gz = (time.perf_counter() - t0) / reps
+        rb = ar.ranks[:1 << 22].cpu().numpy().tobytes()   # 16 MiB sample for the host reference
+        t0 = time.perf_counter()
+        zh = _gz.compress(rb, compresslevel=9)
+        t_h = time.perf_counter() - t0
+        res["gzip_device"] = {"value": round(4 * ar.ranks.numel() / t_gz / 2 ** 30, 3), "ms_per_call": round(1e3 * t_gz, 3),
+                              "ratio": round(len(z) / (4 * ar.ranks.numel()), 4),
+                              "note": "GB of float32 ranks (whole arena incl. alignment gaps) -> host bytes, D2H included"}
+        res["gzip_host_level9"] = {"value": round(len(rb) / t_h / 2 ** 30, 4), "ratio": round(len(zh) / len(rb), 4),
+                                   "sample": "16 MiB of the same ranks, gzip.compress(level 9), 1 thread"}
+
     # quality of the KC result (not timed)
     maps = []
     y = kc_step(ar, maps)
