@@ -295,6 +295,13 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
  * (eden_pipeline.py:771, NumPy scalar arithmetic).  Host pointers. */
 float ofl_serial_sum_f32(const float* x, int64_t n);
 double ofl_serial_sum_f64(const double* x, int64_t n);
+/* ofl_serial_sum_* of n host arrays (f32 or, if f64, double) on up to
+ * nthreads native threads, largest first; out[i] as double (exact for f32). */
+int ofl_serial_sums_many(int n, const void* const* ptrs, const int64_t* lens, int f64, double* out, int nthreads);
+/* n host memcpy's (dst[i] <- src[i], bytes[i]) on up to nthreads threads, the
+ * bytes split evenly: the staging fills and output copies of the batched
+ * pipeline calls (GIL-free from ctypes). */
+int ofl_host_copy_many(int n, void* const* dst, const void* const* src, const int64_t* bytes, int nthreads);
 
 #ifdef __cplusplus
 }

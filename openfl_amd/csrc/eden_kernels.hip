@@ -43,7 +43,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <atomic>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -2428,16 +2430,66 @@ int ofl_eden_plan_profile_collect(ofl_eden_plan_t pl, int encode, double* ms_sum
     return OFL_OK;
 }
 
+// strict IEEE order: the library is built without fast-math/reassociation,
+// so the compiler keeps the dependent add chain (no vectorised partial sums)
 float ofl_serial_sum_f32(const float* x, int64_t n) {
-    volatile float s = 0.0f;
+    float s = 0.0f;
     for (int64_t i = 0; i < n; ++i) s = s + x[i];
     return s;
 }
 
 double ofl_serial_sum_f64(const double* x, int64_t n) {
-    volatile double s = 0.0;
+    double s = 0.0;
     for (int64_t i = 0; i < n; ++i) s = s + x[i];
     return s;
+}
+
+int ofl_serial_sums_many(int n, const void* const* ptrs, const int64_t* lens, int f64, double* out, int nthreads) {
+    if (n <= 0) return OFL_OK;
+    if (!ptrs || !lens || !out) return fail(OFL_EINVAL, "serial_sums: null arrays");
+    std::vector<int> order(n);
+    for (int i = 0; i < n; ++i) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return lens[a] > lens[b]; });  // largest first
+    std::atomic<int> next{0};
+    auto work = [&] {
+        for (int k = next++; k < n; k = next++) {
+            const int i = order[k];
+            out[i] = f64 ? ofl_serial_sum_f64(static_cast<const double*>(ptrs[i]), lens[i])
+                         : (double)ofl_serial_sum_f32(static_cast<const float*>(ptrs[i]), lens[i]);
+        }
+    };
+    const int nt = std::max(1, std::min(nthreads, n));
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work);
+    work();
+    for (auto& x : th) x.join();
+    return OFL_OK;
+}
+
+int ofl_host_copy_many(int n, void* const* dst, const void* const* src, const int64_t* bytes, int nthreads) {
+    if (n <= 0) return OFL_OK;
+    if (!dst || !src || !bytes) return fail(OFL_EINVAL, "copy_many: null arrays");
+    int64_t total = 0;
+    for (int i = 0; i < n; ++i) total += bytes[i] > 0 ? bytes[i] : 0;
+    // split the bytes evenly over the threads (items are cut at thread borders)
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(std::max(nthreads, 1), total >> 20));
+    auto work = [&](int t) {
+        const int64_t lo = total * t / nt, hi = total * (t + 1) / nt;
+        int64_t acc = 0;
+        for (int i = 0; i < n && acc < hi; ++i) {
+            const int64_t b = bytes[i] > 0 ? bytes[i] : 0;
+            const int64_t s0 = std::max(acc, lo), s1 = std::min(acc + b, hi);
+            if (s1 > s0)
+                memcpy(static_cast<char*>(dst[i]) + (s0 - acc), static_cast<const char*>(src[i]) + (s0 - acc),
+                       (size_t)(s1 - s0));
+            acc += b;
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+    return OFL_OK;
 }
 
 }  // extern "C"

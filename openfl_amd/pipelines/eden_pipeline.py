@@ -49,6 +49,28 @@ def _serial_sum(flat):
     return sum(flat)
 
 
+def _serial_sums(flats):
+    """_serial_sum of many arrays: float32 / float64 ones in one native
+    multi-threaded call (ofl_serial_sums_many), others one by one."""
+    out = [None] * len(flats)
+    for dt, f64 in ((np.float32, 0), (np.float64, 1)):
+        idx = [i for i, f in enumerate(flats) if f.dtype == dt]
+        if not idx:
+            continue
+        arrs = [np.ascontiguousarray(flats[i]) for i in idx]
+        ptrs = np.asarray([a.ctypes.data for a in arrs], np.uint64)
+        lens = np.asarray([a.size for a in arrs], np.int64)
+        res = np.zeros(len(idx), np.float64)
+        _lib.check(_lib.lib().ofl_serial_sums_many(len(idx), ptrs.ctypes.data, lens.ctypes.data, f64,
+                                                   res.ctypes.data, 16))
+        for i, v in zip(idx, res):
+            out[i] = dt(v)
+    for i, f in enumerate(flats):
+        if out[i] is None:
+            out[i] = _serial_sum(f)
+    return out
+
+
 def eden_seed(data, mode="reference", total=None):
     """Seed of EdenTransformer.forward (:771-772); draws ONE np.random value.
     total: the precomputed serial sum (forward_batch computes them in parallel)."""
@@ -71,6 +93,17 @@ def eden_seeds(totals):
 
 
 _pool = None
+
+
+def _copy_many(dst, src, nbytes, threads=8):
+    """Host memcpy's on native threads (ofl_host_copy_many, no GIL)."""
+    n = len(dst)
+    if n == 0:
+        return
+    d = np.asarray(dst, np.uint64)
+    s = np.asarray(src, np.uint64)
+    b = np.asarray(nbytes, np.int64)
+    _lib.check(_lib.lib().ofl_host_copy_many(n, d.ctypes.data, s.ctypes.data, b.ctypes.data, threads))
 
 
 def _threads():
@@ -172,12 +205,9 @@ def _batch_encode(eden, arrays, seeds):
     xh = stg.get("x", plan.arena_numel, torch.float32)
     ph = stg.get("planes", plan.planes_bytes, torch.uint8)
     sh = stg.get("scales", plan.n_slices, torch.float32)
-    xn = xh.numpy()
-
-    def fill(i):
-        off = plan.elem_offsets[i]
-        xn[off:off + flats[i].size] = flats[i]
-    list(_threads().map(fill, range(len(flats))))
+    base = xh.data_ptr()
+    _copy_many([base + 4 * plan.elem_offsets[i] for i in range(len(flats))],
+               [f.ctypes.data for f in flats], [4 * f.size for f in flats])
     with torch.cuda.stream(st):
         x = torch.empty(max(plan.arena_numel, 1), dtype=torch.float32, device=eden.device)
         x.copy_(xh[:max(plan.arena_numel, 1)], non_blocking=True)
@@ -213,17 +243,14 @@ def _batch_decode(eden, items):
     stg = eden._staging()
     ph = stg.get("planes_in", plan.planes_bytes, torch.uint8)
     yh = stg.get("y", plan.arena_numel, torch.float32)
-    pn = ph.numpy()
     sc = np.asarray([v for s_ in scales for v in s_] or [0.0], np.float32)
-
-    def fill(t):
-        data = items[t][0]
-        po, pb = plan.planes_offsets[t], plan.planes_nbytes[t]
-        buf = np.frombuffer(data, dtype=np.uint8)
-        if buf.size < pb:
-            raise ValueError(f"Eden payload has {buf.size} bytes, expected {pb}")
-        pn[po:po + pb] = buf[:pb]
-    list(_threads().map(fill, range(len(items))))
+    bufs = [np.frombuffer(items[t][0], dtype=np.uint8) for t in range(len(items))]
+    for t, b in enumerate(bufs):
+        if b.size < plan.planes_nbytes[t]:
+            raise ValueError(f"Eden payload has {b.size} bytes, expected {plan.planes_nbytes[t]}")
+    pbase = ph.data_ptr()
+    _copy_many([pbase + plan.planes_offsets[t] for t in range(len(items))], [b.ctypes.data for b in bufs],
+               [plan.planes_nbytes[t] for t in range(len(items))])
     with torch.cuda.stream(st):
         planes = torch.empty(max(plan.planes_bytes, 1), dtype=torch.uint8, device=eden.device)
         planes.copy_(ph[:max(plan.planes_bytes, 1)], non_blocking=True)
@@ -232,13 +259,10 @@ def _batch_decode(eden, items):
         y = codec.decode_arena(plan, planes, scd, sdd, stream=st)
         yh[:max(plan.arena_numel, 1)].copy_(y[:max(plan.arena_numel, 1)], non_blocking=True)
     st.synchronize()
-    yn = yh.numpy()
-    outs = [None] * len(items)
-
-    def take(t):
-        off = plan.elem_offsets[t]
-        outs[t] = yn[off:off + totals[t]].copy()
-    list(_threads().map(take, range(len(items))))
+    outs = [np.empty(totals[t], np.float32) for t in range(len(items))]
+    ybase = yh.data_ptr()
+    _copy_many([o.ctypes.data for o in outs], [ybase + 4 * plan.elem_offsets[t] for t in range(len(items))],
+               [4 * totals[t] for t in range(len(items))])
     return outs
 
 
@@ -283,10 +307,8 @@ class EdenTransformer(Transformer):
         np.random draws happen in tensor order exactly as per-tensor calls do."""
         arrays = [np.asarray(a) for a in arrays]
 
-        def total(a):
-            flat = a.reshape(-1)
-            return _serial_sum(flat[:_FAST_SEED_PREFIX] if self.seed_mode == "fast" else flat)
-        totals = list(_threads().map(total, arrays))
+        totals = _serial_sums([a.reshape(-1)[:_FAST_SEED_PREFIX] if self.seed_mode == "fast" else a.reshape(-1)
+                               for a in arrays])
         seeds = eden_seeds(totals)
         big = [i for i, a in enumerate(arrays) if a.size > self.dim_threshold]
         enc = _batch_encode(self.eden, [arrays[i] for i in big], [seeds[i] for i in big]) if big else []
