@@ -138,20 +138,44 @@ class Eden:
             sg = self._tls.staging = _Staging()
         return sg
 
+    def _dev(self, name, n, dtype):
+        """Per-thread device buffers of the one-tensor calls (grow only)."""
+        bufs = getattr(self._tls, "dev", None)
+        if bufs is None:
+            bufs = self._tls.dev = {}
+        b = bufs.get(name)
+        if b is None or b.numel() < n or b.dtype != dtype:
+            b = bufs[name] = torch.empty(1 << max(int(n) - 1, 4095).bit_length(), dtype=dtype, device=self.device)
+        return b
+
     def compress(self, vec, seed):
-        """(planes uint8 ndarray, scales list[float], dims list[int], total_dim) (:555-611)."""
+        """(planes uint8 ndarray, scales list[float], dims list[int], total_dim) (:555-611).
+        One tensor: pinned staging, one H2D, the launches, one D2H, one sync."""
         flat = np.ascontiguousarray(np.asarray(vec).reshape(-1), dtype=np.float32)
         n = flat.size
         plan = self.codec.plan([n])
-        st = self._stream()
+        st, stg = self._stream(), self._staging()
+        xh = stg.get("x1", n, torch.float32)
+        sh = stg.get("s1", 1, torch.int32)
+        if n:
+            xh.numpy()[:n] = flat
+        sh.numpy()[0] = int(seed)
+        pb, ns = plan.planes_bytes, plan.n_slices
+        ph = stg.get("p1", pb, torch.uint8)
+        sch = stg.get("c1", ns, torch.float32)
         with torch.cuda.stream(st):
-            x = torch.from_numpy(flat).to(self.device, non_blocking=False) if n else \
-                torch.empty(1, dtype=torch.float32, device=self.device)
-            seeds = torch.tensor([int(seed)], dtype=torch.int32).to(self.device)
-            planes, scales = self.codec.encode_arena(plan, x, seeds, stream=st)
-            planes_h = planes[:plan.planes_bytes].cpu().numpy()
-            scales_h = scales[:plan.n_slices].cpu().numpy()
-        return planes_h, [float(s) for s in scales_h], list(plan.dims[0]), n
+            x = self._dev("x", plan.arena_numel, torch.float32)
+            if n:
+                x[:n].copy_(xh[:n], non_blocking=True)
+            sd = self._dev("s", 1, torch.int32)
+            sd[:1].copy_(sh[:1], non_blocking=True)
+            planes = self._dev("p", pb, torch.uint8)
+            scales = self._dev("c", ns, torch.float32)
+            plan.encode(x, sd, planes, scales, self.codec.ws.get(plan.ws_bytes, self.device), st)
+            ph[:max(pb, 1)].copy_(planes[:max(pb, 1)], non_blocking=True)
+            sch[:max(ns, 1)].copy_(scales[:max(ns, 1)], non_blocking=True)
+        st.synchronize()
+        return ph.numpy()[:pb].copy(), [float(v) for v in sch.numpy()[:ns]], list(plan.dims[0]), n
 
     def decompress(self, bins, metadata):
         """bins: uint8 planes; metadata: int_to_float mapping (:632-659)."""
@@ -169,14 +193,28 @@ class Eden:
         plan = self.codec.plan([total_dim], dims=[dims])
         if planes_h.size < plan.planes_bytes:
             raise ValueError(f"Eden payload has {planes_h.size} bytes, expected {plan.planes_bytes}")
-        st = self._stream()
+        st, stg = self._stream(), self._staging()
+        pb, ns = plan.planes_bytes, plan.n_slices
+        ph = stg.get("pi1", pb, torch.uint8)
+        sch = stg.get("ci1", ns, torch.float32)
+        sh = stg.get("si1", 1, torch.int32)
+        ph.numpy()[:pb] = planes_h[:pb]
+        sch.numpy()[:ns] = np.asarray(scales, np.float32)
+        sh.numpy()[0] = seed
+        yh = stg.get("y1", total_dim, torch.float32)
         with torch.cuda.stream(st):
-            planes = torch.from_numpy(planes_h[:plan.planes_bytes].copy()).to(self.device)
-            sc = torch.tensor(np.asarray(scales, np.float32)).to(self.device)
-            seeds = torch.tensor([seed], dtype=torch.int32).to(self.device)
-            y = self.codec.decode_arena(plan, planes, sc, seeds, stream=st)
-            out = y[:total_dim].cpu().numpy()
-        return out
+            planes = self._dev("pi", pb, torch.uint8)
+            planes[:max(pb, 1)].copy_(ph[:max(pb, 1)], non_blocking=True)
+            sc = self._dev("ci", ns, torch.float32)
+            sc[:max(ns, 1)].copy_(sch[:max(ns, 1)], non_blocking=True)
+            sd = self._dev("si", 1, torch.int32)
+            sd[:1].copy_(sh[:1], non_blocking=True)
+            y = self._dev("y", plan.arena_numel, torch.float32)
+            plan.decode(planes, sd, sc, y, self.codec.ws.get(plan.ws_bytes, self.device), st)
+            if total_dim:
+                yh[:total_dim].copy_(y[:total_dim], non_blocking=True)
+        st.synchronize()
+        return yh.numpy()[:total_dim].copy()
 
 
 class _Staging:
@@ -188,7 +226,8 @@ class _Staging:
     def get(self, name, n, dtype):
         b = self.bufs.get(name)
         if b is None or b.numel() < n or b.dtype != dtype:
-            b = torch.empty(max(int(n), 1), dtype=dtype).pin_memory()
+            # power-of-two growth: pinning is slow, tensor sizes vary call to call
+            b = torch.empty(1 << max(int(n) - 1, 4095).bit_length(), dtype=dtype).pin_memory()
             self.bufs[name] = b
         return b
 
