@@ -336,7 +336,7 @@ def test_gzip_ranks_roundtrip(case):
     assert z == lossy.gzip_ranks(torch.from_numpy(x).to(DEV))      # deterministic
     if case == "kc6":
         ref = len(gzip.compress(x.tobytes(), compresslevel=9))
-        assert len(z) < 2.0 * ref, (len(z), ref)   # ratio 0.20 vs gzip -9's 0.117
+        assert len(z) < 1.35 * ref, (len(z), ref)   # ratio 0.139 vs gzip -9 0.118
 
 
 def test_gzip_ranks_rejects_non_ranks():
