@@ -1649,7 +1649,7 @@ struct Launch {
     int count;       // list entries
     int64_t blocks;  // grid size
     int nu = 0;      // column: tile 0 of each slice writes the slice norm
-    int stream = 0;  // 0: the caller's stream, 1: the plan's side stream
+    int stream = 0;  // 0: the caller's stream, 1: the plan's side stream, 2: its small-slice stream
     int join = 0;    // the caller's stream waits for the side stream before this launch
     int tl = 15;     // column: log2 of the tile (16: k_col6 with 1024 threads)
     int64_t bytes_moved = 0;  // fp32/plane bytes this launch reads + writes (intermediates included)
@@ -1688,7 +1688,8 @@ struct ofl_eden_plan {
     bool uploaded = false;
     std::mutex mu;
     hipStream_t side = nullptr;  // nstreams == 2 (created on first use)
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipStream_t side2 = nullptr; // the tiny / small slices, beside both wave streams
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr;
     std::mutex run_mu;          // serialises runs that use the side stream
 };
 
@@ -1769,6 +1770,11 @@ bool use_col6() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_COL6"); return !(s && s[0] == '0'); }();
     return on;
 }
+// tiny / small slices on a third stream when the waves use two
+bool use_small_stream() {
+    static const bool on = [] { const char* s = getenv("OFL_EDEN_SMALLSTREAM"); return !(s && s[0] == '0'); }();
+    return on;
+}
 // one k_col_multi launch per wave for the single-level heights 1..5
 bool use_colmulti() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_COLMULTI"); return !(s && s[0] == '0'); }();
@@ -1815,8 +1821,9 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
         lk.lock();
         HIP_TRY(hipEventRecord(pl->ev_fork, caller));
         HIP_TRY(hipStreamWaitEvent(pl->side, pl->ev_fork, 0));
+        if (pl->side2) HIP_TRY(hipStreamWaitEvent(pl->side2, pl->ev_fork, 0));
     }
-    const hipStream_t streams[2] = {caller, two ? pl->side : caller};
+    const hipStream_t streams[3] = {caller, two ? pl->side : caller, pl->side2 ? pl->side2 : caller};
     bool joined = !two;
     std::vector<hipEvent_t>* evs = nullptr;
     if (pl->prof) {  // one event before and one after every launch, on its stream
@@ -1930,6 +1937,10 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
         HIP_TRY(hipEventRecord(pl->ev_join, pl->side));
         HIP_TRY(hipStreamWaitEvent(caller, pl->ev_join, 0));
     }
+    if (two && pl->side2) {
+        HIP_TRY(hipEventRecord(pl->ev_join2, pl->side2));
+        HIP_TRY(hipStreamWaitEvent(caller, pl->ev_join2, 0));
+    }
     return OFL_OK;
 }
 
@@ -1999,13 +2010,18 @@ void build_schedule(ofl_eden_plan* pl) {
     }
     pl->nwaves = (int)waves.size();
     const int nbuf = waves.size() > 1 ? pl->nstreams : 1;
-    // the tiny / small slices are independent of the waves: they go on the
-    // stream with fewer large-slice elements, so they overlap the other's waves
+    // the tiny / small slices are independent of the waves: with two wave
+    // streams they get a third (or, OFL_EDEN_SMALLSTREAM=0, the wave stream
+    // with fewer large-slice elements)
     if (nbuf == 2) {
-        int64_t load[2] = {0, 0};
-        for (size_t w = 0; w < waves.size(); ++w)
-            for (int32_t si : waves[w]) load[w % 2] += 1ll << pl->slices[si].logp;
-        for (Launch& l : common) l.stream = load[1] < load[0] ? 1 : 0;
+        if (use_small_stream()) {  // their own stream: latency-bound, they fill CUs beside both waves
+            for (Launch& l : common) l.stream = 2;
+        } else {
+            int64_t load[2] = {0, 0};
+            for (size_t w = 0; w < waves.size(); ++w)
+                for (int32_t si : waves[w]) load[w % 2] += 1ll << pl->slices[si].logp;
+            for (Launch& l : common) l.stream = load[1] < load[0] ? 1 : 0;
+        }
     }
     pl->enc = common;
     pl->dec = common;
@@ -2264,10 +2280,17 @@ static int ensure_device(ofl_eden_plan_t pl) {
     bool side = false;
     for (const Launch& l : pl->enc) side |= l.stream != 0;
     for (const Launch& l : pl->dec) side |= l.stream != 0;
+    bool side3 = false;
+    for (const Launch& l : pl->enc) side3 |= l.stream == 2;
+    for (const Launch& l : pl->dec) side3 |= l.stream == 2;
     if (side) {
         HIP_TRY(hipStreamCreateWithFlags(&pl->side, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&pl->ev_fork, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&pl->ev_join, hipEventDisableTiming));
+        if (side3) {
+            HIP_TRY(hipStreamCreateWithFlags(&pl->side2, hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&pl->ev_join2, hipEventDisableTiming));
+        }
     }
     pl->uploaded = true;
     return OFL_OK;
@@ -2280,6 +2303,8 @@ void ofl_eden_plan_destroy(ofl_eden_plan_t pl) {
     if (pl->d_slices) (void)hipFree(pl->d_slices);
     if (pl->d_ints) (void)hipFree(pl->d_ints);
     if (pl->side) (void)hipStreamDestroy(pl->side);
+    if (pl->side2) (void)hipStreamDestroy(pl->side2);
+    if (pl->ev_join2) (void)hipEventDestroy(pl->ev_join2);
     if (pl->ev_fork) (void)hipEventDestroy(pl->ev_fork);
     if (pl->ev_join) (void)hipEventDestroy(pl->ev_join);
     delete pl;
