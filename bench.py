@@ -82,7 +82,8 @@ def secondary(name, n_bits, steps, warmup, dev, wave_mib, streams):
     planes = torch.empty(max(plan.planes_bytes, 1), dtype=torch.uint8, device=dev)
     scales = torch.empty(max(plan.n_slices, 1), dtype=torch.float32, device=dev)
     ws = torch.empty(max(plan.ws_bytes, 256), dtype=torch.uint8, device=dev)
-    seeds = torch.arange(len(numels), dtype=torch.int32, device=dev)
+    seeds = torch.tensor(np.random.RandomState(1234).randint(0, 2 ** 16, size=len(numels)), dtype=torch.int32,
+                         device=dev)
     for _ in range(warmup):
         plan.encode(x, seeds, planes, scales, ws)
         plan.decode(planes, seeds, scales, y, ws)

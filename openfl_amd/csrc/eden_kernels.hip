@@ -1687,7 +1687,7 @@ struct ofl_eden_plan {
     int ncu = 256;              // persistent row launches: one block per CU
     bool uploaded = false;
     std::mutex mu;
-    hipStream_t side = nullptr;  // nstreams == 2 (created on first use)
+    hipStream_t side = nullptr;  // nstreams == 2: the device's shared side streams (shared_side_streams)
     hipStream_t side2 = nullptr; // the tiny / small slices, beside both wave streams
     hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr;
     std::mutex run_mu;          // serialises runs that use the side stream
@@ -2263,6 +2263,24 @@ int ofl_eden_plan_create(int ntensors, const int64_t* numel, const int64_t* elem
 // Descriptor tables go to the device on first use (one synchronous copy), so
 // plans can be built and inspected on hosts without a GPU.  The first
 // encode/decode of a plan must therefore not be inside a graph capture.
+// The side streams are shared by every plan of a device (created once):
+// each plan owning its own would soon exceed the HW queues (GPU_MAX_HW_QUEUES,
+// 4 by default), and streams that share a queue serialise -- the small-slice
+// stream then waits behind a wave stream.  Runs of different plans on the
+// shared streams stay correct (fork/join events per plan); they may wait for
+// each other's work enqueued in between.
+static int shared_side_streams(int dev, bool two, hipStream_t& s1, hipStream_t& s2) {
+    static std::mutex mu;
+    static std::map<int, std::pair<hipStream_t, hipStream_t>> pool;
+    std::lock_guard<std::mutex> g(mu);
+    auto& e = pool[dev];
+    if (!e.first) HIP_TRY(hipStreamCreateWithFlags(&e.first, hipStreamNonBlocking));
+    if (two && !e.second) HIP_TRY(hipStreamCreateWithFlags(&e.second, hipStreamNonBlocking));
+    s1 = e.first;
+    s2 = two ? e.second : nullptr;
+    return OFL_OK;
+}
+
 static int ensure_device(ofl_eden_plan_t pl) {
     std::lock_guard<std::mutex> g(pl->mu);
     if (pl->uploaded) return OFL_OK;
@@ -2284,13 +2302,10 @@ static int ensure_device(ofl_eden_plan_t pl) {
     for (const Launch& l : pl->enc) side3 |= l.stream == 2;
     for (const Launch& l : pl->dec) side3 |= l.stream == 2;
     if (side) {
-        HIP_TRY(hipStreamCreateWithFlags(&pl->side, hipStreamNonBlocking));
+        if (int rc = shared_side_streams(pl->device, side3, pl->side, pl->side2)) return rc;
         HIP_TRY(hipEventCreateWithFlags(&pl->ev_fork, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&pl->ev_join, hipEventDisableTiming));
-        if (side3) {
-            HIP_TRY(hipStreamCreateWithFlags(&pl->side2, hipStreamNonBlocking));
-            HIP_TRY(hipEventCreateWithFlags(&pl->ev_join2, hipEventDisableTiming));
-        }
+        if (side3) HIP_TRY(hipEventCreateWithFlags(&pl->ev_join2, hipEventDisableTiming));
     }
     pl->uploaded = true;
     return OFL_OK;
@@ -2302,8 +2317,6 @@ void ofl_eden_plan_destroy(ofl_eden_plan_t pl) {
     for (hipEvent_t e : pl->ev_pool) (void)hipEventDestroy(e);
     if (pl->d_slices) (void)hipFree(pl->d_slices);
     if (pl->d_ints) (void)hipFree(pl->d_ints);
-    if (pl->side) (void)hipStreamDestroy(pl->side);
-    if (pl->side2) (void)hipStreamDestroy(pl->side2);
     if (pl->ev_join2) (void)hipEventDestroy(pl->ev_join2);
     if (pl->ev_fork) (void)hipEventDestroy(pl->ev_fork);
     if (pl->ev_join) (void)hipEventDestroy(pl->ev_join);
