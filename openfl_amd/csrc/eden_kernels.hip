@@ -2023,8 +2023,12 @@ void build_schedule(ofl_eden_plan* pl) {
             for (Launch& l : common) l.stream = load[1] < load[0] ? 1 : 0;
         }
     }
-    pl->enc = common;
-    pl->dec = common;
+    // on their own stream the small-slice launches are enqueued after the
+    // waves' (the critical path reaches the GPU first; each host enqueue costs
+    // microseconds); on a shared stream they go first as before
+    const bool small_last = !common.empty() && common[0].stream == 2;
+    pl->enc = small_last ? std::vector<Launch>{} : common;
+    pl->dec = small_last ? std::vector<Launch>{} : common;
     pl->ws_floats = nbuf * wmax;
     for (size_t w = 0; w < waves.size(); ++w) {
         int64_t off = (int64_t)(w % nbuf) * wmax;
@@ -2111,6 +2115,10 @@ void build_schedule(ofl_eden_plan* pl) {
         pl->dec.push_back(ra);
         pl->dec.insert(pl->dec.end(), cd.begin(), cd.end());
         pl->dec.push_back(rc);
+    }
+    if (small_last) {
+        pl->enc.insert(pl->enc.end(), common.begin(), common.end());
+        pl->dec.insert(pl->dec.end(), common.begin(), common.end());
     }
     if (!large.empty()) {  // scales need every wave's dot partials
         Launch f{K_FINAL, 0, 0, 0, add_list(large), -1, (int)large.size(), (int64_t)large.size()};
