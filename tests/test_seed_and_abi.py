@@ -124,3 +124,26 @@ def test_batched_seed_draws_match_single_calls():
         np.random.seed(s)
         assert eden_seeds(totals) == one
         assert np.random.randint(0, 2 ** 31) == after
+
+
+def test_host_copy_many_and_serial_sums_many():
+    """Host helpers of the batched pipeline path (no GPU): parallel memcpy's
+    land where they should; batched serial sums equal the one-array sums."""
+    from openfl_amd import _lib
+    from openfl_amd.pipelines.eden_pipeline import _copy_many, _serial_sum, _serial_sums
+    rng = np.random.default_rng(5)
+    srcs = [rng.standard_normal(n).astype(np.float32) for n in (0, 1, 1000, 300_000, 77)]
+    dst = np.full(sum(s.size for s in srcs) + 40, -1.0, np.float32)
+    offs, acc = [], 0
+    for s_ in srcs:
+        offs.append(acc)
+        acc += s_.size + 8
+    _copy_many([dst.ctypes.data + 4 * o for o in offs], [s_.ctypes.data for s_ in srcs], [4 * s_.size for s_ in srcs])
+    for o, s_ in zip(offs, srcs):
+        np.testing.assert_array_equal(dst[o:o + s_.size], s_)
+    flats = srcs + [rng.standard_normal(5000), np.float32([1e8, 1.0, -1e8])]
+    got = _serial_sums(flats)
+    for g, f in zip(got, flats):
+        ref = _serial_sum(f)
+        assert g == ref and type(g) is type(ref)
+    assert _lib.lib().ofl_host_copy_many(0, None, None, None, 4) == 0
