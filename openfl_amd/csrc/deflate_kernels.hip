@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "ofl_codec.h"
+#include "ofl_util.h"
 
 #define DEVI __device__ __forceinline__
 
@@ -538,17 +539,15 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
                    size_t ws_bytes, void* stream) {
     if (n < 1 || !x || !out || !out_len) return gzfail(OFL_EINVAL, "gzip ranks: empty input");
     if (!ws || ws_bytes < ofl_gzip_ranks_workspace_bytes(n)) return gzfail(OFL_ESPACE, "gzip ranks: workspace too small");
-    static std::once_flag once;
-    static hipError_t init = hipSuccess;
-    std::call_once(once, [] {
+    GZHIP(ofl_util::per_device_once([] {  // __constant__ tables and attributes are per device
         uint32_t m[17][32];
         crc_matrices(m);
-        init = hipMemcpyToSymbol(HIP_SYMBOL(gz::c_adv), m, sizeof(m));
-        if (init == hipSuccess)
-            init = hipFuncSetAttribute((const void*)gz::k_gzip_members, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)sizeof(gz::Smem));
-    });
-    GZHIP(init);
+        hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(gz::c_adv), m, sizeof(m));
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)gz::k_gzip_members, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)sizeof(gz::Smem));
+        return e;
+    }));
     hipStream_t st = static_cast<hipStream_t>(stream);
     const int64_t members = (n + gz::kTok - 1) / gz::kTok;
     const int64_t batch = std::min<int64_t>(members, gz::kBatch);

@@ -51,6 +51,7 @@
 
 #include "eden_tables.h"
 #include "ofl_codec.h"
+#include "ofl_util.h"
 
 #define DEVI __device__ __forceinline__
 
@@ -1809,9 +1810,7 @@ hipError_t set_all_attrs() {
 }
 
 int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller) {
-    static std::once_flag attrs_once;
-    static hipError_t attrs_err = hipSuccess;
-    std::call_once(attrs_once, [] { attrs_err = set_all_attrs(); });
+    const hipError_t attrs_err = ofl_util::per_device_once([] { return set_all_attrs(); });
     if (attrs_err != hipSuccess) return fail(OFL_EHIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(attrs_err));
     const std::vector<Launch>& L = enc ? pl->enc : pl->dec;
     // waves on the side stream fork from and join back into the caller's stream

@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "ofl_codec.h"
+#include "ofl_util.h"
 
 #define DEVI __device__ __forceinline__
 
@@ -1216,13 +1217,10 @@ int ofl_kmeans1d_batch(int ntensors, const float* x_arena, const int64_t* offset
     const BkmLayout L = bkm_layout(ntensors, numels);
     if (!ws || ws_bytes < L.total) return lfail(OFL_ESPACE, "kmeans: workspace too small");
     if (L.blocks > 0x7fffffff) return lfail(OFL_EINVAL, "kmeans: batch too large");
-    static std::once_flag once;
-    static hipError_t attr = hipSuccess;
-    std::call_once(once, [] {
-        attr = hipFuncSetAttribute((const void*)lossy::k_bkm_seed, hipFuncAttributeMaxDynamicSharedMemorySize,
+    LHIP(ofl_util::per_device_once([] {
+        return hipFuncSetAttribute((const void*)lossy::k_bkm_seed, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)lossy::kBkmSeedLds);
-    });
-    LHIP(attr);
+    }));
     hipStream_t st = static_cast<hipStream_t>(stream);
     char* w = static_cast<char*>(ws);
     std::vector<lossy::BkmTensor> td(ntensors);
