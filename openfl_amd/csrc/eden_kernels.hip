@@ -72,6 +72,8 @@ struct SliceDesc {
     int32_t tensor;
     int32_t scale_idx;
     int32_t part_off;   // offset of this slice's partials (large slices)
+    int32_t perm;       // ws layout of a 2^25 slice: element bit 15 stored at bit 5 (ws_pos)
+    int32_t pad_;
 };
 
 struct KArgs {
@@ -871,11 +873,11 @@ constexpr size_t kRowSmemC = kRowExtra + sizeof(float) * 256;
 typedef const __attribute__((address_space(4))) uint32_t cu32;
 DEVI uint32_t sld(const void* p, int64_t i) { return ((cu32*)p)[i]; }
 DEVI SliceDesc udesc(const SliceDesc* d, int si) {
-    static_assert(sizeof(SliceDesc) == 72, "SliceDesc layout");
+    static_assert(sizeof(SliceDesc) == 80, "SliceDesc layout");
     cu32* p = (cu32*)(d + si);
-    uint32_t w[18];
+    uint32_t w[20];
 #pragma unroll
-    for (int i = 0; i < 18; ++i) w[i] = p[i];
+    for (int i = 0; i < 20; ++i) w[i] = p[i];
     return __builtin_bit_cast(SliceDesc, w);
 }
 DEVI float sldf(const float* p, int64_t i) { return __builtin_bit_cast(float, sld(p, i)); }
@@ -1032,16 +1034,42 @@ DEVI void store_y(const KArgs& a, const SliceDesc& D, uint32_t tile, uint32_t ba
             }
     }
 }
-// ws tiles are always whole (P is a multiple of the row)
+// ws tiles are always whole (P is a multiple of the row).
+// Interleaved layout of 2^25 slices (D.perm): the element bits (0..4, 15,
+// 5..14, 16..) are stored in that order, i.e. bit 15 moves next to the 32
+// columns, so the 2^25 middle pass (k_col6<10>: 32 columns x 1024 rows per
+// tile) reads and writes 256-B row segments instead of 128-B ones.  A row
+// tile t then lives at ((t >> 1) << 16) | ((t & 1) << 5) with a zero bit
+// inserted at position 5 of its element index; L3's register bits (5..10)
+// simply double.
+DEVI constexpr uint32_t ws_row_idx(uint32_t j) { return (j & 31u) | ((j >> 5) << 6); }
+DEVI float* ws_row_base(const KArgs& a, const SliceDesc& D, uint32_t tile) {
+    return D.perm ? a.ws + D.ws_off + ((size_t)(tile >> 1) << (kRowLog + 1)) + ((tile & 1u) << 5)
+                  : a.ws + D.ws_off + ((size_t)tile << kRowLog);
+}
 DEVI void fetch_ws(const KArgs& a, const SliceDesc& D, uint32_t tile, bool live, uint32_t base3, float (&v)[64]) {
-    const rsrc_t r = mk_rsrc(a.ws + D.ws_off + ((size_t)tile << kRowLog), live ? (4u << kRowLog) : 0u);
+    if (D.perm) {
+        const rsrc_t r = mk_rsrc(ws_row_base(a, D, tile), live ? (4u << (kRowLog + 1)) - 128u : 0u);
+        const uint32_t b = ws_row_idx(base3);
 #pragma unroll
-    for (int k = 0; k < 64; ++k) v[k] = bload1(r, base3, LT<RS::L3>::off(k));
+        for (int k = 0; k < 64; ++k) v[k] = bload1(r, b, LT<RS::L3>::off(k) << 1);
+    } else {
+        const rsrc_t r = mk_rsrc(ws_row_base(a, D, tile), live ? (4u << kRowLog) : 0u);
+#pragma unroll
+        for (int k = 0; k < 64; ++k) v[k] = bload1(r, base3, LT<RS::L3>::off(k));
+    }
 }
 DEVI void store_ws(const KArgs& a, const SliceDesc& D, uint32_t tile, uint32_t base3, const float (&v)[64]) {
-    const rsrc_t r = mk_rsrc(a.ws + D.ws_off + ((size_t)tile << kRowLog), 4u << kRowLog);
+    if (D.perm) {
+        const rsrc_t r = mk_rsrc(ws_row_base(a, D, tile), (4u << (kRowLog + 1)) - 128u);
+        const uint32_t b = ws_row_idx(base3);
 #pragma unroll
-    for (int k = 0; k < 64; ++k) bstore1(r, base3, LT<RS::L3>::off(k), v[k]);
+        for (int k = 0; k < 64; ++k) bstore1(r, b, LT<RS::L3>::off(k) << 1, v[k]);
+    } else {
+        const rsrc_t r = mk_rsrc(ws_row_base(a, D, tile), 4u << kRowLog);
+#pragma unroll
+        for (int k = 0; k < 64; ++k) bstore1(r, base3, LT<RS::L3>::off(k), v[k]);
+    }
 }
 // the tile's 8-byte word of every plane (planes >= nbits read as 0).  A8: the
 // launch's plane rows are 8-byte aligned; otherwise bytes.
@@ -1458,7 +1486,19 @@ __global__ __launch_bounds__(col6_nt<TL>(), 4) void k_col6(KArgs a) {
     }
     float v[64];
     const uint32_t base1 = LT<CS::L1>::base(tid);
-    {
+    // interleaved ws layout of 2^25 slices (see ws_row_base): position of
+    // element e = ws_pos(e); a row offset (bits 15..20) moves bit 15 to bit 5
+    constexpr bool PERM = M == 10 && MID && TL == 15;
+    auto ws_pos = [](uint32_t e) -> uint32_t {
+        return (e & 31u) | (((e >> 15) & 1u) << 5) | (((e >> 5) & 1023u) << 6) | ((e >> 16) << 16);
+    };
+    const bool perm = PERM && D.perm;
+    if (perm) {
+        const uint32_t vo = opaque(ws_pos(map(base1)) * 4u);
+#pragma unroll
+        for (int r = 0; r < 64; ++r)
+            v[r] = raw_load_f32(rw, (int)vo, (int)ws_pos((LT<CS::L1>::off(r) >> K) << 15) * 4, 0);
+    } else {
         const uint32_t vo = opaque(map(base1) * 4u);
 #pragma unroll
         for (int r = 0; r < 64; ++r)
@@ -1488,12 +1528,19 @@ __global__ __launch_bounds__(col6_nt<TL>(), 4) void k_col6(KArgs a) {
             exchange_half<CS::L2, CS::L1, CS::HB>(v, s, tid);
         }
         stages<CS::L1, CS::A1>(v);
-        const uint32_t vo = opaque(map(base1) * 4u);
-        int los = lo;
-        asm volatile("" : "+s"(los));  // recompute the row offsets: 64 SGPRs kept live would spill
+        if (perm) {
+            const uint32_t vo = opaque(ws_pos(map(base1)) * 4u);
 #pragma unroll
-        for (int r = 0; r < 64; ++r)
-            raw_store_f32(v[r], rw, (int)vo, (int)uu((LT<CS::L1>::off(r) >> K) << los) * 4, 0);
+            for (int r = 0; r < 64; ++r)
+                raw_store_f32(v[r], rw, (int)vo, (int)ws_pos((LT<CS::L1>::off(r) >> K) << 15) * 4, 0);
+        } else {
+            const uint32_t vo = opaque(map(base1) * 4u);
+            int los = lo;
+            asm volatile("" : "+s"(los));  // recompute the row offsets: 64 SGPRs kept live would spill
+#pragma unroll
+            for (int r = 0; r < 64; ++r)
+                raw_store_f32(v[r], rw, (int)vo, (int)uu((LT<CS::L1>::off(r) >> K) << los) * 4, 0);
+        }
     } else {
         const uint32_t bcw = LT<LC>::base(tid);
         const uint32_t vo = opaque(map(bcw) * 4u);
@@ -1771,6 +1818,11 @@ bool use_col6() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_COL6"); return !(s && s[0] == '0'); }();
     return on;
 }
+// interleaved ws layout for 2^25 slices (256-B segments in the middle pass)
+bool use_perm25() {
+    static const bool on = [] { const char* s = getenv("OFL_EDEN_PERM25"); return !(s && s[0] == '0'); }();
+    return on;
+}
 // tiny / small slices on a third stream when the waves use two
 bool use_small_stream() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_SMALLSTREAM"); return !(s && s[0] == '0'); }();
@@ -1992,6 +2044,7 @@ void build_schedule(ofl_eden_plan* pl) {
             common.push_back({K_SMALL, 11 + k, 0, 0, add_list(pl->small[k]), -1, (int)pl->small[k].size(),
                               (int64_t)pl->small[k].size()});
     const std::vector<int32_t>& large = pl->large;
+    for (auto& D : pl->slices) D.perm = 0;
     std::vector<std::vector<int32_t>> waves;
     int64_t cap = pl->wave_bytes > 0 ? pl->wave_bytes / 4 : INT64_MAX;
     if (pl->nstreams == 2) {  // at least two waves, so both streams have work
@@ -2092,6 +2145,8 @@ void build_schedule(ofl_eden_plan* pl) {
                     seq.push_back(l);
                 } else {
                     seq.push_back({K_COL, r, ofl::kRowLog, 1, lo_c, tp, cnt, tiles});
+                    if (r == 10 && use_col6() && use_perm25())  // k_col6<10, true, 15>: interleaved ws
+                        for (int32_t si : kv.second) pl->slices[si].perm = 1;
                 }
             } else {  // two column levels; the middle launch carries D2
                 const int m1 = r / 2, m2 = r - m1;
