@@ -263,6 +263,20 @@ size_t ofl_wavg_range_sums_workspace_bytes(int ncollab, int nranges, int64_t tot
 int ofl_wavg_delta_range_sums(int ncollab, const float* const* xs, const double* weights, double wsum,
                               const float* base, int nranges, const int64_t* starts, const int64_t* counts,
                               const int32_t* single, double* sums, void* ws, size_t ws_bytes, void* stream);
+/* ofl_wavg_delta_seeds  the Eden seeds of a round end without a host round
+ *                 trip: the float64 delta on the listed ranges (packed_dev,
+ *                 total doubles), their left-to-right sums (sums_dev), and
+ *                 seeds_dev[r] = (hash(sum*13 + 7) + draws_dev[r]) % 2^16 with
+ *                 CPython's float hash (eden_pipeline.py:771-772).  Every
+ *                 pointer is DEVICE memory (xs_dev: ncollab pointers,
+ *                 weights_dev, starts_dev [nranges], dst_dev [nranges + 1]
+ *                 prefix of the range lengths, single_dev [nranges]).  Async.
+ * ofl_py_hash_doubles  CPython's hash() of n device doubles (NaN -> 0). */
+int ofl_wavg_delta_seeds(int ncollab, const float* const* xs_dev, const double* weights_dev, double wsum,
+                         const float* base, int nranges, const int64_t* starts_dev, const int64_t* dst_dev,
+                         const int32_t* single_dev, int64_t total, const int64_t* draws_dev, uint32_t* seeds_dev,
+                         double* sums_dev, double* packed_dev, void* stream);
+int ofl_py_hash_doubles(const double* v_dev, int n, int64_t* out_dev, void* stream);
 size_t ofl_wavg_points_workspace_bytes(int ncollab, int npoints);
 int ofl_wavg_delta_points(int ncollab, const float* const* xs, const double* weights, double wsum, const float* base,
                           int npoints, const int64_t* idx, double* agg_out, double* delta64_out, float* delta32_out,

@@ -30,7 +30,8 @@ EXPORTS = (
     "ofl_sparsify_topk_batch_workspace_bytes", "ofl_sparsify_topk_batch",
     "ofl_ternary_ranks_batch_workspace_bytes", "ofl_ternary_ranks_batch",
     "ofl_agg_last_error", "ofl_wavg_delta", "ofl_wavg_ranges_workspace_bytes", "ofl_wavg_delta_ranges",
-    "ofl_wavg_range_sums_workspace_bytes", "ofl_wavg_delta_range_sums",
+    "ofl_wavg_range_sums_workspace_bytes", "ofl_wavg_delta_range_sums", "ofl_wavg_delta_seeds",
+    "ofl_py_hash_doubles",
     "ofl_wavg_points_workspace_bytes", "ofl_wavg_delta_points", "ofl_apply_delta",
     "ofl_apply_delta_ranges",
     "ofl_gzip_last_error", "ofl_gzip_ranks_workspace_bytes", "ofl_gzip_ranks_bound", "ofl_gzip_ranks",
@@ -121,6 +122,10 @@ def _bind(L):
     L.ofl_wavg_range_sums_workspace_bytes.restype = sz
     L.ofl_wavg_delta_range_sums.argtypes = [i32, vp, vp, ctypes.c_double, vp, i32, vp, vp, vp, vp, vp, sz, vp]
     L.ofl_wavg_delta_range_sums.restype = i32
+    L.ofl_wavg_delta_seeds.argtypes = [i32, vp, vp, ctypes.c_double, vp, i32, vp, vp, vp, i64, vp, vp, vp, vp, vp]
+    L.ofl_wavg_delta_seeds.restype = i32
+    L.ofl_py_hash_doubles.argtypes = [vp, i32, vp, vp]
+    L.ofl_py_hash_doubles.restype = i32
     L.ofl_wavg_points_workspace_bytes.argtypes = [i32, i32]
     L.ofl_wavg_points_workspace_bytes.restype = sz
     L.ofl_wavg_delta_points.argtypes = [i32, vp, vp, ctypes.c_double, vp, i32, vp, vp, vp, vp, vp, sz, vp]

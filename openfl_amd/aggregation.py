@@ -16,7 +16,8 @@ sequence over flat arenas (csrc/agg_kernels.hip + the Eden plan): average +
 delta in one kernel (float64 arithmetic in NumPy's order, delta rounded to
 float32 as Eden.compress does), the seeds' serial sums from the delta's values
 summed on the device (fast mode: a 4096-element prefix per tensor, reference
-mode: all of it, one thread per tensor in Python's left-to-right order), one
+mode: all of it, one lane per tensor in Python's left-to-right order) and
+hashed there with CPython's float hash (no host round trip), one
 Eden encode and decode of all the big tensors, and apply_delta in place.  The
 payloads, metadata, np.random draws and new model are identical to calling
 the reference's functions tensor by tensor with an openfl_amd EdenPipeline
@@ -28,7 +29,7 @@ import torch
 
 from openfl_amd import _lib
 from openfl_amd.codec import EdenPlan, resolve_device
-from openfl_amd.pipelines.eden_pipeline import _FAST_SEED_PREFIX, eden_seeds
+from openfl_amd.pipelines.eden_pipeline import _FAST_SEED_PREFIX
 
 _ALIGN = 64
 
@@ -163,6 +164,21 @@ class RoundEnd:
         dst = np.cumsum([0] + [self.numels[i] for i in rest]).astype(np.int64)
         self._rest_start = torch.tensor([self.offsets[i] for i in rest] or [0], dtype=torch.int64).to(self.device)
         self._rest_dst = torch.from_numpy(dst).to(self.device)
+        # seed ranges (a prefix per tensor in fast mode, all of it in reference
+        # mode) as device tables: the seeds are computed without a host round trip
+        T = len(self.numels)
+        counts = [min(n, _FAST_SEED_PREFIX) if self.seed_mode == "fast" else n for n in self.numels]
+        self._seed_total = int(sum(counts))
+        self._seed_start = torch.tensor(self.offsets or [0], dtype=torch.int64).to(self.device)
+        self._seed_dst = torch.from_numpy(np.cumsum([0] + counts).astype(np.int64)).to(self.device)
+        self._seed_single = torch.tensor([1 if n == 1 else 0 for n in self.numels] or [0], dtype=torch.int32).to(self.device)
+        self._seed_sums = torch.empty(max(T, 1), dtype=torch.float64, device=self.device)
+        self._seeds = torch.empty(max(T, 1), dtype=torch.int32, device=self.device)
+        self._packed = torch.empty(max(self._seed_total, 1), dtype=torch.float64, device=self.device)
+        self._big_idx = torch.tensor(self.big or [0], dtype=torch.int64).to(self.device)
+        self._host_args = None   # pinned [collaborator pointers | weights | draws], reused after _args_done
+        self._dev_args = None
+        self._args_done = None
 
     # -- arenas --
     def arena(self):
@@ -196,7 +212,8 @@ class RoundEnd:
         into `out` (default: a new arena; may be base_arena) and, if given,
         the float64 average into agg_out (arena_numel elements).
         -> (new model arena, [(payload bytes, [metadata])] per tensor or None,
-        seeds)."""
+        seeds: a list with payloads, else the device int32 tensor -- without
+        payloads nothing synchronises with the host)."""
         dev = self.device
         xs = list(collab_arenas)
         for x in xs + ([base_arena] if base_arena is not None else []):
@@ -216,26 +233,37 @@ class RoundEnd:
             if self.single:
                 _points_launch(xs, w64, wsum, base_arena, [self.offsets[i] for i in self.single], agg_out, delta,
                                dev, self._ws)
-            # 2. seeds: serial sums of the float64 delta, one np.random draw per tensor in order
-            fast = self.seed_mode == "fast"
-            counts = [min(n, _FAST_SEED_PREFIX) if fast else n for n in self.numels]
-            single = np.asarray([1 if n == 1 else 0 for n in self.numels], np.int32)
-            tot = sum(counts)
-            ptrs = np.asarray([x.data_ptr() for x in xs], np.uint64)
-            st_ = np.asarray(self.offsets, np.int64)
-            ct_ = np.asarray(counts, np.int64)
-            sums = np.zeros(len(counts), np.float64)
-            buf = self._ws(int(L.ofl_wavg_range_sums_workspace_bytes(len(xs), len(counts), tot)))
-            _lib.check_agg(L.ofl_wavg_delta_range_sums(
-                len(xs), ptrs.ctypes.data, w64.ctypes.data, wsum,
-                base_arena.data_ptr() if base_arena is not None else None, len(counts), st_.ctypes.data,
-                ct_.ctypes.data, single.ctypes.data, sums.ctypes.data, buf.data_ptr(), buf.numel(), _stream(dev)))
-            seeds = eden_seeds(list(sums))
+            # 2. seeds on the device: serial sums of the float64 delta, CPython's
+            # float hash, one np.random draw per tensor in order (drawn here)
+            T = len(self.numels)
+            C = len(xs)
+            draws = np.random.randint(1, 2 ** 16, size=T).astype(np.int64) if T else np.zeros(0, np.int64)
+            need = 2 * C + max(T, 1)
+            if self._host_args is None or self._host_args.numel() < need:
+                self._host_args = torch.empty(need, dtype=torch.int64).pin_memory()
+                self._dev_args = torch.empty(need, dtype=torch.int64, device=dev)
+                self._args_done = torch.cuda.Event()
+            else:
+                self._args_done.synchronize()  # the previous call's copy has left the pinned buffer
+            ha = self._host_args.numpy()
+            ha[:C] = np.asarray([x.data_ptr() for x in xs], np.uint64).view(np.int64)
+            ha[C:2 * C] = w64.view(np.int64)
+            ha[2 * C:2 * C + T] = draws
+            self._dev_args[:need].copy_(self._host_args[:need], non_blocking=True)
+            self._args_done.record()
+            dp = self._dev_args.data_ptr()
+            _lib.check_agg(L.ofl_wavg_delta_seeds(
+                C, dp, dp + 8 * C, wsum, base_arena.data_ptr() if base_arena is not None else None, T,
+                self._seed_start.data_ptr(), self._seed_dst.data_ptr(), self._seed_single.data_ptr(), self._seed_total,
+                dp + 16 * C, self._seeds.data_ptr(), self._seed_sums.data_ptr(), self._packed.data_ptr(), _stream(dev)))
+            seeds = None
+            if payloads:
+                seeds = [int(v) for v in self._seeds[:T].cpu().numpy()]
             # 3. encode, (payloads), decode in place, apply
             result = [None] * len(self.numels) if payloads else None
             if self.plan is not None:
                 p = self.plan
-                sd = torch.tensor([seeds[i] for i in self.big], dtype=torch.int32).to(dev)
+                sd = self._seeds.index_select(0, self._big_idx)
                 planes = torch.empty(max(p.planes_bytes, 1), dtype=torch.uint8, device=dev)
                 scales = torch.empty(max(p.n_slices, 1), dtype=torch.float32, device=dev)
                 if self._codec_ws is None or self._codec_ws.numel() < p.ws_bytes:
@@ -277,4 +305,4 @@ class RoundEnd:
                                                      out.data_ptr(), _stream(dev)))
             else:
                 out.copy_(delta)
-        return out, result, seeds
+        return out, result, (seeds if payloads else self._seeds[:len(self.numels)])

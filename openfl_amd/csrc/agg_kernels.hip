@@ -232,6 +232,45 @@ __global__ __launch_bounds__(256) void k_range_sums(const double* packed, const 
     if (threadIdx.x == 0) sums[r] = s;
 }
 
+// CPython's hash of a finite float (Objects/object.c _Py_HashDouble, modulus
+// 2^61 - 1): the 28-bit chunks of the mantissa folded with a rotation, then the
+// exponent as a rotation, the sign, and -1 -> -2.  inf -> +-314159; NaN (an
+// object-id hash in CPython >= 3.10, not reproducible) -> 0.
+__device__ int64_t py_hash_double(double v) {
+    const uint64_t MOD = (1ull << 61) - 1ull;
+    if (isinf(v)) return v > 0 ? 314159 : -314159;
+    if (isnan(v)) return 0;
+    int e;
+    double m = frexp(v, &e);
+    int sign = 1;
+    if (m < 0) { sign = -1; m = -m; }
+    uint64_t x = 0;
+    while (m != 0.0) {
+        x = ((x << 28) & MOD) | x >> (61 - 28);
+        m *= 268435456.0;
+        e -= 28;
+        const uint64_t y = (uint64_t)m;
+        m -= (double)y;
+        x += y;
+        if (x >= MOD) x -= MOD;
+    }
+    e = e >= 0 ? e % 61 : 61 - 1 - ((-1 - e) % 61);
+    x = ((x << e) & MOD) | x >> (61 - e);
+    x = x * (uint64_t)(int64_t)sign;
+    if (x == ~0ull) x = ~0ull - 1ull;
+    return (int64_t)x;
+}
+// the Eden seed of each tensor from its serial float64 sum and its np.random
+// draw (eden_pipeline.py:771-772): (hash(sum * 13 + 7) + draw) % 2^16
+__global__ __launch_bounds__(64) void k_seeds(const double* sums, const int64_t* draws, int n, uint32_t* seeds) {
+#pragma clang fp contract(off)
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= n) return;
+    const double t = sums[i] * 13.0 + 7.0;
+    const int64_t h = py_hash_double(t) + draws[i];
+    seeds[i] = (uint32_t)(((h % 65536) + 65536) % 65536);
+}
+
 // apply_delta: out = base + delta (float32)
 __global__ __launch_bounds__(kNT) void k_apply(const float* base, const float* delta, int64_t n, float* out) {
     const int64_t stride = (int64_t)gridDim.x * kNT;
@@ -261,6 +300,11 @@ __global__ __launch_bounds__(kNT) void k_apply_ranges(const float* base, const f
         const int64_t i = start[lo] + (j - dst[lo]);
         out[i] = base[i] + delta[i];
     }
+}
+
+__global__ __launch_bounds__(64) void k_py_hash(const double* v, int n, int64_t* out) {
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i < n) out[i] = py_hash_double(v[i]);
 }
 
 }  // namespace agg
@@ -405,6 +449,40 @@ int ofl_wavg_delta_range_sums(int ncollab, const float* const* xs, const double*
     AHIP(hipGetLastError());
     AHIP(hipMemcpyAsync(sums, dsums, 8 * (size_t)nranges, hipMemcpyDeviceToHost, st));
     AHIP(hipStreamSynchronize(st));
+    return OFL_OK;
+}
+
+int ofl_wavg_delta_seeds(int ncollab, const float* const* xs_dev, const double* weights_dev, double wsum,
+                         const float* base, int nranges, const int64_t* starts_dev, const int64_t* dst_dev,
+                         const int32_t* single_dev, int64_t total, const int64_t* draws_dev, uint32_t* seeds_dev,
+                         double* sums_dev, double* packed_dev, void* stream) {
+    if (ncollab < 1 || ncollab > 2048 || nranges < 1) return afail(OFL_EINVAL, "wavg seeds: bad sizes");
+    if (!xs_dev || !weights_dev || !starts_dev || !dst_dev || !single_dev || !draws_dev || !seeds_dev || !sums_dev ||
+        (total > 0 && !packed_dev))
+        return afail(OFL_EINVAL, "wavg seeds: null pointer");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    agg::RangeArgs r{};
+    r.p.x = xs_dev;
+    r.p.w = weights_dev;
+    r.p.nc = ncollab;
+    r.p.wsum = wsum;
+    r.p.base = base;
+    r.start = starts_dev;
+    r.dst = dst_dev;
+    r.single = single_dev;
+    r.nr = nranges;
+    if (total > 0) hipLaunchKernelGGL(agg::k_wavg_ranges, dim3(grid_for(total, 1)), dim3(agg::kNT), 0, st, r, packed_dev);
+    hipLaunchKernelGGL(agg::k_range_sums, dim3(nranges), dim3(256), 0, st, packed_dev, dst_dev, sums_dev);
+    hipLaunchKernelGGL(agg::k_seeds, dim3((nranges + 63) / 64), dim3(64), 0, st, sums_dev, draws_dev, nranges, seeds_dev);
+    AHIP(hipGetLastError());
+    return OFL_OK;
+}
+
+int ofl_py_hash_doubles(const double* v_dev, int n, int64_t* out_dev, void* stream) {
+    if (n <= 0) return OFL_OK;
+    hipLaunchKernelGGL(agg::k_py_hash, dim3((n + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), v_dev, n,
+                       out_dev);
+    AHIP(hipGetLastError());
     return OFL_OK;
 }
 

@@ -121,3 +121,22 @@ def test_round_end_many_collaborators_chained():
         np.testing.assert_array_equal(re.view(agg, i).cpu().numpy(), ref_aggs[i])
         assert pay[i] == ref_pay[i]
         np.testing.assert_array_equal(re.view(new, i).cpu().numpy(), ref_models[i])
+
+
+def test_device_python_float_hash():
+    """ofl_py_hash_doubles = CPython's hash() of a float (the Eden seed hashes
+    sum * 13 + 7, eden_pipeline.py:771), incl. negatives, integers, tiny,
+    huge, subnormal and infinite values."""
+    from openfl_amd import _lib
+    rng = np.random.default_rng(1)
+    vals = np.concatenate([rng.standard_normal(2000) * 10.0 ** rng.integers(-30, 30, 2000),
+                           np.float64([0.0, -0.0, 1.0, -1.0, 2.0 ** 61, -(2.0 ** 61) + 1, 7.0, 1e308, -1e-308, 5e-324,
+                                       np.inf, -np.inf, 0.5, -1.5, 123456789.125, float(2 ** 53 + 1)]),
+                           rng.integers(-2 ** 40, 2 ** 40, 500).astype(np.float64)])
+    v = torch.from_numpy(vals).to(DEV)
+    out = torch.empty(vals.size, dtype=torch.int64, device=DEV)
+    _lib.check_agg(_lib.lib().ofl_py_hash_doubles(v.data_ptr(), vals.size, out.data_ptr(),
+                                                  torch.cuda.current_stream().cuda_stream))
+    got = out.cpu().numpy()
+    ref = np.asarray([hash(float(x)) for x in vals], np.int64)
+    np.testing.assert_array_equal(got, ref)
