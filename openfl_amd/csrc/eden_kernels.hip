@@ -2174,9 +2174,16 @@ void build_schedule(ofl_eden_plan* pl) {
         pl->enc.insert(pl->enc.end(), common.begin(), common.end());
         pl->dec.insert(pl->dec.end(), common.begin(), common.end());
     }
-    if (!large.empty()) {  // scales need every wave's dot partials
-        Launch f{K_FINAL, 0, 0, 0, add_list(large), -1, (int)large.size(), (int64_t)large.size()};
-        f.join = 1;
+    // scales: one k_finalize per wave stream, after that stream's last row C,
+    // over the slices of its own waves.  A single finalize on the caller's
+    // stream would need a mid-call join, and a cross-queue wait costs the
+    // caller's queue ~10 us even when it is already satisfied (ResNet-50 trace)
+    for (int s = 0; s < nbuf; ++s) {
+        std::vector<int32_t> fl;
+        for (size_t w = s; w < waves.size(); w += nbuf) fl.insert(fl.end(), waves[w].begin(), waves[w].end());
+        if (fl.empty()) continue;
+        Launch f{K_FINAL, 0, 0, 0, add_list(fl), -1, (int)fl.size(), (int64_t)fl.size()};
+        f.stream = s;
         pl->enc.push_back(f);
     }
     // per-launch byte accounting (bench / DESIGN.md roofline)

@@ -85,11 +85,13 @@ def test_wave_schedule_layout():
         d = "enc" if enc else "dec"
         assert names.count(f"ofl::k_{d}_rowA") == 4
         assert sum(n.startswith(f"ofl::k_{d}_rowC") for n in names) == 4
-        assert names.count("ofl::k_finalize") == (1 if enc else 0)
+        # one k_finalize per wave stream (no mid-call join)
+        assert names.count("ofl::k_finalize") == (2 if enc else 0)
         # same algorithmic bytes whatever the schedule
         assert sum(l["bytes_alg"] for l in w2.launches(enc)) == sum(l["bytes_alg"] for l in one.launches(enc))
     w1 = EdenPlan(numels, 8, wave_mib=32, streams=1)
     assert w1.n_waves == 4 and w1.ws_bytes < w2.ws_bytes
+    assert [l["name"] for l in w1.launches(True)].count("ofl::k_finalize") == 1
     big = EdenPlan([1 << 25, 1 << 22], 8, wave_mib=16, streams=1)   # a slice above the wave size
     assert big.n_waves == 2
     with pytest.raises(_lib.CodecError, match="streams"):
