@@ -1253,10 +1253,10 @@ __global__ __launch_bounds__(kRowNT) void k_dec_rowC(KArgs a) {
         stages<RS::L2, RS::F1b>(v);
         exchange<RS::L2, RS::L1>(v, s, tid);
         stages<RS::L1, RS::F1a>(v);
-        apply_signs_direct<RS::L1>(v, tile << kRowLog, base1, D.logp, b1, pow2i(-((D.logp + 1) / 2)));
+        // scale folded into the 2^-k normalisation: 2^-k is exact, so
+        // v * (sc * 2^-k) rounds like (v * 2^-k) * sc (normal range)
         const float sc = sldf(a.scales_in, D.scale_idx);
-#pragma unroll
-        for (int r = 0; r < 64; ++r) v[r] = sc * v[r];
+        apply_signs_direct<RS::L1>(v, tile << kRowLog, base1, D.logp, b1, sc * pow2i(-((D.logp + 1) / 2)));
         store_y(a, D, tile, base1, v);
         if (!more) break;
         t = tn; si = sn; tile = tln;
