@@ -8,17 +8,26 @@ bit planes + scales in HBM) and decode them back (-> fp32 arena in HBM), the
 per-round codec work of openfl/pipelines/eden_pipeline.py:555-659 for one
 model update.  Inputs are resident before the timed region.
 
-Multi-GPU (launched by torch.distributed.run, one rank per GPU): the path
-shards with no data exchange, so every rank codes its own update set
-("weak" scaling: one collaborator update per GPU; --scaling strong instead
-LPT-partitions ONE set over the ranks).  The only collectives are the
-barrier and the max-over-ranks of the timed region.
+Multi-GPU: one process per GPU.  `--gpus N` with N > 1 started directly
+spawns N ranks (torch.distributed.run, 127.0.0.1) before anything touches a
+GPU; under torch.distributed.run (WORLD_SIZE set) the ranks run as launched.
+The default is "strong" scaling -- ONE update set (BASELINE config 4: one
+Llama-3-8B update) LPT-partitioned over the ranks per tensor, the unit the
+aggregator codes (aggregator.py:816 compress, :826 decompress), balanced by
+the bytes each tensor's passes move (openfl_amd.sharding.tensor_cost).
+`--scaling weak` gives every rank its own set instead.  The path shards with
+no data exchange: the only collectives are the barriers around the timed
+region and the max over ranks of its duration.
 
-Prints ONE JSON line on rank 0 (fields documented in DESIGN.md section 6).
+`--dry-run` runs the sharding and the rank plumbing only (no GPU, gloo).
+
+Prints ONE JSON line on rank 0 (fields documented in DESIGN.md section 4).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -29,26 +38,80 @@ sys.path.insert(0, ROOT)
 
 METRIC = "GiB/s device-resident Eden encode+decode, fp32 update tensors, 1/2/4/8 GPU"
 PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+DEFAULT_ALSO = "uniform_1gib,resnet50_fp32,kc_uniform_1gib"
 
 
-def cpu_baseline(shapes, x_host_fn, n_bits, sample_mib):
-    """The C oracle (oracle/eden_oracle.c, single thread) on a bounded sample
-    of the same workload: leading tensors (after a leading embedding, if any)
-    until sample_mib is reached."""
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="llama3_8b_fp32_update")
+    ap.add_argument("--n-bits", type=int, default=8)
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="strong")
+    ap.add_argument("--cpu-budget-s", type=float, default=15.0,
+                    help="CPU baseline: oracle time budget on the main workload's tensors")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-events", action="store_true",
+                    help="do not record per-launch HIP events in the timed region")
+    ap.add_argument("--traffic-json", default=None,
+                    help="rocprofv3 PMC-derived HBM bytes per step (tools/pmc_traffic.py output)")
+    ap.add_argument("--wave-mib", type=float, default=None,
+                    help="large-slice wave size (ofl_eden_plan_set_schedule; default: library's)")
+    ap.add_argument("--streams", type=int, default=None, help="1 or 2 (default: library's)")
+    ap.add_argument("--also", default=DEFAULT_ALSO,
+                    help="secondary workloads timed after the main one (rank 0 line, 'also'); '' = none")
+    ap.add_argument("--also-steps", type=int, default=20)
+    ap.add_argument("--profile-steps", type=int, default=3,
+                    help="steps of the serialized per-kernel profile pass (two-stream schedules)")
+    ap.add_argument("--dry-run", action="store_true", help="sharding + rank plumbing only (CPU, gloo)")
+    ap.add_argument("--master-port", type=int, default=0)
+    return ap.parse_args(argv)
+
+
+# --------------------------------------------------------------- launcher ---
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, argv, port=0):
+    """Run this script as n ranks under torch.distributed.run (127.0.0.1) and
+    return its exit code.  Called before this process touches a GPU: the
+    ranks are children, nothing is exec'd over a GPU-initialised process."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port or _free_port()),
+           os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+# ---------------------------------------------------------- CPU baselines ---
+def _oracle_threads():
     from oracle import eden as O
+    cores = O.host_cores()
+    O.set_threads(cores)
+    return O, cores
+
+
+def cpu_baseline(shapes, x_host_fn, n_bits, budget_s, indices=None):
+    """The C oracle (oracle/eden_oracle.c, OpenMP over the host cores this
+    process may use) on the workload's tensors in order until budget_s of
+    CPU time has been spent (tensors above 1 GiB are left out; the Llama
+    embedding alone would take the whole budget)."""
     from openfl_amd.workloads import numel
-    picked, tot = [], 0
-    start = 1 if shapes and numel(shapes[0][1]) * 4 > 2 * sample_mib * 2 ** 20 else 0
-    for i in range(start, len(shapes)):
-        if tot >= sample_mib * 2 ** 20:
+    O, cores = _oracle_threads()
+    idx = list(range(len(shapes))) if indices is None else list(indices)
+    picked, skipped, tot, t_enc, t_dec = [], [], 0, 0.0, 0.0
+    for i in idx:
+        if t_enc + t_dec >= budget_s:
             break
         n = numel(shapes[i][1])
-        if n * 4 > 2 * sample_mib * 2 ** 20:
+        if 4 * n > 2 ** 30:
+            skipped.append(shapes[i][0])
             continue
-        picked.append(i)
-        tot += 4 * n
-    t_enc = t_dec = 0.0
-    for i in picked:
         x = x_host_fn(i)
         t0 = time.perf_counter()
         planes, scales, dims, total = O.compress(x, 4242, n_bits)
@@ -57,27 +120,40 @@ def cpu_baseline(shapes, x_host_fn, n_bits, sample_mib):
         t2 = time.perf_counter()
         t_enc += t1 - t0
         t_dec += t2 - t1
-    gib = tot / 2 ** 30
-    return {"value": round(gib / (t_enc + t_dec), 5), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": f"{len(picked)} tensors ({tot / 2 ** 20:.1f} MiB) of the same workload, "
-                      f"oracle/eden_oracle.c single-threaded; enc {t_enc:.2f} s + dec {t_dec:.2f} s"}
+        picked.append(i)
+        tot += 4 * n
+    full = len(picked) == len(idx)
+    what = "the whole set" if full else (f"tensors {picked[0]}..{picked[-1]} in workload order "
+                                         f"({len(picked)} of {len(idx)}; skipped >1 GiB: {skipped or 'none'})")
+    return {"value": round(tot / 2 ** 30 / (t_enc + t_dec), 5), "unit": "GiB/s", "cores": cores, "kind": "port",
+            "sample": f"{what}, {tot / 2 ** 20:.1f} MiB; oracle/eden_oracle.c with {cores} OpenMP threads; "
+                      f"enc {t_enc:.2f} s + dec {t_dec:.2f} s"}
 
 
-def secondary(name, n_bits, steps, warmup, dev, wave_mib, streams):
-    """One more workload on this GPU (same step definition, inputs resident):
-    the north_star's 1 GiB set and BASELINE config 2 (ResNet-50) next to the
-    main line.  Device time from events around the timed steps."""
+# --------------------------------------------------- secondary workloads ---
+def _fill_arena(plan, numels, dev, seed0=0):
     import torch
-    from openfl_amd.codec import EdenPlan
-    from openfl_amd.workloads import WORKLOADS, numel
-    numels = [numel(s) for _, s in WORKLOADS[name]()]
-    plan = EdenPlan(numels, n_bits, wave_mib=wave_mib, streams=streams)
     x = torch.empty(max(plan.arena_numel, 1), dtype=torch.float32, device=dev)
     gen = torch.Generator(device=dev)
     for j, n in enumerate(numels):
-        gen.manual_seed(j)
+        gen.manual_seed(seed0 + j)
         off = plan.elem_offsets[j]
         x[off:off + n].normal_(0.0, 0.01, generator=gen)
+    return x
+
+
+def secondary(name, n_bits, steps, warmup, dev, wave_mib, streams, cpu=False):
+    """One more workload on this GPU (same step definition, inputs resident):
+    the north_star's 1 GiB set and BASELINE config 2 (ResNet-50) next to the
+    main line.  Device time from events around the timed steps.  cpu=True
+    also times the C oracle on the WHOLE set (all host cores)."""
+    import torch
+    from openfl_amd.codec import EdenPlan
+    from openfl_amd.workloads import WORKLOADS, numel
+    shapes = WORKLOADS[name]()
+    numels = [numel(s) for _, s in shapes]
+    plan = EdenPlan(numels, n_bits, wave_mib=wave_mib, streams=streams)
+    x = _fill_arena(plan, numels, dev)
     y = torch.empty_like(x)
     planes = torch.empty(max(plan.planes_bytes, 1), dtype=torch.uint8, device=dev)
     scales = torch.empty(max(plan.n_slices, 1), dtype=torch.float32, device=dev)
@@ -99,40 +175,156 @@ def secondary(name, n_bits, steps, warmup, dev, wave_mib, streams):
     wall = time.perf_counter() - t0
     gpu_s = ev0.elapsed_time(ev1) / 1e3
     alg = sum(l["bytes_alg"] for e in (True, False) for l in plan.launches(e))
-    return {"value": round(4 * sum(numels) * steps / wall / 2 ** 30, 2), "unit": "GiB/s",
-            "ms_per_step": round(1e3 * wall / steps, 4), "gpu_ms_per_step": round(1e3 * gpu_s / steps, 4),
-            "roofline_frac": round(alg * steps / gpu_s / 1e9 / PEAK_HBM_GBPS, 4),
-            "bytes": 4 * sum(numels), "tensors": len(numels), "slices": plan.n_slices, "waves": plan.n_waves,
-            "streams": plan.n_streams, "steps": steps}
+    out = {"value": round(4 * sum(numels) * steps / wall / 2 ** 30, 2), "unit": "GiB/s",
+           "ms_per_step": round(1e3 * wall / steps, 4), "gpu_ms_per_step": round(1e3 * gpu_s / steps, 4),
+           "roofline_frac": round(alg * steps / gpu_s / 1e9 / PEAK_HBM_GBPS, 4),
+           "bytes": 4 * sum(numels), "tensors": len(numels), "slices": plan.n_slices, "waves": plan.n_waves,
+           "streams": plan.n_streams, "steps": steps}
+    if cpu:
+        def x_host(i):
+            off = plan.elem_offsets[i]
+            return x[off:off + numels[i]].cpu().numpy()
+        out["cpu_baseline"] = cpu_baseline(shapes, x_host, n_bits, budget_s=float("inf"))
+    return out
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="llama3_8b_fp32_update")
-    ap.add_argument("--n-bits", type=int, default=8)
-    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
-    ap.add_argument("--cpu-sample-mib", type=float, default=384.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-kernel-events", action="store_true",
-                    help="do not record per-launch HIP events in the timed region")
-    ap.add_argument("--traffic-json", default=None,
-                    help="rocprofv3 PMC-derived HBM bytes per step (tools/pmc_traffic.py output)")
-    ap.add_argument("--wave-mib", type=float, default=None,
-                    help="large-slice wave size (ofl_eden_plan_set_schedule; default: library's)")
-    ap.add_argument("--streams", type=int, default=None, help="1 or 2 (default: library's)")
-    ap.add_argument("--also", default="uniform_1gib,resnet50_fp32",
-                    help="secondary workloads timed after the main one (rank 0 line, 'also'); '' = none")
-    ap.add_argument("--also-steps", type=int, default=20)
-    ap.add_argument("--profile-steps", type=int, default=3,
-                    help="steps of the serialized per-kernel profile pass (two-stream schedules)")
-    args = ap.parse_args()
+def kc_pipeline(steps, warmup, dev):
+    """KCPipeline (keras_cnn_with_compression, BASELINE config 3: k-means k=6
+    + GZIPTransformer, kc_pipeline.py:36-63, :128-156, :160-181) on the 1 GiB
+    set, gzip INCLUDED.  encode: batched device k-means -> float32 ranks ->
+    device gzip (member-indexed stream, D2H of the compressed bytes); decode:
+    host inflate on native threads straight into pinned staging -> H2D ->
+    batched device LUT.  Also: the device part alone, and the host gzip -9
+    compressor (the reference's GZIPTransformer.forward) timed on a sample."""
+    import torch
+    from oracle import eden as O  # host_cores only
+    from openfl_amd import lossy
+    from openfl_amd.workloads import WORKLOADS, numel
+    cores = O.host_cores()
+    shapes = WORKLOADS["uniform_1gib"]()
+    numels = [numel(s) for _, s in shapes]
+    offs = list(np.cumsum([0] + [(n + 63) // 64 * 64 for n in numels[:-1]]))
+    tot = offs[-1] + numels[-1]
+    x = torch.empty(tot, dtype=torch.float32, device=dev)
+    g = torch.Generator(device=dev)
+    for j, (o, n) in enumerate(zip(offs, numels)):
+        g.manual_seed(j)
+        x[o:o + n].normal_(0.0, 0.01, generator=g)
+    ranks = torch.empty_like(x)
+    y = torch.empty_like(x)
+    stage = torch.empty(4 * tot, dtype=torch.uint8).pin_memory()
+    stage_np = stage.numpy()
+    rng = np.random.RandomState(7)
+    ph = {"kmeans": 0.0, "gzip": 0.0, "gunzip": 0.0, "h2d_lut": 0.0}
 
+    def encode():
+        t0 = time.perf_counter()
+        _, _, _, uniq = lossy.kmeans_batch(x, offs, numels, 6, n_init=6, seed=int(rng.randint(0, 2 ** 31 - 1)),
+                                           ranks_out=ranks)
+        t1 = time.perf_counter()
+        z = lossy.gzip_ranks(ranks)
+        t2 = time.perf_counter()
+        ph["kmeans"] += t1 - t0
+        ph["gzip"] += t2 - t1
+        return z, [{i: u for i, u in enumerate(uq)} for uq in uniq]
+
+    def decode(z, maps):
+        t0 = time.perf_counter()
+        lossy.gunzip(z, cores, out=stage_np)
+        t1 = time.perf_counter()
+        ranks.copy_(stage.view(torch.float32)[:tot], non_blocking=True)
+        lossy.lut_decode_batch(ranks, offs, numels, maps, y)
+        torch.cuda.synchronize()
+        ph["h2d_lut"] += time.perf_counter() - t1
+        ph["gunzip"] += t1 - t0
+
+    for _ in range(warmup):
+        decode(*encode())
+    for k in ph:
+        ph[k] = 0.0
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        z, maps = encode()
+        decode(z, maps)
+    wall = (time.perf_counter() - t0) / steps
+    nbytes = 4 * sum(numels)
+    # device part alone (k-means + ranks, LUT decode; the previous KC line)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        _, _, _, uniq = lossy.kmeans_batch(x, offs, numels, 6, n_init=6, seed=int(rng.randint(0, 2 ** 31 - 1)),
+                                           ranks_out=ranks)
+        lossy.lut_decode_batch(ranks, offs, numels, [{i: u for i, u in enumerate(uq)} for uq in uniq], y)
+    torch.cuda.synchronize()
+    dev_only = (time.perf_counter() - t0) / steps
+    rel = float(torch.linalg.vector_norm((y - x).double()) / torch.linalg.vector_norm(x.double()))
+    # host gzip -9 (the reference compressor) on a 4-tensor sample of the ranks, all host cores
+    sample = ranks[:4 * numels[0]].cpu().numpy().tobytes()
+    t0 = time.perf_counter()
+    zh = lossy.gzip_compress(sample, 9, cores)
+    t_h = time.perf_counter() - t0
+    host_gz_gibs = len(sample) / t_h / 2 ** 30
+    t_host_pipe = wall - ph["gzip"] / steps + nbytes / (host_gz_gibs * 2 ** 30)
+    return {"value": round(nbytes / wall / 2 ** 30, 3), "unit": "GiB/s", "ms_per_step": round(1e3 * wall, 3),
+            "phases_ms": {k: round(1e3 * v / steps, 3) for k, v in ph.items()},
+            "wire_ratio": round(len(z) / nbytes, 4), "check_rel_l2": round(rel, 5),
+            "device_only": {"value": round(nbytes / dev_only / 2 ** 30, 2), "ms_per_step": round(1e3 * dev_only, 3),
+                            "scope": "batched k-means fit + ranks and LUT decode, no gzip"},
+            "host_gzip9_variant": {"value": round(nbytes / t_host_pipe / 2 ** 30, 4),
+                                   "gzip9_GiBps": round(host_gz_gibs, 4), "ratio": round(len(zh) / len(sample), 4),
+                                   "sample": f"gzip -9 of 4 tensors' ranks (64 MiB) on {cores} threads, "
+                                             "extrapolated to the set in place of the device gzip"},
+            "tensors": len(numels), "bytes": nbytes, "steps": steps, "host_threads": cores,
+            "scope": "KCPipeline forward+backward of the set, gzip in the timed region (one member-indexed "
+                     "stream for the arena; each tensor's payload is its run of members)"}
+
+
+# ---------------------------------------------------------------- dry run ---
+def dry_run(args, rank, world):
+    import torch.distributed as dist
+    from openfl_amd.sharding import imbalance, lpt_partition, shard_indices, tensor_cost
+    from openfl_amd.workloads import WORKLOADS, numel
+    if world > 1:
+        dist.init_process_group("gloo")
+    sizes = [numel(s) for _, s in WORKLOADS[args.workload]()]
+    mine = shard_indices(sizes, rank, world, args.scaling)
+    gathered = [mine]
+    if world > 1:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, mine)
+    out = None
+    if rank == 0:
+        flat = sorted(i for g in gathered for i in g)
+        out = {"dry_run": True, "n_gpus": world, "gpus_arg": args.gpus, "scaling": args.scaling,
+               "workload": args.workload, "tensors": len(sizes),
+               "covered": flat == list(range(len(sizes))) if args.scaling == "strong" else
+               all(sorted(g) == list(range(len(sizes))) for g in gathered),
+               "per_rank_tensors": [len(g) for g in gathered],
+               "imbalance": round(imbalance(sizes, gathered), 4) if args.scaling == "strong" else 1.0,
+               "imbalance_8": round(imbalance(sizes, lpt_partition(sizes, 8, tensor_cost)), 4)}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return out
+
+
+# ------------------------------------------------------------------- main ---
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args.gpus, argv, args.master_port)
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}; measuring {world} ranks", file=sys.stderr)
+    if args.dry_run:
+        dry_run(args, rank, world)
+        return 0
+
     import torch
     import torch.distributed as dist
     from openfl_amd.codec import EdenPlan
@@ -162,11 +354,12 @@ def main():
     scales = torch.empty(max(plan.n_slices, 1), dtype=torch.float32, device=dev)
     ws = torch.empty(max(plan.ws_bytes, 256), dtype=torch.uint8, device=dev)
     rs = np.random.RandomState(1234 + rank)
-    seeds = torch.tensor(rs.randint(0, 2 ** 16, size=len(numels)), dtype=torch.int32, device=dev)
+    seeds = torch.tensor(rs.randint(0, 2 ** 16, size=max(len(numels), 1)), dtype=torch.int32, device=dev)
 
     def step():
-        plan.encode(x, seeds, planes, scales, ws)
-        plan.decode(planes, seeds, scales, y, ws)
+        if numels:
+            plan.encode(x, seeds, planes, scales, ws)
+            plan.decode(planes, seeds, scales, y, ws)
 
     for _ in range(args.warmup):
         step()
@@ -202,7 +395,7 @@ def main():
     # serialized profile pass over the same tensors (two streams)
     kernels = {}
     kernels_source = None
-    if not args.no_kernel_events:
+    if not args.no_kernel_events and numels:
         pplan, pws = plan, ws
         if two:
             pplan = EdenPlan(numels, args.n_bits, wave_mib=args.wave_mib, streams=1)
@@ -235,22 +428,25 @@ def main():
 
     # quality check (not timed): relative L2 error of decode(encode(x))
     with torch.no_grad():
-        rel = float(torch.linalg.vector_norm((y - x).double()) / torch.linalg.vector_norm(x.double()))
+        rel = float(torch.linalg.vector_norm((y - x).double()) / torch.linalg.vector_norm(x.double())) \
+            if numels else 0.0
 
     in_bytes_rank = 4 * sum(numels)
     value = throughput_gib_s(in_bytes_rank, world, args.steps, elapsed, args.scaling, 4 * sum(sizes))
 
     alg_step = sum(l["bytes_alg"] for e in (True, False) for l in plan.launches(e))
     step_s = gpu_ms / 1e3 / args.steps
-    achieved = alg_step / step_s / 1e9
+    achieved = alg_step / step_s / 1e9 if step_s > 0 else 0.0
     traffic = None
     traffic_src = args.traffic_json
+    default_sched = (args.wave_mib is None and args.streams is None
+                     and not any(k.startswith("OFL_EDEN_") for k in os.environ))
     if traffic_src is None and args.workload == "llama3_8b_fp32_update" and args.n_bits == 8 \
-            and args.scaling == "weak":
-        # PMC counters cannot be read from inside this process: default to the
-        # committed rocprofv3 --pmc passes of this same workload (tools/pmc_run.sh)
-        traffic_src = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
-                                   "r01_llama3_8b_hbm_traffic_final.json")
+            and world == 1 and default_sched:
+        # PMC counters cannot be read from inside this process: the committed
+        # rocprofv3 --pmc passes of this same workload and default schedule
+        # (tools/pmc_run.sh), only when this run uses that schedule
+        traffic_src = os.path.join(ROOT, "profiles", "r02_llama3_8b_hbm_traffic.json")
     if traffic_src and os.path.exists(traffic_src):
         with open(traffic_src) as f:
             traffic = json.load(f).get("hbm_bytes_per_step")
@@ -263,7 +459,7 @@ def main():
                      "+ 4n (y write) (SURVEY 8(d)); FWHT intermediates not counted",
             "alg_bytes_per_step": alg_step,
             "traffic_unit": "HBM bytes per step (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction)",
-            "traffic_source": (os.path.relpath(traffic_src, os.path.dirname(os.path.abspath(__file__)))
+            "traffic_source": (os.path.relpath(traffic_src, ROOT)
                                + " (rocprofv3 --pmc passes of this workload, not this run)")
                               if traffic_src else None}
     if kernels:
@@ -275,6 +471,8 @@ def main():
             "share_of_step": round(k["ms"] / tot_ms, 3),
             "bytes_moved_per_launch": k["bytes_moved"] // k["launches"],
             "bytes_alg_per_launch": k["bytes_alg"] // k["launches"],
+            "alg_GBps": round(k["bytes_alg"] / (k["ms"] / 1e3) / 1e9, 1),
+            "alg_frac": round(k["bytes_alg"] / (k["ms"] / 1e3) / 1e9 / PEAK_HBM_GBPS, 4),
             "moved_GBps": round(k["bytes_moved"] / (k["ms"] / 1e3) / 1e9, 1),
             "moved_frac": round(k["bytes_moved"] / (k["ms"] / 1e3) / 1e9 / PEAK_HBM_GBPS, 4)}
         if traffic_src:
@@ -292,7 +490,11 @@ def main():
     also = {}
     if world == 1 and args.also:
         for name in [a for a in args.also.split(",") if a]:
-            also[name] = secondary(name, args.n_bits, args.also_steps, 3, dev, args.wave_mib, args.streams)
+            if name == "kc_uniform_1gib":
+                also[name] = kc_pipeline(max(2, args.also_steps // 10), 1, dev)
+            else:
+                also[name] = secondary(name, args.n_bits, args.also_steps, 3, dev, args.wave_mib, args.streams,
+                                       cpu=(name == "uniform_1gib" and not args.no_cpu_baseline))
 
     out = None
     if rank == 0:
@@ -302,8 +504,7 @@ def main():
                 j = mine.index(i)
                 off = plan.elem_offsets[j]
                 return x[off:off + numels[j]].cpu().numpy()
-            cpu = cpu_baseline(shapes, x_host, args.n_bits, args.cpu_sample_mib)
-            cpu["cores"] = 1
+            cpu = cpu_baseline(shapes, x_host, args.n_bits, args.cpu_budget_s, indices=mine)
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -312,13 +513,14 @@ def main():
             "dtype": "f32",
             "data": "synthetic: seeded N(0, 0.01^2) fp32 tensors of the workload's shapes, "
                     "resident in HBM; no checkpoint",
-            "config": {"workload": args.workload, "tensors": len(numels), "numel_per_rank": sum(numels),
-                       "bytes_per_rank": in_bytes_rank, "n_bits": args.n_bits, "slices": plan.n_slices,
-                       "planes_bytes_per_rank": plan.planes_bytes, "waves": plan.n_waves,
-                       "streams": plan.n_streams, "wave_mib": plan.wave_mib,
+            "config": {"workload": args.workload, "tensors": len(sizes), "tensors_rank0": len(numels),
+                       "set_bytes": 4 * sum(sizes), "bytes_rank0": in_bytes_rank, "n_bits": args.n_bits,
+                       "slices_rank0": plan.n_slices, "planes_bytes_rank0": plan.planes_bytes,
+                       "waves": plan.n_waves, "streams": plan.n_streams, "wave_mib": plan.wave_mib,
                        "parallelism": (f"{world} independent replicas, one update set per GPU"
-                                       if args.scaling == "weak" else f"LPT-sharded over {world} GPUs")},
-            "gpu_ms_per_step": round(gpu_ms / args.steps, 3),
+                                       if args.scaling == "weak" else
+                                       f"one update set, per-tensor LPT shards over {world} GPU(s)")},
+            "gpu_ms_per_step_rank0": round(gpu_ms / args.steps, 3),
             "check_rel_l2": round(rel, 6),
             "roofline": roof,
             "cpu_baseline": cpu,
@@ -328,8 +530,8 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    return out
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

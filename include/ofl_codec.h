@@ -36,6 +36,7 @@ extern "C" {
 #define OFL_EINVAL -1  /* bad argument (n_bits outside 1..8, dims not powers of two, ...) */
 #define OFL_EHIP -2    /* a HIP runtime call failed */
 #define OFL_ESPACE -3  /* workspace too small */
+#define OFL_EFORMAT -4 /* input is not in the format the call handles (caller may fall back) */
 
 /* Library version string. */
 const char* ofl_version(void);
@@ -292,6 +293,8 @@ int ofl_apply_delta_ranges(const float* base, const float* delta, float* out, in
  * multi-member gzip stream (4096 float32 values per member, one
  * dynamic-Huffman deflate block each: copies of each value's previous
  * occurrence, literals at first occurrences), CRC-32 and ISIZE per member.
+ * Every member header carries an RFC 1952 extra field 'BC' (SLEN 2) holding
+ * the member's byte size - 1 (as BGZF does), which gzip.decompress skips.
  * x: DEVICE float32 [n], every value an integer 0..31 (the ranks the lossy
  * pipelines write; anything else -> OFL_EINVAL, nothing written).  out: HOST
  * buffer of out_cap >= ofl_gzip_ranks_bound(n) bytes; *out_len = stream
@@ -302,6 +305,13 @@ size_t ofl_gzip_ranks_workspace_bytes(int64_t n);
 size_t ofl_gzip_ranks_bound(int64_t n);
 int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size_t* out_len, void* ws,
                    size_t ws_bytes, void* stream);
+/* GZIPTransformer.backward (kc_pipeline.py:152-156: gzip.decompress) for a
+ * stream whose members all carry the 'BC' size field: members are located
+ * from their headers and inflated (zlib) on nthreads host threads into dst
+ * (HOST, cap bytes; NULL: only *out_len = decompressed size), with each
+ * member's ISIZE and CRC-32 checked.  OFL_EFORMAT if the stream is not
+ * member-indexed (e.g. gzip.compress output): use gzip.decompress then. */
+int ofl_gunzip_members(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len, int nthreads);
 
 /* ---- host helpers ----------------------------------------------------------
  * Left-to-right serial sums in the array's own precision: the

@@ -15,6 +15,7 @@ _lock = threading.Lock()
 _lib = None
 
 OFL_OK = 0
+OFL_EFORMAT = -4
 
 EXPORTS = (
     "ofl_version", "ofl_last_error", "ofl_eden_slice_plan", "ofl_eden_plan_create",
@@ -35,6 +36,7 @@ EXPORTS = (
     "ofl_wavg_points_workspace_bytes", "ofl_wavg_delta_points", "ofl_apply_delta",
     "ofl_apply_delta_ranges",
     "ofl_gzip_last_error", "ofl_gzip_ranks_workspace_bytes", "ofl_gzip_ranks_bound", "ofl_gzip_ranks",
+    "ofl_gunzip_members",
 )
 
 
@@ -141,6 +143,8 @@ def _bind(L):
     L.ofl_gzip_ranks_bound.restype = sz
     L.ofl_gzip_ranks.argtypes = [vp, i64, vp, sz, vp, vp, sz, vp]
     L.ofl_gzip_ranks.restype = i32
+    L.ofl_gunzip_members.argtypes = [vp, sz, vp, sz, vp, i32]
+    L.ofl_gunzip_members.restype = i32
     L.ofl_serial_sum_f32.argtypes = [vp, i64]
     L.ofl_serial_sum_f32.restype = ctypes.c_float
     L.ofl_serial_sum_f64.argtypes = [vp, i64]

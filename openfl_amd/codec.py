@@ -174,6 +174,13 @@ class Workspace:
             bufs[key] = b
         return b
 
+    def trim(self, device, limit):
+        """Drop this thread's buffer for device if it exceeds limit bytes."""
+        bufs = getattr(self._tls, "bufs", None) or {}
+        b = bufs.get(str(device))
+        if b is not None and b.numel() > limit:
+            del bufs[str(device)]
+
 
 def resolve_device(device):
     """Map a reference `device` setting to a ROCm device.

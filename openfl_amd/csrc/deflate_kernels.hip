@@ -30,6 +30,9 @@
 #include <string>
 #include <vector>
 
+#include <thread>
+#include <zlib.h>
+
 #include "ofl_codec.h"
 #include "ofl_util.h"
 
@@ -45,6 +48,7 @@ constexpr int kOutWords = 8192;            // 32 KiB bit buffer >= worst-case me
 constexpr int kOutBytes = 4 * kOutWords;
 constexpr int kLit = 286, kDist = 30, kCL = 19;
 constexpr int kBatch = 4096;               // members per launch (host loop)
+constexpr int kHdr = 18;                   // gzip member header incl. the 'BC' extra field
 
 __constant__ uint16_t c_dbase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129,
                                      193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
@@ -371,8 +375,12 @@ __global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
         int ncl = kCL;
         while (ncl > 4 && S.lc[c_clord[ncl - 1]] == 0) --ncl;
         uint32_t pos = 0;
-        const uint8_t hdr[10] = {0x1f, 0x8b, 0x08, 0x00, 0, 0, 0, 0, 0x00, 0xff};
-        for (int i = 0; i < 10; ++i) { put_bits(S.out, pos, hdr[i], 8); pos += 8; }
+        // member header with a BGZF-style extra field (RFC 1952 FEXTRA,
+        // subfield 'BC' = member size - 1, filled in at the end): a reader
+        // can find every member without inflating (ofl_gunzip_members);
+        // gzip.decompress skips the field
+        const uint8_t hdr[kHdr] = {0x1f, 0x8b, 0x08, 0x04, 0, 0, 0, 0, 0x00, 0xff, 6, 0, 'B', 'C', 2, 0, 0, 0};
+        for (int i = 0; i < kHdr; ++i) { put_bits(S.out, pos, hdr[i], 8); pos += 8; }
         put_bits(S.out, pos, 1u, 1); pos += 1;          // BFINAL
         put_bits(S.out, pos, 2u, 2); pos += 2;          // BTYPE = dynamic
         put_bits(S.out, pos, (uint32_t)(nlit - 257), 5); pos += 5;
@@ -454,6 +462,7 @@ __global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
         put_bits(S.out, p, crc32, 32); p += 32;
         put_bits(S.out, p, S.crc_n[0], 32); p += 32;
         S.total_bits = p;
+        put_bits(S.out, 8 * (kHdr - 2), (p >> 3) - 1u, 16);  // BSIZE
         a.sizes[blockIdx.x] = p >> 3;
     }
     __syncthreads();
@@ -578,6 +587,73 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
         total += tot;
     }
     *out_len = total;
+    return OFL_OK;
+}
+
+// Host inflate of a member-indexed gzip stream (every member carries the
+// 'BC' extra field that k_gzip_members writes): the members are found from
+// their headers alone and inflated on nthreads host threads straight into
+// dst (each member's ISIZE gives its output offset).  Streams without the
+// field (e.g. gzip.compress output) return OFL_EFORMAT so the caller can use
+// gzip.decompress instead; dst == nullptr only measures.
+int ofl_gunzip_members(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len, int nthreads) {
+    if (!src || !out_len) return gzfail(OFL_EINVAL, "gunzip: null argument");
+    struct M { size_t in, in_len, out; uint32_t isize, crc; };
+    std::vector<M> mem;
+    size_t pos = 0, total = 0;
+    while (pos < n) {
+        const uint8_t* h = src + pos;
+        if (n - pos < 26 || h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || h[3] != 0x04)
+            return gzfail(OFL_EFORMAT, "gunzip: not a member-indexed gzip stream");
+        const size_t xlen = (size_t)h[10] | ((size_t)h[11] << 8);
+        size_t bsize = 0;
+        for (size_t q = 12; q + 4 <= 12 + xlen && 12 + xlen <= n - pos;) {
+            const size_t sl = (size_t)h[q + 2] | ((size_t)h[q + 3] << 8);
+            if (h[q] == 'B' && h[q + 1] == 'C' && sl == 2) bsize = ((size_t)h[q + 4] | ((size_t)h[q + 5] << 8)) + 1;
+            q += 4 + sl;
+        }
+        if (bsize < 12 + xlen + 8 || bsize > n - pos)
+            return gzfail(OFL_EFORMAT, "gunzip: not a member-indexed gzip stream");
+        const uint8_t* t = src + pos + bsize - 8;
+        M m;
+        m.in = pos + 12 + xlen;
+        m.in_len = bsize - 12 - xlen - 8;
+        m.crc = (uint32_t)t[0] | ((uint32_t)t[1] << 8) | ((uint32_t)t[2] << 16) | ((uint32_t)t[3] << 24);
+        m.isize = (uint32_t)t[4] | ((uint32_t)t[5] << 8) | ((uint32_t)t[6] << 16) | ((uint32_t)t[7] << 24);
+        m.out = total;
+        total += m.isize;
+        mem.push_back(m);
+        pos += bsize;
+    }
+    *out_len = total;
+    if (!dst) return OFL_OK;
+    if (total > cap) return gzfail(OFL_ESPACE, "gunzip: output buffer too small");
+    const int nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::max(nthreads, 1), mem.size()));
+    std::vector<int> bad(nt, 0);
+    auto work = [&](int t) {
+        z_stream z;
+        memset(&z, 0, sizeof(z));
+        if (inflateInit2(&z, -15) != Z_OK) { bad[t] = 1; return; }
+        const size_t m0 = mem.size() * t / nt, m1 = mem.size() * (t + 1) / nt;
+        for (size_t i = m0; i < m1 && !bad[t]; ++i) {
+            const M& m = mem[i];
+            inflateReset(&z);
+            z.next_in = const_cast<Bytef*>(src + m.in);
+            z.avail_in = (uInt)m.in_len;
+            z.next_out = dst + m.out;
+            z.avail_out = m.isize;
+            if (inflate(&z, Z_FINISH) != Z_STREAM_END || z.total_out != m.isize ||
+                crc32(0L, dst + m.out, m.isize) != m.crc)
+                bad[t] = 1;
+        }
+        inflateEnd(&z);
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+    for (int b : bad)
+        if (b) return gzfail(OFL_EINVAL, "gunzip: corrupt member (inflate, size or CRC-32 mismatch)");
     return OFL_OK;
 }
 

@@ -19,6 +19,22 @@ GZIP_CHUNK = 8 << 20
 _pool = None
 
 
+def _on_device(fn):
+    """Run fn with its first device-tensor argument's GPU current: per-device
+    setup inside the library (CRC tables, kernel attributes, CU counts) keys
+    on hipGetDevice(), and the launches go to that tensor's stream."""
+    import functools
+
+    @functools.wraps(fn)
+    def wrap(*args, **kwargs):
+        for a in list(args) + list(kwargs.values()):
+            if isinstance(a, torch.Tensor) and a.is_cuda:
+                with torch.cuda.device(a.device):
+                    return fn(*args, **kwargs)
+        return fn(*args, **kwargs)
+    return wrap
+
+
 def _ws(device, n):
     need = int(_lib.lib().ofl_lossy_workspace_bytes(int(n)))
     bufs = getattr(_tls, "ws", None)
@@ -49,6 +65,7 @@ def _check_dev(x):
         raise _lib.CodecError("lossy ops take contiguous float32 device tensors")
 
 
+@_on_device
 def kmeans_fit(x, k=6, n_init=6, seed=0, max_exact=8):
     """1-D k-means of a float32 device vector (replaces sklearn KMeans.fit,
     kc_pipeline.py:49-56): -> (sorted centres float64[k], counts int64[k], inertia)."""
@@ -64,6 +81,7 @@ def kmeans_fit(x, k=6, n_init=6, seed=0, max_exact=8):
     return c, cnt, inertia.value
 
 
+@_on_device
 def kmeans_batch(x_arena, offsets, numels, k=6, n_init=6, seed=0, max_exact=8, value_f64=False, ranks_out=None):
     """Device k-means of many tensors of one float32 arena (ofl_kmeans1d_batch):
     tensor t = x_arena[offsets[t]:offsets[t] + numels[t]].  Writes float32
@@ -93,6 +111,7 @@ def kmeans_batch(x_arena, offsets, numels, k=6, n_init=6, seed=0, max_exact=8, v
     return c, cnt, inertia, [uq[t, :nu[t]].astype(dt) for t in range(T)]
 
 
+@_on_device
 def kmeans_label(x, centres, rank_of_cluster):
     """out[i] = rank_of_cluster[nearest centre of x[i]] as float32 (device)."""
     _check_dev(x)
@@ -104,6 +123,7 @@ def kmeans_label(x, centres, rank_of_cluster):
     return out
 
 
+@_on_device
 def sparsify_topk(x, k):
     """SparsityTransformer top-k (skc_pipeline.py:33-54, 72-94) -> (sparse
     float32 device array, stats dict)."""
@@ -123,6 +143,7 @@ def sparsify_topk(x, k):
                  "abs_sum": asum.value, "shifted": bool(shifted.value), "k": int(k)}
 
 
+@_on_device
 def sparsify_topk_batch(x_arena, offsets, numels, ks, sparse_out):
     """sparsify_topk for every tensor of a float32 arena in one device pass
     sequence (ofl_sparsify_topk_batch): tensor t = x_arena[offsets[t]:
@@ -149,6 +170,7 @@ def sparsify_topk_batch(x_arena, offsets, numels, ks, sparse_out):
             "shifted": shifted.astype(bool), "k": kk}
 
 
+@_on_device
 def ternary_ranks_batch(sparse_arena, offsets, numels, ranks3, out_arena):
     """ternary_ranks for every tensor of an arena (ranks3[t] = (rank_neg,
     rank_zero, rank_pos) of tensor t) in one launch."""
@@ -166,6 +188,7 @@ def ternary_ranks_batch(sparse_arena, offsets, numels, ranks3, out_arena):
     return out_arena
 
 
+@_on_device
 def ternary_stats(x):
     """(n_pos, n_neg, fp64 sum |x|) of a float32 device vector."""
     _check_dev(x)
@@ -177,6 +200,7 @@ def ternary_stats(x):
     return npos.value, nneg.value, asum.value
 
 
+@_on_device
 def ternary_ranks(sparse, rank_neg, rank_zero, rank_pos):
     _check_dev(sparse)
     out = torch.empty_like(sparse)
@@ -186,6 +210,7 @@ def ternary_ranks(sparse, rank_neg, rank_zero, rank_pos):
     return out
 
 
+@_on_device
 def lut_decode(ranks, int_to_float):
     """Reference backward: `for key in map: data[data == key] = map[key]` on a
     float32 array, in the mapping's own iteration order (kc_pipeline.py:81-83)."""
@@ -199,6 +224,7 @@ def lut_decode(ranks, int_to_float):
     return out
 
 
+@_on_device
 def lut_decode_batch(ranks_arena, offsets, numels, maps, out_arena):
     """lut_decode for every tensor of an arena in one launch (maps[t]: the
     tensor's int_to_float mapping, iteration order kept)."""
@@ -224,6 +250,7 @@ def lut_decode_batch(ranks_arena, offsets, numels, maps, out_arena):
     return out_arena
 
 
+@_on_device
 def gzip_ranks(x):
     """gzip.compress of a float32 device array of ranks (integers 0..31), on
     the GPU (ofl_gzip_ranks): a multi-member gzip stream that gzip.decompress
@@ -242,6 +269,32 @@ def gzip_ranks(x):
     _lib.check_gzip(L.ofl_gzip_ranks(x.data_ptr(), n, out.data_ptr(), cap, ctypes.byref(ln), ws.data_ptr(),
                                      ws.numel(), _stream(x.device)))
     return out[:ln.value].numpy().tobytes()
+
+
+def gunzip(data, threads=8, out=None):
+    """gzip.decompress (kc_pipeline.py:152-156) of `data` -> uint8 numpy array.
+    Member-indexed streams (the device gzip's, every member carrying the 'BC'
+    size field) inflate in parallel on native threads (ofl_gunzip_members),
+    into `out` (a uint8 numpy array, e.g. a pinned staging view) when given;
+    any other stream goes through gzip.decompress."""
+    L = _lib.lib()
+    src = np.frombuffer(data, np.uint8)
+    need = ctypes.c_size_t()
+    rc = L.ofl_gunzip_members(src.ctypes.data if src.size else None, src.size, None, 0, ctypes.byref(need),
+                              threads)
+    if rc == _lib.OFL_EFORMAT or src.size == 0:
+        raw = np.frombuffer(gzip.decompress(bytes(data)), np.uint8)
+        if out is None:
+            return raw
+        out[:raw.size] = raw
+        return out[:raw.size]
+    _lib.check_gzip(rc)
+    dst = out if out is not None else np.empty(need.value, np.uint8)
+    if dst.size < need.value:
+        raise _lib.CodecError("gunzip: output buffer too small")
+    _lib.check_gzip(L.ofl_gunzip_members(src.ctypes.data, src.size, dst.ctypes.data, dst.size,
+                                         ctypes.byref(need), threads))
+    return dst[:need.value]
 
 
 def rank_map(values):

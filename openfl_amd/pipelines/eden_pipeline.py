@@ -34,6 +34,10 @@ from openfl_amd.codec import EdenCodec, resolve_device
 from openfl_amd.pipelines.pipeline import Float32NumpyArrayToBytes, TransformationPipeline, Transformer
 
 _FAST_SEED_PREFIX = 4096
+# host staging / per-thread device buffers above this size are dropped at the
+# end of the call instead of being kept for the next one (a Llama-sized batch
+# would otherwise pin tens of GB per gRPC worker thread for the process life)
+_RETAIN_BYTES = 512 << 20
 
 
 def _serial_sum(flat):
@@ -139,7 +143,8 @@ class Eden:
         return sg
 
     def _dev(self, name, n, dtype):
-        """Per-thread device buffers of the one-tensor calls (grow only)."""
+        """Per-thread device buffers of the one-tensor calls (power-of-two
+        growth; ones above _RETAIN_BYTES are released by _trim)."""
         bufs = getattr(self._tls, "dev", None)
         if bufs is None:
             bufs = self._tls.dev = {}
@@ -147,6 +152,17 @@ class Eden:
         if b is None or b.numel() < n or b.dtype != dtype:
             b = bufs[name] = torch.empty(1 << max(int(n) - 1, 4095).bit_length(), dtype=dtype, device=self.device)
         return b
+
+    def _trim(self):
+        """Drop this thread's oversized staging and device buffers (after the
+        call's stream has been synchronised)."""
+        bufs = getattr(self._tls, "dev", None) or {}
+        for k in [k for k, b in bufs.items() if b.numel() * b.element_size() > _RETAIN_BYTES]:
+            del bufs[k]
+        sg = getattr(self._tls, "staging", None)
+        if sg is not None:
+            sg.trim(_RETAIN_BYTES)
+        self.codec.ws.trim(self.device, _RETAIN_BYTES)
 
     def compress(self, vec, seed):
         """(planes uint8 ndarray, scales list[float], dims list[int], total_dim) (:555-611).
@@ -175,7 +191,11 @@ class Eden:
             ph[:max(pb, 1)].copy_(planes[:max(pb, 1)], non_blocking=True)
             sch[:max(ns, 1)].copy_(scales[:max(ns, 1)], non_blocking=True)
         st.synchronize()
-        return ph.numpy()[:pb].copy(), [float(v) for v in sch.numpy()[:ns]], list(plan.dims[0]), n
+        # one host copy, pinned -> bytes; the array is a zero-copy view of it
+        out = (np.frombuffer(ph.numpy()[:pb].tobytes(), np.uint8), [float(v) for v in sch.numpy()[:ns]],
+               list(plan.dims[0]), n)
+        self._trim()
+        return out
 
     def decompress(self, bins, metadata):
         """bins: uint8 planes; metadata: int_to_float mapping (:632-659)."""
@@ -214,14 +234,21 @@ class Eden:
             if total_dim:
                 yh[:total_dim].copy_(y[:total_dim], non_blocking=True)
         st.synchronize()
-        return yh.numpy()[:total_dim].copy()
+        y = yh.numpy()[:total_dim].copy()
+        self._trim()
+        return y
 
 
 class _Staging:
-    """Pinned host buffers of one batch shape (grown on demand)."""
+    """Pinned host buffers of one batch shape (grown on demand; trim() drops
+    the oversized ones)."""
 
     def __init__(self):
         self.bufs = {}
+
+    def trim(self, limit):
+        for k in [k for k, b in self.bufs.items() if b.numel() * b.element_size() > limit]:
+            del self.bufs[k]
 
     def get(self, name, n, dtype):
         b = self.bufs.get(name)
@@ -260,7 +287,11 @@ def _batch_encode(eden, arrays, seeds):
     for t in range(len(flats)):
         po, pb, fs = plan.planes_offsets[t], plan.planes_nbytes[t], plan.first_slice[t]
         dims = plan.dims[t]
+        # the one host copy a `bytes` payload needs (protobuf's data_bytes
+        # takes bytes only), straight from the pinned D2H buffer
         out.append((pn[po:po + pb].tobytes(), [float(v) for v in sn[fs:fs + len(dims)]], list(dims)))
+    del x, planes, scales
+    eden._trim()
     return out
 
 
@@ -302,6 +333,8 @@ def _batch_decode(eden, items):
     ybase = yh.data_ptr()
     _copy_many([o.ctypes.data for o in outs], [ybase + 4 * plan.elem_offsets[t] for t in range(len(items))],
                [4 * totals[t] for t in range(len(items))])
+    del planes, y
+    eden._trim()
     return outs
 
 
@@ -328,7 +361,8 @@ class EdenTransformer(Transformer):
                 metadata["int_to_float"][k] = scale
                 metadata["int_to_float"][k + 1] = float(dim)
                 k += 2
-            return int_array.tobytes(), metadata
+            b = int_array.base
+            return (b if isinstance(b, bytes) and len(b) == int_array.nbytes else int_array.tobytes()), metadata
         return self.no_comp.forward(data)
 
     def backward(self, data, metadata, **kwargs):

@@ -7,7 +7,6 @@ The k-means / top-k / ternary numerics run on the GPU (openfl_amd.lossy);
 gzip and tiny (n < n_clusters) cases run on the host exactly as the
 reference does.
 """
-import gzip
 
 import numpy as np
 import torch
@@ -55,7 +54,8 @@ class GZIPTransformer(Transformer):
         return self.forward(ranks_dev.cpu().numpy())
 
     def backward(self, data, metadata, **kwargs):
-        return np.frombuffer(gzip.decompress(data), dtype=np.float32)
+        # member-indexed streams inflate on native threads; others via gzip.decompress
+        return lossy.gunzip(data, self.threads).view(np.float32)
 
 
 def to_device(data, device):

@@ -40,8 +40,29 @@ def lib():
         L.oracle_serial_sum_f32.restype = ctypes.c_float
         L.oracle_serial_sum_f64.argtypes = [vp, i64]
         L.oracle_serial_sum_f64.restype = ctypes.c_double
+        L.oracle_set_threads.argtypes = [i32]
+        L.oracle_get_threads.restype = i32
         _lib = L
     return _lib
+
+
+def host_cores():
+    """Host cores this process may use: the affinity mask, capped by
+    OMP_NUM_THREADS when set (the GPU box exports the job's CPU share there)."""
+    n = len(os.sched_getaffinity(0))
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return max(1, n)
+
+
+def set_threads(n):
+    """OpenMP threads of the oracle's loops (results do not depend on it)."""
+    lib().oracle_set_threads(int(n))
+
+
+def get_threads():
+    return int(lib().oracle_get_threads())
 
 
 def tables(nbits):

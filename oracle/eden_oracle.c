@@ -29,8 +29,17 @@
  *
  * Pinned by: tests/golden/eden_golden.{npz,json} generated from the reference
  * itself by tests/golden/make_golden.py (see tests/test_oracle_golden.py).
+ *
+ * Threading (OpenMP, oracle_set_threads): every loop below is split over
+ * element ranges without changing any float operation or its order --
+ * butterflies are independent within a stage, stages run in the reference's
+ * order (the first 2^15-wide stages are blocked per 2^15 elements, which
+ * touches the same pairs in the same stage order), and the two reductions
+ * use fixed 2^16-element blocks summed in block order, so results do not
+ * depend on the thread count.
  */
 #include <math.h>
+#include <omp.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -73,9 +82,15 @@ void oracle_rand_signs(int64_t P, int64_t seed, uint8_t* bits) {
     }
 }
 
+#define PAR_MIN (1ll << 16) /* below this, loops stay on the calling thread */
+
+void oracle_set_threads(int n) { omp_set_num_threads(n > 0 ? n : 1); }
+int oracle_get_threads(void) { return omp_get_max_threads(); }
+
 static void apply_signs(float* v, int64_t P, int64_t seed) {
     int64_t S = P / 8 + (P % 8 != 0);
     uint64_t s = seed_hash(seed);
+#pragma omp parallel for schedule(static) if (P >= PAR_MIN)
     for (int64_t j = 0; j < S; ++j) {
         uint32_t r = rd_word((uint64_t)j, s);
         for (int k = 0; k < 8; ++k) {
@@ -88,19 +103,40 @@ static void apply_signs(float* v, int64_t P, int64_t seed) {
 
 /* ---- hadamard (:451-473): stride-1 stages first, a'=a+b, b'=a'-2b, then
  * divide by float32(sqrt(P)) ---- */
+static void fwht_stage(float* v, int64_t P, int64_t h) {
+    int64_t hf = h >> 1;
+#pragma omp parallel for schedule(static) if (P >= PAR_MIN)
+    for (int64_t q = 0; q < P / 2; ++q) {
+        int64_t i = (q / hf) * h + (q % hf);
+        float a = v[i], b = v[i + hf];
+        float s = a + b;
+        v[i] = s;
+        v[i + hf] = s - 2.0f * b;
+    }
+}
+
+#define FWHT_BLK (1ll << 15)
 void oracle_fwht(float* v, int64_t P) {
-    for (int64_t h = 2; h <= P; h <<= 1) {
-        int64_t hf = h >> 1;
-        for (int64_t base = 0; base < P; base += h) {
-            for (int64_t k = 0; k < hf; ++k) {
-                float a = v[base + k], b = v[base + hf + k];
-                float s = a + b;
-                v[base + k] = s;
-                v[base + hf + k] = s - 2.0f * b;
+    /* stages h <= FWHT_BLK stay inside aligned FWHT_BLK blocks: run them
+     * block by block (same pairs, same stage order per pair) */
+    int64_t bl = P < FWHT_BLK ? P : FWHT_BLK;
+#pragma omp parallel for schedule(static) if (P >= PAR_MIN)
+    for (int64_t base = 0; base < P; base += bl) {
+        for (int64_t h = 2; h <= bl; h <<= 1) {
+            int64_t hf = h >> 1;
+            for (int64_t b0 = base; b0 < base + bl; b0 += h) {
+                for (int64_t k = 0; k < hf; ++k) {
+                    float a = v[b0 + k], b = v[b0 + hf + k];
+                    float s = a + b;
+                    v[b0 + k] = s;
+                    v[b0 + hf + k] = s - 2.0f * b;
+                }
             }
         }
     }
+    for (int64_t h = bl << 1; h <= P; h <<= 1) fwht_stage(v, P, h);
     float d = (float)sqrt((double)P);
+#pragma omp parallel for schedule(static) if (P >= PAR_MIN)
     for (int64_t i = 0; i < P; ++i) v[i] = v[i] / d;
 }
 
@@ -141,6 +177,7 @@ static int bucketize(float z, const float* B, int nb) {
 
 /* ---- compress_slice + quantize (:527-553, :505-525) ----
  * bins_out has P entries; returns scale (float32 value). */
+#define RED_BLK (1ll << 16)
 static float compress_slice(const float* x, int64_t len, int64_t P, int64_t seed,
                             const float* C, const float* B, int nbits, int32_t* bins_out,
                             float* work) {
@@ -152,23 +189,43 @@ static float compress_slice(const float* x, int64_t len, int64_t P, int64_t seed
     }
     /* torch.norm squares in float32 (under/overflow as in the reference, e.g.
      * 1e-32 inputs give norm 0 and 1e28 inputs give norm inf), accumulates
-     * accurately; restated as float32 squares summed in double. */
+     * accurately; restated as float32 squares summed in double (fixed
+     * blocks, block order). */
+    int64_t nblk = (P + RED_BLK - 1) / RED_BLK;
+    double* part = (double*)malloc(sizeof(double) * (size_t)nblk);
+#pragma omp parallel for schedule(static) if (P >= PAR_MIN)
+    for (int64_t k = 0; k < nblk; ++k) {
+        double ss = 0.0;
+        int64_t e1 = (k + 1) * RED_BLK < P ? (k + 1) * RED_BLK : P;
+        for (int64_t i = k * RED_BLK; i < e1; ++i) { float q = work[i] * work[i]; ss += (double)q; }
+        part[k] = ss;
+    }
     double ss = 0.0;
-    for (int64_t i = 0; i < P; ++i) { float q = work[i] * work[i]; ss += (double)q; }
+    for (int64_t k = 0; k < nblk; ++k) ss += part[k];
     float nu = sqrtf((float)ss);          /* float32 sum: overflows to inf past FLT_MAX */
     int nb = (1 << nbits) - 1;
     if (nu > 0.0f) {
         float rp = (float)sqrt((double)P);
-        double dot = 0.0;
-        for (int64_t i = 0; i < P; ++i) {
-            float z = (work[i] * rp) / nu;
-            int b = bucketize(z, B, nb);
-            bins_out[i] = b;
-            float pr = C[b] * work[i];       /* float32 products, as torch.dot */
-            dot += (double)pr;
+#pragma omp parallel for schedule(static) if (P >= PAR_MIN)
+        for (int64_t k = 0; k < nblk; ++k) {
+            double dot = 0.0;
+            int64_t e1 = (k + 1) * RED_BLK < P ? (k + 1) * RED_BLK : P;
+            for (int64_t i = k * RED_BLK; i < e1; ++i) {
+                float z = (work[i] * rp) / nu;
+                int b = bucketize(z, B, nb);
+                bins_out[i] = b;
+                float pr = C[b] * work[i];   /* float32 products, as torch.dot */
+                dot += (double)pr;
+            }
+            part[k] = dot;
         }
+        double dot = 0.0;
+        for (int64_t k = 0; k < nblk; ++k) dot += part[k];
+        free(part);
         float scale = (nu * nu) / (float)dot;
         if (!isnan(scale)) return scale;
+    } else {
+        free(part);
     }
     for (int64_t i = 0; i < P; ++i) bins_out[i] = 0;
     return 0.0f;
@@ -178,10 +235,13 @@ static float compress_slice(const float* x, int64_t len, int64_t P, int64_t seed
  * byte j bit t = bit i of bin[8j+t] ---- */
 static void to_bits(const int32_t* bins, int64_t Ptot, int nbits, uint8_t* planes) {
     int64_t L = Ptot / 8;
-    memset(planes, 0, (size_t)(L * nbits));
-    for (int64_t e = 0; e < Ptot; ++e)
-        for (int i = 0; i < nbits; ++i)
-            if ((bins[e] >> i) & 1) planes[i * L + (e >> 3)] |= (uint8_t)(1u << (e & 7));
+#pragma omp parallel for schedule(static) if (Ptot >= PAR_MIN)
+    for (int64_t j = 0; j < L; ++j)
+        for (int i = 0; i < nbits; ++i) {
+            uint8_t by = 0;
+            for (int t = 0; t < 8; ++t) by |= (uint8_t)(((bins[8 * j + t] >> i) & 1) << t);
+            planes[i * L + j] = by;
+        }
 }
 
 /* Full Eden.compress.  planes must hold nbits*P_tot/8 bytes, scales/dims
@@ -221,6 +281,7 @@ void oracle_eden_decompress(const uint8_t* planes, int64_t total_dim, const floa
     int64_t off = 0, out = 0;
     for (int k = 0; k < nslices; ++k) {
         int64_t P = dims[k];
+#pragma omp parallel for schedule(static) if (P >= PAR_MIN)
         for (int64_t e = 0; e < P; ++e) {
             int64_t g = off + e;
             int b = 0;
@@ -232,7 +293,10 @@ void oracle_eden_decompress(const uint8_t* planes, int64_t total_dim, const floa
             apply_signs(work, P, seed + i);
         }
         float sc = scales[k];
-        for (int64_t e = 0; e < P && out < total_dim; ++e) y[out++] = sc * work[e];
+        int64_t m = total_dim - out < P ? total_dim - out : P;
+#pragma omp parallel for schedule(static) if (P >= PAR_MIN)
+        for (int64_t e = 0; e < m; ++e) y[out + e] = sc * work[e];
+        out += m > 0 ? m : 0;
         off += P;
     }
     free(work);

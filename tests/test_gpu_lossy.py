@@ -334,6 +334,14 @@ def test_gzip_ranks_roundtrip(case):
     z = lossy.gzip_ranks(torch.from_numpy(x).to(DEV))
     assert gzip.decompress(z) == x.tobytes()
     assert z == lossy.gzip_ranks(torch.from_numpy(x).to(DEV))      # deterministic
+    # every member carries its 'BC' size field: the native parallel inflate reads it
+    import ctypes
+    from openfl_amd import _lib
+    src = np.frombuffer(z, np.uint8)
+    need = ctypes.c_size_t()
+    assert _lib.lib().ofl_gunzip_members(src.ctypes.data, src.size, None, 0, ctypes.byref(need), 4) == 0
+    assert need.value == x.nbytes
+    assert lossy.gunzip(z, 4).tobytes() == x.tobytes()
     if case == "kc6":
         ref = len(gzip.compress(x.tobytes(), compresslevel=9))
         assert len(z) < 1.35 * ref, (len(z), ref)   # ratio 0.139 vs gzip -9 0.118
@@ -358,3 +366,37 @@ def test_kc_pipeline_device_gzip_backend():
         outs.append((gzip.decompress(payload), pipe.backward(payload, mds)))
     assert outs[0][0] == outs[1][0]
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.timeout(900)
+def test_kc_2p22_tensor_vs_sklearn():
+    """BASELINE config 3 at its own tensor size: one 4096 x 1024 tensor of the
+    1 GiB set (N(0, 0.01^2)) through KmeansTransformer: inertia <= 1.01 x
+    sklearn KMeans(6, n_init=6) on the same data, labels = nearest of our
+    centres; then the whole KCPipeline with the device gzip: the payload
+    decodes (native member-parallel inflate) to centres[ranks] exactly."""
+    from sklearn.cluster import KMeans
+    from openfl_amd.pipelines import KCPipeline
+    from openfl_amd.pipelines.kc_pipeline import KmeansTransformer
+    g = torch.Generator(device=DEV).manual_seed(0)
+    x = torch.empty(4096 * 1024, device=DEV).normal_(0.0, 0.01, generator=g).cpu().numpy().reshape(4096, 1024)
+    t = KmeansTransformer(6, DEV)
+    np.random.seed(11)
+    ints, md = t.forward(x)
+    centres = np.array([md["int_to_float"][k] for k in sorted(md["int_to_float"])])
+    assert len(centres) == 6 and centres.dtype == np.float32
+    ref = KMeans(n_clusters=6, n_init=6, random_state=0).fit(x.reshape(-1, 1).astype(np.float64))
+    ours = _inertia(x, centres)
+    assert ours <= 1.01 * ref.inertia_, (ours, ref.inertia_)
+    xf = x.reshape(-1).astype(np.float64)
+    near = np.argmin(np.abs(xf[:, None] - centres[None, :].astype(np.float64)), axis=1)
+    assert np.mean(ints.reshape(-1) == near) >= 0.9999
+    pipe = KCPipeline(n_clusters=6, device=DEV, gzip_backend="device")
+    np.random.seed(11)
+    payload, mds = pipe.forward(x)
+    ranks = np.frombuffer(gzip.decompress(payload), np.float32).astype(np.int64)
+    cen = np.array([mds[0]["int_to_float"][k] for k in sorted(mds[0]["int_to_float"])], np.float32)
+    y = pipe.backward(payload, mds)
+    assert y.shape == x.shape and y.dtype == np.float32
+    np.testing.assert_array_equal(y.reshape(-1), cen[ranks])
+    assert len(payload) < 0.16 * x.nbytes

@@ -150,6 +150,93 @@ def test_edge_cases(tag):
             _finite_scales_close(scales, case["scales"])
 
 
+def _bins_mismatch_chunked(pa, pb, P, bits, chunk=1 << 24):
+    """(mismatching elements, max |dbin|) of two to_bits plane sets, in
+    chunks (a 2^29-element unpack would need tens of GiB at once)."""
+    L = P // 8
+    pa = np.frombuffer(bytes(pa) if not isinstance(pa, np.ndarray) else pa, np.uint8).reshape(bits, L)
+    pb = np.frombuffer(bytes(pb) if not isinstance(pb, np.ndarray) else pb, np.uint8).reshape(bits, L)
+    bad, worst = 0, 0
+    w = (1 << np.arange(bits, dtype=np.int32))[:, None]
+    for j0 in range(0, L, chunk // 8):
+        j1 = min(L, j0 + chunk // 8)
+        if np.array_equal(pa[:, j0:j1], pb[:, j0:j1]):
+            continue
+        ba = (np.unpackbits(pa[:, j0:j1], axis=1, bitorder="little").astype(np.int32) * w).sum(0)
+        bb = (np.unpackbits(pb[:, j0:j1], axis=1, bitorder="little").astype(np.int32) * w).sum(0)
+        d = np.abs(ba - bb)
+        bad += int(np.count_nonzero(d))
+        worst = max(worst, int(d.max()))
+    return bad, worst
+
+
+def _decode_err_chunked(y, ref, chunk=1 << 24):
+    """(relative L2, max |err| / max |ref|) in float64, chunked."""
+    se = sr = 0.0
+    me = mr = 0.0
+    for i in range(0, ref.size, chunk):
+        r = ref[i:i + chunk].astype(np.float64)
+        e = y[i:i + chunk].astype(np.float64) - r
+        se += float(np.dot(e, e))
+        sr += float(np.dot(r, r))
+        me = max(me, float(np.max(np.abs(e))))
+        mr = max(mr, float(np.max(np.abs(r))))
+    return np.sqrt(se / sr), me / max(mr, 1e-30)
+
+
+# The five-pass large-slice FWHT (2^26 <= P <= 2^29: two column levels, the
+# middle one carrying D2) against the oracle (eden_pipeline.py:451-473 hadamard,
+# :403-449 rand_diag, :661-690 to_bits): one 2^26 slice, a 2^27 slice with a
+# ragged tail (valid length ends inside a float4), and the Llama-3-8B
+# embed_tokens / lm_head tensor 128256 x 4096 (one 2^29 slice).  Same bars as
+# above; the encode is run twice over differently pre-filled plane buffers,
+# so every plane byte is shown to be written.
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("n", [1 << 26, (1 << 27) - 99_997, 128256 * 4096])
+def test_five_pass_slices_vs_oracle(n):
+    from openfl_amd.codec import EdenPlan
+    bits, seed = 8, (n * 13 + 5) % 65536
+    x = np.random.default_rng(n % 1000).standard_normal(n).astype(np.float32) * np.float32(0.01)
+    c = _codec(bits)
+    plan = c.plan([n])
+    P = sum(plan.dims[0])
+    assert plan.dims[0] == O.slice_plan(n)[0] and max(plan.dims[0]) >= 1 << 26
+    xd = torch.from_numpy(x).to(DEV)
+    sd = torch.tensor([seed], dtype=torch.int32, device=DEV)
+    outs = []
+    for fill in (0x00, 0xFF):
+        planes = torch.full((plan.planes_bytes,), fill, dtype=torch.uint8, device=DEV)
+        scales = torch.full((plan.n_slices,), float("nan"), dtype=torch.float32, device=DEV)
+        ws = c.ws.get(plan.ws_bytes, c.device)
+        plan.encode(xd, sd, planes, scales, ws)
+        torch.cuda.synchronize()
+        outs.append((planes.cpu().numpy(), scales.cpu().numpy()))
+        del planes, scales
+    del xd
+    torch.cuda.empty_cache()
+    (gp, gs), (gp2, gs2) = outs
+    assert np.array_equal(gp, gp2) and np.array_equal(gs, gs2)  # every byte written
+    assert gp.size == bits * P // 8
+    print(f"[five-pass n={n}] GPU encodes done; oracle compress on {O.get_threads()} threads", flush=True)
+    op, osc, odims, _ = O.compress(x, seed, bits)
+    assert odims == plan.dims[0] and op.size == gp.size
+    bad, worst = _bins_mismatch_chunked(gp, op, P, bits)
+    assert bad <= (1 - BIN_AGREE) * P and worst <= 1, (bad, worst)
+    _finite_scales_close(gs, osc)
+    del gp2, gs2, outs
+    # cross-decode the oracle's (= reference) bytes with the HIP decoder
+    print(f"[five-pass n={n}] bins {bad} mismatches; decoding", flush=True)
+    y = gpu_decode(op, n, osc, odims, seed, bits)
+    yo = O.decompress(op, n, osc, odims, seed, bits)
+    rel, mx = _decode_err_chunked(y, yo)
+    assert rel <= 2e-6 and mx <= 2e-6, (rel, mx)
+    # and the end-to-end quantisation error of the HIP round trip is Eden's
+    y2 = gpu_decode(gp, n, gs, plan.dims[0], seed, bits)
+    e2e, _ = _decode_err_chunked(y2, x)
+    assert 5.5e-3 < e2e < 7.5e-3
+    torch.cuda.empty_cache()
+
+
 def test_large_slice_property_2p29():
     """Llama-3-8B embed/lm_head size (one 2^29 slice, 128256 x 4096 elements):
     too big for the oracle in test time, so check size-independent properties:
