@@ -142,7 +142,11 @@ __global__ __launch_bounds__(kNT) void k_ternary(const float* sparse, int64_t n,
 
 // TernaryTransformer statistics (stc_pipeline.py:120-123): fp64 sum of |x| and
 // counts of x > 0, x < 0 (the rest are zeros)
-__global__ __launch_bounds__(kNT) void k_tstats(const float* x, int64_t n, unsigned long long* cnt, double* abs_sum) {
+// per-wave partials (sign counts, sum |x| in fp64), then one wave sums them in
+// a fixed order: the ternary mean (stc_pipeline.py:120-123) is the same on
+// every run (fp64 atomics would make its last bits depend on arrival order)
+__global__ __launch_bounds__(kNT) void k_tstats(const float* x, int64_t n, unsigned long long* cnt_p,
+                                                 double* abs_p) {
     uint32_t cp = 0, cn = 0;
     double as = 0.0;
     for (int64_t i = gtid(); i < n; i += gstride()) {
@@ -152,7 +156,20 @@ __global__ __launch_bounds__(kNT) void k_tstats(const float* x, int64_t n, unsig
         as += fabs((double)v);
     }
     cp = wave_sum(cp); cn = wave_sum(cn); as = wave_sum(as);
-    if ((threadIdx.x & 63) == 0) { atomicAdd(&cnt[0], (unsigned long long)cp); atomicAdd(&cnt[1], (unsigned long long)cn); atomicAdd(abs_sum, as); }
+    if ((threadIdx.x & 63) == 0) {
+        const int64_t w = (int64_t)blockIdx.x * (kNT / 64) + (threadIdx.x >> 6);
+        cnt_p[2 * w] = cp;
+        cnt_p[2 * w + 1] = cn;
+        abs_p[w] = as;
+    }
+}
+__global__ __launch_bounds__(64) void k_tstats_final(const unsigned long long* cnt_p, const double* abs_p, int nw,
+                                                     unsigned long long* cnt, double* abs_sum) {
+    unsigned long long cp = 0, cn = 0;
+    double as = 0.0;
+    for (int w = threadIdx.x; w < nw; w += 64) { cp += cnt_p[2 * w]; cn += cnt_p[2 * w + 1]; as += abs_p[w]; }
+    cp = wave_sum(cp); cn = wave_sum(cn); as = wave_sum(as);
+    if (threadIdx.x == 0) { cnt[0] = cp; cnt[1] = cn; abs_sum[0] = as; }
 }
 
 // reference backward (kc_pipeline.py:81-83): for key in order: data[data == key] = value,
@@ -1480,12 +1497,14 @@ int ofl_ternary_stats(const float* x, int64_t n, int64_t* n_pos, int64_t* n_neg,
                       size_t ws_bytes, void* stream) {
     hipStream_t st = static_cast<hipStream_t>(stream);
     Scratch sc{static_cast<char*>(ws), ws_bytes};
+    const int grid = grid_for(n), nw = grid * (lossy::kNT / 64);
     unsigned long long* c = sc.take<unsigned long long>(2);
     double* a = sc.take<double>(1);
-    if (!a) return lfail(OFL_ESPACE, "ternary: workspace too small");
-    LHIP(hipMemsetAsync(c, 0, 16, st));
-    LHIP(hipMemsetAsync(a, 0, 8, st));
-    hipLaunchKernelGGL(lossy::k_tstats, dim3(grid_for(n)), dim3(lossy::kNT), 0, st, x, n, c, a);
+    unsigned long long* cp = sc.take<unsigned long long>(2 * (size_t)nw);
+    double* ap = sc.take<double>((size_t)nw);
+    if (!c || !a || !cp || !ap) return lfail(OFL_ESPACE, "ternary: workspace too small");
+    hipLaunchKernelGGL(lossy::k_tstats, dim3(grid), dim3(lossy::kNT), 0, st, x, n, cp, ap);
+    hipLaunchKernelGGL(lossy::k_tstats_final, dim3(1), dim3(64), 0, st, cp, ap, nw, c, a);
     unsigned long long ch[2];
     LHIP(hipMemcpyAsync(ch, c, 16, hipMemcpyDeviceToHost, st));
     LHIP(hipMemcpyAsync(abs_sum, a, 8, hipMemcpyDeviceToHost, st));

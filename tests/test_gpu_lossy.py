@@ -400,3 +400,16 @@ def test_kc_2p22_tensor_vs_sklearn():
     assert y.shape == x.shape and y.dtype == np.float32
     np.testing.assert_array_equal(y.reshape(-1), cen[ranks])
     assert len(payload) < 0.16 * x.nbytes
+
+
+def test_ternary_stats_deterministic():
+    """TernaryTransformer.forward's mean (stc_pipeline.py:120-123) is the same
+    on every run: per-wave fp64 partials summed in a fixed order."""
+    from openfl_amd import lossy
+    x = np.random.default_rng(4).standard_normal(3_000_001).astype(np.float32)
+    xd = torch.from_numpy(x).to(DEV)
+    runs = {lossy.ternary_stats(xd) for _ in range(5)}
+    assert len(runs) == 1
+    npos, nneg, asum = runs.pop()
+    assert npos == int(np.sum(x > 0)) and nneg == int(np.sum(x < 0))
+    np.testing.assert_allclose(asum, np.sum(np.abs(x.astype(np.float64))), rtol=1e-12)
