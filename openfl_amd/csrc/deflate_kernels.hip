@@ -299,13 +299,40 @@ __global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
         if (bl >= kMinMatch) { S.bestL[i] = (uint8_t)bl; S.bestG[i] = (uint16_t)bg; }
     }
     __syncthreads();
-    // greedy parse with one-step lazy matching (thread 0)
-    if (tid == 0) {
-        int i = 0;
-        while (i < ntok) {
+    // greedy parse with one-step lazy matching: from position i the parse
+    // moves to nxt(i) = i + L(i) if a match starts there (L(i) >= 3 and not
+    // L(i+1) > L(i)), else i + 1.  In parallel: thread t's segment
+    // [kPer t, kPer t + kPer) maps every entry position to the first parse
+    // position past the segment (a match can jump over whole segments);
+    // thread 0 chains the kNT segments (kNT dependent steps instead of up to
+    // kTok); each thread then walks its segment from its entry and marks the
+    // ops.  The ops are exactly the sequential parse's.
+    {
+        int16_t (*fent)[kPer] = reinterpret_cast<int16_t (*)[kPer]>(S.u.key);  // sort keys are dead
+        int16_t* entry = reinterpret_cast<int16_t*>(S.u.key) + kNT * kPer;
+        auto nxt = [&](int i) -> int {
             const int L = S.bestL[i];
-            if (L >= kMinMatch && !(i + 1 < ntok && S.bestL[i + 1] > L)) { S.op[i] = 2; i += L; }
-            else { S.op[i] = 1; i += 1; }
+            return (L >= kMinMatch && !(i + 1 < ntok && S.bestL[i + 1] > L)) ? i + L : i + 1;
+        };
+        const int s0 = tid * kPer, s1 = s0 + kPer;
+        for (int e = 0; e < kPer; ++e) {
+            int p = s0 + e;
+            while (p < s1 && p < ntok) p = nxt(p);
+            fent[tid][e] = (int16_t)p;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int p = 0;
+            for (int t = 0; t < kNT; ++t) {
+                entry[t] = (int16_t)p;
+                if (p < t * kPer + kPer && p < ntok) p = fent[t][p - t * kPer];
+            }
+        }
+        __syncthreads();
+        for (int p = entry[tid]; p < s1 && p < ntok;) {
+            const int q = nxt(p);
+            S.op[p] = q - p > 1 ? 2 : 1;
+            p = q;
         }
     }
     // CRC of the member: tree of (raw crc, byte count) pairs

@@ -1598,6 +1598,28 @@ DEVI void exchange_half_pad(float (&v)[64], float* s, uint32_t tid) {
     }
 }
 
+// registers [32 h, 32 h + 32) of a ws tile (L3 layout), as fetch_ws
+template <int H>
+DEVI void fetch_ws_half(const KArgs& a, const SliceDesc& D, uint32_t tile, bool live, uint32_t base3,
+                        float (&v)[64]) {
+    if (D.perm) {
+        const rsrc_t r = mk_rsrc(ws_row_base(a, D, tile), live ? (4u << (kRowLog + 1)) - 128u : 0u);
+        const uint32_t b = ws_row_idx(base3);
+#pragma unroll
+        for (int k = 32 * H; k < 32 * H + 32; ++k) v[k] = bload1(r, b, LT<RS::L3>::off(k) << 1);
+    } else {
+        const rsrc_t r = mk_rsrc(ws_row_base(a, D, tile), live ? (4u << kRowLog) : 0u);
+#pragma unroll
+        for (int k = 32 * H; k < 32 * H + 32; ++k) v[k] = bload1(r, base3, LT<RS::L3>::off(k));
+    }
+}
+
+// ROLL: the next tile's intermediate is loaded into the registers the
+// quantiser has just freed (its first half after the first 32-element run,
+// the second after the second), so the loads are in flight across the second
+// run, the plane stores and the dot reduction, with no extra registers (the
+// kernel sits at the 128-VGPR cap of two blocks per CU).
+template <bool ROLL>
 __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowC2(KArgs a) {
     using R = RowC2Set;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1609,17 +1631,28 @@ __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowC2(KArgs a) {
     __syncthreads();
     const int total = (int)sld(a.tstart, a.count);
     const uint32_t base3 = LT<R::L3>::base(tid), base5 = LT<R::L5>::base(tid);
-    for (int t = (int)blockIdx.x; t < total; t += (int)gridDim.x) {
+    auto locate = [&](int t, int& si, uint32_t& tile) {
         int lo = 0, hi = a.count - 1;  // block-uniform search of the tile table (scalar loads)
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
             if ((int)sld(a.tstart, mid) <= t) lo = mid; else hi = mid - 1;
         }
-        const int si = (int)sld(a.list, lo);
-        const uint32_t tile = (uint32_t)(t - (int)sld(a.tstart, lo));
+        si = (int)sld(a.list, lo);
+        tile = (uint32_t)(t - (int)sld(a.tstart, lo));
+    };
+    int t = (int)blockIdx.x;
+    if (t >= total) return;
+    int si; uint32_t tile;
+    locate(t, si, tile);
+    float v[64];
+    if (ROLL) fetch_ws(a, udesc(a.d, si), tile, true, base3, v);
+    for (;;) {
         const SliceDesc D = udesc(a.d, si);
-        float v[64];
-        fetch_ws(a, D, tile, true, base3, v);
+        const int tn = t + (int)gridDim.x;
+        const bool more = tn < total;
+        int sn; uint32_t tln;
+        locate(more ? tn : t, sn, tln);
+        if (!ROLL) fetch_ws(a, D, tile, true, base3, v);
         stages<R::L3, R::F2c>(v);
         exchange_half_pad<R::L3, R::L4, R::HB>(v, s, tid);
         stages<R::L4, R::F2d>(v);
@@ -1639,12 +1672,18 @@ __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowC2(KArgs a) {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) w[i] = 0;
             }
+            if (ROLL) {  // this half's registers are free: start the next tile's
+                if (g == 0) fetch_ws_half<0>(a, udesc(a.d, sn), tln, more, base3, v);
+                else fetch_ws_half<1>(a, udesc(a.d, sn), tln, more, base3, v);
+            }
             store_planes(a.pout + D.pl_off, (tile << kRowLog) + base5 + ((uint32_t)g << R::HB), D.pl_stride,
                          a.nbits, w);
         }
         if (!pos) dot = 0.f;
         dot = block_sum<kRowNT>(dot, red);
         if (tid == 0) a.part[D.part_off + tile] = dot;
+        if (!more) break;
+        t = tn; si = sn; tile = tln;
     }
 }
 
@@ -1811,6 +1850,13 @@ bool use_rowc2() {
     return on;
 }
 
+// k_enc_rowC2 loads the next tile into the quantiser's freed registers
+// (OFL_EDEN_ROLL=0: load at the top of each tile, A/B)
+bool use_roll() {
+    static const bool on = [] { const char* s = getenv("OFL_EDEN_ROLL"); return !(s && s[0] == '0'); }();
+    return on;
+}
+
 // column passes with M >= 8 rows, or a middle pass with M >= 6, use k_col6
 // (measured: the 1024-thread k_col is ~4 % faster on the plain M = 7 pass);
 // OFL_EDEN_COL6=0 forces k_col everywhere (A/B)
@@ -1843,7 +1889,8 @@ hipError_t set_all_attrs() {
     if ((e = set_small_attr<15>()) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_enc_rowA, ofl::kRowSmemA)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_enc_rowC, ofl::kRowSmemQ)) != hipSuccess) return e;
-    if ((e = set_lds((const void*)ofl::k_enc_rowC2, ofl::kRowC2Smem)) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_enc_rowC2<true>, ofl::kRowC2Smem)) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_enc_rowC2<false>, ofl::kRowC2Smem)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_dec_rowA<true>, ofl::kRowSmemC)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_dec_rowA<false>, ofl::kRowSmemC)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_dec_rowC, ofl::kRowSmemA)) != hipSuccess) return e;
@@ -1935,7 +1982,10 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
         case K_ROWC: {
             const int64_t g = std::min<int64_t>(l.blocks, pl->ncu);
             if (enc && use_rowc2())
-                e = launch(ofl::k_enc_rowC2, std::min<int64_t>(l.blocks, 2 * pl->ncu), ofl::kRowNT, ofl::kRowC2Smem, st, a);
+                e = use_roll() ? launch(ofl::k_enc_rowC2<true>, std::min<int64_t>(l.blocks, 2 * pl->ncu), ofl::kRowNT,
+                                        ofl::kRowC2Smem, st, a)
+                               : launch(ofl::k_enc_rowC2<false>, std::min<int64_t>(l.blocks, 2 * pl->ncu), ofl::kRowNT,
+                                        ofl::kRowC2Smem, st, a);
             else
                 e = enc ? launch(ofl::k_enc_rowC, g, ofl::kRowNT, ofl::kRowSmemQ, st, a)
                         : launch(ofl::k_dec_rowC, g, ofl::kRowNT, ofl::kRowSmemA, st, a);
@@ -2001,7 +2051,9 @@ std::string launch_name(const Launch& l, bool enc) {
     case K_TINY: return std::string("ofl::k_") + d + "_tiny";
     case K_SMALL: return std::string("ofl::k_") + d + "_small<" + std::to_string(l.param) + ">";
     case K_ROWA: return std::string("ofl::k_") + d + "_rowA";
-    case K_ROWC: return std::string("ofl::k_") + d + (enc && use_rowc2() ? "_rowC2" : "_rowC");
+    case K_ROWC:
+        if (enc && use_rowc2()) return std::string("ofl::k_enc_rowC2<") + (use_roll() ? "true" : "false") + ">";
+        return std::string("ofl::k_") + d + "_rowC";
     case K_COL:
         if (l.tl == 16) return "ofl::k_col6<" + std::to_string(l.param) + ", " + (l.mid ? "true" : "false") + ", 16>";
         return std::string((l.param >= 8 || (l.param >= 6 && l.mid)) && use_col6() ? "ofl::k_col6<" : "ofl::k_col<") +

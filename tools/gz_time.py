@@ -1,0 +1,23 @@
+"""Time lossy.gzip_ranks (device gzip of float32 ranks) on a KC-like 1 GiB
+rank array; prints ms per call and the compressed ratio."""
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from openfl_amd import lossy  # noqa: E402
+
+n = 1 << 28
+g = torch.Generator(device="cuda").manual_seed(0)
+p = torch.tensor([0.07, 0.2, 0.23, 0.23, 0.2, 0.07], device="cuda")
+x = torch.multinomial(p, n, replacement=True, generator=g).to(torch.float32)
+z = lossy.gzip_ranks(x)
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(3):
+    z = lossy.gzip_ranks(x)
+dt = (time.perf_counter() - t0) / 3
+print(f"gzip_ranks 1 GiB: {1e3 * dt:.1f} ms, {4 * n / dt / 2**30:.2f} GiB/s, ratio {len(z) / (4 * n):.4f}")
