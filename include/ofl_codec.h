@@ -283,6 +283,10 @@ int ofl_wavg_delta_points(int ncollab, const float* const* xs, const double* wei
                           int npoints, const int64_t* idx, double* agg_out, double* delta64_out, float* delta32_out,
                           void* ws, size_t ws_bytes, void* stream);
 int ofl_apply_delta(const float* base, const float* delta, int64_t n, float* out, void* stream);
+/* out = (double)data - shift in float64 (device arrays): RandomShiftTransformer.backward
+ * (random_shift_pipeline.py:45-68) with float64 shifts (metadata off the wire);
+ * its forward (data + shift, float32) is ofl_apply_delta. */
+int ofl_sub_f32_f64(const float* data, const double* shift, int64_t n, double* out, void* stream);
 int ofl_apply_delta_ranges(const float* base, const float* delta, float* out, int nranges, const int64_t* starts,
                            const int64_t* dst, int64_t total, void* stream);
 

@@ -34,7 +34,7 @@ EXPORTS = (
     "ofl_wavg_range_sums_workspace_bytes", "ofl_wavg_delta_range_sums", "ofl_wavg_delta_seeds",
     "ofl_py_hash_doubles",
     "ofl_wavg_points_workspace_bytes", "ofl_wavg_delta_points", "ofl_apply_delta",
-    "ofl_apply_delta_ranges",
+    "ofl_apply_delta_ranges", "ofl_sub_f32_f64",
     "ofl_gzip_last_error", "ofl_gzip_ranks_workspace_bytes", "ofl_gzip_ranks_bound", "ofl_gzip_ranks",
     "ofl_gunzip_members",
 )
@@ -134,6 +134,8 @@ def _bind(L):
     L.ofl_wavg_delta_points.restype = i32
     L.ofl_apply_delta.argtypes = [vp, vp, i64, vp, vp]
     L.ofl_apply_delta.restype = i32
+    L.ofl_sub_f32_f64.argtypes = [vp, vp, i64, vp, vp]
+    L.ofl_sub_f32_f64.restype = i32
     L.ofl_apply_delta_ranges.argtypes = [vp, vp, vp, i32, vp, vp, i64, vp]
     L.ofl_apply_delta_ranges.restype = i32
     L.ofl_gzip_last_error.restype = ctypes.c_char_p

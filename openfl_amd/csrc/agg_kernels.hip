@@ -286,6 +286,13 @@ __global__ __launch_bounds__(kNT) void k_apply(const float* base, const float* d
     for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += stride) out[i] = base[i] + delta[i];
 }
 
+// RandomShiftTransformer.backward with wire metadata (random_shift_pipeline.py:
+// 45-68): data (float32) - shift (float64) in float64, as NumPy promotes
+__global__ __launch_bounds__(kNT) void k_unshift64(const float* data, const double* shift, int64_t n, double* out) {
+    for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT)
+        out[i] = (double)data[i] - shift[i];
+}
+
 // apply_delta on listed ranges (device tables): the tensors the codec does
 // not touch when the decode itself adds the base (ofl_eden_decode_add)
 __global__ __launch_bounds__(kNT) void k_apply_ranges(const float* base, const float* delta, float* out,
@@ -527,6 +534,15 @@ int ofl_apply_delta(const float* base, const float* delta, int64_t n, float* out
     if (n == 0) return OFL_OK;
     hipLaunchKernelGGL(agg::k_apply, dim3(grid_for(n, 16)), dim3(agg::kNT), 0, static_cast<hipStream_t>(stream), base,
                        delta, n, out);
+    AHIP(hipGetLastError());
+    return OFL_OK;
+}
+
+int ofl_sub_f32_f64(const float* data, const double* shift, int64_t n, double* out, void* stream) {
+    if (n < 0 || (n && (!data || !shift || !out))) return afail(OFL_EINVAL, "sub_f32_f64: bad arguments");
+    if (n == 0) return OFL_OK;
+    hipLaunchKernelGGL(agg::k_unshift64, dim3(grid_for(n, 16)), dim3(agg::kNT), 0, static_cast<hipStream_t>(stream),
+                       data, shift, n, out);
     AHIP(hipGetLastError());
     return OFL_OK;
 }

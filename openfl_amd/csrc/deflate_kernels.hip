@@ -86,7 +86,7 @@ struct Smem {
     uint16_t kl[kLit], kd[kDist], kc[kCL];  // bit-reversed canonical codes
     uint32_t scan[kNT / 64];
     uint32_t crc_r[kNT], crc_n[kNT];
-    uint32_t hdr_bits, total_bits, nrle;
+    uint32_t hdr_bits, total_bits, nrle, nlit_ndist;
     int bad;
 };
 static_assert(sizeof(HScratch) <= sizeof(int16_t) * kNT * kTypes, "Huffman scratch fits the token tables");
@@ -170,6 +170,118 @@ DEVI void huff_codes(const uint8_t* len, int n, uint16_t* code) {
     uint32_t c = 0;
     for (int b = 1; b < 16; ++b) { c = (c + cnt[b - 1]) << 1; next[b] = c; }
     for (int s = 0; s < n; ++s) code[s] = len[s] ? (uint16_t)rev_bits(next[len[s]]++, len[s]) : 0;
+}
+
+// ---- the same on one wave (lanes 0..63 of the block) ----------------------
+// The serial versions above are latency-bound on one lane (~60 % of a
+// member's time).  The rank alphabets use a few dozen literal bytes and
+// length / distance codes, so one symbol per lane fits: the used symbols are
+// compacted in symbol order, bitonic-sorted by (weight, symbol) across the
+// lanes (shfl_xor), and the two-queue merge (leaves in sorted order, internal
+// nodes in creation order, both nondecreasing) runs on wave-uniform values
+// through readlane / writelane; depths are assigned top-down.  Returns false
+// (lengths zeroed) when more than 64 symbols occur: the caller then runs the
+// serial huff_lengths on lane 0.  scratch: 64 LDS words.
+DEVI uint32_t rdl(uint32_t v, int i) { return (uint32_t)__builtin_amdgcn_readlane((int)v, i); }
+DEVI uint32_t wrl(uint32_t v, int i, uint32_t old) { return (int)(threadIdx.x & 63u) == i ? v : old; }
+
+DEVI bool huff_lengths_wave(const uint32_t* freq, int n, int maxlen, uint8_t* len, uint32_t* scratch, bool complete) {
+    const int lane = (int)(threadIdx.x & 63u);
+    int m = 0;
+    for (int b = 0; b < n; b += 64) {
+        const int s = b + lane;
+        const uint32_t f = s < n ? freq[s] : 0u;
+        const uint64_t mask = __ballot(f != 0u);
+        const int rank = __popcll(mask & ((1ull << lane) - 1ull));
+        if (f != 0u && m + rank < 64) scratch[m + rank] = (f << 9) | (uint32_t)s;
+        if (s < n) len[s] = 0;
+        m += __popcll(mask);
+    }
+    if (m > 64) return false;
+    if (m == 0) return true;
+    if (m == 1) {
+        const int s = (int)(scratch[0] & 511u);
+        if (lane == 0) {
+            len[s] = 1;
+            if (complete) len[s == 0 ? 1 : 0] = 1;
+        }
+        return true;
+    }
+    uint32_t key0 = lane < m ? scratch[lane] : 0xffffffffu;
+    for (;;) {
+        uint32_t key = key0;
+        for (int k = 2; k <= 64; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                const uint32_t o = (uint32_t)__shfl_xor((int)key, j, 64);
+                const bool up = (lane & k) == 0, lower = (lane & j) == 0;
+                key = (lower == up) ? min(key, o) : max(key, o);
+            }
+        const uint32_t w = key >> 9;  // lane i: the i-th smallest leaf weight
+        uint32_t iw = 0, ca = 0, cb = 0;  // lane k: internal node k's weight and children
+        int li = 0, ij = 0, ni = 0;
+        for (int step = 0; step < m - 1; ++step) {
+            uint32_t cw0, cw1;
+            int c0, c1;
+            {
+                const uint32_t lw = li < m ? rdl(w, li) : 0xffffffffu, nw = ij < ni ? rdl(iw, ij) : 0xffffffffu;
+                if (li < m && (ij >= ni || lw <= nw)) { c0 = li; cw0 = lw; ++li; } else { c0 = 64 + ij; cw0 = nw; ++ij; }
+            }
+            {
+                const uint32_t lw = li < m ? rdl(w, li) : 0xffffffffu, nw = ij < ni ? rdl(iw, ij) : 0xffffffffu;
+                if (li < m && (ij >= ni || lw <= nw)) { c1 = li; cw1 = lw; ++li; } else { c1 = 64 + ij; cw1 = nw; ++ij; }
+            }
+            iw = wrl(cw0 + cw1, ni, iw);
+            ca = wrl((uint32_t)c0, ni, ca);
+            cb = wrl((uint32_t)c1, ni, cb);
+            ++ni;
+        }
+        uint32_t di = 0, dl = 0;  // depth of internal node k (lane k) / of the i-th leaf (lane i)
+        int deepest = 0;
+        for (int k = ni - 1; k >= 0; --k) {
+            const uint32_t d = rdl(di, k) + 1u;
+            const int a = (int)rdl(ca, k), b = (int)rdl(cb, k);
+            if (a >= 64) di = wrl(d, a - 64, di); else { dl = wrl(d, a, dl); deepest = max(deepest, (int)d); }
+            if (b >= 64) di = wrl(d, b - 64, di); else { dl = wrl(d, b, dl); deepest = max(deepest, (int)d); }
+        }
+        if (deepest <= maxlen) {
+            if (lane < m) len[key & 511u] = (uint8_t)dl;
+            return true;
+        }
+        // too deep: flatten the weights (>= 1) and rebuild, as huff_lengths
+        key0 = lane < m ? (((((key0 >> 9) >> 1) | 1u)) << 9) | (key0 & 511u) : 0xffffffffu;
+    }
+}
+
+// canonical codes on one wave: counts per length and ranks by ballots
+DEVI void huff_codes_wave(const uint8_t* len, int n, uint16_t* code) {
+    const int lane = (int)(threadIdx.x & 63u);
+    const uint64_t below = (1ull << lane) - 1ull;
+    uint32_t cnt[16];
+#pragma unroll
+    for (int b = 0; b < 16; ++b) cnt[b] = 0;
+    for (int base = 0; base < n; base += 64) {
+        const int s = base + lane;
+        const int L = s < n ? len[s] : 0;
+#pragma unroll
+        for (int b = 1; b < 16; ++b) cnt[b] += (uint32_t)__popcll(__ballot(L == b));
+    }
+    uint32_t run[16];
+    uint32_t c = 0;
+    run[0] = 0;
+#pragma unroll
+    for (int b = 1; b < 16; ++b) { c = (c + (b > 1 ? cnt[b - 1] : 0u)) << 1; run[b] = c; }
+    for (int base = 0; base < n; base += 64) {
+        const int s = base + lane;
+        const int L = s < n ? len[s] : 0;
+        uint32_t mine = 0;
+#pragma unroll
+        for (int b = 1; b < 16; ++b) {
+            const uint64_t mk = __ballot(L == b);
+            if (L == b) mine = run[b] + (uint32_t)__popcll(mk & below);
+            run[b] += (uint32_t)__popcll(mk);
+        }
+        if (s < n) code[s] = L ? (uint16_t)rev_bits(mine, L) : 0;
+    }
 }
 
 struct GzArgs {
@@ -362,15 +474,21 @@ __global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
         }
     }
     __syncthreads();
-    // ---- thread 0: codes and the headers ----
+    // ---- wave 0: code lengths and codes (lane 0: the code-length RLE and the
+    // header bits) ----
+    if (tid < 64) {
+        HScratch& h = S.u.h;
+        if (tid == 0) S.hl[256] = 1;  // end of block
+        if (!huff_lengths_wave(S.hl, kLit, 15, S.ll, h.w, true) && tid == 0) huff_lengths(S.hl, kLit, 15, S.ll, h, true);
+        if (tid == 0) {
+            bool anyd = false;
+            for (int i = 0; i < kDist; ++i) anyd = anyd || S.hd[i];
+            if (!anyd) S.hd[0] = 1;  // one (unused) distance code
+        }
+        if (!huff_lengths_wave(S.hd, kDist, 15, S.ld, h.w, false) && tid == 0) huff_lengths(S.hd, kDist, 15, S.ld, h, false);
+    }
     if (tid == 0) {
         HScratch& h = S.u.h;
-        S.hl[256] = 1;  // end of block
-        huff_lengths(S.hl, kLit, 15, S.ll, h, true);
-        bool anyd = false;
-        for (int i = 0; i < kDist; ++i) anyd = anyd || S.hd[i];
-        if (!anyd) S.hd[0] = 1;  // one (unused) distance code
-        huff_lengths(S.hd, kDist, 15, S.ld, h, false);
         int nlit = kLit;
         while (nlit > 257 && S.ll[nlit - 1] == 0) --nlit;
         int ndist = kDist;
@@ -395,10 +513,20 @@ __global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
             i += run;
         }
         for (int i = 0; i < nr; ++i) S.hc[h.rle_sym[i]]++;
-        huff_lengths(S.hc, kCL, 7, S.lc, h, true);
-        huff_codes(S.ll, kLit, S.kl);
-        huff_codes(S.ld, kDist, S.kd);
-        huff_codes(S.lc, kCL, S.kc);
+        S.nrle = (uint32_t)nr;
+        S.nlit_ndist = (uint32_t)(nlit | (ndist << 16));
+    }
+    if (tid < 64) {
+        HScratch& h = S.u.h;
+        if (!huff_lengths_wave(S.hc, kCL, 7, S.lc, h.w + 2 * kLit - 64, true) && tid == 0)
+            huff_lengths(S.hc, kCL, 7, S.lc, h, true);
+        huff_codes_wave(S.ll, kLit, S.kl);
+        huff_codes_wave(S.ld, kDist, S.kd);
+        huff_codes_wave(S.lc, kCL, S.kc);
+    }
+    if (tid == 0) {
+        HScratch& h = S.u.h;
+        const int nr = (int)S.nrle, nlit = (int)(S.nlit_ndist & 0xffffu), ndist = (int)(S.nlit_ndist >> 16);
         int ncl = kCL;
         while (ncl > 4 && S.lc[c_clord[ncl - 1]] == 0) --ncl;
         uint32_t pos = 0;

@@ -24,7 +24,7 @@ def main():
     for f in glob.glob(os.path.join(root, "pass*", "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"]
-            if "ofl::" not in k:
+            if not any(ns in k for ns in ("ofl::", "lossy::", "gz::")):
                 continue
             vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     kernels = {}
