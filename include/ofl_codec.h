@@ -316,6 +316,21 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
  * member's ISIZE and CRC-32 checked.  OFL_EFORMAT if the stream is not
  * member-indexed (e.g. gzip.compress output): use gzip.decompress then. */
 int ofl_gunzip_members(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len, int nthreads);
+/* The same decode on the GPU, in two steps.  ofl_gzip_member_index (HOST, no
+ * GPU): the members of a member-indexed stream src[n] (OFL_EFORMAT otherwise)
+ * -> *nmembers, *out_len (decompressed size), *max_isize and, when index is
+ * not NULL (cap_members entries), per member four int64: deflate data offset,
+ * data length, output offset, ISIZE | CRC-32 << 32.  ofl_inflate_members:
+ * inflates every member (one wavefront each; stored, fixed and dynamic
+ * blocks) from src (DEVICE copy of the stream) into out (DEVICE, out_cap
+ * bytes) at its output offset, checking ISIZE and CRC-32; index is the DEVICE
+ * copy of the index; members must produce <= 64 KiB each (OFL_EFORMAT
+ * otherwise); ws: DEVICE, >= 256 bytes.  Synchronous; OFL_EINVAL for corrupt
+ * data (what gzip.decompress would raise on). */
+int ofl_gzip_member_index(const uint8_t* src, size_t n, int64_t* index, int64_t cap_members, int64_t* nmembers,
+                          size_t* out_len, uint32_t* max_isize);
+int ofl_inflate_members(const uint8_t* src, const int64_t* index, int64_t nmembers, uint32_t max_isize, uint8_t* out,
+                        size_t out_cap, void* ws, size_t ws_bytes, void* stream);
 
 /* ---- host helpers ----------------------------------------------------------
  * Left-to-right serial sums in the array's own precision: the

@@ -15,7 +15,7 @@ _lock = threading.Lock()
 _lib = None
 
 OFL_OK = 0
-OFL_EFORMAT = -4
+OFL_EINVAL, OFL_EHIP, OFL_ESPACE, OFL_EFORMAT = -1, -2, -3, -4
 
 EXPORTS = (
     "ofl_version", "ofl_last_error", "ofl_eden_slice_plan", "ofl_eden_plan_create",
@@ -36,7 +36,7 @@ EXPORTS = (
     "ofl_wavg_points_workspace_bytes", "ofl_wavg_delta_points", "ofl_apply_delta",
     "ofl_apply_delta_ranges", "ofl_sub_f32_f64",
     "ofl_gzip_last_error", "ofl_gzip_ranks_workspace_bytes", "ofl_gzip_ranks_bound", "ofl_gzip_ranks",
-    "ofl_gunzip_members",
+    "ofl_gunzip_members", "ofl_gzip_member_index", "ofl_inflate_members",
 )
 
 
@@ -147,6 +147,10 @@ def _bind(L):
     L.ofl_gzip_ranks.restype = i32
     L.ofl_gunzip_members.argtypes = [vp, sz, vp, sz, vp, i32]
     L.ofl_gunzip_members.restype = i32
+    L.ofl_gzip_member_index.argtypes = [vp, sz, vp, i64, vp, vp, vp]
+    L.ofl_gzip_member_index.restype = i32
+    L.ofl_inflate_members.argtypes = [vp, vp, i64, ctypes.c_uint32, vp, sz, vp, sz, vp]
+    L.ofl_inflate_members.restype = i32
     L.ofl_serial_sum_f32.argtypes = [vp, i64]
     L.ofl_serial_sum_f32.restype = ctypes.c_float
     L.ofl_serial_sum_f64.argtypes = [vp, i64]

@@ -25,6 +25,8 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -76,7 +78,7 @@ struct Smem {
         uint32_t key[kTok];                // then: (3-token key << 12 | position), sorted
         HScratch h;                        // then: Huffman scratch
     } u;
-    uint8_t tk[kTok + 64];                 // the member's tokens
+    alignas(16) uint8_t tk[kTok + 64];     // the member's tokens
     uint8_t bestL[kTok];                   // longest earlier match at a position (tokens, 0 = none >= 3)
     uint16_t bestG[kTok];                  // and its distance in tokens
     uint8_t op[kTok];                      // parse: 0 covered, 1 one-token op, 2 match start
@@ -85,7 +87,7 @@ struct Smem {
     uint8_t ll[kLit], ld[kDist], lc[kCL];
     uint16_t kl[kLit], kd[kDist], kc[kCL];  // bit-reversed canonical codes
     uint32_t scan[kNT / 64];
-    uint32_t crc_r[kNT], crc_n[kNT];
+    uint32_t crc_r[kNT / 64];               // per wave: XOR of its lanes' advanced raw CRCs
     uint32_t hdr_bits, total_bits, nrle, nlit_ndist;
     int bad;
 };
@@ -98,20 +100,38 @@ DEVI void put_bits(uint32_t* out, uint32_t pos, uint32_t val, int nb) {
     if (sh + (uint32_t)nb > 32u) atomicOr(&out[w + 1], val >> (32u - sh));
 }
 DEVI uint32_t rev_bits(uint32_t c, int n) { return __brev(c) >> (32 - n); }
+// distance code of a distance d in 1..32768 (RFC 1951 3.2.5): codes 0..3 are
+// d - 1, then two codes per power of two
 DEVI int dist_code(uint32_t d) {
-    int c = 29;
-    while (c > 0 && c_dbase[c] > d) --c;
-    return c;
+    if (d <= 4u) return (int)d - 1;
+    const uint32_t m = d - 1u;
+    const int b = 31 - __builtin_clz(m);
+    return 2 * b + (int)((m >> (b - 1)) & 1u);
 }
-DEVI int len_code(uint32_t l) {  // index into c_lbase (symbol 257 + index) for a length of l bytes
-    int c = 28;
-    while (c > 0 && c_lbase[c] > l) --c;
-    return c;
+// index into c_lbase (symbol 257 + index) of a length of l bytes, 3..258
+DEVI int len_code(uint32_t l) {
+    if (l == 258u) return 28;
+    const uint32_t m = l - 3u;
+    if (m < 8u) return (int)m;
+    const int b = 31 - __builtin_clz(m);
+    return 4 * (b - 1) + (int)((m >> (b - 2)) & 3u);
+}
+// 4 tokens at token offset o (tk is 4-byte aligned and padded)
+DEVI uint32_t tk4(const uint8_t* tk, int o) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(tk);
+    return __builtin_amdgcn_alignbyte(w[(o >> 2) + 1], w[o >> 2], (uint32_t)(o & 3));
 }
 constexpr int kMinMatch = 3;    // tokens (12 bytes); shorter runs use the one-token op
 constexpr int kMaxMatch = 64;   // tokens (256 of deflate's 258 bytes)
 constexpr int kCand = 8;        // nearest earlier positions with the same 3-token key tried (32: ratio 0.1381 vs 0.1386, 15 % slower)
 
+// advance by 2^k zero bytes (k uniform: the matrix columns are scalar loads)
+DEVI uint32_t crc_adv_pow2(uint32_t v, int k) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) r ^= ((v >> i) & 1u) ? c_adv[k][i] : 0u;
+    return r;
+}
 DEVI uint32_t crc_adv(uint32_t v, uint32_t len) {
     for (int k = 0; k < 17; ++k)
         if ((len >> k) & 1u) {
@@ -291,7 +311,13 @@ struct GzArgs {
     uint8_t* slots;      // [members][kOutBytes]
     uint32_t* sizes;     // [members]
     int* bad;            // set if a value is not a rank 0..31
+    uint64_t* phases;    // diagnostics (OFL_GZ_PHASES): thread 0 of blocks 0..3 stamps each phase; else null
 };
+constexpr int kPhases = 12;
+#define GZ_STAMP(k)                                                                       \
+    do {                                                                                  \
+        if (a.phases && tid == 0 && blockIdx.x < 4) a.phases[blockIdx.x * kPhases + (k)] = wall_clock64(); \
+    } while (0)
 
 __global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -300,6 +326,7 @@ __global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
     const int64_t c = a.chunk0 + blockIdx.x;
     const int64_t e0 = c * kTok;
     const int ntok = (int)std::min<int64_t>(kTok, a.n - e0);
+    GZ_STAMP(0);
     for (int i = tid; i < kOutWords; i += kNT) S.out[i] = 0;
     for (int i = tid; i < 256; i += kNT) {
         uint32_t r = (uint32_t)i;
@@ -338,13 +365,31 @@ __global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
         }
     }
     if (bad) atomicOr(&S.bad, 1);
-    S.crc_r[tid] = crc;
-    S.crc_n[tid] = 4u * (uint32_t)nv;
+    // raw CRC of the member: crc(A | B) = adv(crc(A), |B|) ^ crc(B)
+    if (ntok == kTok) {
+        // full member, 64 bytes per thread: a tree over the lanes whose level-l
+        // shift (64 * 2^l bytes) is the same for every lane (scalar matrix)
+        const int lane = tid & 63;
+        uint32_t v = crc;
+#pragma unroll
+        for (int l = 0; l < 6; ++l) {
+            const uint32_t o = (uint32_t)__shfl_xor((int)v, 1 << l, 64);
+            const uint32_t sh = crc_adv_pow2(v, 6 + l);  // adv over 2^(6+l) bytes
+            // the lower lane of a pair holds the earlier bytes
+            v = (lane & (1 << l)) ? v : (sh ^ o);
+        }
+        if (lane == 0) S.crc_r[tid >> 6] = v;
+    } else {  // ragged last member: each thread advances over the bytes after it
+        uint32_t v = crc_adv(crc, 4u * (uint32_t)std::max(0, ntok - i0 - nv));
+        for (int o = 32; o > 0; o >>= 1) v ^= (uint32_t)__shfl_xor((int)v, o, 64);
+        if ((tid & 63) == 0) S.crc_r[tid >> 6] = v;
+    }
     __syncthreads();
     if (S.bad) {  // block-uniform
         if (tid == 0) { atomicOr(a.bad, 1); a.sizes[blockIdx.x] = 0; }
         return;
     }
+    GZ_STAMP(1);
     // exclusive prefix max of the per-thread last indices, per type (in place):
     // thread (type t, part p) walks rows 32p..32p+31, then parts are combined
     {
@@ -371,27 +416,68 @@ __global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
         }
     }
     __syncthreads();  // the last-occurrence tables are dead from here
+    GZ_STAMP(2);
     // ---- LZ77 at token granularity: sort (3-token key, position) ----
+    // Bitonic network over index tid * kPer + q with the keys in registers:
+    // partners < kPer apart are in the same thread, < 64 kPer apart in the
+    // same wave (shfl_xor), only the 3 stages with partners 1024 / 2048 apart
+    // go through LDS.  Keys are unique (the position is in the low bits), so the
+    // order is total.
     for (int i = tid; i < kTok; i += kNT) {
-        const bool k3 = i + 2 < ntok;
-        const uint32_t key = k3 ? ((uint32_t)S.tk[i] | ((uint32_t)S.tk[i + 1] << 5) | ((uint32_t)S.tk[i + 2] << 10)) : 0x7fffu;
-        S.u.key[i] = (key << 12) | (uint32_t)i;
         S.bestL[i] = 0;
         S.bestG[i] = 0;
         S.op[i] = 0;
     }
-    __syncthreads();
-    for (int k = 2; k <= kTok; k <<= 1)
+    uint32_t kv[kPer];
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        const int i = i0 + q;
+        const bool k3 = i + 2 < ntok;
+        const uint32_t key = k3 ? ((uint32_t)S.tk[i] | ((uint32_t)S.tk[i + 1] << 5) | ((uint32_t)S.tk[i + 2] << 10)) : 0x7fffu;
+        kv[q] = (key << 12) | (uint32_t)i;
+    }
+#pragma unroll
+    for (int k = 2; k <= kTok; k <<= 1) {
+#pragma unroll
         for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = tid; i < kTok; i += kNT) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const uint32_t x = S.u.key[i], y = S.u.key[ixj];
-                    if ((x > y) == ((i & k) == 0)) { S.u.key[i] = y; S.u.key[ixj] = x; }
+            if (j >= 64 * kPer) {  // across waves: through LDS
+                __syncthreads();
+#pragma unroll
+                for (int q = 0; q < kPer; ++q) S.u.key[i0 + q] = kv[q];
+                __syncthreads();
+#pragma unroll
+                for (int q = 0; q < kPer; ++q) {
+                    const int i = i0 + q;
+                    const uint32_t o = S.u.key[i ^ j];
+                    const bool lower = (i & j) == 0, up = (i & k) == 0;
+                    kv[q] = (lower == up) ? min(kv[q], o) : max(kv[q], o);
+                }
+            } else if (j >= kPer) {  // across lanes of this wave
+#pragma unroll
+                for (int q = 0; q < kPer; ++q) {
+                    const int i = i0 + q;
+                    const uint32_t o = (uint32_t)__shfl_xor((int)kv[q], j / kPer, 64);
+                    const bool lower = (i & j) == 0, up = (i & k) == 0;
+                    kv[q] = (lower == up) ? min(kv[q], o) : max(kv[q], o);
+                }
+            } else {  // inside this thread
+#pragma unroll
+                for (int q = 0; q < kPer; ++q) {
+                    if ((q & j) == 0) {
+                        const bool up = ((i0 + q) & k) == 0;
+                        const uint32_t lo = min(kv[q], kv[q + j]), hi = max(kv[q], kv[q + j]);
+                        kv[q] = up ? lo : hi;
+                        kv[q + j] = up ? hi : lo;
+                    }
                 }
             }
-            __syncthreads();
         }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) S.u.key[i0 + q] = kv[q];
+    __syncthreads();
+    GZ_STAMP(3);
     // longest match among the kCand nearest earlier positions with the same key
     for (int sidx = tid; sidx < kTok; sidx += kNT) {
         const uint32_t me = S.u.key[sidx];
@@ -403,14 +489,20 @@ __global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
             const uint32_t o = S.u.key[sidx - c2];
             if ((o >> 12) != (me >> 12)) break;
             const int jj = (int)(o & 0xfffu);
-            int L = 3;
-            while (L < lim && S.tk[i + L] == S.tk[jj + L]) ++L;
+            int L = 3;  // the keys are equal: 3 tokens match
+            while (L < lim) {
+                const uint32_t d = tk4(S.tk, i + L) ^ tk4(S.tk, jj + L);
+                if (d) { L += __builtin_ctz(d) >> 3; break; }
+                L += 4;
+            }
+            L = min(L, lim);
             if (L > bl) { bl = L; bg = i - jj; }
             if (bl == lim) break;
         }
         if (bl >= kMinMatch) { S.bestL[i] = (uint8_t)bl; S.bestG[i] = (uint16_t)bg; }
     }
     __syncthreads();
+    GZ_STAMP(4);
     // greedy parse with one-step lazy matching: from position i the parse
     // moves to nxt(i) = i + L(i) if a match starts there (L(i) >= 3 and not
     // L(i+1) > L(i)), else i + 1.  In parallel: thread t's segment
@@ -427,10 +519,14 @@ __global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
             return (L >= kMinMatch && !(i + 1 < ntok && S.bestL[i + 1] > L)) ? i + L : i + 1;
         };
         const int s0 = tid * kPer, s1 = s0 + kPer;
-        for (int e = 0; e < kPer; ++e) {
-            int p = s0 + e;
-            while (p < s1 && p < ntok) p = nxt(p);
-            fent[tid][e] = (int16_t)p;
+        for (int e = kPer - 1; e >= 0; --e) {  // backwards: fent of a later entry is known
+            const int p = s0 + e;
+            int f = p;
+            if (p < ntok) {
+                const int q = nxt(p);
+                f = (q < s1 && q < ntok) ? fent[tid][q - s0] : q;
+            }
+            fent[tid][e] = (int16_t)f;
         }
         __syncthreads();
         if (tid == 0) {
@@ -447,46 +543,51 @@ __global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
             p = q;
         }
     }
-    // CRC of the member: tree of (raw crc, byte count) pairs
-    for (int st = 1; st < kNT; st <<= 1) {
-        __syncthreads();
-        if ((tid & (2 * st - 1)) == 0) {
-            S.crc_r[tid] = crc_adv(S.crc_r[tid], S.crc_n[tid + st]) ^ S.crc_r[tid + st];
-            S.crc_n[tid] += S.crc_n[tid + st];
-        }
-    }
     __syncthreads();
+    GZ_STAMP(5);
+    __syncthreads();
+    GZ_STAMP(6);
     // ---- symbol histograms of this thread's ops ----
 #pragma unroll
     for (int q = 0; q < kPer; ++q) {
-        if (q < nv) {
-            const int p = i0 + q, o = S.op[p];
-            if (o == 2) {
-                atomicAdd(&S.hl[257 + len_code(4u * S.bestL[p])], 1u);
-                atomicAdd(&S.hd[dist_code(4u * S.bestG[p])], 1u);
-            } else if (o == 1 && prev[q] > 0) {
-                atomicAdd(&S.hl[258], 1u);
-                atomicAdd(&S.hd[dist_code(4u * (uint32_t)prev[q])], 1u);
-            } else if (o == 1) {
-                const uint32_t bits = __float_as_uint((float)tok[q]);
-                for (int b = 0; b < 4; ++b) atomicAdd(&S.hl[(bits >> (8 * b)) & 0xffu], 1u);
-            }
-        }
+        const int p = i0 + q, o = q < nv ? S.op[p] : 0;
+        const bool match = o == 2, copy = o == 1 && prev[q] > 0, lit = o == 1 && !copy;
+        const uint32_t bits = __float_as_uint((float)tok[q]);
+        const int sa = match ? 257 + len_code(4u * S.bestL[p]) : copy ? 258 : (int)(bits & 0xffu);
+        const int sd = dist_code(match ? 4u * S.bestG[p] : copy ? 4u * (uint32_t)prev[q] : 1u);
+        // the one-token copy (symbol 258) is most positions' op: counted by
+        // ballot; the rest by LDS atomics
+        const uint64_t nc = __ballot(copy);
+        if ((tid & 63) == 0 && nc) atomicAdd(&S.hl[258], (uint32_t)__popcll(nc));
+        if (o != 0 && !copy) atomicAdd(&S.hl[sa], 1u);
+        if (match || copy) atomicAdd(&S.hd[sd], 1u);
+        if (lit)
+#pragma unroll
+            for (int b = 1; b < 4; ++b) atomicAdd(&S.hl[(bits >> (8 * b)) & 0xffu], 1u);
     }
     __syncthreads();
+    GZ_STAMP(7);
     // ---- wave 0: code lengths and codes (lane 0: the code-length RLE and the
     // header bits) ----
-    if (tid < 64) {
+    // (wave 0: literal/length code, wave 1: distance code, concurrently; the
+    // serial fallback for > 64 literal symbols uses h.w..h.dead, wave 1's
+    // scratch is h.rle_ext, free until the RLE below)
+    const int wv = tid >> 6, ln = tid & 63;
+    if (wv == 0) {
         HScratch& h = S.u.h;
-        if (tid == 0) S.hl[256] = 1;  // end of block
-        if (!huff_lengths_wave(S.hl, kLit, 15, S.ll, h.w, true) && tid == 0) huff_lengths(S.hl, kLit, 15, S.ll, h, true);
-        if (tid == 0) {
-            bool anyd = false;
-            for (int i = 0; i < kDist; ++i) anyd = anyd || S.hd[i];
-            if (!anyd) S.hd[0] = 1;  // one (unused) distance code
-        }
-        if (!huff_lengths_wave(S.hd, kDist, 15, S.ld, h.w, false) && tid == 0) huff_lengths(S.hd, kDist, 15, S.ld, h, false);
+        if (ln == 0) S.hl[256] = 1;  // end of block
+        __builtin_amdgcn_wave_barrier();
+        if (!huff_lengths_wave(S.hl, kLit, 15, S.ll, h.w, true) && ln == 0) huff_lengths(S.hl, kLit, 15, S.ll, h, true);
+    } else if (wv == 1) {
+        HScratch& h = S.u.h;
+        const bool anyd = __ballot(ln < kDist && S.hd[ln] != 0u) != 0ull;
+        if (!anyd && ln == 0) S.hd[0] = 1;  // one (unused) distance code
+        __builtin_amdgcn_wave_barrier();
+        huff_lengths_wave(S.hd, kDist, 15, S.ld, reinterpret_cast<uint32_t*>(h.rle_ext), false);  // <= 30 symbols
     }
+    __syncthreads();
+    if (wv == 1) huff_codes_wave(S.ll, kLit, S.kl);
+    if (wv == 2) huff_codes_wave(S.ld, kDist, S.kd);
     if (tid == 0) {
         HScratch& h = S.u.h;
         int nlit = kLit;
@@ -516,12 +617,10 @@ __global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
         S.nrle = (uint32_t)nr;
         S.nlit_ndist = (uint32_t)(nlit | (ndist << 16));
     }
-    if (tid < 64) {
+    __syncthreads();
+    if (wv == 0) {
         HScratch& h = S.u.h;
-        if (!huff_lengths_wave(S.hc, kCL, 7, S.lc, h.w + 2 * kLit - 64, true) && tid == 0)
-            huff_lengths(S.hc, kCL, 7, S.lc, h, true);
-        huff_codes_wave(S.ll, kLit, S.kl);
-        huff_codes_wave(S.ld, kDist, S.kd);
+        huff_lengths_wave(S.hc, kCL, 7, S.lc, h.w, true);  // <= 19 symbols
         huff_codes_wave(S.lc, kCL, S.kc);
     }
     if (tid == 0) {
@@ -551,6 +650,7 @@ __global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
         S.hdr_bits = pos;
     }
     __syncthreads();
+    GZ_STAMP(8);
     // ---- op bits: block scan of the costs, then OR into the buffer ----
     uint32_t mine = 0;
 #pragma unroll
@@ -581,41 +681,66 @@ __global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
     uint32_t pos = S.hdr_bits + inc - mine;
     for (int j = 0; j < w; ++j) pos += S.scan[j];
     if (tid == kNT - 1) S.total_bits = pos + mine;
+    // this thread's ops are one contiguous bit range: gather them in a 64-bit
+    // accumulator and store whole words; only the first and the last word
+    // can be shared with a neighbour (OR-ed atomically)
+    {
+        uint64_t acc = 0;
+        int nb = (int)(pos & 31u);
+        uint32_t wi = pos >> 5;
+        bool first = true;
+        auto put = [&](uint32_t v, int n) {
+            acc |= (uint64_t)v << nb;
+            nb += n;
+            if (nb >= 32) {
+                if (first) { atomicOr(&S.out[wi], (uint32_t)acc); first = false; }
+                else S.out[wi] = (uint32_t)acc;
+                ++wi;
+                acc >>= 32;
+                nb -= 32;
+            }
+        };
 #pragma unroll
-    for (int q = 0; q < kPer; ++q) {
-        if (q < nv) {
-            const int p = i0 + q, o = S.op[p];
-            if (o == 2) {
-                const uint32_t l = 4u * S.bestL[p], d = 4u * S.bestG[p];
-                const int lc = len_code(l), dc = dist_code(d);
-                put_bits(S.out, pos, S.kl[257 + lc], S.ll[257 + lc]); pos += S.ll[257 + lc];
-                put_bits(S.out, pos, l - c_lbase[lc], c_lext[lc]); pos += c_lext[lc];
-                put_bits(S.out, pos, S.kd[dc], S.ld[dc]); pos += S.ld[dc];
-                put_bits(S.out, pos, d - c_dbase[dc], c_dext[dc]); pos += c_dext[dc];
-            } else if (o == 1 && prev[q] > 0) {
-                const uint32_t d = 4u * (uint32_t)prev[q];
-                const int dc = dist_code(d);
-                put_bits(S.out, pos, S.kl[258], S.ll[258]); pos += S.ll[258];
-                put_bits(S.out, pos, S.kd[dc], S.ld[dc]); pos += S.ld[dc];
-                put_bits(S.out, pos, d - c_dbase[dc], c_dext[dc]); pos += c_dext[dc];
-            } else if (o == 1) {
-                const uint32_t bits = __float_as_uint((float)tok[q]);
-                for (int b = 0; b < 4; ++b) {
-                    const uint32_t by = (bits >> (8 * b)) & 0xffu;
-                    put_bits(S.out, pos, S.kl[by], S.ll[by]); pos += S.ll[by];
+        for (int q = 0; q < kPer; ++q) {
+            if (q < nv) {
+                const int p = i0 + q, o = S.op[p];
+                if (o == 2) {
+                    const uint32_t l = 4u * S.bestL[p], d = 4u * S.bestG[p];
+                    const int lc = len_code(l), dc = dist_code(d);
+                    put(S.kl[257 + lc], S.ll[257 + lc]);
+                    put(l - c_lbase[lc], c_lext[lc]);
+                    put(S.kd[dc], S.ld[dc]);
+                    put(d - c_dbase[dc], c_dext[dc]);
+                } else if (o == 1 && prev[q] > 0) {
+                    const uint32_t d = 4u * (uint32_t)prev[q];
+                    const int dc = dist_code(d);
+                    put(S.kl[258], S.ll[258]);
+                    put(S.kd[dc], S.ld[dc]);
+                    put(d - c_dbase[dc], c_dext[dc]);
+                } else if (o == 1) {
+                    const uint32_t bits = __float_as_uint((float)tok[q]);
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        const uint32_t by = (bits >> (8 * b)) & 0xffu;
+                        put(S.kl[by], S.ll[by]);
+                    }
                 }
             }
         }
+        if (nb > 0) atomicOr(&S.out[wi], (uint32_t)acc);
     }
     __syncthreads();
+    GZ_STAMP(9);
     // ---- end of block, byte padding, CRC-32 and ISIZE ----
     if (tid == 0) {
         uint32_t p = S.total_bits;
         put_bits(S.out, p, S.kl[256], S.ll[256]); p += S.ll[256];
         p = (p + 7u) & ~7u;
-        const uint32_t crc32 = crc_adv(0xffffffffu, S.crc_n[0]) ^ S.crc_r[0] ^ 0xffffffffu;
+        uint32_t raw = 0;  // full member: waves cover 4096 bytes each; ragged: already advanced
+        for (int j = 0; j < kNT / 64; ++j) raw = (ntok == kTok ? crc_adv_pow2(raw, 12) : raw) ^ S.crc_r[j];
+        const uint32_t crc32 = crc_adv(0xffffffffu, 4u * (uint32_t)ntok) ^ raw ^ 0xffffffffu;
         put_bits(S.out, p, crc32, 32); p += 32;
-        put_bits(S.out, p, S.crc_n[0], 32); p += 32;
+        put_bits(S.out, p, 4u * (uint32_t)ntok, 32); p += 32;
         S.total_bits = p;
         put_bits(S.out, 8 * (kHdr - 2), (p >> 3) - 1u, 16);  // BSIZE
         a.sizes[blockIdx.x] = p >> 3;
@@ -624,6 +749,7 @@ __global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
     const uint32_t nbytes = S.total_bits >> 3;
     uint32_t* dst = reinterpret_cast<uint32_t*>(a.slots + (int64_t)blockIdx.x * kOutBytes);
     for (uint32_t i = tid; i < (nbytes + 3u) / 4u; i += kNT) dst[i] = S.out[i];
+    GZ_STAMP(10);
 }
 
 // exclusive scan of the member sizes (one block) -> offsets, total at [n]
@@ -655,6 +781,342 @@ __global__ __launch_bounds__(256) void k_gzip_pack(const uint8_t* slots, const u
     for (uint32_t i = threadIdx.x; i < sizes[blockIdx.x]; i += 256) dst[i] = src[i];
 }
 
+
+// ============================================================================
+// Device inflate of member-indexed streams (GZIPTransformer.backward,
+// kc_pipeline.py:152-156: gzip.decompress).  One wavefront per member; the
+// Huffman decode is inherently serial, so every lane runs it on the same
+// (wave-uniform) values and the lanes split the work that is parallel: table
+// construction, each copy's bytes (an overlapping copy d < L is the periodic
+// extension out[p + i] = out[p - d + i % d]), the CRC-32 and the store.  The
+// member's output (its window, <= WIN bytes) stays in LDS until it is
+// complete; the compressed bytes stream through a small LDS ring.  Any valid
+// deflate data decodes (stored, fixed and dynamic blocks, RFC 1951); every
+// member's ISIZE and CRC-32 are checked.
+constexpr int kRing = 1024;                // compressed-input ring per wave (bytes)
+constexpr int kFastBits = 9;               // first-level decode table: codes of <= 9 bits
+constexpr int kFast = 1 << kFastBits;
+
+struct InfCode {                           // one canonical Huffman code
+    uint16_t fast[kFast];                  // (symbol << 4) | length; 0: longer (or unused) code
+    uint16_t cnt[16];                      // codes per length
+    uint16_t sorted[288];                  // symbols ordered by (length, symbol)
+};
+template <int WIN>
+struct InfSmem {
+    uint8_t win[WIN];                      // the member's output
+    alignas(4) uint8_t ring[kRing];
+    InfCode lit, dist;
+    uint8_t lens[320];                     // code lengths (literal/length | distance)
+    uint32_t crct[256];
+};
+
+struct InfArgs {
+    const uint8_t* src;                    // device copy of the stream
+    const int64_t* idx;                    // per member: data offset, data length, output offset, isize | crc << 32
+    int64_t nmem;
+    uint8_t* out;
+    uint64_t out_cap;
+    int* status;                           // OR of OFL_INF_* flags over the members
+};
+constexpr int kInfCorrupt = 1, kInfSize = 2, kInfCrc = 4, kInfRange = 8;
+
+// base value and extra-bit count of a length code c (0..28) / a distance code
+// c (0..29), RFC 1951 3.2.5, in closed form
+DEVI uint32_t len_base(int c, int& ext) {
+    if (c < 8) { ext = 0; return 3u + (uint32_t)c; }
+    if (c == 28) { ext = 0; return 258u; }
+    ext = (c >> 2) - 1;
+    return ((4u + (uint32_t)(c & 3)) << ext) + 3u;
+}
+DEVI uint32_t dist_base(int c, int& ext) {
+    if (c < 4) { ext = 0; return 1u + (uint32_t)c; }
+    ext = (c >> 1) - 1;
+    return ((2u + (uint32_t)(c & 1)) << ext) + 1u;
+}
+
+// canonical code from lengths (wave-parallel): counts and ranks by ballots,
+// the fast table filled by the symbols' lanes.  false: over-subscribed.
+DEVI bool inf_build(InfCode& c, const uint8_t* lens, int n) {
+    const int lane = (int)(threadIdx.x & 63u);
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (int k = lane; k < kFast; k += 64) c.fast[k] = 0;
+    uint32_t cnt[16];
+#pragma unroll
+    for (int b = 0; b < 16; ++b) cnt[b] = 0;
+    for (int base = 0; base < n; base += 64) {
+        const int s = base + lane;
+        const int L = s < n ? lens[s] : 0;
+#pragma unroll
+        for (int b = 1; b < 16; ++b) cnt[b] += (uint32_t)__popcll(__ballot(L == b));
+    }
+    int left = 1;
+#pragma unroll
+    for (int b = 1; b < 16; ++b) { left = (left << 1) - (int)cnt[b]; if (left < 0) return false; }
+    if (lane < 16) c.cnt[lane] = (uint16_t)(lane ? cnt[lane] : 0u);
+    uint32_t off[16], next[16];
+    uint32_t o = 0, code = 0;
+#pragma unroll
+    for (int b = 1; b < 16; ++b) {
+        off[b] = o;
+        o += cnt[b];
+        code = (code + (b > 1 ? cnt[b - 1] : 0u)) << 1;
+        next[b] = code;
+    }
+    for (int base = 0; base < n; base += 64) {
+        const int s = base + lane;
+        const int L = s < n ? lens[s] : 0;
+        uint32_t my_off = 0, my_code = 0;
+#pragma unroll
+        for (int b = 1; b < 16; ++b) {
+            const uint64_t mk = __ballot(L == b);
+            if (L == b) {
+                const uint32_t r = (uint32_t)__popcll(mk & below);
+                my_off = off[b] + r;
+                my_code = next[b] + r;
+            }
+            off[b] += (uint32_t)__popcll(mk);
+            next[b] += (uint32_t)__popcll(mk);
+        }
+        if (L) {
+            c.sorted[my_off] = (uint16_t)s;
+            if (L <= kFastBits)
+                for (uint32_t k = rev_bits(my_code, L); k < (uint32_t)kFast; k += 1u << L)
+                    c.fast[k] = (uint16_t)((s << 4) | L);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    return true;
+}
+
+// one symbol (needs >= 15 bits in bb); -1 if the bits are no code
+DEVI int inf_decode(const InfCode& c, uint64_t& bb, int& bc) {
+    const uint32_t e = c.fast[bb & (uint64_t)(kFast - 1)];
+    if (e & 15u) {
+        const int l = (int)(e & 15u);
+        bb >>= l;
+        bc -= l;
+        return (int)(e >> 4);
+    }
+    // canonical walk: codes are sent most significant bit first
+    int code = 0, first = 0, index = 0;
+    for (int len = 1; len <= 15; ++len) {
+        code |= (int)(bb & 1u);
+        bb >>= 1;
+        --bc;
+        const int n = c.cnt[len];
+        if (code - first < n) return c.sorted[index + code - first];
+        index += n;
+        first = (first + n) << 1;
+        code <<= 1;
+    }
+    return -1;
+}
+
+template <int WIN>
+__global__ __launch_bounds__(64) void k_inflate_members(InfArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    InfSmem<WIN>& S = *reinterpret_cast<InfSmem<WIN>*>(smem_raw);
+    const int lane = threadIdx.x;
+    const int64_t m = blockIdx.x;
+    if (m >= a.nmem) return;
+    const int64_t* ix = a.idx + 4 * m;
+    const uint8_t* src = a.src + ix[0];
+    const uint32_t in_len = (uint32_t)ix[1];
+    const int64_t out_off = ix[2];
+    const uint32_t isize = (uint32_t)((uint64_t)ix[3] & 0xffffffffu), want_crc = (uint32_t)((uint64_t)ix[3] >> 32);
+    if (isize > (uint32_t)WIN || out_off < 0 || (uint64_t)out_off + isize > a.out_cap) {
+        if (lane == 0) atomicOr(a.status, kInfRange);
+        return;
+    }
+    for (int i = lane; i < 256; i += 64) {
+        uint32_t r = (uint32_t)i;
+        for (int k = 0; k < 8; ++k) r = (r & 1u) ? (r >> 1) ^ 0xEDB88320u : r >> 1;
+        S.crct[i] = r;
+    }
+    // bit reader: bb holds bc bits; pos = next ring byte; the ring holds [fill - kRing, fill)
+    uint64_t bb = 0;
+    int bc = 0;
+    uint32_t pos = 0, fill = 0;
+    auto refill = [&]() {  // the next kRing / 2 bytes (zeros past the end)
+        for (int k = lane; k < kRing / 2; k += 64) {
+            const uint32_t g = fill + (uint32_t)k;
+            S.ring[g & (kRing - 1)] = g < in_len ? src[g] : 0;
+        }
+        fill += kRing / 2;
+        __builtin_amdgcn_wave_barrier();
+    };
+    auto topup = [&]() {  // >= 33 bits in bb
+        while (bc <= 32) {
+            if (pos + 8u > fill) refill();
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(S.ring);
+            const uint32_t q = (pos & (kRing - 1)) >> 2;
+            const uint32_t v = __builtin_amdgcn_alignbyte(w[(q + 1) & (kRing / 4 - 1)], w[q], pos & 3u);
+            bb |= (uint64_t)v << bc;
+            bc += 32;
+            pos += 4;
+        }
+    };
+    auto bits = [&](int n) -> uint32_t {  // n <= 32 - 0 and bb holds >= n bits
+        const uint32_t v = (uint32_t)(bb & ((1ull << n) - 1ull));
+        bb >>= n;
+        bc -= n;
+        return v;
+    };
+    int err = 0;
+    uint32_t p = 0;  // output bytes so far
+    bool last = false;
+    while (!last && !err) {
+        if (pos > in_len + 16u) { err = kInfCorrupt; break; }  // past the data (zeros)
+        topup();
+        last = bits(1) != 0;
+        const int type = (int)bits(2);
+        if (type == 0) {  // stored: byte-align, LEN, NLEN, raw bytes
+            bits(bc & 7);
+            topup();
+            const uint32_t len = bits(16), nlen = bits(16);
+            if ((len ^ 0xffffu) != nlen || p + len > isize) { err = kInfCorrupt; break; }
+            pos -= (uint32_t)(bc >> 3);  // hand the buffered whole bytes back to the ring
+            bb = 0;
+            bc = 0;
+            uint32_t left = len;
+            while (left) {
+                if (pos + 64u > fill) refill();
+                const uint32_t ch = min(left, 64u);
+                if ((uint32_t)lane < ch) S.win[p + lane] = S.ring[(pos + lane) & (kRing - 1)];
+                __builtin_amdgcn_wave_barrier();
+                p += ch;
+                pos += ch;
+                left -= ch;
+            }
+            continue;
+        }
+        if (type == 3) { err = kInfCorrupt; break; }
+        if (type == 1) {  // fixed codes (RFC 1951 3.2.6)
+            for (int i = lane; i < 320; i += 64)
+                S.lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : i < 288 ? 8 : 5;
+            __builtin_amdgcn_wave_barrier();
+            inf_build(S.lit, S.lens, 288);
+            inf_build(S.dist, S.lens + 288, 30);
+        } else {  // dynamic: code-length code, then the literal/length and distance lengths
+            topup();
+            const int nlit = (int)bits(5) + 257, ndist = (int)bits(5) + 1, ncl = (int)bits(4) + 4;
+            if (nlit > 286 || ndist > 30) { err = kInfCorrupt; break; }
+            for (int i = lane; i < 19; i += 64) S.lens[i] = 0;
+            __builtin_amdgcn_wave_barrier();
+            for (int i = 0; i < ncl; ++i) {
+                topup();
+                const uint32_t v = bits(3);
+                if (lane == 0) S.lens[c_clord[i]] = (uint8_t)v;
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (!inf_build(S.lit, S.lens, 19)) { err = kInfCorrupt; break; }
+            const int total = nlit + ndist;
+            int i = 0;
+            while (i < total) {
+                topup();
+                const int sy = inf_decode(S.lit, bb, bc);
+                if (sy < 0) { err = kInfCorrupt; break; }
+                if (sy < 16) {
+                    if (lane == 0) S.lens[i] = (uint8_t)sy;
+                    ++i;
+                    continue;
+                }
+                int rep, val = 0;
+                if (sy == 16) {
+                    if (i == 0) { err = kInfCorrupt; break; }
+                    val = S.lens[i - 1];
+                    rep = 3 + (int)bits(2);
+                } else if (sy == 17) {
+                    rep = 3 + (int)bits(3);
+                } else {
+                    rep = 11 + (int)bits(7);
+                }
+                if (i + rep > total) { err = kInfCorrupt; break; }
+                __builtin_amdgcn_wave_barrier();
+                for (int k = lane; k < rep; k += 64) S.lens[i + k] = (uint8_t)val;
+                __builtin_amdgcn_wave_barrier();
+                i += rep;
+            }
+            if (err) break;
+            __builtin_amdgcn_wave_barrier();
+            if (S.lens[256] == 0) { err = kInfCorrupt; break; }
+            // the distance lengths move out of the literal range before the builds
+            uint8_t dl = lane < ndist ? S.lens[nlit + lane] : 0;
+            __builtin_amdgcn_wave_barrier();
+            for (int k = nlit + lane; k < 288; k += 64) S.lens[k] = 0;
+            __builtin_amdgcn_wave_barrier();
+            if (lane < 32) S.lens[288 + lane] = lane < ndist ? dl : 0;
+            __builtin_amdgcn_wave_barrier();
+            if (!inf_build(S.lit, S.lens, nlit) || !inf_build(S.dist, S.lens + 288, ndist)) { err = kInfCorrupt; break; }
+        }
+        // symbols of the block
+        for (;;) {
+            topup();
+            const int sy = inf_decode(S.lit, bb, bc);
+            if (sy < 0) { err = kInfCorrupt; break; }
+            if (sy < 256) {
+                if (p >= isize) { err = kInfSize; break; }
+                if (lane == 0) S.win[p] = (uint8_t)sy;
+                ++p;
+                continue;
+            }
+            if (sy == 256) break;
+            if (sy > 285) { err = kInfCorrupt; break; }
+            int le, de;
+            const uint32_t len = len_base(sy - 257, le) + bits(le);
+            topup();
+            const int ds = inf_decode(S.dist, bb, bc);
+            if (ds < 0 || ds > 29) { err = kInfCorrupt; break; }
+            const uint32_t d = dist_base(ds, de) + bits(de);
+            if (d > p) { err = kInfCorrupt; break; }
+            if (p + len > isize) { err = kInfSize; break; }
+            __builtin_amdgcn_wave_barrier();
+            if (d >= len) {
+                for (uint32_t k = lane; k < len; k += 64) S.win[p + k] = S.win[p - d + k];
+            } else {
+                for (uint32_t k = lane; k < len; k += 64) S.win[p + k] = S.win[p - d + k % d];
+            }
+            __builtin_amdgcn_wave_barrier();
+            p += len;
+        }
+    }
+    // every byte of the deflate data used, none past it; the whole ISIZE produced
+    if (!err && (pos - (uint32_t)(bc >> 3) != in_len)) err = kInfCorrupt;
+    if (!err && p != isize) err = kInfSize;
+    if (err) {
+        if (lane == 0) atomicOr(a.status, err);
+        return;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // CRC-32: the output as the tail of 64 * Sg bytes whose leading zeros do
+    // not change a zero-initialised CRC; lane l takes bytes [l Sg, (l+1) Sg)
+    // of that, then a tree with the same shift per level for every lane
+    int lg = 0;
+    while ((64u << lg) < isize) ++lg;
+    const int sg = 1 << lg;
+    const int a0 = lane * sg - (int)((64u << lg) - isize);
+    uint32_t r = 0;
+    for (int i = max(a0, 0); i < a0 + sg; ++i) r = S.crct[(r ^ S.win[i]) & 0xffu] ^ (r >> 8);
+#pragma unroll
+    for (int l = 0; l < 6; ++l) {
+        const uint32_t o = (uint32_t)__shfl_xor((int)r, 1 << l, 64);
+        const uint32_t sh = crc_adv_pow2(r, lg + l);
+        r = (lane & (1 << l)) ? r : (sh ^ o);
+    }
+    const uint32_t crc = crc_adv(0xffffffffu, isize) ^ (uint32_t)__shfl((int)r, 0, 64) ^ 0xffffffffu;
+    if (crc != want_crc) {
+        if (lane == 0) atomicOr(a.status, kInfCrc);
+        return;
+    }
+    uint8_t* dst = a.out + out_off;
+    if (((out_off | (int64_t)isize) & 3) == 0) {
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(S.win);
+        for (uint32_t i = lane; i < isize / 4u; i += 64) reinterpret_cast<uint32_t*>(dst)[i] = w[i];
+    } else {
+        for (uint32_t i = lane; i < isize; i += 64) dst[i] = S.win[i];
+    }
+}
 }  // namespace gz
 
 namespace {
@@ -682,6 +1144,39 @@ void crc_matrices(uint32_t (&m)[17][32]) {
     };
     for (int k = 1; k < 17; ++k)
         for (int i = 0; i < 32; ++i) m[k][i] = apply(m[k - 1], apply(m[k - 1], 1u << i));
+}
+// the members of a member-indexed stream (every header carries the 'BC'
+// size field): deflate data range, output offset, ISIZE and CRC-32 of each
+struct GzMember { size_t in, in_len, out; uint32_t isize, crc; };
+int parse_members(const uint8_t* src, size_t n, std::vector<GzMember>& mem, size_t& total) {
+    size_t pos = 0;
+    total = 0;
+    mem.clear();
+    while (pos < n) {
+        const uint8_t* h = src + pos;
+        if (n - pos < 26 || h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || h[3] != 0x04)
+            return gzfail(OFL_EFORMAT, "gunzip: not a member-indexed gzip stream");
+        const size_t xlen = (size_t)h[10] | ((size_t)h[11] << 8);
+        size_t bsize = 0;
+        for (size_t q = 12; q + 4 <= 12 + xlen && 12 + xlen <= n - pos;) {
+            const size_t sl = (size_t)h[q + 2] | ((size_t)h[q + 3] << 8);
+            if (h[q] == 'B' && h[q + 1] == 'C' && sl == 2) bsize = ((size_t)h[q + 4] | ((size_t)h[q + 5] << 8)) + 1;
+            q += 4 + sl;
+        }
+        if (bsize < 12 + xlen + 8 || bsize > n - pos)
+            return gzfail(OFL_EFORMAT, "gunzip: not a member-indexed gzip stream");
+        const uint8_t* t = src + pos + bsize - 8;
+        GzMember m;
+        m.in = pos + 12 + xlen;
+        m.in_len = bsize - 12 - xlen - 8;
+        m.crc = (uint32_t)t[0] | ((uint32_t)t[1] << 8) | ((uint32_t)t[2] << 16) | ((uint32_t)t[3] << 24);
+        m.isize = (uint32_t)t[4] | ((uint32_t)t[5] << 8) | ((uint32_t)t[6] << 16) | ((uint32_t)t[7] << 24);
+        m.out = total;
+        total += m.isize;
+        mem.push_back(m);
+        pos += bsize;
+    }
+    return OFL_OK;
 }
 }  // namespace
 
@@ -722,10 +1217,16 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
     uint64_t* off = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(sizes) + ((4 * (size_t)batch + 7) & ~(size_t)7));
     int* bad = reinterpret_cast<int*>(off + batch + 1);
     GZHIP(hipMemsetAsync(bad, 0, sizeof(int), st));
+    // diagnostics: OFL_GZ_PHASES=1 prints the phase stamps (10 ns ticks) of
+    // blocks 0..3 of the first launch to stderr
+    static const bool phases = getenv("OFL_GZ_PHASES") != nullptr;
+    uint64_t* d_ph = nullptr;
+    if (phases) GZHIP(hipMalloc(&d_ph, 8 * 4 * gz::kPhases));
+    if (phases) GZHIP(hipMemsetAsync(d_ph, 0, 8 * 4 * gz::kPhases, st));
     size_t total = 0;
     for (int64_t c0 = 0; c0 < members; c0 += batch) {
         const int nb = (int)std::min<int64_t>(batch, members - c0);
-        gz::GzArgs a{x, n, c0, slots, sizes, bad};
+        gz::GzArgs a{x, n, c0, slots, sizes, bad, c0 == 0 ? d_ph : nullptr};
         hipLaunchKernelGGL(gz::k_gzip_members, dim3(nb), dim3(gz::kNT), sizeof(gz::Smem), st, a);
         hipLaunchKernelGGL(gz::k_gzip_scan, dim3(1), dim3(1024), 0, st, sizes, nb, off);
         hipLaunchKernelGGL(gz::k_gzip_pack, dim3(nb), dim3(256), 0, st, slots, sizes, off, packed);
@@ -741,6 +1242,16 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
         GZHIP(hipStreamSynchronize(st));
         total += tot;
     }
+    if (d_ph) {
+        uint64_t h[4 * gz::kPhases];
+        GZHIP(hipMemcpy(h, d_ph, sizeof(h), hipMemcpyDeviceToHost));
+        GZHIP(hipFree(d_ph));
+        for (int b = 0; b < 4; ++b) {
+            fprintf(stderr, "gz phases block %d:", b);
+            for (int k = 1; k <= 10; ++k) fprintf(stderr, " %llu", (unsigned long long)(h[b * gz::kPhases + k] - h[b * gz::kPhases + k - 1]));
+            fprintf(stderr, "\n");
+        }
+    }
     *out_len = total;
     return OFL_OK;
 }
@@ -753,33 +1264,10 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
 // gzip.decompress instead; dst == nullptr only measures.
 int ofl_gunzip_members(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len, int nthreads) {
     if (!src || !out_len) return gzfail(OFL_EINVAL, "gunzip: null argument");
-    struct M { size_t in, in_len, out; uint32_t isize, crc; };
-    std::vector<M> mem;
-    size_t pos = 0, total = 0;
-    while (pos < n) {
-        const uint8_t* h = src + pos;
-        if (n - pos < 26 || h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || h[3] != 0x04)
-            return gzfail(OFL_EFORMAT, "gunzip: not a member-indexed gzip stream");
-        const size_t xlen = (size_t)h[10] | ((size_t)h[11] << 8);
-        size_t bsize = 0;
-        for (size_t q = 12; q + 4 <= 12 + xlen && 12 + xlen <= n - pos;) {
-            const size_t sl = (size_t)h[q + 2] | ((size_t)h[q + 3] << 8);
-            if (h[q] == 'B' && h[q + 1] == 'C' && sl == 2) bsize = ((size_t)h[q + 4] | ((size_t)h[q + 5] << 8)) + 1;
-            q += 4 + sl;
-        }
-        if (bsize < 12 + xlen + 8 || bsize > n - pos)
-            return gzfail(OFL_EFORMAT, "gunzip: not a member-indexed gzip stream");
-        const uint8_t* t = src + pos + bsize - 8;
-        M m;
-        m.in = pos + 12 + xlen;
-        m.in_len = bsize - 12 - xlen - 8;
-        m.crc = (uint32_t)t[0] | ((uint32_t)t[1] << 8) | ((uint32_t)t[2] << 16) | ((uint32_t)t[3] << 24);
-        m.isize = (uint32_t)t[4] | ((uint32_t)t[5] << 8) | ((uint32_t)t[6] << 16) | ((uint32_t)t[7] << 24);
-        m.out = total;
-        total += m.isize;
-        mem.push_back(m);
-        pos += bsize;
-    }
+    std::vector<GzMember> mem;
+    size_t total = 0;
+    if (int rc = parse_members(src, n, mem, total)) return rc;
+    using M = GzMember;
     *out_len = total;
     if (!dst) return OFL_OK;
     if (total > cap) return gzfail(OFL_ESPACE, "gunzip: output buffer too small");
@@ -812,4 +1300,61 @@ int ofl_gunzip_members(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, s
     return OFL_OK;
 }
 
+int ofl_gzip_member_index(const uint8_t* src, size_t n, int64_t* index, int64_t cap_members, int64_t* nmembers,
+                          size_t* out_len, uint32_t* max_isize) {
+    if (!src || !nmembers || !out_len) return gzfail(OFL_EINVAL, "member index: null argument");
+    std::vector<GzMember> mem;
+    size_t total = 0;
+    if (int rc = parse_members(src, n, mem, total)) return rc;
+    *nmembers = (int64_t)mem.size();
+    *out_len = total;
+    uint32_t mx = 0;
+    for (const GzMember& m : mem) mx = std::max(mx, m.isize);
+    if (max_isize) *max_isize = mx;
+    if (!index) return OFL_OK;
+    if (cap_members < (int64_t)mem.size()) return gzfail(OFL_ESPACE, "member index: index array too small");
+    for (size_t i = 0; i < mem.size(); ++i) {
+        index[4 * i + 0] = (int64_t)mem[i].in;
+        index[4 * i + 1] = (int64_t)mem[i].in_len;
+        index[4 * i + 2] = (int64_t)mem[i].out;
+        index[4 * i + 3] = (int64_t)((uint64_t)mem[i].isize | ((uint64_t)mem[i].crc << 32));
+    }
+    return OFL_OK;
+}
+
+int ofl_inflate_members(const uint8_t* src, const int64_t* index, int64_t nmembers, uint32_t max_isize, uint8_t* out,
+                        size_t out_cap, void* ws, size_t ws_bytes, void* stream) {
+    if (nmembers < 0 || (nmembers && (!src || !index || !out))) return gzfail(OFL_EINVAL, "inflate: null argument");
+    if (!ws || ws_bytes < 256) return gzfail(OFL_ESPACE, "inflate: workspace too small (256 bytes)");
+    if (max_isize > 65536u) return gzfail(OFL_EFORMAT, "inflate: members above 64 KiB of output are not supported on the device");
+    if (nmembers == 0) return OFL_OK;
+    GZHIP(ofl_util::per_device_once([] {
+        uint32_t m[17][32];
+        crc_matrices(m);
+        hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(gz::c_adv), m, sizeof(m));
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)gz::k_inflate_members<65536>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)sizeof(gz::InfSmem<65536>));
+        return e;
+    }));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    int* status = static_cast<int*>(ws);
+    GZHIP(hipMemsetAsync(status, 0, sizeof(int), st));
+    gz::InfArgs a{src, index, nmembers, out, (uint64_t)out_cap, status};
+    if (max_isize <= 16384u)
+        hipLaunchKernelGGL(gz::k_inflate_members<16384>, dim3((unsigned)nmembers), dim3(64), sizeof(gz::InfSmem<16384>), st, a);
+    else
+        hipLaunchKernelGGL(gz::k_inflate_members<65536>, dim3((unsigned)nmembers), dim3(64), sizeof(gz::InfSmem<65536>), st, a);
+    GZHIP(hipGetLastError());
+    int h = 0;
+    GZHIP(hipMemcpyAsync(&h, status, sizeof(int), hipMemcpyDeviceToHost, st));
+    GZHIP(hipStreamSynchronize(st));
+    if (h & gz::kInfRange) return gzfail(OFL_ESPACE, "inflate: a member's output falls outside out (or above its window)");
+    if (h & gz::kInfCorrupt) return gzfail(OFL_EINVAL, "inflate: corrupt deflate data");
+    if (h & gz::kInfSize) return gzfail(OFL_EINVAL, "inflate: member size differs from its ISIZE");
+    if (h & gz::kInfCrc) return gzfail(OFL_EINVAL, "inflate: CRC-32 mismatch");
+    return OFL_OK;
+}
+
 }  // extern "C"
+

@@ -297,6 +297,66 @@ def gunzip(data, threads=8, out=None):
     return dst[:need.value]
 
 
+def _buf(device, name, nbytes, pinned=False):
+    """Thread-local scratch buffers (device, or pinned host) that only grow."""
+    bufs = getattr(_tls, "bufs", None)
+    if bufs is None:
+        bufs = _tls.bufs = {}
+    key = (str(device), name)
+    b = bufs.get(key)
+    if b is None or b.numel() < nbytes:
+        if pinned:
+            b = torch.empty(max(nbytes, 1), dtype=torch.uint8).pin_memory()
+        else:
+            b = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+        bufs[key] = b
+    return b
+
+
+@_on_device
+def gunzip_device(data, out):
+    """gzip.decompress (kc_pipeline.py:152-156) of `data` into `out`, a uint8
+    DEVICE tensor (returns the view of the decompressed bytes).  Member-indexed
+    streams (the device gzip's) inflate on the GPU (ofl_gzip_member_index on
+    the host, ofl_inflate_members: one wavefront per member, ISIZE and CRC-32
+    checked): the compressed bytes cross PCIe instead of the decompressed ones.
+    Any other gzip stream (e.g. gzip.compress output) is a different format:
+    gzip.decompress on the host, then one H2D."""
+    if not (out.is_cuda and out.dtype == torch.uint8 and out.is_contiguous()):
+        raise _lib.CodecError("gunzip_device: out must be a contiguous uint8 device tensor")
+    L = _lib.lib()
+    src = np.frombuffer(data, np.uint8)
+    nm, tot, mx = ctypes.c_int64(), ctypes.c_size_t(), ctypes.c_uint32()
+    rc = L.ofl_gzip_member_index(src.ctypes.data if src.size else None, src.size, None, 0, ctypes.byref(nm),
+                                 ctypes.byref(tot), ctypes.byref(mx)) if src.size else _lib.OFL_EFORMAT
+    if rc == _lib.OFL_EFORMAT:
+        raw = np.frombuffer(gzip.decompress(bytes(data)), np.uint8)
+        if raw.size > out.numel():
+            raise _lib.CodecError("gunzip_device: output buffer too small")
+        if raw.size:
+            out[:raw.size].copy_(torch.from_numpy(raw.copy()))
+        return out[:raw.size]
+    _lib.check_gzip(rc)
+    if tot.value > out.numel():
+        raise _lib.CodecError("gunzip_device: output buffer too small")
+    idx = np.empty((nm.value, 4), np.int64)
+    _lib.check_gzip(L.ofl_gzip_member_index(src.ctypes.data, src.size, idx.ctypes.data, nm.value, ctypes.byref(nm),
+                                            ctypes.byref(tot), ctypes.byref(mx)))
+    dev = out.device
+    ioff = (src.size + 7) // 8 * 8  # the stream, then the index, in one H2D
+    need = ioff + idx.nbytes
+    stage = _buf("host", "gz_in", need, pinned=True)
+    sn = stage.numpy()
+    sn[:src.size] = src
+    sn[ioff:need] = idx.view(np.uint8).reshape(-1)
+    d_in = _buf(dev, "gz_in", need)
+    d_in[:need].copy_(stage[:need], non_blocking=True)
+    ws = _buf(dev, "gz_status", 256)
+    _lib.check_gzip(L.ofl_inflate_members(d_in.data_ptr(), d_in.data_ptr() + ioff, nm.value, mx.value, out.data_ptr(),
+                                          out.numel(), ws.data_ptr(), ws.numel(), _stream(dev)))
+    return out[:tot.value]
+
+
 def rank_map(values):
     """_float_to_int (kc_pipeline.py:88-114): sorted unique values -> ranks.
     Returns (unique sorted values, rank index per input value)."""

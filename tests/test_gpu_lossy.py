@@ -342,6 +342,11 @@ def test_gzip_ranks_roundtrip(case):
     assert _lib.lib().ofl_gunzip_members(src.ctypes.data, src.size, None, 0, ctypes.byref(need), 4) == 0
     assert need.value == x.nbytes
     assert lossy.gunzip(z, 4).tobytes() == x.tobytes()
+    # and the device inflate (ofl_inflate_members) straight into HBM
+    out = torch.full((x.nbytes + 64,), 7, dtype=torch.uint8, device=DEV)
+    got = lossy.gunzip_device(z, out)
+    assert got.numel() == x.nbytes and got.cpu().numpy().tobytes() == x.tobytes()
+    assert int(out[x.nbytes:].eq(7).all())                            # nothing written past the data
     if case == "kc6":
         ref = len(gzip.compress(x.tobytes(), compresslevel=9))
         assert len(z) < 1.35 * ref, (len(z), ref)   # ratio 0.139 vs gzip -9 0.118
@@ -413,3 +418,59 @@ def test_ternary_stats_deterministic():
     npos, nneg, asum = runs.pop()
     assert npos == int(np.sum(x > 0)) and nneg == int(np.sum(x < 0))
     np.testing.assert_allclose(asum, np.sum(np.abs(x.astype(np.float64))), rtol=1e-12)
+
+
+@pytest.mark.parametrize("kind", ["stored", "fixed", "dynamic", "flushes", "member64k", "empty", "text"])
+def test_inflate_members_foreign_streams(kind):
+    """ofl_inflate_members decodes any member-indexed deflate data, not only
+    the device gzip's: stored, fixed and dynamic blocks, several blocks per
+    member (full flushes emit empty stored blocks), 64 KiB members, empty
+    members; the result equals gzip.decompress's."""
+    from openfl_amd import lossy
+    from tests.bgzf import member_indexed
+    rng = np.random.default_rng(sum(map(ord, kind)))
+    words = [bytes(rng.integers(97, 123, rng.integers(2, 9)).astype(np.uint8)) for _ in range(300)]
+    text = b" ".join(words[i] for i in rng.integers(0, 300, 60_000))
+    noise = rng.integers(0, 256, 50_000).astype(np.uint8).tobytes()
+    data = (text[:150_000] + noise + text[150_000:])
+    args = {"stored": dict(level=0), "fixed": dict(strategy="fixed"), "dynamic": dict(level=9),
+            "flushes": dict(level=6, flush_every=3000), "member64k": dict(level=6, chunk=65536),
+            "empty": dict(level=6, empty_members=True), "text": dict(level=1, chunk=20_000)}[kind]
+    z = member_indexed(data, **args)
+    assert gzip.decompress(z) == data
+    out = torch.zeros(len(data) + 64, dtype=torch.uint8, device=DEV)
+    got = lossy.gunzip_device(z, out)
+    assert got.cpu().numpy().tobytes() == data
+
+
+def test_inflate_members_rejects_corrupt_streams():
+    """Corrupt data fails loudly (gzip.decompress raises on the same bytes),
+    a stream without the 'BC' field decodes on the host, output too small is
+    refused."""
+    from openfl_amd import _lib, lossy
+    from tests.bgzf import member_indexed
+    data = bytes(np.random.default_rng(4).integers(0, 6, 100_000).astype(np.uint8))
+    z = member_indexed(data, level=6)
+    out = torch.zeros(len(data), dtype=torch.uint8, device=DEV)
+    assert lossy.gunzip_device(z, out).cpu().numpy().tobytes() == data
+    bad_crc = bytearray(z)
+    first = int.from_bytes(z[16:18], "little") + 1          # the first member's size
+    bad_crc[first - 8] ^= 0x5A                               # its CRC-32
+    with pytest.raises(_lib.CodecError, match="CRC"):
+        lossy.gunzip_device(bytes(bad_crc), out)
+    for off in (30, 200, first // 2):
+        bad = bytearray(z)
+        bad[off] ^= 0xFF
+        with pytest.raises((_lib.CodecError, EOFError, OSError, zlib_error())):
+            gzip.decompress(bytes(bad))
+        with pytest.raises(_lib.CodecError):
+            lossy.gunzip_device(bytes(bad), out)
+    plain = gzip.compress(data)                              # no member index: host inflate
+    assert lossy.gunzip_device(plain, out).cpu().numpy().tobytes() == data
+    with pytest.raises(_lib.CodecError, match="too small"):
+        lossy.gunzip_device(z, out[:len(data) - 1])
+
+
+def zlib_error():
+    import zlib
+    return zlib.error

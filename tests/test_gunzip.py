@@ -3,25 +3,15 @@ GZIPTransformer.backward fast path; kc_pipeline.py:152-156 gzip.decompress).
 CPU only: streams are built here with zlib in the device gzip's member format
 (RFC 1952 header with the 'BC' extra field = member size - 1)."""
 import gzip
-import struct
-import zlib
-
 import numpy as np
 import pytest
 
 from openfl_amd import _lib, lossy
-
-
-def member(raw, level=6):
-    c = zlib.compressobj(level, zlib.DEFLATED, -15)
-    body = c.compress(raw) + c.flush()
-    size = 18 + len(body) + 8
-    hdr = bytes([0x1F, 0x8B, 8, 4, 0, 0, 0, 0, 0, 0xFF]) + struct.pack("<HBBHH", 6, ord("B"), ord("C"), 2, size - 1)
-    return hdr + body + struct.pack("<II", zlib.crc32(raw) & 0xFFFFFFFF, len(raw))
+from tests.bgzf import member_indexed
 
 
 def stream(raw, chunk=16384):
-    return b"".join(member(raw[i:i + chunk]) for i in range(0, len(raw), chunk)) if raw else member(b"")
+    return member_indexed(raw, chunk=chunk)
 
 
 @pytest.mark.parametrize("n", [0, 1, 5000, 16384, 16385, 300_000])
@@ -53,3 +43,31 @@ def test_corrupt_member_raises():
     z[-8] ^= 0xFF                                  # last member's CRC-32
     with pytest.raises(_lib.CodecError):
         lossy.gunzip(bytes(z))
+
+
+def test_member_index_for_the_device_inflate():
+    """ofl_gzip_member_index (host half of ofl_inflate_members): data range,
+    output offset, ISIZE and CRC-32 of every member."""
+    import ctypes
+    import zlib
+    raw = np.random.default_rng(3).integers(0, 6, 50_000).astype(np.float32).tobytes()
+    z = member_indexed(raw, chunk=16384)
+    L = _lib.lib()
+    src = np.frombuffer(z, np.uint8)
+    nm, tot, mx = ctypes.c_int64(), ctypes.c_size_t(), ctypes.c_uint32()
+    assert L.ofl_gzip_member_index(src.ctypes.data, src.size, None, 0, ctypes.byref(nm), ctypes.byref(tot),
+                                   ctypes.byref(mx)) == 0
+    assert (nm.value, tot.value, mx.value) == (13, len(raw), 16384)
+    idx = np.zeros((nm.value, 4), np.int64)
+    assert L.ofl_gzip_member_index(src.ctypes.data, src.size, idx.ctypes.data, nm.value - 1, ctypes.byref(nm),
+                                   ctypes.byref(tot), ctypes.byref(mx)) == _lib.OFL_ESPACE
+    assert L.ofl_gzip_member_index(src.ctypes.data, src.size, idx.ctypes.data, nm.value, ctypes.byref(nm),
+                                   ctypes.byref(tot), ctypes.byref(mx)) == 0
+    for k, (off, ln, out, meta) in enumerate(idx.tolist()):
+        meta &= (1 << 64) - 1
+        part = raw[16384 * k:16384 * (k + 1)]
+        assert out == 16384 * k and (meta & 0xFFFFFFFF) == len(part) and (meta >> 32) == zlib.crc32(part)
+        assert zlib.decompress(z[off:off + ln], -15) == part
+    plain = np.frombuffer(gzip.compress(raw), np.uint8)
+    assert L.ofl_gzip_member_index(plain.ctypes.data, plain.size, None, 0, ctypes.byref(nm), ctypes.byref(tot),
+                                   ctypes.byref(mx)) == _lib.OFL_EFORMAT

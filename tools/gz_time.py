@@ -21,3 +21,26 @@ for _ in range(3):
     z = lossy.gzip_ranks(x)
 dt = (time.perf_counter() - t0) / 3
 print(f"gzip_ranks 1 GiB: {1e3 * dt:.1f} ms, {4 * n / dt / 2**30:.2f} GiB/s, ratio {len(z) / (4 * n):.4f}")
+# the pinned -> bytes copy inside gzip_ranks, timed alone on the same size
+buf = torch.empty(len(z), dtype=torch.uint8).pin_memory()
+t0 = time.perf_counter()
+for _ in range(3):
+    b = buf.numpy().tobytes()
+print(f"pinned -> bytes copy of {len(z) / 2**20:.1f} MiB: {1e3 * (time.perf_counter() - t0) / 3:.1f} ms")
+# decode: device inflate of the same stream (H2D of the compressed bytes included) vs host inflate on 16 threads
+out = torch.empty(4 * n, dtype=torch.uint8, device="cuda")
+lossy.gunzip_device(z, out)
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(3):
+    lossy.gunzip_device(z, out)
+torch.cuda.synchronize()
+dt = (time.perf_counter() - t0) / 3
+ok = torch.equal(out.view(torch.float32), x)
+print(f"gunzip_device 1 GiB: {1e3 * dt:.1f} ms, {4 * n / dt / 2**30:.2f} GiB/s, exact {ok}")
+stage = torch.empty(4 * n, dtype=torch.uint8).pin_memory()
+t0 = time.perf_counter()
+for _ in range(3):
+    lossy.gunzip(z, 16, out=stage.numpy())
+dt = (time.perf_counter() - t0) / 3
+print(f"gunzip host (16 threads) 1 GiB: {1e3 * dt:.1f} ms, {4 * n / dt / 2**30:.2f} GiB/s")
