@@ -59,7 +59,7 @@ __constant__ uint8_t c_clord[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12,
 __constant__ uint16_t c_lbase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31, 35, 43, 51, 59,
                                      67, 83, 99, 115, 131, 163, 195, 227, 258};
 __constant__ uint8_t c_lext[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-__constant__ uint32_t c_adv[17][32];       // raw CRC advance by 2^k zero bytes: GF(2) matrix columns
+__constant__ uint32_t c_adv[32][32];       // raw CRC advance by 2^k zero bytes: GF(2) matrix columns
 
 // Huffman scratch (thread 0), overlaid on the token tables once they are consumed
 struct HScratch {
@@ -133,7 +133,7 @@ DEVI uint32_t crc_adv_pow2(uint32_t v, int k) {
     return r;
 }
 DEVI uint32_t crc_adv(uint32_t v, uint32_t len) {
-    for (int k = 0; k < 17; ++k)
+    for (int k = 0; k < 32; ++k)
         if ((len >> k) & 1u) {
             uint32_t r = 0;
             for (int i = 0; i < 32; ++i) r ^= ((v >> i) & 1u) ? c_adv[k][i] : 0u;
@@ -788,12 +788,13 @@ __global__ __launch_bounds__(256) void k_gzip_pack(const uint8_t* slots, const u
 // Huffman decode is inherently serial, so every lane runs it on the same
 // (wave-uniform) values and the lanes split the work that is parallel: table
 // construction, each copy's bytes (an overlapping copy d < L is the periodic
-// extension out[p + i] = out[p - d + i % d]), the CRC-32 and the store.  The
-// member's output (its window, <= WIN bytes) stays in LDS until it is
-// complete; the compressed bytes stream through a small LDS ring.  Any valid
-// deflate data decodes (stored, fixed and dynamic blocks, RFC 1951); every
-// member's ISIZE and CRC-32 are checked.
-constexpr int kRing = 1024;                // compressed-input ring per wave (bytes)
+// extension out[p + i] = out[p - d + i % d]) and the store.  The member's
+// output stays in LDS until it is complete (WIN = 16 KiB for the device gzip's
+// members: 8 members decode per CU at once, the decode being latency-bound;
+// 64 KiB otherwise); the compressed bytes stream through a small LDS ring.
+// Any valid deflate data decodes (stored, fixed and dynamic blocks, RFC 1951).
+// ISIZE is checked here, the CRC-32 by k_crc_members over the stored output.
+constexpr int kRing = 512;                 // compressed-input ring per wave (bytes)
 constexpr int kFastBits = 9;               // first-level decode table: codes of <= 9 bits
 constexpr int kFast = 1 << kFastBits;
 
@@ -804,11 +805,10 @@ struct InfCode {                           // one canonical Huffman code
 };
 template <int WIN>
 struct InfSmem {
-    uint8_t win[WIN];                      // the member's output
+    alignas(16) uint8_t win[WIN];          // the member's output
     alignas(4) uint8_t ring[kRing];
     InfCode lit, dist;
     uint8_t lens[320];                     // code lengths (literal/length | distance)
-    uint32_t crct[256];
 };
 
 struct InfArgs {
@@ -817,7 +817,7 @@ struct InfArgs {
     int64_t nmem;
     uint8_t* out;
     uint64_t out_cap;
-    int* status;                           // OR of OFL_INF_* flags over the members
+    int* status;                           // OR of kInf* flags over the members
 };
 constexpr int kInfCorrupt = 1, kInfSize = 2, kInfCrc = 4, kInfRange = 8;
 
@@ -889,9 +889,14 @@ DEVI bool inf_build(InfCode& c, const uint8_t* lens, int n) {
     return true;
 }
 
+// wave-uniform value from LDS into a scalar register: the decode state then
+// lives in SGPRs and its arithmetic runs on the scalar unit (one wave-wide
+// VALU op per step of the serial decode would cost 4+ cycles each)
+DEVI uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
 // one symbol (needs >= 15 bits in bb); -1 if the bits are no code
 DEVI int inf_decode(const InfCode& c, uint64_t& bb, int& bc) {
-    const uint32_t e = c.fast[bb & (uint64_t)(kFast - 1)];
+    const uint32_t e = uni(c.fast[bb & (uint64_t)(kFast - 1)]);
     if (e & 15u) {
         const int l = (int)(e & 15u);
         bb >>= l;
@@ -904,8 +909,8 @@ DEVI int inf_decode(const InfCode& c, uint64_t& bb, int& bc) {
         code |= (int)(bb & 1u);
         bb >>= 1;
         --bc;
-        const int n = c.cnt[len];
-        if (code - first < n) return c.sorted[index + code - first];
+        const int n = (int)uni(c.cnt[len]);
+        if (code - first < n) return (int)uni(c.sorted[index + code - first]);
         index += n;
         first = (first + n) << 1;
         code <<= 1;
@@ -925,14 +930,10 @@ __global__ __launch_bounds__(64) void k_inflate_members(InfArgs a) {
     const uint32_t in_len = (uint32_t)ix[1];
     const int64_t out_off = ix[2];
     const uint32_t isize = (uint32_t)((uint64_t)ix[3] & 0xffffffffu), want_crc = (uint32_t)((uint64_t)ix[3] >> 32);
+    (void)want_crc;
     if (isize > (uint32_t)WIN || out_off < 0 || (uint64_t)out_off + isize > a.out_cap) {
         if (lane == 0) atomicOr(a.status, kInfRange);
         return;
-    }
-    for (int i = lane; i < 256; i += 64) {
-        uint32_t r = (uint32_t)i;
-        for (int k = 0; k < 8; ++k) r = (r & 1u) ? (r >> 1) ^ 0xEDB88320u : r >> 1;
-        S.crct[i] = r;
     }
     // bit reader: bb holds bc bits; pos = next ring byte; the ring holds [fill - kRing, fill)
     uint64_t bb = 0;
@@ -951,13 +952,13 @@ __global__ __launch_bounds__(64) void k_inflate_members(InfArgs a) {
             if (pos + 8u > fill) refill();
             const uint32_t* w = reinterpret_cast<const uint32_t*>(S.ring);
             const uint32_t q = (pos & (kRing - 1)) >> 2;
-            const uint32_t v = __builtin_amdgcn_alignbyte(w[(q + 1) & (kRing / 4 - 1)], w[q], pos & 3u);
+            const uint32_t v = uni(__builtin_amdgcn_alignbyte(w[(q + 1) & (kRing / 4 - 1)], w[q], pos & 3u));
             bb |= (uint64_t)v << bc;
             bc += 32;
             pos += 4;
         }
     };
-    auto bits = [&](int n) -> uint32_t {  // n <= 32 - 0 and bb holds >= n bits
+    auto bits = [&](int n) -> uint32_t {  // n <= 32, bb holds >= n bits
         const uint32_t v = (uint32_t)(bb & ((1ull << n) - 1ull));
         bb >>= n;
         bc -= n;
@@ -1025,7 +1026,7 @@ __global__ __launch_bounds__(64) void k_inflate_members(InfArgs a) {
                 int rep, val = 0;
                 if (sy == 16) {
                     if (i == 0) { err = kInfCorrupt; break; }
-                    val = S.lens[i - 1];
+                    val = (int)uni(S.lens[i - 1]);
                     rep = 3 + (int)bits(2);
                 } else if (sy == 17) {
                     rep = 3 + (int)bits(3);
@@ -1040,9 +1041,9 @@ __global__ __launch_bounds__(64) void k_inflate_members(InfArgs a) {
             }
             if (err) break;
             __builtin_amdgcn_wave_barrier();
-            if (S.lens[256] == 0) { err = kInfCorrupt; break; }
+            if (uni(S.lens[256]) == 0) { err = kInfCorrupt; break; }
             // the distance lengths move out of the literal range before the builds
-            uint8_t dl = lane < ndist ? S.lens[nlit + lane] : 0;
+            const uint8_t dl = lane < ndist ? S.lens[nlit + lane] : 0;
             __builtin_amdgcn_wave_barrier();
             for (int k = nlit + lane; k < 288; k += 64) S.lens[k] = 0;
             __builtin_amdgcn_wave_barrier();
@@ -1059,26 +1060,27 @@ __global__ __launch_bounds__(64) void k_inflate_members(InfArgs a) {
                 if (p >= isize) { err = kInfSize; break; }
                 if (lane == 0) S.win[p] = (uint8_t)sy;
                 ++p;
-                continue;
-            }
-            if (sy == 256) break;
-            if (sy > 285) { err = kInfCorrupt; break; }
-            int le, de;
-            const uint32_t len = len_base(sy - 257, le) + bits(le);
-            topup();
-            const int ds = inf_decode(S.dist, bb, bc);
-            if (ds < 0 || ds > 29) { err = kInfCorrupt; break; }
-            const uint32_t d = dist_base(ds, de) + bits(de);
-            if (d > p) { err = kInfCorrupt; break; }
-            if (p + len > isize) { err = kInfSize; break; }
-            __builtin_amdgcn_wave_barrier();
-            if (d >= len) {
-                for (uint32_t k = lane; k < len; k += 64) S.win[p + k] = S.win[p - d + k];
+            } else if (sy == 256) {
+                break;
             } else {
-                for (uint32_t k = lane; k < len; k += 64) S.win[p + k] = S.win[p - d + k % d];
+                if (sy > 285) { err = kInfCorrupt; break; }
+                int le, de;
+                const uint32_t len = len_base(sy - 257, le) + bits(le);
+                topup();
+                const int ds = inf_decode(S.dist, bb, bc);
+                if (ds < 0 || ds > 29) { err = kInfCorrupt; break; }
+                const uint32_t d = dist_base(ds, de) + bits(de);
+                if (d > p) { err = kInfCorrupt; break; }
+                if (p + len > isize) { err = kInfSize; break; }
+                __builtin_amdgcn_wave_barrier();
+                if (d >= len) {
+                    for (uint32_t k = lane; k < len; k += 64) S.win[p + k] = S.win[p - d + k];
+                } else {
+                    for (uint32_t k = lane; k < len; k += 64) S.win[p + k] = S.win[p - d + k % d];
+                }
+                __builtin_amdgcn_wave_barrier();
+                p += len;
             }
-            __builtin_amdgcn_wave_barrier();
-            p += len;
         }
     }
     // every byte of the deflate data used, none past it; the whole ISIZE produced
@@ -1089,32 +1091,54 @@ __global__ __launch_bounds__(64) void k_inflate_members(InfArgs a) {
         return;
     }
     __builtin_amdgcn_wave_barrier();
-    // CRC-32: the output as the tail of 64 * Sg bytes whose leading zeros do
-    // not change a zero-initialised CRC; lane l takes bytes [l Sg, (l+1) Sg)
-    // of that, then a tree with the same shift per level for every lane
-    int lg = 0;
-    while ((64u << lg) < isize) ++lg;
-    const int sg = 1 << lg;
-    const int a0 = lane * sg - (int)((64u << lg) - isize);
-    uint32_t r = 0;
-    for (int i = max(a0, 0); i < a0 + sg; ++i) r = S.crct[(r ^ S.win[i]) & 0xffu] ^ (r >> 8);
-#pragma unroll
-    for (int l = 0; l < 6; ++l) {
-        const uint32_t o = (uint32_t)__shfl_xor((int)r, 1 << l, 64);
-        const uint32_t sh = crc_adv_pow2(r, lg + l);
-        r = (lane & (1 << l)) ? r : (sh ^ o);
-    }
-    const uint32_t crc = crc_adv(0xffffffffu, isize) ^ (uint32_t)__shfl((int)r, 0, 64) ^ 0xffffffffu;
-    if (crc != want_crc) {
-        if (lane == 0) atomicOr(a.status, kInfCrc);
-        return;
-    }
     uint8_t* dst = a.out + out_off;
-    if (((out_off | (int64_t)isize) & 3) == 0) {
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(S.win);
-        for (uint32_t i = lane; i < isize / 4u; i += 64) reinterpret_cast<uint32_t*>(dst)[i] = w[i];
+    if (((reinterpret_cast<uintptr_t>(dst) | isize) & 15u) == 0) {
+        const uint4* w = reinterpret_cast<const uint4*>(S.win);
+        for (uint32_t i = lane; i < isize / 16u; i += 64) reinterpret_cast<uint4*>(dst)[i] = w[i];
     } else {
         for (uint32_t i = lane; i < isize; i += 64) dst[i] = S.win[i];
+    }
+}
+
+// CRC-32 of every member's output (after k_inflate_members), one 256-thread
+// block per member: the output seen as the tail of 256 * sg bytes (leading
+// zeros do not change a zero-initialised CRC), thread t takes bytes
+// [t sg, (t+1) sg) of that, then a tree whose level-l shift (sg 2^l bytes) is
+// the same for every thread
+__global__ __launch_bounds__(256) void k_crc_members(InfArgs a) {
+    __shared__ uint32_t crct[256];
+    __shared__ uint32_t part[4];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int64_t m = blockIdx.x;
+    if (m >= a.nmem) return;
+    const int64_t* ix = a.idx + 4 * m;
+    const int64_t out_off = ix[2];
+    const uint32_t isize = (uint32_t)((uint64_t)ix[3] & 0xffffffffu), want = (uint32_t)((uint64_t)ix[3] >> 32);
+    if (out_off < 0 || (uint64_t)out_off + isize > a.out_cap) return;  // reported by the inflate
+    {
+        uint32_t r = (uint32_t)tid;
+        for (int k = 0; k < 8; ++k) r = (r & 1u) ? (r >> 1) ^ 0xEDB88320u : r >> 1;
+        crct[tid] = r;
+    }
+    __syncthreads();
+    int lg = 0;
+    while ((256ull << lg) < isize) ++lg;
+    const int64_t sg = 1ll << lg;
+    const int64_t b0 = (int64_t)tid * sg - (int64_t)((256ull << lg) - isize);
+    const uint8_t* o = a.out + out_off;
+    uint32_t r = 0;
+    for (int64_t i = b0 < 0 ? 0 : b0; i < b0 + sg; ++i) r = crct[(r ^ o[i]) & 0xffu] ^ (r >> 8);
+    for (int l = 0; l < 6; ++l) {
+        const uint32_t x = (uint32_t)__shfl_xor((int)r, 1 << l, 64);
+        const uint32_t sh = crc_adv_pow2(r, lg + l);
+        r = (lane & (1 << l)) ? r : (sh ^ x);
+    }
+    if (lane == 0) part[tid >> 6] = r;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t raw = 0;
+        for (int w = 0; w < 4; ++w) raw = crc_adv(raw, (uint32_t)(64ull * sg)) ^ part[w];
+        if ((crc_adv(0xffffffffu, isize) ^ raw ^ 0xffffffffu) != want) atomicOr(a.status, kInfCrc);
     }
 }
 }  // namespace gz
@@ -1129,7 +1153,7 @@ int gzfail(int code, const std::string& m) { g_gzerr = m; return code; }
     } while (0)
 
 // raw CRC-32 advance matrices for 2^k zero bytes
-void crc_matrices(uint32_t (&m)[17][32]) {
+void crc_matrices(uint32_t (&m)[32][32]) {
     uint32_t tab[256];
     for (uint32_t i = 0; i < 256; ++i) {
         uint32_t r = i;
@@ -1142,7 +1166,7 @@ void crc_matrices(uint32_t (&m)[17][32]) {
         for (int i = 0; i < 32; ++i) if ((v >> i) & 1u) r ^= M[i];
         return r;
     };
-    for (int k = 1; k < 17; ++k)
+    for (int k = 1; k < 32; ++k)
         for (int i = 0; i < 32; ++i) m[k][i] = apply(m[k - 1], apply(m[k - 1], 1u << i));
 }
 // the members of a member-indexed stream (every header carries the 'BC'
@@ -1199,7 +1223,7 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
     if (n < 1 || !x || !out || !out_len) return gzfail(OFL_EINVAL, "gzip ranks: empty input");
     if (!ws || ws_bytes < ofl_gzip_ranks_workspace_bytes(n)) return gzfail(OFL_ESPACE, "gzip ranks: workspace too small");
     GZHIP(ofl_util::per_device_once([] {  // __constant__ tables and attributes are per device
-        uint32_t m[17][32];
+        uint32_t m[32][32];
         crc_matrices(m);
         hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(gz::c_adv), m, sizeof(m));
         if (e == hipSuccess)
@@ -1329,7 +1353,7 @@ int ofl_inflate_members(const uint8_t* src, const int64_t* index, int64_t nmembe
     if (max_isize > 65536u) return gzfail(OFL_EFORMAT, "inflate: members above 64 KiB of output are not supported on the device");
     if (nmembers == 0) return OFL_OK;
     GZHIP(ofl_util::per_device_once([] {
-        uint32_t m[17][32];
+        uint32_t m[32][32];
         crc_matrices(m);
         hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(gz::c_adv), m, sizeof(m));
         if (e == hipSuccess)
@@ -1345,11 +1369,12 @@ int ofl_inflate_members(const uint8_t* src, const int64_t* index, int64_t nmembe
         hipLaunchKernelGGL(gz::k_inflate_members<16384>, dim3((unsigned)nmembers), dim3(64), sizeof(gz::InfSmem<16384>), st, a);
     else
         hipLaunchKernelGGL(gz::k_inflate_members<65536>, dim3((unsigned)nmembers), dim3(64), sizeof(gz::InfSmem<65536>), st, a);
+    hipLaunchKernelGGL(gz::k_crc_members, dim3((unsigned)nmembers), dim3(256), 0, st, a);
     GZHIP(hipGetLastError());
     int h = 0;
     GZHIP(hipMemcpyAsync(&h, status, sizeof(int), hipMemcpyDeviceToHost, st));
     GZHIP(hipStreamSynchronize(st));
-    if (h & gz::kInfRange) return gzfail(OFL_ESPACE, "inflate: a member's output falls outside out (or above its window)");
+    if (h & gz::kInfRange) return gzfail(OFL_ESPACE, "inflate: a member's output falls outside out");
     if (h & gz::kInfCorrupt) return gzfail(OFL_EINVAL, "inflate: corrupt deflate data");
     if (h & gz::kInfSize) return gzfail(OFL_EINVAL, "inflate: member size differs from its ISIZE");
     if (h & gz::kInfCrc) return gzfail(OFL_EINVAL, "inflate: CRC-32 mismatch");

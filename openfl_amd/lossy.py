@@ -297,6 +297,18 @@ def gunzip(data, threads=8, out=None):
     return dst[:need.value]
 
 
+def _parallel_copy(dst, src, nbytes, threads=8, piece=4 << 20):
+    """memcpy of a large host buffer in pieces on native threads
+    (ofl_host_copy_many, no GIL)."""
+    if nbytes <= 0:
+        return
+    offs = np.arange(0, nbytes, piece, dtype=np.int64)
+    sizes = np.minimum(piece, nbytes - offs).astype(np.int64)
+    d = (np.uint64(dst) + offs.astype(np.uint64))
+    s = (np.uint64(src) + offs.astype(np.uint64))
+    _lib.check(_lib.lib().ofl_host_copy_many(offs.size, d.ctypes.data, s.ctypes.data, sizes.ctypes.data, threads))
+
+
 def _buf(device, name, nbytes, pinned=False):
     """Thread-local scratch buffers (device, or pinned host) that only grow."""
     bufs = getattr(_tls, "bufs", None)
@@ -347,7 +359,7 @@ def gunzip_device(data, out):
     need = ioff + idx.nbytes
     stage = _buf("host", "gz_in", need, pinned=True)
     sn = stage.numpy()
-    sn[:src.size] = src
+    _parallel_copy(sn.ctypes.data, src.ctypes.data, src.size)
     sn[ioff:need] = idx.view(np.uint8).reshape(-1)
     d_in = _buf(dev, "gz_in", need)
     d_in[:need].copy_(stage[:need], non_blocking=True)

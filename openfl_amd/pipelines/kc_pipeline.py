@@ -62,3 +62,26 @@ class KCPipeline(TransformationPipeline):
             return super().forward(data, **kwargs)
         payload, gz_md = gz.forward_device(ranks)
         return payload, [{"int_list": list(data.shape), "int_to_float": m}, gz_md]
+
+    def backward(self, data, transformer_metadata, **kwargs):
+        """With the device gzip backend: inflate on the GPU straight into the
+        rank array (lossy.gunzip_device), LUT-decode there, one D2H of the
+        result -- the same values as GZIPTransformer.backward followed by
+        KmeansTransformer.backward, metadata consumed the same way (pop)."""
+        km, gz = self.transformers
+        if gz.backend != "device":
+            return super().backward(data, transformer_metadata, **kwargs)
+        import torch
+        from openfl_amd import lossy
+        transformer_metadata.pop()  # GZIPTransformer's (empty)
+        md = transformer_metadata.pop()
+        shape = list(md["int_list"])
+        n = int(np.prod(shape)) if shape else 1
+        buf = torch.empty(4 * max(n, 1), dtype=torch.uint8, device=km.device)
+        raw = lossy.gunzip_device(data, buf)
+        if raw.numel() != 4 * n:
+            raise lossy._lib.CodecError("KC payload size does not match its int_list")
+        if n == 0:
+            return np.zeros(shape, np.float32)
+        y = lossy.lut_decode(raw.view(torch.float32), md["int_to_float"])
+        return y.cpu().numpy().reshape(shape)

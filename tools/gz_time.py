@@ -44,3 +44,27 @@ for _ in range(3):
     lossy.gunzip(z, 16, out=stage.numpy())
 dt = (time.perf_counter() - t0) / 3
 print(f"gunzip host (16 threads) 1 GiB: {1e3 * dt:.1f} ms, {4 * n / dt / 2**30:.2f} GiB/s")
+# phases of gunzip_device: host member index, pinned staging copy, H2D, kernel
+import ctypes  # noqa: E402
+from openfl_amd import _lib  # noqa: E402
+L = _lib.lib()
+src = np.frombuffer(z, np.uint8)
+nm, tot, mx = ctypes.c_int64(), ctypes.c_size_t(), ctypes.c_uint32()
+t0 = time.perf_counter()
+L.ofl_gzip_member_index(src.ctypes.data, src.size, None, 0, ctypes.byref(nm), ctypes.byref(tot), ctypes.byref(mx))
+idx = np.empty((nm.value, 4), np.int64)
+L.ofl_gzip_member_index(src.ctypes.data, src.size, idx.ctypes.data, nm.value, ctypes.byref(nm), ctypes.byref(tot),
+                        ctypes.byref(mx))
+t1 = time.perf_counter()
+pin = torch.empty(src.size + idx.nbytes + 8, dtype=torch.uint8).pin_memory()
+pn = pin.numpy()
+pn[:src.size] = src
+t2 = time.perf_counter()
+d = torch.empty_like(pin, device="cuda")
+torch.cuda.synchronize()
+t3 = time.perf_counter()
+d.copy_(pin)
+torch.cuda.synchronize()
+t4 = time.perf_counter()
+print(f"gunzip_device phases: index {1e3 * (t1 - t0):.1f} ms ({nm.value} members), staging copy {1e3 * (t2 - t1):.1f} ms, "
+      f"H2D {1e3 * (t4 - t3):.1f} ms")
