@@ -131,6 +131,23 @@ int ofl_eden_decode_add(ofl_eden_plan_t plan, const uint8_t* planes_arena, const
                         const float* scales, const float* base_arena, float* y_arena, void* ws,
                         size_t ws_bytes, void* stream);
 
+/* The one-tensor plugin path (Eden.compress / Eden.decompress,
+ * eden_pipeline.py:555-659, one tensor per TensorCodec call) in one native
+ * call: one H2D of a pinned host block, the launches, one D2H of a device
+ * block, then a synchronize of `stream` -- no per-copy runtime calls from the
+ * caller.  Encode input block (in_host pinned -> in_dev, in_bytes): x arena
+ * at 0, seeds (uint32 per tensor) at off_seeds >= 4 * arena length; output
+ * block (out_dev -> out_host, out_bytes): planes arena at 0, scales (fp32 per
+ * slice) at off_scales >= planes bytes.  Decode input block: planes arena at
+ * 0, scales at off_scales, seeds at off_seeds; output block: the y arena
+ * (out_bytes <= 4 * arena length copied back). */
+int ofl_eden_encode_host(ofl_eden_plan_t plan, const void* in_host, void* in_dev, size_t in_bytes, size_t off_seeds,
+                         void* out_dev, void* out_host, size_t out_bytes, size_t off_scales, void* ws, size_t ws_bytes,
+                         void* stream);
+int ofl_eden_decode_host(ofl_eden_plan_t plan, const void* in_host, void* in_dev, size_t in_bytes, size_t off_scales,
+                         size_t off_seeds, void* out_dev, void* out_host, size_t out_bytes, void* ws, size_t ws_bytes,
+                         void* stream);
+
 /* ---- profiling (bench.py) --------------------------------------------------
  * While enabled, every encode/decode of the plan records a HIP event before
  * and after each launch, on the launch's stream.  collect() waits for

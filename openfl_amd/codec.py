@@ -95,6 +95,11 @@ class EdenPlan:
             self._L.ofl_eden_plan_destroy(h)
             self._h = None
 
+    @property
+    def handle(self):
+        """The C-ABI plan (ofl_eden_plan_t) for direct library calls."""
+        return self._h
+
     # -- raw launches (all pointers are device tensors) --
     def encode(self, x_arena, seeds, planes, scales, ws, stream=None):
         """x_arena fp32[arena_numel] -> planes u8[planes_bytes], scales f32[n_slices]."""

@@ -1756,6 +1756,7 @@ struct ofl_eden_plan {
     int64_t ws_floats = 0;      // intermediates
     int64_t part_floats = 0;    // partials
     int64_t nlarge = 0;         // large slices (informational)
+    int64_t arena = 0;          // fp32 arena length: max over tensors of elem_offset + numel
     // slice ids per kernel class (fixed by the batch) and the schedule built
     // from them (build_schedule)
     std::vector<int32_t> tiny, small[5], large;
@@ -2305,6 +2306,7 @@ int ofl_eden_plan_create(int ntensors, const int64_t* numel, const int64_t* elem
     auto* pl = new ofl_eden_plan();
     pl->nbits = n_bits;
     pl->ntensors = ntensors;
+    for (int t = 0; t < ntensors; ++t) pl->arena = std::max(pl->arena, elem_offset[t] + numel[t]);
     int64_t dims_pos = 0;
     // per-class slice lists
     std::vector<int32_t>& tiny = pl->tiny;
@@ -2536,6 +2538,45 @@ int ofl_eden_decode_add(ofl_eden_plan_t pl, const uint8_t* planes_arena, const u
     a.seeds = seeds;
     a.scales_in = scales;
     return run(pl, false, a, static_cast<hipStream_t>(stream));
+}
+
+int ofl_eden_encode_host(ofl_eden_plan_t pl, const void* in_host, void* in_dev, size_t in_bytes, size_t off_seeds,
+                         void* out_dev, void* out_host, size_t out_bytes, size_t off_scales, void* ws, size_t ws_bytes,
+                         void* stream) {
+    if (!pl || !in_host || !in_dev || !out_dev || !out_host) return fail(OFL_EINVAL, "encode_host: null argument");
+    if (off_seeds + 4 * (size_t)pl->ntensors > in_bytes || off_seeds < 4 * (size_t)pl->arena ||
+        off_scales < (size_t)pl->planes_bytes || off_scales + 4 * pl->slices.size() > out_bytes)
+        return fail(OFL_EINVAL, "encode_host: block layout does not fit the plan");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    HIP_TRY(hipMemcpyAsync(in_dev, in_host, in_bytes, hipMemcpyHostToDevice, st));
+    char* o = static_cast<char*>(out_dev);
+    const char* i = static_cast<const char*>(in_dev);
+    if (int rc = ofl_eden_encode(pl, reinterpret_cast<const float*>(i), reinterpret_cast<const uint32_t*>(i + off_seeds),
+                                 reinterpret_cast<uint8_t*>(o), reinterpret_cast<float*>(o + off_scales), ws, ws_bytes,
+                                 stream))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(out_host, out_dev, out_bytes, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return OFL_OK;
+}
+
+int ofl_eden_decode_host(ofl_eden_plan_t pl, const void* in_host, void* in_dev, size_t in_bytes, size_t off_scales,
+                         size_t off_seeds, void* out_dev, void* out_host, size_t out_bytes, void* ws, size_t ws_bytes,
+                         void* stream) {
+    if (!pl || !in_host || !in_dev || !out_dev || !out_host) return fail(OFL_EINVAL, "decode_host: null argument");
+    if (off_scales < (size_t)pl->planes_bytes || off_seeds < off_scales + 4 * pl->slices.size() ||
+        off_seeds + 4 * (size_t)pl->ntensors > in_bytes || out_bytes > 4 * (size_t)pl->arena)
+        return fail(OFL_EINVAL, "decode_host: block layout does not fit the plan");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    HIP_TRY(hipMemcpyAsync(in_dev, in_host, in_bytes, hipMemcpyHostToDevice, st));
+    const char* i = static_cast<const char*>(in_dev);
+    if (int rc = ofl_eden_decode(pl, reinterpret_cast<const uint8_t*>(i), reinterpret_cast<const uint32_t*>(i + off_seeds),
+                                 reinterpret_cast<const float*>(i + off_scales), static_cast<float*>(out_dev), ws, ws_bytes,
+                                 stream))
+        return rc;
+    if (out_bytes) HIP_TRY(hipMemcpyAsync(out_host, out_dev, out_bytes, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return OFL_OK;
 }
 
 int ofl_eden_plan_profile(ofl_eden_plan_t pl, int enable) {

@@ -23,6 +23,7 @@ Deliberate differences (DESIGN.md "Reference quirks"):
     in the metadata either way, so decoding never depends on it.
   * device="cpu" (the reference default) selects the current GPU.
 """
+import contextlib
 import threading
 from concurrent.futures import ThreadPoolExecutor
 
@@ -166,39 +167,42 @@ class Eden:
 
     def compress(self, vec, seed):
         """(planes uint8 ndarray, scales list[float], dims list[int], total_dim) (:555-611).
-        One tensor: pinned staging, one H2D, the launches, one D2H, one sync."""
+        One tensor in one native call (ofl_eden_encode_host): pinned input
+        block [x | seed] -> one H2D, the launches, one D2H of [planes |
+        scales], one sync."""
         flat = np.ascontiguousarray(np.asarray(vec).reshape(-1), dtype=np.float32)
         n = flat.size
         plan = self.codec.plan([n])
-        st, stg = self._stream(), self._staging()
-        xh = stg.get("x1", n, torch.float32)
-        sh = stg.get("s1", 1, torch.int32)
-        if n:
-            xh.numpy()[:n] = flat
-        sh.numpy()[0] = int(seed)
         pb, ns = plan.planes_bytes, plan.n_slices
-        ph = stg.get("p1", pb, torch.uint8)
-        sch = stg.get("c1", ns, torch.float32)
-        with torch.cuda.stream(st):
-            x = self._dev("x", plan.arena_numel, torch.float32)
-            if n:
-                x[:n].copy_(xh[:n], non_blocking=True)
-            sd = self._dev("s", 1, torch.int32)
-            sd[:1].copy_(sh[:1], non_blocking=True)
-            planes = self._dev("p", pb, torch.uint8)
-            scales = self._dev("c", ns, torch.float32)
-            plan.encode(x, sd, planes, scales, self.codec.ws.get(plan.ws_bytes, self.device), st)
-            ph[:max(pb, 1)].copy_(planes[:max(pb, 1)], non_blocking=True)
-            sch[:max(ns, 1)].copy_(scales[:max(ns, 1)], non_blocking=True)
-        st.synchronize()
+        off_seeds = _al256(4 * plan.arena_numel)
+        in_bytes = off_seeds + 4
+        off_scales = _al256(pb)
+        out_bytes = off_scales + 4 * ns
+        stg = self._staging()
+        ih = stg.get("in1", in_bytes, torch.uint8)
+        ia = ih.numpy()
+        if n:
+            ia[:4 * n].view(np.float32)[:] = flat
+        ia[off_seeds:off_seeds + 4].view(np.uint32)[0] = int(seed) & 0xFFFFFFFF
+        oh = stg.get("out1", out_bytes, torch.uint8)
+        idev = self._dev("in", in_bytes, torch.uint8)
+        odev = self._dev("out", out_bytes, torch.uint8)
+        ws = self.codec.ws.get(plan.ws_bytes, self.device)
+        with _device_guard(self.device):
+            _lib.check(_lib.lib().ofl_eden_encode_host(
+                plan.handle, ih.data_ptr(), idev.data_ptr(), in_bytes, off_seeds, odev.data_ptr(), oh.data_ptr(),
+                out_bytes, off_scales, ws.data_ptr(), ws.numel(), self._stream().cuda_stream))
+        oa = oh.numpy()
         # one host copy, pinned -> bytes; the array is a zero-copy view of it
-        out = (np.frombuffer(ph.numpy()[:pb].tobytes(), np.uint8), [float(v) for v in sch.numpy()[:ns]],
-               list(plan.dims[0]), n)
+        out = (np.frombuffer(oa[:pb].tobytes(), np.uint8),
+               [float(v) for v in oa[off_scales:off_scales + 4 * ns].view(np.float32)], list(plan.dims[0]), n)
         self._trim()
         return out
 
     def decompress(self, bins, metadata):
-        """bins: uint8 planes; metadata: int_to_float mapping (:632-659)."""
+        """bins: uint8 planes; metadata: int_to_float mapping (:632-659).  One
+        native call (ofl_eden_decode_host): [planes | scales | seed] -> one H2D,
+        the launches, one D2H of y, one sync."""
         seed = int(metadata[0])
         total_dim = int(metadata[1])
         keys = list(metadata.keys())
@@ -208,35 +212,45 @@ class Eden:
             dims.append(int(metadata[k + 1]))
         if total_dim > sum(dims):
             raise ValueError(f"Eden metadata: total_dim {total_dim} exceeds the slices ({sum(dims)})")
-        planes_h = np.frombuffer(bytes(bins) if not isinstance(bins, np.ndarray) else bins.tobytes(),
-                                 dtype=np.uint8)
+        planes_h = np.frombuffer(bins, dtype=np.uint8) if isinstance(bins, (bytes, bytearray, memoryview)) \
+            else np.asarray(bins, dtype=np.uint8).reshape(-1)
         plan = self.codec.plan([total_dim], dims=[dims])
         if planes_h.size < plan.planes_bytes:
             raise ValueError(f"Eden payload has {planes_h.size} bytes, expected {plan.planes_bytes}")
-        st, stg = self._stream(), self._staging()
         pb, ns = plan.planes_bytes, plan.n_slices
-        ph = stg.get("pi1", pb, torch.uint8)
-        sch = stg.get("ci1", ns, torch.float32)
-        sh = stg.get("si1", 1, torch.int32)
-        ph.numpy()[:pb] = planes_h[:pb]
-        sch.numpy()[:ns] = np.asarray(scales, np.float32)
-        sh.numpy()[0] = seed
-        yh = stg.get("y1", total_dim, torch.float32)
-        with torch.cuda.stream(st):
-            planes = self._dev("pi", pb, torch.uint8)
-            planes[:max(pb, 1)].copy_(ph[:max(pb, 1)], non_blocking=True)
-            sc = self._dev("ci", ns, torch.float32)
-            sc[:max(ns, 1)].copy_(sch[:max(ns, 1)], non_blocking=True)
-            sd = self._dev("si", 1, torch.int32)
-            sd[:1].copy_(sh[:1], non_blocking=True)
-            y = self._dev("y", plan.arena_numel, torch.float32)
-            plan.decode(planes, sd, sc, y, self.codec.ws.get(plan.ws_bytes, self.device), st)
-            if total_dim:
-                yh[:total_dim].copy_(y[:total_dim], non_blocking=True)
-        st.synchronize()
+        off_scales = _al256(pb)
+        off_seeds = _al256(off_scales + 4 * ns)
+        in_bytes = off_seeds + 4
+        out_bytes = 4 * total_dim
+        stg = self._staging()
+        ih = stg.get("in1", in_bytes, torch.uint8)
+        ia = ih.numpy()
+        ia[:pb] = planes_h[:pb]
+        ia[off_scales:off_scales + 4 * ns].view(np.float32)[:] = np.asarray(scales, np.float32)
+        ia[off_seeds:off_seeds + 4].view(np.uint32)[0] = seed & 0xFFFFFFFF
+        yh = stg.get("y1", max(total_dim, 1), torch.float32)
+        idev = self._dev("in", in_bytes, torch.uint8)
+        ydev = self._dev("y", max(plan.arena_numel, 1), torch.float32)
+        ws = self.codec.ws.get(plan.ws_bytes, self.device)
+        with _device_guard(self.device):
+            _lib.check(_lib.lib().ofl_eden_decode_host(
+                plan.handle, ih.data_ptr(), idev.data_ptr(), in_bytes, off_scales, off_seeds, ydev.data_ptr(),
+                yh.data_ptr(), out_bytes, ws.data_ptr(), ws.numel(), self._stream().cuda_stream))
         y = yh.numpy()[:total_dim].copy()
         self._trim()
         return y
+
+
+def _al256(b):
+    return (int(b) + 255) // 256 * 256
+
+
+def _device_guard(dev):
+    """Make dev current for a library call when it is not (plans and their
+    device tables belong to the device current at their first use)."""
+    if dev.index is None or dev.index == torch.cuda.current_device():
+        return contextlib.nullcontext()
+    return torch.cuda.device(dev)
 
 
 class _Staging:
@@ -368,9 +382,9 @@ class EdenTransformer(Transformer):
     def backward(self, data, metadata, **kwargs):
         if np.prod(metadata["int_list"]) > self.dim_threshold:  # reference: >= (:808), see module doc
             out = self.eden.decompress(np.frombuffer(data, dtype=np.uint8), metadata["int_to_float"])
-            out = out.reshape(list(metadata["int_list"]))
-        else:
-            out = self.no_comp.backward(data, metadata)
+            # already a fresh float32 array: astype would only copy it again
+            return out.reshape(list(metadata["int_list"]))
+        out = self.no_comp.backward(data, metadata)
         return out.astype(np.float32)
 
     # -- many tensors per call (same results as forward/backward in order) --

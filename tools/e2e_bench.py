@@ -11,7 +11,7 @@ Modes (wall-clock, both collaborators, second of two rounds):
            encode launch sequence, one D2H of the planes arena; the receiver
            does one H2D of all payloads, one decode, one D2H (also with
            seed_mode="fast": "batched_fast_seed")
-  cpu      the C oracle (oracle/eden_oracle.c, 1 thread) in the same flow
+  cpu      the C oracle (oracle/eden_oracle.c, on all host cores) in the same flow
            (the CPU pipeline timed beside it; test infrastructure)
 Prints one JSON line (also written to --out).
 """
@@ -147,10 +147,13 @@ def main():
                         "wire_bytes": sum(o[1] for o in outs), "rel_err": round(rel_err(sds[-1], outs[-1][0]), 6),
                         "last_collaborator_phases": dict(run_batched.phases)}
     if "cpu" in modes:
+        from oracle import eden as O
+        cores = O.host_cores()
+        O.set_threads(cores)
         t0 = time.perf_counter()
         outs = [run_cpu(sd, P) for sd in sds]
         dt = time.perf_counter() - t0
-        res["cpu"] = {"s": round(dt, 3), "GiB_s": round(in_bytes / dt / 2 ** 30, 4), "cores": 1, "kind": "port",
+        res["cpu"] = {"s": round(dt, 3), "GiB_s": round(in_bytes / dt / 2 ** 30, 4), "cores": cores, "kind": "port",
                       "wire_bytes": sum(o[1] for o in outs), "rel_err": round(rel_err(sds[0], outs[0][0]), 6)}
     line = json.dumps(res)
     print(line)

@@ -1,0 +1,28 @@
+"""cProfile of the per-tensor plugin path (EdenPipeline.forward / backward per
+tensor + NamedTensor build / parse, tools/e2e_bench.py 'plugin' mode) on
+ResNet-50 shapes: where the host time of one-tensor calls goes."""
+import cProfile
+import os
+import pstats
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import torch  # noqa: E402
+
+from e2e_bench import run_plugin, state_dict  # noqa: E402
+from openfl_amd import protocols as P  # noqa: E402
+from openfl_amd.pipelines import EdenPipeline  # noqa: E402
+from openfl_amd.workloads import WORKLOADS  # noqa: E402
+
+sd = state_dict(WORKLOADS["resnet50_fp32"](), 100)
+pipe = EdenPipeline(n_bits=8, dim_threshold=100, device="cuda:0")
+run_plugin(sd, pipe, P)
+torch.cuda.synchronize()
+pr = cProfile.Profile()
+pr.enable()
+for _ in range(3):
+    run_plugin(sd, pipe, P)
+pr.disable()
+pstats.Stats(pr).sort_stats("tottime").print_stats(25)
