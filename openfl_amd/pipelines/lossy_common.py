@@ -58,6 +58,22 @@ class GZIPTransformer(Transformer):
         return lossy.gunzip(data, self.threads).view(np.float32)
 
 
+def gzip_lut_backward_device(data, int2float_map, n, device):
+    """GZIPTransformer.backward followed by the LUT backward of the lossy
+    transformer before it (KmeansTransformer / TernaryTransformer:
+    kc_pipeline.py:79-83, :152-156; stc_pipeline.py:126-130), fused on the
+    GPU: the payload inflates straight into HBM (lossy.gunzip_device), the
+    LUT decodes it there.  n: element count the payload must decode to.
+    -> float32 device tensor of n elements."""
+    buf = torch.empty(4 * max(n, 1), dtype=torch.uint8, device=device)
+    raw = lossy.gunzip_device(data, buf)
+    if raw.numel() != 4 * n:
+        raise lossy._lib.CodecError(f"payload decodes to {raw.numel()} bytes, expected {4 * n}")
+    if n == 0:
+        return torch.empty(0, dtype=torch.float32, device=device)
+    return lossy.lut_decode(raw.view(torch.float32), int2float_map)
+
+
 def to_device(data, device):
     flat = np.ascontiguousarray(np.asarray(data).reshape(-1), dtype=np.float32)
     if not flat.flags.writeable:  # torch.from_numpy needs a writable buffer
@@ -88,4 +104,5 @@ def lut_backward(data, int2float_map, device):
     return out.cpu().numpy().reshape(arr.shape)
 
 
-__all__ = ["GZIPTransformer", "float_to_int", "kmeans_ranks", "lut_backward", "resolve_device", "to_device"]
+__all__ = ["GZIPTransformer", "float_to_int", "gzip_lut_backward_device", "kmeans_ranks", "lut_backward",
+           "resolve_device", "to_device"]

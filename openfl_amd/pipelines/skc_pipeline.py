@@ -6,8 +6,8 @@ on the GPU (see stc_pipeline / kc_pipeline for the parity notes).
 """
 import numpy as np
 
-from openfl_amd.pipelines.lossy_common import (GZIPTransformer, float_to_int, kmeans_ranks, lut_backward,
-                                               resolve_device, to_device)
+from openfl_amd.pipelines.lossy_common import (GZIPTransformer, float_to_int, gzip_lut_backward_device,
+                                               kmeans_ranks, lut_backward, resolve_device, to_device)
 from openfl_amd.pipelines.pipeline import TransformationPipeline, Transformer
 from openfl_amd.pipelines.stc_pipeline import SparsityTransformer
 
@@ -52,6 +52,19 @@ class SKCPipeline(TransformationPipeline):
             payload, gz_md = gz.forward_device(ranks)
             return payload, [{"int_list": list(data.shape)}, {"int_to_float": m}, gz_md]
         return super().forward(data, **kwargs)
+
+    def backward(self, data, transformer_metadata, **kwargs):
+        """With the device gzip backend: inflate + LUT fused on the GPU
+        (lossy_common.gzip_lut_backward_device), then the sparsity backward's
+        reshape; metadata consumed the same way (pop)."""
+        sp, lut_t, gz = self.transformers
+        if gz.backend != "device":
+            return super().backward(data, transformer_metadata, **kwargs)
+        transformer_metadata.pop()  # GZIPTransformer's (empty)
+        m = transformer_metadata.pop()["int_to_float"]
+        shape = list(transformer_metadata.pop()["int_list"])
+        y = gzip_lut_backward_device(data, m, int(np.prod(shape)) if shape else 1, sp.device)
+        return y.cpu().numpy().reshape(shape)
 
 
 __all__ = ["GZIPTransformer", "KmeansTransformer", "SKCPipeline", "SparsityTransformer"]

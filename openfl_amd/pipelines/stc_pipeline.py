@@ -9,7 +9,8 @@ introsort's, i.e. unspecified).
 import numpy as np
 
 from openfl_amd import lossy
-from openfl_amd.pipelines.lossy_common import GZIPTransformer, float_to_int, lut_backward, resolve_device, to_device
+from openfl_amd.pipelines.lossy_common import (GZIPTransformer, float_to_int, gzip_lut_backward_device, lut_backward,
+                                               resolve_device, to_device)
 from openfl_amd.pipelines.pipeline import TransformationPipeline, Transformer
 
 
@@ -88,7 +89,17 @@ class STCPipeline(TransformationPipeline):
         return payload, [{"int_list": list(data.shape)}, {"int_to_float": m}, gz_md]
 
     def backward(self, data, transformer_metadata, **kwargs):
-        return super().backward(data, transformer_metadata, **kwargs)
+        """With the device gzip backend: inflate + LUT fused on the GPU
+        (lossy_common.gzip_lut_backward_device), then the sparsity backward's
+        reshape; metadata consumed the same way (pop)."""
+        sp, lut_t, gz = self.transformers
+        if gz.backend != "device":
+            return super().backward(data, transformer_metadata, **kwargs)
+        transformer_metadata.pop()  # GZIPTransformer's (empty)
+        m = transformer_metadata.pop()["int_to_float"]
+        shape = list(transformer_metadata.pop()["int_list"])
+        y = gzip_lut_backward_device(data, m, int(np.prod(shape)) if shape else 1, sp.device)
+        return y.cpu().numpy().reshape(shape)
 
 
 __all__ = ["GZIPTransformer", "STCPipeline", "SparsityTransformer", "TernaryTransformer", "float_to_int"]

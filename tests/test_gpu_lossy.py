@@ -360,17 +360,33 @@ def test_gzip_ranks_rejects_non_ranks():
             lossy.gzip_ranks(torch.from_numpy(bad).to(DEV))
 
 
-def test_kc_pipeline_device_gzip_backend():
-    from openfl_amd.pipelines import KCPipeline
-    x = np.random.default_rng(2).standard_normal((300, 200)).astype(np.float32)
+@pytest.mark.parametrize("name", ["KCPipeline", "STCPipeline", "SKCPipeline"])
+@pytest.mark.parametrize("shape", [(300, 200), (4,)])
+def test_lossy_pipeline_device_gzip_backend(name, shape):
+    """gzip_backend="device": device gzip on forward, fused device inflate +
+    LUT on backward -- same payload bytes (after gzip.decompress), same
+    decoded array and the metadata list consumed exactly like the host
+    backend's (the reference's pop semantics); host-gzip payloads (the tiny
+    path) decode through the same fused backward."""
+    import openfl_amd.pipelines as P
+    x = np.random.default_rng(2).standard_normal(shape).astype(np.float32)
     outs = []
     for backend in ("host", "device"):
-        pipe = KCPipeline(n_clusters=6, device=DEV, gzip_backend=backend)
+        pipe = getattr(P, name)(n_clusters=6, device=DEV, gzip_backend=backend)
         np.random.seed(1)
         payload, mds = pipe.forward(x)
-        outs.append((gzip.decompress(payload), pipe.backward(payload, mds)))
+        raw = gzip.decompress(payload)
+        y = pipe.backward(payload, mds)
+        assert mds == []
+        outs.append((raw, y))
+        # the other backend's payload decodes the same way
+        if backend == "device":
+            np.random.seed(1)
+            p2, m2 = getattr(P, name)(n_clusters=6, device=DEV, gzip_backend="host").forward(x)
+            np.testing.assert_array_equal(pipe.backward(p2, m2), y)
     assert outs[0][0] == outs[1][0]
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    assert outs[1][1].dtype == np.float32 and outs[1][1].shape == shape
 
 
 @pytest.mark.timeout(900)
