@@ -1619,6 +1619,12 @@ DEVI void fetch_ws_half(const KArgs& a, const SliceDesc& D, uint32_t tile, bool 
 // the second after the second), so the loads are in flight across the second
 // run, the plane stores and the dot reduction, with no extra registers (the
 // kernel sits at the 128-VGPR cap of two blocks per CU).
+// diagnostic builds only (-DOFL_DIAG_ROWC2=mask, wrong results, tools/ab):
+// 1 = no F2 exchanges, 2 = no quantiser, 4 = no dot reduction
+#ifndef OFL_DIAG_ROWC2
+#define OFL_DIAG_ROWC2 0
+#endif
+constexpr int kDiagRowC2 = OFL_DIAG_ROWC2;
 template <bool ROLL>
 __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowC2(KArgs a) {
     using R = RowC2Set;
@@ -1654,9 +1660,9 @@ __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowC2(KArgs a) {
         locate(more ? tn : t, sn, tln);
         if (!ROLL) fetch_ws(a, D, tile, true, base3, v);
         stages<R::L3, R::F2c>(v);
-        exchange_half_pad<R::L3, R::L4, R::HB>(v, s, tid);
+        if (!(kDiagRowC2 & 1)) exchange_half_pad<R::L3, R::L4, R::HB>(v, s, tid);
         stages<R::L4, R::F2d>(v);
-        exchange_half_pad<R::L4, R::L5, R::HB>(v, s, tid);
+        if (!(kDiagRowC2 & 1)) exchange_half_pad<R::L4, R::L5, R::HB>(v, s, tid);
         stages<R::L5, R::F2e>(v);
         __builtin_amdgcn_sched_barrier(0);
         const float nu = sldf(a.nu, si);
@@ -1667,7 +1673,13 @@ __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowC2(KArgs a) {
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
             uint32_t w[8];
-            dot += quant_pack32(*reinterpret_cast<const float(*)[32]>(&v[32 * g]), ysc, zm64, qt, w);
+            if (kDiagRowC2 & 2) {  // diagnostic: no quantiser (wrong output)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) w[i] = __float_as_uint(v[32 * g + 4 * i]) ^ __float_as_uint(v[32 * g + 4 * i + 1]);
+                dot += v[32 * g];
+            } else {
+                dot += quant_pack32(*reinterpret_cast<const float(*)[32]>(&v[32 * g]), ysc, zm64, qt, w);
+            }
             if (!pos) {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) w[i] = 0;
@@ -1680,7 +1692,7 @@ __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowC2(KArgs a) {
                          a.nbits, w);
         }
         if (!pos) dot = 0.f;
-        dot = block_sum<kRowNT>(dot, red);
+        if (!(kDiagRowC2 & 4)) dot = block_sum<kRowNT>(dot, red);
         if (tid == 0) a.part[D.part_off + tile] = dot;
         if (!more) break;
         t = tn; si = sn; tile = tln;
