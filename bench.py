@@ -142,7 +142,7 @@ def _fill_arena(plan, numels, dev, seed0=0):
     return x
 
 
-def secondary(name, n_bits, steps, warmup, dev, wave_mib, streams, cpu=False):
+def secondary(name, n_bits, steps, warmup, dev, wave_mib, streams, cpu=False, graph=False):
     """One more workload on this GPU (same step definition, inputs resident):
     the north_star's 1 GiB set and BASELINE config 2 (ResNet-50) next to the
     main line.  Device time from events around the timed steps.  cpu=True
@@ -180,6 +180,26 @@ def secondary(name, n_bits, steps, warmup, dev, wave_mib, streams, cpu=False):
            "roofline_frac": round(alg * steps / gpu_s / 1e9 / PEAK_HBM_GBPS, 4),
            "bytes": 4 * sum(numels), "tensors": len(numels), "slices": plan.n_slices, "waves": plan.n_waves,
            "streams": plan.n_streams, "steps": steps}
+    if graph:
+        # the same step replayed from a captured hipGraph (EdenStepGraph):
+        # every launch of the step, submitted as one graph
+        from openfl_amd.codec import EdenStepGraph
+        g = EdenStepGraph(plan, x, seeds, planes, scales, y, ws)
+        for _ in range(warmup):
+            g.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev0.record()
+        for _ in range(steps):
+            g.replay()
+        ev1.record()
+        torch.cuda.synchronize()
+        gw = time.perf_counter() - t0
+        gg = ev0.elapsed_time(ev1) / 1e3
+        out["graph"] = {"value": round(4 * sum(numels) * steps / gw / 2 ** 30, 2),
+                        "ms_per_step": round(1e3 * gw / steps, 4), "gpu_ms_per_step": round(1e3 * gg / steps, 4),
+                        "roofline_frac": round(alg * steps / gg / 1e9 / PEAK_HBM_GBPS, 4),
+                        "scope": "the same encode+decode step replayed from a captured hipGraph"}
     if cpu:
         def x_host(i):
             off = plan.elem_offsets[i]
@@ -504,8 +524,10 @@ def main(argv=None):
             if name == "kc_uniform_1gib":
                 also[name] = kc_pipeline(max(2, args.also_steps // 10), 1, dev)
             else:
-                also[name] = secondary(name, args.n_bits, args.also_steps, 3, dev, args.wave_mib, args.streams,
-                                       cpu=(name == "uniform_1gib" and not args.no_cpu_baseline))
+                # a ResNet-50 step is ~0.35 ms: more steps for a stable rate
+                st = max(args.also_steps, 200) if name == "resnet50_fp32" else args.also_steps
+                also[name] = secondary(name, args.n_bits, st, 3, dev, args.wave_mib, args.streams,
+                                       cpu=(name == "uniform_1gib" and not args.no_cpu_baseline), graph=True)
 
     out = None
     if rank == 0:

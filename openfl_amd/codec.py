@@ -162,6 +162,32 @@ class EdenPlan:
             raise _lib.CodecError(f"buffer must be contiguous {dtype} with >= {min_numel} elements")
 
 
+class EdenStepGraph:
+    """One plan's encode + decode over fixed device buffers, captured once as a
+    hipGraph (torch.cuda.CUDAGraph around the C-ABI calls; the plan's
+    side-stream fork/join becomes graph edges) and replayed: the launches of a
+    step are submitted as one graph instead of one by one.  Outputs are
+    bit-identical to the eager calls (tools/graph_ab.py).  The plan runs once
+    eagerly first: its descriptor tables go to the device on first use, which
+    must not happen inside a capture (ofl_codec.h)."""
+
+    def __init__(self, plan, x, seeds, planes, scales, y, ws):
+        dev = x.device
+        plan.encode(x, seeds, planes, scales, ws)
+        plan.decode(planes, seeds, scales, y, ws)
+        torch.cuda.synchronize(dev)
+        self._stream = torch.cuda.Stream(device=dev)
+        self._stream.wait_stream(torch.cuda.current_stream(dev))
+        self._graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self._graph, stream=self._stream):
+            plan.encode(x, seeds, planes, scales, ws)
+            plan.decode(planes, seeds, scales, y, ws)
+        self._keep = (plan, x, seeds, planes, scales, y, ws)  # the graph holds their addresses
+
+    def replay(self):
+        self._graph.replay()
+
+
 class Workspace:
     """Per-(thread, device) growable device scratch buffer."""
 

@@ -450,3 +450,30 @@ def test_pipeline_concurrent_threads():
         t.join()
     for a, b in zip(results, ref_out):
         np.testing.assert_array_equal(a, b)
+
+
+def test_step_graph_replay_bit_identical():
+    """EdenStepGraph (a captured hipGraph of a plan's encode + decode, the
+    side-stream fork/join included) replays the same bytes and values as the
+    eager launches, on a mixed set (tiny, small and large slices, two wave
+    streams plus the small-slice stream)."""
+    from openfl_amd.codec import EdenPlan, EdenStepGraph
+    numels = [50_000, 3000, 1 << 20, 700, (1 << 22) + 123, 1 << 15]
+    plan = EdenPlan(numels, 8, wave_mib=8, streams=2)
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x = torch.empty(plan.arena_numel, device=DEV).normal_(0, 0.01, generator=g)
+    seeds = torch.tensor([11, 12, 13, 14, 15, 16], dtype=torch.int32, device=DEV)
+    ws = torch.empty(max(plan.ws_bytes, 256), dtype=torch.uint8, device=DEV)
+    p0 = torch.empty(plan.planes_bytes, dtype=torch.uint8, device=DEV)
+    s0 = torch.empty(plan.n_slices, dtype=torch.float32, device=DEV)
+    y0 = torch.zeros_like(x)
+    plan.encode(x, seeds, p0, s0, ws)
+    plan.decode(p0, seeds, s0, y0, ws)
+    p1, s1, y1 = torch.zeros_like(p0), torch.zeros_like(s0), torch.zeros_like(x)
+    gr = EdenStepGraph(plan, x, seeds, p1, s1, y1, ws)
+    for fill in (p1, s1, y1):
+        fill.zero_()
+    gr.replay()
+    gr.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(p0, p1) and torch.equal(s0, s1) and torch.equal(y0, y1)
