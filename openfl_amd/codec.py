@@ -248,12 +248,15 @@ class EdenCodec:
         self._lock = threading.Lock()
         self.ws = Workspace()
 
-    def plan(self, numels, dims=None):
-        key = (tuple(int(n) for n in numels), None if dims is None else tuple(tuple(d) for d in dims))
+    def plan(self, numels, dims=None, streams=None):
+        """Cached plan of a batch shape.  streams: the large-slice schedule's
+        stream count (None: the library default, two)."""
+        key = (tuple(int(n) for n in numels), None if dims is None else tuple(tuple(d) for d in dims), streams)
         with self._lock:
             p = self._plans.get(key)
             if p is None:
-                p = EdenPlan(key[0], self.n_bits, dims=None if dims is None else [list(d) for d in key[1]])
+                p = EdenPlan(key[0], self.n_bits, dims=None if dims is None else [list(d) for d in key[1]],
+                             streams=streams)
                 self._plans[key] = p
                 self._order.append(key)
                 if len(self._order) > self._max:

@@ -172,7 +172,7 @@ class Eden:
         scales], one sync."""
         flat = np.ascontiguousarray(np.asarray(vec).reshape(-1), dtype=np.float32)
         n = flat.size
-        plan = self.codec.plan([n])
+        plan = self.codec.plan([n], streams=_one_tensor_streams(n))
         pb, ns = plan.planes_bytes, plan.n_slices
         off_seeds = _al256(4 * plan.arena_numel)
         in_bytes = off_seeds + 4
@@ -214,7 +214,7 @@ class Eden:
             raise ValueError(f"Eden metadata: total_dim {total_dim} exceeds the slices ({sum(dims)})")
         planes_h = np.frombuffer(bins, dtype=np.uint8) if isinstance(bins, (bytes, bytearray, memoryview)) \
             else np.asarray(bins, dtype=np.uint8).reshape(-1)
-        plan = self.codec.plan([total_dim], dims=[dims])
+        plan = self.codec.plan([total_dim], dims=[dims], streams=_one_tensor_streams(sum(dims)))
         if planes_h.size < plan.planes_bytes:
             raise ValueError(f"Eden payload has {planes_h.size} bytes, expected {plan.planes_bytes}")
         pb, ns = plan.planes_bytes, plan.n_slices
@@ -239,6 +239,13 @@ class Eden:
         y = yh.numpy()[:total_dim].copy()
         self._trim()
         return y
+
+
+def _one_tensor_streams(n):
+    """Stream count of a one-tensor plan: up to 2^24 elements one stream (no
+    side-stream fork/join per call: the per-tensor path is latency-bound);
+    larger tensors keep the two-stream wave schedule."""
+    return 1 if n <= (1 << 24) else None
 
 
 def _al256(b):
