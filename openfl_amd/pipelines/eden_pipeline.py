@@ -280,24 +280,57 @@ class _Staging:
         return b
 
 
-def _batch_encode(eden, arrays, seeds):
-    """Eden-encode many host arrays with one plan: pinned staging, one H2D, one
-    launch sequence, one D2H of the planes arena.  -> [(planes bytes, scales,
-    dims)] per array, the per-tensor Eden.compress results."""
+_CHUNKS = 4  # host <-> device copies of a batch go in this many pieces, overlapped
+
+
+def _pieces(offsets, sizes, k):
+    """Split tensors [0, n) (arena order) into <= k contiguous runs of about
+    equal bytes: [(first, last + 1), ...]."""
+    n = len(sizes)
+    tot = sum(sizes)
+    runs, start, acc = [], 0, 0
+    for i, sz in enumerate(sizes):
+        acc += sz
+        if acc * k >= tot * (len(runs) + 1) and i + 1 < n and len(runs) + 1 < k:
+            runs.append((start, i + 1))
+            start = i + 1
+    runs.append((start, n))
+    return [r for r in runs if r[1] > r[0]]
+
+
+def _batch_stage(eden, arrays):
+    """First half of a batch encode: plan, then the fill of the pinned arena
+    and its H2D in pieces, so that the copy of piece k+1 (native threads)
+    overlaps the DMA of piece k.  Returns the state _batch_encode finishes."""
     codec = eden.codec
     flats = [np.ascontiguousarray(np.asarray(a).reshape(-1), dtype=np.float32) for a in arrays]
     plan = codec.plan([f.size for f in flats])
     st = eden._stream()
+    xh = eden._staging().get("x", plan.arena_numel, torch.float32)
+    base = xh.data_ptr()
+    x = torch.empty(max(plan.arena_numel, 1), dtype=torch.float32, device=eden.device)
+    offs = plan.elem_offsets
+    for lo, hi in _pieces(offs, [f.size for f in flats], _CHUNKS):
+        _copy_many([base + 4 * offs[i] for i in range(lo, hi)], [flats[i].ctypes.data for i in range(lo, hi)],
+                   [4 * flats[i].size for i in range(lo, hi)])
+        e0, e1 = offs[lo], offs[hi - 1] + flats[hi - 1].size
+        if e1 > e0:
+            with torch.cuda.stream(st):
+                x[e0:e1].copy_(xh[e0:e1], non_blocking=True)
+    return plan, flats, x
+
+
+def _batch_encode(eden, staged, seeds):
+    """Second half: seeds, the launch sequence, one D2H of planes + scales.
+    -> [(planes bytes, scales, dims)] per array, the per-tensor Eden.compress
+    results."""
+    plan, flats, x = staged
+    codec = eden.codec
+    st = eden._stream()
     stg = eden._staging()
-    xh = stg.get("x", plan.arena_numel, torch.float32)
     ph = stg.get("planes", plan.planes_bytes, torch.uint8)
     sh = stg.get("scales", plan.n_slices, torch.float32)
-    base = xh.data_ptr()
-    _copy_many([base + 4 * plan.elem_offsets[i] for i in range(len(flats))],
-               [f.ctypes.data for f in flats], [4 * f.size for f in flats])
     with torch.cuda.stream(st):
-        x = torch.empty(max(plan.arena_numel, 1), dtype=torch.float32, device=eden.device)
-        x.copy_(xh[:max(plan.arena_numel, 1)], non_blocking=True)
         sd = torch.tensor(seeds, dtype=torch.int32).pin_memory().to(eden.device, non_blocking=True)
         planes, scales = codec.encode_arena(plan, x, sd, stream=st)
         ph[:max(plan.planes_bytes, 1)].copy_(planes[:max(plan.planes_bytes, 1)], non_blocking=True)
@@ -318,7 +351,9 @@ def _batch_encode(eden, arrays, seeds):
 
 def _batch_decode(eden, items):
     """Eden-decode many payloads (planes bytes, int_to_float metadata) with one
-    plan.  -> fresh float32 arrays (flat, total_dim elements each)."""
+    plan.  -> fresh float32 arrays (flat, total_dim elements each).  The D2H of
+    the decoded arena goes in pieces; each piece is copied out to its arrays
+    (native threads) while the next one is in flight."""
     codec = eden.codec
     totals, dims, scales, seeds = [], [], [], []
     for data, md in items:
@@ -342,18 +377,29 @@ def _batch_decode(eden, items):
     pbase = ph.data_ptr()
     _copy_many([pbase + plan.planes_offsets[t] for t in range(len(items))], [b.ctypes.data for b in bufs],
                [plan.planes_nbytes[t] for t in range(len(items))])
+    offs = plan.elem_offsets
+    pieces = _pieces(offs, totals, _CHUNKS)
+    events = []
     with torch.cuda.stream(st):
         planes = torch.empty(max(plan.planes_bytes, 1), dtype=torch.uint8, device=eden.device)
         planes.copy_(ph[:max(plan.planes_bytes, 1)], non_blocking=True)
         scd = torch.from_numpy(sc).pin_memory().to(eden.device, non_blocking=True)
         sdd = torch.tensor(seeds, dtype=torch.int32).pin_memory().to(eden.device, non_blocking=True)
         y = codec.decode_arena(plan, planes, scd, sdd, stream=st)
-        yh[:max(plan.arena_numel, 1)].copy_(y[:max(plan.arena_numel, 1)], non_blocking=True)
-    st.synchronize()
+        for lo, hi in pieces:
+            e0, e1 = offs[lo], offs[hi - 1] + totals[hi - 1]
+            if e1 > e0:
+                yh[e0:e1].copy_(y[e0:e1], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(st)
+            events.append(ev)
     outs = [np.empty(totals[t], np.float32) for t in range(len(items))]
     ybase = yh.data_ptr()
-    _copy_many([o.ctypes.data for o in outs], [ybase + 4 * plan.elem_offsets[t] for t in range(len(items))],
-               [4 * totals[t] for t in range(len(items))])
+    for (lo, hi), ev in zip(pieces, events):
+        ev.synchronize()
+        _copy_many([outs[t].ctypes.data for t in range(lo, hi)], [ybase + 4 * offs[t] for t in range(lo, hi)],
+                   [4 * totals[t] for t in range(lo, hi)])
+    st.synchronize()
     del planes, y
     eden._trim()
     return outs
@@ -400,12 +446,14 @@ class EdenTransformer(Transformer):
         batch: the seeds' serial sums run in parallel host threads, then the
         np.random draws happen in tensor order exactly as per-tensor calls do."""
         arrays = [np.asarray(a) for a in arrays]
-
-        totals = _serial_sums([a.reshape(-1)[:_FAST_SEED_PREFIX] if self.seed_mode == "fast" else a.reshape(-1)
-                               for a in arrays])
-        seeds = eden_seeds(totals)
         big = [i for i, a in enumerate(arrays) if a.size > self.dim_threshold]
-        enc = _batch_encode(self.eden, [arrays[i] for i in big], [seeds[i] for i in big]) if big else []
+        # the seeds' serial sums (native threads, no GIL) run while this
+        # thread stages the Eden tensors and starts their H2D
+        sums = _threads().submit(_serial_sums, [a.reshape(-1)[:_FAST_SEED_PREFIX] if self.seed_mode == "fast"
+                                                else a.reshape(-1) for a in arrays])
+        staged = _batch_stage(self.eden, [arrays[i] for i in big]) if big else None
+        seeds = eden_seeds(sums.result())
+        enc = _batch_encode(self.eden, staged, [seeds[i] for i in big]) if big else []
         out = [None] * len(arrays)
         for i, (planes, scales, dims) in zip(big, enc):
             md = {"int_list": list(arrays[i].shape), "int_to_float": {0: float(seeds[i]), 1: float(arrays[i].size)}}

@@ -464,8 +464,9 @@ def test_step_graph_replay_bit_identical():
     x = torch.empty(plan.arena_numel, device=DEV).normal_(0, 0.01, generator=g)
     seeds = torch.tensor([11, 12, 13, 14, 15, 16], dtype=torch.int32, device=DEV)
     ws = torch.empty(max(plan.ws_bytes, 256), dtype=torch.uint8, device=DEV)
-    p0 = torch.empty(plan.planes_bytes, dtype=torch.uint8, device=DEV)
-    s0 = torch.empty(plan.n_slices, dtype=torch.float32, device=DEV)
+    # zero-filled: the alignment gaps between tensors' plane runs are never written
+    p0 = torch.zeros(plan.planes_bytes, dtype=torch.uint8, device=DEV)
+    s0 = torch.zeros(plan.n_slices, dtype=torch.float32, device=DEV)
     y0 = torch.zeros_like(x)
     plan.encode(x, seeds, p0, s0, ws)
     plan.decode(p0, seeds, s0, y0, ws)
