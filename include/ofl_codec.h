@@ -319,7 +319,10 @@ int ofl_apply_delta_ranges(const float* base, const float* delta, float* out, in
  * x: DEVICE float32 [n], every value an integer 0..31 (the ranks the lossy
  * pipelines write; anything else -> OFL_EINVAL, nothing written).  out: HOST
  * buffer of out_cap >= ofl_gzip_ranks_bound(n) bytes; *out_len = stream
- * length.  ws: device, ofl_gzip_ranks_workspace_bytes(n).  Synchronous.
+ * length.  When out is mapped pinned memory (hipHostMalloc, torch
+ * pin_memory) the kernels write the stream into it directly and the batches
+ * of members run without host round trips; pageable memory gets one D2H per
+ * batch.  ws: device, ofl_gzip_ranks_workspace_bytes(n).  Synchronous.
  * Errors: ofl_gzip_last_error(). */
 const char* ofl_gzip_last_error(void);
 size_t ofl_gzip_ranks_workspace_bytes(int64_t n);

@@ -753,7 +753,11 @@ __global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
 }
 
 // exclusive scan of the member sizes (one block) -> offsets, total at [n]
-__global__ __launch_bounds__(1024) void k_gzip_scan(const uint32_t* sizes, int n, uint64_t* off) {
+// running (nullable): the stream bytes of earlier batches, added to every
+// offset and advanced by this batch's total; cap: the output's size (a batch
+// that would not fit sets *bad = 2 and advances nothing)
+__global__ __launch_bounds__(1024) void k_gzip_scan(const uint32_t* sizes, int n, uint64_t* off, uint64_t* running,
+                                                    uint64_t cap, int* bad) {
     __shared__ uint64_t part[1024 / 64];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int per = (n + 1023) / 1024;
@@ -767,15 +771,25 @@ __global__ __launch_bounds__(1024) void k_gzip_scan(const uint32_t* sizes, int n
     }
     if (lane == 63) part[w] = inc;
     __syncthreads();
-    uint64_t base = inc - s;
+    const uint64_t run0 = running ? *running : 0;
+    uint64_t tot = 0;
+    for (int j = 0; j < 1024 / 64; ++j) tot += part[j];
+    const bool fits = run0 + tot <= cap;
+    uint64_t base = inc - s + run0;
     for (int j = 0; j < w; ++j) base += part[j];
-    for (int i = b0; i < b1; ++i) { off[i] = base; base += sizes[i]; }
+    for (int i = b0; i < b1; ++i) { off[i] = fits ? base : ~0ull; base += sizes[i]; }
     if (tid == 1023) off[n] = base;
+    __syncthreads();
+    if (tid == 0 && running) {
+        if (fits) *running = run0 + tot;
+        else atomicOr(bad, 2);
+    }
 }
 
 // members -> one contiguous stream
 __global__ __launch_bounds__(256) void k_gzip_pack(const uint8_t* slots, const uint32_t* sizes, const uint64_t* off,
                                                    uint8_t* packed) {
+    if (off[blockIdx.x] == ~0ull) return;  // the batch does not fit the output (reported by the scan)
     const uint8_t* src = slots + (int64_t)blockIdx.x * kOutBytes;
     uint8_t* dst = packed + off[blockIdx.x];
     for (uint32_t i = threadIdx.x; i < sizes[blockIdx.x]; i += 256) dst[i] = src[i];
@@ -1239,8 +1253,19 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
     uint8_t* packed = slots + (size_t)batch * gz::kOutBytes;
     uint32_t* sizes = reinterpret_cast<uint32_t*>(packed + (size_t)batch * gz::kOutBytes);
     uint64_t* off = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(sizes) + ((4 * (size_t)batch + 7) & ~(size_t)7));
-    int* bad = reinterpret_cast<int*>(off + batch + 1);
+    uint64_t* running = off + batch + 1;
+    int* bad = reinterpret_cast<int*>(running + 1);
     GZHIP(hipMemsetAsync(bad, 0, sizeof(int), st));
+    // out is mapped pinned host memory (e.g. torch pin_memory): the pack
+    // kernel writes the stream straight into it and the batches run back to
+    // back with one synchronisation at the end; otherwise one D2H per batch
+    uint8_t* dout = nullptr;
+    {
+        hipPointerAttribute_t pa;
+        if (hipPointerGetAttributes(&pa, out) == hipSuccess && pa.type == hipMemoryTypeHost && pa.devicePointer)
+            dout = static_cast<uint8_t*>(pa.devicePointer);
+        (void)hipGetLastError();  // a pageable pointer is not an error here
+    }
     // diagnostics: OFL_GZ_PHASES=1 prints the phase stamps (10 ns ticks) of
     // blocks 0..3 of the first launch to stderr
     static const bool phases = getenv("OFL_GZ_PHASES") != nullptr;
@@ -1248,11 +1273,32 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
     if (phases) GZHIP(hipMalloc(&d_ph, 8 * 4 * gz::kPhases));
     if (phases) GZHIP(hipMemsetAsync(d_ph, 0, 8 * 4 * gz::kPhases, st));
     size_t total = 0;
-    for (int64_t c0 = 0; c0 < members; c0 += batch) {
+    if (dout) {
+        GZHIP(hipMemsetAsync(running, 0, sizeof(uint64_t), st));
+        for (int64_t c0 = 0; c0 < members; c0 += batch) {
+            const int nb = (int)std::min<int64_t>(batch, members - c0);
+            gz::GzArgs a{x, n, c0, slots, sizes, bad, c0 == 0 ? d_ph : nullptr};
+            hipLaunchKernelGGL(gz::k_gzip_members, dim3(nb), dim3(gz::kNT), sizeof(gz::Smem), st, a);
+            hipLaunchKernelGGL(gz::k_gzip_scan, dim3(1), dim3(1024), 0, st, sizes, nb, off, running,
+                               (uint64_t)out_cap, bad);
+            hipLaunchKernelGGL(gz::k_gzip_pack, dim3(nb), dim3(256), 0, st, slots, sizes, off, dout);
+            GZHIP(hipGetLastError());
+        }
+        uint64_t tot = 0;
+        int badh = 0;
+        GZHIP(hipMemcpyAsync(&tot, running, 8, hipMemcpyDeviceToHost, st));
+        GZHIP(hipMemcpyAsync(&badh, bad, sizeof(int), hipMemcpyDeviceToHost, st));
+        GZHIP(hipStreamSynchronize(st));
+        if (badh & 1) return gzfail(OFL_EINVAL, "gzip ranks: values must be float32 integers 0..31");
+        if (badh & 2) return gzfail(OFL_ESPACE, "gzip ranks: output buffer too small");
+        total = tot;
+    }
+    for (int64_t c0 = 0; !dout && c0 < members; c0 += batch) {
         const int nb = (int)std::min<int64_t>(batch, members - c0);
         gz::GzArgs a{x, n, c0, slots, sizes, bad, c0 == 0 ? d_ph : nullptr};
         hipLaunchKernelGGL(gz::k_gzip_members, dim3(nb), dim3(gz::kNT), sizeof(gz::Smem), st, a);
-        hipLaunchKernelGGL(gz::k_gzip_scan, dim3(1), dim3(1024), 0, st, sizes, nb, off);
+        hipLaunchKernelGGL(gz::k_gzip_scan, dim3(1), dim3(1024), 0, st, sizes, nb, off, (uint64_t*)nullptr,
+                           ~0ull, bad);
         hipLaunchKernelGGL(gz::k_gzip_pack, dim3(nb), dim3(256), 0, st, slots, sizes, off, packed);
         GZHIP(hipGetLastError());
         uint64_t tot = 0;

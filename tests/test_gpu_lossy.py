@@ -342,6 +342,18 @@ def test_gzip_ranks_roundtrip(case):
     assert _lib.lib().ofl_gunzip_members(src.ctypes.data, src.size, None, 0, ctypes.byref(need), 4) == 0
     assert need.value == x.nbytes
     assert lossy.gunzip(z, 4).tobytes() == x.tobytes()
+    # pageable output (one D2H per batch) gives the same stream as the pinned one
+    # (the kernels write into mapped pinned memory directly)
+    from openfl_amd import _lib as LB
+    xd = torch.from_numpy(x).to(DEV)
+    L = LB.lib()
+    cap = int(L.ofl_gzip_ranks_bound(x.size))
+    pageable = np.zeros(cap, np.uint8)
+    wsb = torch.empty(int(L.ofl_gzip_ranks_workspace_bytes(x.size)), dtype=torch.uint8, device=DEV)
+    ln = ctypes.c_size_t()
+    LB.check_gzip(L.ofl_gzip_ranks(xd.data_ptr(), x.size, pageable.ctypes.data, cap, ctypes.byref(ln), wsb.data_ptr(),
+                                   wsb.numel(), torch.cuda.current_stream().cuda_stream))
+    assert pageable[:ln.value].tobytes() == z
     # and the device inflate (ofl_inflate_members) straight into HBM
     out = torch.full((x.nbytes + 64,), 7, dtype=torch.uint8, device=DEV)
     got = lossy.gunzip_device(z, out)
