@@ -1186,34 +1186,104 @@ void crc_matrices(uint32_t (&m)[32][32]) {
 // the members of a member-indexed stream (every header carries the 'BC'
 // size field): deflate data range, output offset, ISIZE and CRC-32 of each
 struct GzMember { size_t in, in_len, out; uint32_t isize, crc; };
-int parse_members(const uint8_t* src, size_t n, std::vector<GzMember>& mem, size_t& total) {
-    size_t pos = 0;
-    total = 0;
-    mem.clear();
-    while (pos < n) {
-        const uint8_t* h = src + pos;
-        if (n - pos < 26 || h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || h[3] != 0x04)
-            return gzfail(OFL_EFORMAT, "gunzip: not a member-indexed gzip stream");
-        const size_t xlen = (size_t)h[10] | ((size_t)h[11] << 8);
-        size_t bsize = 0;
-        for (size_t q = 12; q + 4 <= 12 + xlen && 12 + xlen <= n - pos;) {
-            const size_t sl = (size_t)h[q + 2] | ((size_t)h[q + 3] << 8);
-            if (h[q] == 'B' && h[q + 1] == 'C' && sl == 2) bsize = ((size_t)h[q + 4] | ((size_t)h[q + 5] << 8)) + 1;
-            q += 4 + sl;
-        }
-        if (bsize < 12 + xlen + 8 || bsize > n - pos)
-            return gzfail(OFL_EFORMAT, "gunzip: not a member-indexed gzip stream");
-        const uint8_t* t = src + pos + bsize - 8;
-        GzMember m;
-        m.in = pos + 12 + xlen;
-        m.in_len = bsize - 12 - xlen - 8;
-        m.crc = (uint32_t)t[0] | ((uint32_t)t[1] << 8) | ((uint32_t)t[2] << 16) | ((uint32_t)t[3] << 24);
-        m.isize = (uint32_t)t[4] | ((uint32_t)t[5] << 8) | ((uint32_t)t[6] << 16) | ((uint32_t)t[7] << 24);
-        m.out = total;
-        total += m.isize;
-        mem.push_back(m);
-        pos += bsize;
+// one member at pos: its size (0 if the bytes there are not a member header
+// with the 'BC' field) and its record
+size_t member_at(const uint8_t* src, size_t n, size_t pos, GzMember& m) {
+    const uint8_t* h = src + pos;
+    if (n - pos < 26 || h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || h[3] != 0x04) return 0;
+    const size_t xlen = (size_t)h[10] | ((size_t)h[11] << 8);
+    size_t bsize = 0;
+    for (size_t q = 12; q + 4 <= 12 + xlen && 12 + xlen <= n - pos;) {
+        const size_t sl = (size_t)h[q + 2] | ((size_t)h[q + 3] << 8);
+        if (h[q] == 'B' && h[q + 1] == 'C' && sl == 2) bsize = ((size_t)h[q + 4] | ((size_t)h[q + 5] << 8)) + 1;
+        q += 4 + sl;
     }
+    if (bsize < 12 + xlen + 8 || bsize > n - pos) return 0;
+    const uint8_t* t = src + pos + bsize - 8;
+    m.in = pos + 12 + xlen;
+    m.in_len = bsize - 12 - xlen - 8;
+    m.crc = (uint32_t)t[0] | ((uint32_t)t[1] << 8) | ((uint32_t)t[2] << 16) | ((uint32_t)t[3] << 24);
+    m.isize = (uint32_t)t[4] | ((uint32_t)t[5] << 8) | ((uint32_t)t[6] << 16) | ((uint32_t)t[7] << 24);
+    return bsize;
+}
+
+// walk the member chain over [pos, end); false if a header is not one.
+// out offsets are relative to the walk's start
+bool walk_members(const uint8_t* src, size_t n, size_t pos, size_t end, std::vector<GzMember>& mem, size_t& reached) {
+    size_t out = 0;
+    while (pos < end) {
+        GzMember m;
+        const size_t bs = member_at(src, n, pos, m);
+        if (!bs) return false;
+        m.out = out;
+        out += m.isize;
+        mem.push_back(m);
+        pos += bs;
+    }
+    reached = pos;
+    return true;
+}
+
+// The chain is a dependent walk (each header gives the next one's offset), so
+// one thread pays a cache miss per member.  Large streams are cut in pieces;
+// each thread finds the first header at or after its piece's start (the 'BC'
+// member signature) and walks to the end of its piece; the pieces are then
+// checked to link exactly (thread k's walk ends where thread k+1's starts), so
+// a signature found inside compressed data can only send the parse back to
+// the serial walk, never give a wrong index.
+int parse_members(const uint8_t* src, size_t n, std::vector<GzMember>& mem, size_t& total) {
+    mem.clear();
+    total = 0;
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const int nt = (int)std::min<size_t>(std::min<unsigned>(hw, 16u), n >> 22);  // >= 4 MiB per piece
+    bool par_ok = nt > 1;
+    if (par_ok) {
+        std::vector<std::vector<GzMember>> part(nt);
+        std::vector<size_t> start(nt + 1, n), reached(nt, 0);
+        std::vector<char> ok(nt, 0);
+        auto work = [&](int t) {
+            size_t p = n * t / nt;
+            const size_t lim = n * (t + 1) / nt;
+            if (t > 0) {  // the first member signature at or after p
+                GzMember m;
+                while (p < lim) {
+                    const uint8_t* h = src + p;
+                    if (h[0] == 0x1f && p + 16 <= n && h[1] == 0x8b && h[2] == 8 && h[3] == 4 && h[12] == 'B' &&
+                        h[13] == 'C' && member_at(src, n, p, m))
+                        break;
+                    ++p;
+                }
+            }
+            start[t] = p;
+            ok[t] = p < lim && walk_members(src, n, p, lim, part[t], reached[t]);
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
+        work(0);
+        for (auto& x : th) x.join();
+        // members are <= 64 KiB and pieces >= 4 MiB: every piece holds a
+        // header; piece t's walk (from a true header, by induction from 0)
+        // ends on a true header, which must be where piece t + 1 starts
+        par_ok = start[0] == 0;
+        for (int t = 0; t < nt && par_ok; ++t)
+            par_ok = ok[t] && !part[t].empty() && reached[t] == (t + 1 < nt ? start[t + 1] : n);
+        if (par_ok) {
+            size_t cnt = 0;
+            for (auto& p : part) cnt += p.size();
+            mem.reserve(cnt);
+            for (auto& p : part) mem.insert(mem.end(), p.begin(), p.end());
+            for (GzMember& m : mem) { m.out = total; total += m.isize; }  // absolute output offsets
+            return OFL_OK;
+        }
+        mem.clear();
+        total = 0;
+    }
+    size_t reached0 = 0;
+    if (!walk_members(src, n, 0, n, mem, reached0)) {
+        mem.clear();
+        return gzfail(OFL_EFORMAT, "gunzip: not a member-indexed gzip stream");
+    }
+    for (const GzMember& m : mem) total += m.isize;
     return OFL_OK;
 }
 }  // namespace

@@ -3,6 +3,8 @@ GZIPTransformer.backward fast path; kc_pipeline.py:152-156 gzip.decompress).
 CPU only: streams are built here with zlib in the device gzip's member format
 (RFC 1952 header with the 'BC' extra field = member size - 1)."""
 import gzip
+import struct
+
 import numpy as np
 import pytest
 
@@ -71,3 +73,27 @@ def test_member_index_for_the_device_inflate():
     plain = np.frombuffer(gzip.compress(raw), np.uint8)
     assert L.ofl_gzip_member_index(plain.ctypes.data, plain.size, None, 0, ctypes.byref(nm), ctypes.byref(tot),
                                    ctypes.byref(mx)) == _lib.OFL_EFORMAT
+
+
+@pytest.mark.parametrize("fake", [False, True])
+def test_large_stream_parallel_index(fake):
+    """Streams above 8 MiB are indexed by several threads that each look for
+    the first member signature in their piece, then must link up exactly; a
+    signature planted in stored (level 0) data makes a piece start on a fake
+    header, which the linkage check rejects (serial walk, same index)."""
+    rng = np.random.default_rng(11)
+    raw = bytearray(rng.integers(0, 256, 24 << 20, dtype=np.uint8).tobytes())
+    if fake:  # a fake 'BC' member header every 700 KB (verbatim in stored blocks)
+        sig = bytes([0x1F, 0x8B, 8, 4, 0, 0, 0, 0, 0, 0xFF, 6, 0]) + b"BC" + struct.pack("<HH", 2, 99)
+        for off in range(1000, len(raw) - 64, 700_000):
+            raw[off:off + len(sig)] = sig
+    raw = bytes(raw)
+    z = member_indexed(raw, chunk=60_000, level=0)
+    assert lossy.gunzip(z, 8).tobytes() == raw
+    import ctypes
+    L = _lib.lib()
+    src = np.frombuffer(z, np.uint8)
+    nm, tot, mx = ctypes.c_int64(), ctypes.c_size_t(), ctypes.c_uint32()
+    assert L.ofl_gzip_member_index(src.ctypes.data, src.size, None, 0, ctypes.byref(nm), ctypes.byref(tot),
+                                   ctypes.byref(mx)) == 0
+    assert nm.value == -(-len(raw) // 60_000) and tot.value == len(raw)
