@@ -261,14 +261,21 @@ def gzip_ranks(x):
     if n == 0:
         return gzip.compress(b"", compresslevel=9)
     ws = _ws_bytes(x.device, int(L.ofl_gzip_ranks_workspace_bytes(n)))
-    cap = int(L.ofl_gzip_ranks_bound(n))
-    out = getattr(_tls, "gz_out", None)
-    if out is None or out.numel() < cap:
-        out = _tls.gz_out = torch.empty(cap, dtype=torch.uint8).pin_memory()
-    ln = ctypes.c_size_t()
-    _lib.check_gzip(L.ofl_gzip_ranks(x.data_ptr(), n, out.data_ptr(), cap, ctypes.byref(ln), ws.data_ptr(),
-                                     ws.numel(), _stream(x.device)))
-    return out[:ln.value].numpy().tobytes()
+    bound = int(L.ofl_gzip_ranks_bound(n))
+    # pinned output sized for a rank stream (a quarter of the input: rank
+    # streams compress to 0.05-0.2); the worst-case bound (8x the input) only
+    # after an OFL_ESPACE
+    for cap in (min(bound, n + (1 << 20)), bound):
+        out = _buf("host", "gz_out", cap, pinned=True)
+        ln = ctypes.c_size_t()
+        rc = L.ofl_gzip_ranks(x.data_ptr(), n, out.data_ptr(), cap, ctypes.byref(ln), ws.data_ptr(), ws.numel(),
+                              _stream(x.device))
+        if rc != _lib.OFL_ESPACE or cap == bound:
+            break
+    _lib.check_gzip(rc)
+    payload = out[:ln.value].numpy().tobytes()
+    _trim_bufs()
+    return payload
 
 
 def gunzip(data, threads=8, out=None):
@@ -307,6 +314,18 @@ def _parallel_copy(dst, src, nbytes, threads=8, piece=4 << 20):
     d = (np.uint64(dst) + offs.astype(np.uint64))
     s = (np.uint64(src) + offs.astype(np.uint64))
     _lib.check(_lib.lib().ofl_host_copy_many(offs.size, d.ctypes.data, s.ctypes.data, sizes.ctypes.data, threads))
+
+
+_RETAIN_BYTES = 512 << 20
+
+
+def _trim_bufs():
+    """Release this thread's scratch buffers above _RETAIN_BYTES (after the
+    call that needed them): a one-off large call does not keep gigabytes
+    pinned per thread."""
+    bufs = getattr(_tls, "bufs", None) or {}
+    for k in [k for k, b in bufs.items() if b.numel() * b.element_size() > _RETAIN_BYTES]:
+        del bufs[k]
 
 
 def _buf(device, name, nbytes, pinned=False):
@@ -366,6 +385,7 @@ def gunzip_device(data, out):
     ws = _buf(dev, "gz_status", 256)
     _lib.check_gzip(L.ofl_inflate_members(d_in.data_ptr(), d_in.data_ptr() + ioff, nm.value, mx.value, out.data_ptr(),
                                           out.numel(), ws.data_ptr(), ws.numel(), _stream(dev)))
+    _trim_bufs()
     return out[:tot.value]
 
 
