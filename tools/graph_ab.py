@@ -32,7 +32,8 @@ def run(name, steps, warmup, streams):
         o = plan.elem_offsets[j]
         x[o:o + n].normal_(0.0, 0.01, generator=g)
     y = torch.zeros_like(x)
-    planes = torch.empty(max(plan.planes_bytes, 1), dtype=torch.uint8, device=dev)
+    # zero-filled: the alignment gaps between tensors' plane runs are never written
+    planes = torch.zeros(max(plan.planes_bytes, 1), dtype=torch.uint8, device=dev)
     scales = torch.empty(max(plan.n_slices, 1), dtype=torch.float32, device=dev)
     ws = torch.empty(max(plan.ws_bytes, 256), dtype=torch.uint8, device=dev)
     seeds = torch.tensor(np.random.RandomState(1).randint(0, 2 ** 16, size=len(numels)), dtype=torch.int32,
