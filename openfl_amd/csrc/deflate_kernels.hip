@@ -123,7 +123,7 @@ DEVI uint32_t tk4(const uint8_t* tk, int o) {
 }
 constexpr int kMinMatch = 3;    // tokens (12 bytes); shorter runs use the one-token op
 constexpr int kMaxMatch = 64;   // tokens (256 of deflate's 258 bytes)
-constexpr int kCand = 8;        // nearest earlier positions with the same 3-token key tried (32: ratio 0.1381 vs 0.1386, 15 % slower)
+constexpr int kCand = 4;        // nearest earlier positions with the same 3-token key tried (KC ranks: 4 -> ratio 0.1406, 8 -> 0.1390 at 2x the match time, 32 -> 0.1381)
 
 // advance by 2^k zero bytes (k uniform: the matrix columns are scalar loads)
 DEVI uint32_t crc_adv_pow2(uint32_t v, int k) {
