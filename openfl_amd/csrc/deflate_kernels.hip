@@ -588,34 +588,57 @@ __global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
     __syncthreads();
     if (wv == 1) huff_codes_wave(S.ll, kLit, S.kl);
     if (wv == 2) huff_codes_wave(S.ld, kDist, S.kd);
-    if (tid == 0) {
+    if (wv == 0) {
+        // run-length code of the concatenated code lengths: the wave finds
+        // the used lengths' extents and the run starts by ballots; lane 0
+        // then walks the runs (a few dozen) instead of every length
         HScratch& h = S.u.h;
-        int nlit = kLit;
-        while (nlit > 257 && S.ll[nlit - 1] == 0) --nlit;
-        int ndist = kDist;
-        while (ndist > 1 && S.ld[ndist - 1] == 0) --ndist;
-        // run-length code of the concatenated code lengths
-        const int N = nlit + ndist;
-        int nr = 0;
-        for (int i = 0; i < N;) {
-            const uint8_t cur = i < nlit ? S.ll[i] : S.ld[i - nlit];
-            int run = 1;
-            while (i + run < N && (i + run < nlit ? S.ll[i + run] : S.ld[i + run - nlit]) == cur) ++run;
-            int left = run;
-            if (cur == 0) {
-                while (left >= 11) { const int r = left < 138 ? left : 138; h.rle_sym[nr] = 18; h.rle_ext[nr++] = (uint16_t)(r - 11); left -= r; }
-                if (left >= 3) { h.rle_sym[nr] = 17; h.rle_ext[nr++] = (uint16_t)(left - 3); left = 0; }
-                while (left > 0) { h.rle_sym[nr] = 0; h.rle_ext[nr++] = 0; --left; }
-            } else {
-                h.rle_sym[nr] = cur; h.rle_ext[nr++] = 0; --left;
-                while (left >= 3) { const int r = left < 6 ? left : 6; h.rle_sym[nr] = 16; h.rle_ext[nr++] = (uint16_t)(r - 3); left -= r; }
-                while (left > 0) { h.rle_sym[nr] = cur; h.rle_ext[nr++] = 0; --left; }
-            }
-            i += run;
+        int nlit = 257, ndist = 1;
+        for (int c = 0; c < (kLit + 63) / 64; ++c) {
+            const int i = 64 * c + ln;
+            const uint64_t m = __ballot(i < kLit && S.ll[i] != 0);
+            if (m) nlit = max(nlit, 64 * c + 64 - __builtin_clzll(m));
         }
-        for (int i = 0; i < nr; ++i) S.hc[h.rle_sym[i]]++;
-        S.nrle = (uint32_t)nr;
-        S.nlit_ndist = (uint32_t)(nlit | (ndist << 16));
+        {
+            const uint64_t m = __ballot(ln < kDist && S.ld[ln] != 0);
+            if (m) ndist = max(ndist, 64 - __builtin_clzll(m));
+        }
+        const int N = nlit + ndist;
+        auto val = [&](int i) -> int { return i < nlit ? S.ll[i] : S.ld[i - nlit]; };
+        uint64_t starts[(kLit + kDist + 63) / 64];
+#pragma unroll
+        for (int c = 0; c < (kLit + kDist + 63) / 64; ++c) {
+            const int i = 64 * c + ln;
+            starts[c] = __ballot(i < N && (i == 0 || val(i) != val(i - 1)));
+        }
+        if (ln == 0) {
+            int nr = 0;
+            int c = 0;
+            uint64_t m = starts[0];
+            int s0 = 0;  // the run start being emitted (position 0 always starts one)
+            m &= m - 1;
+            for (;;) {
+                while (!m && c + 1 < (kLit + kDist + 63) / 64) m = starts[++c];
+                const int s1 = m ? 64 * c + __builtin_ctzll(m) : N;
+                if (m) m &= m - 1;
+                const int cur = val(s0);
+                int left = s1 - s0;
+                if (cur == 0) {
+                    while (left >= 11) { const int r = left < 138 ? left : 138; h.rle_sym[nr] = 18; h.rle_ext[nr++] = (uint16_t)(r - 11); left -= r; }
+                    if (left >= 3) { h.rle_sym[nr] = 17; h.rle_ext[nr++] = (uint16_t)(left - 3); left = 0; }
+                    while (left > 0) { h.rle_sym[nr] = 0; h.rle_ext[nr++] = 0; --left; }
+                } else {
+                    h.rle_sym[nr] = (uint16_t)cur; h.rle_ext[nr++] = 0; --left;
+                    while (left >= 3) { const int r = left < 6 ? left : 6; h.rle_sym[nr] = 16; h.rle_ext[nr++] = (uint16_t)(r - 3); left -= r; }
+                    while (left > 0) { h.rle_sym[nr] = (uint16_t)cur; h.rle_ext[nr++] = 0; --left; }
+                }
+                if (s1 >= N) break;
+                s0 = s1;
+            }
+            for (int i = 0; i < nr; ++i) S.hc[h.rle_sym[i]]++;
+            S.nrle = (uint32_t)nr;
+            S.nlit_ndist = (uint32_t)(nlit | (ndist << 16));
+        }
     }
     __syncthreads();
     if (wv == 0) {
@@ -628,25 +651,36 @@ __global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
         const int nr = (int)S.nrle, nlit = (int)(S.nlit_ndist & 0xffffu), ndist = (int)(S.nlit_ndist >> 16);
         int ncl = kCL;
         while (ncl > 4 && S.lc[c_clord[ncl - 1]] == 0) --ncl;
-        uint32_t pos = 0;
+        // thread 0 owns the header's words: a 64-bit accumulator and plain
+        // stores (the ops' first word is OR-ed in after the barrier)
+        uint64_t acc = 0;
+        int nb = 0;
+        uint32_t wi = 0, pos = 0;
+        auto put = [&](uint32_t v, int n) {
+            acc |= (uint64_t)v << nb;
+            nb += n;
+            pos += (uint32_t)n;
+            if (nb >= 32) { S.out[wi++] = (uint32_t)acc; acc >>= 32; nb -= 32; }
+        };
         // member header with a BGZF-style extra field (RFC 1952 FEXTRA,
         // subfield 'BC' = member size - 1, filled in at the end): a reader
         // can find every member without inflating (ofl_gunzip_members);
         // gzip.decompress skips the field
         const uint8_t hdr[kHdr] = {0x1f, 0x8b, 0x08, 0x04, 0, 0, 0, 0, 0x00, 0xff, 6, 0, 'B', 'C', 2, 0, 0, 0};
-        for (int i = 0; i < kHdr; ++i) { put_bits(S.out, pos, hdr[i], 8); pos += 8; }
-        put_bits(S.out, pos, 1u, 1); pos += 1;          // BFINAL
-        put_bits(S.out, pos, 2u, 2); pos += 2;          // BTYPE = dynamic
-        put_bits(S.out, pos, (uint32_t)(nlit - 257), 5); pos += 5;
-        put_bits(S.out, pos, (uint32_t)(ndist - 1), 5); pos += 5;
-        put_bits(S.out, pos, (uint32_t)(ncl - 4), 4); pos += 4;
-        for (int i = 0; i < ncl; ++i) { put_bits(S.out, pos, S.lc[c_clord[i]], 3); pos += 3; }
+        for (int i = 0; i < kHdr; ++i) put(hdr[i], 8);
+        put(1u, 1);  // BFINAL
+        put(2u, 2);  // BTYPE = dynamic
+        put((uint32_t)(nlit - 257), 5);
+        put((uint32_t)(ndist - 1), 5);
+        put((uint32_t)(ncl - 4), 4);
+        for (int i = 0; i < ncl; ++i) put(S.lc[c_clord[i]], 3);
         for (int i = 0; i < nr; ++i) {
             const int sy = h.rle_sym[i];
-            put_bits(S.out, pos, S.kc[sy], S.lc[sy]); pos += S.lc[sy];
+            put(S.kc[sy], S.lc[sy]);
             const int eb = sy == 16 ? 2 : (sy == 17 ? 3 : (sy == 18 ? 7 : 0));
-            put_bits(S.out, pos, h.rle_ext[i], eb); pos += eb;
+            put(h.rle_ext[i], eb);
         }
+        if (nb > 0) S.out[wi] = (uint32_t)acc;
         S.hdr_bits = pos;
     }
     __syncthreads();
