@@ -344,8 +344,7 @@ int ofl_gunzip_members(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, s
  * inflates every member (one wavefront each; stored, fixed and dynamic
  * blocks) from src (DEVICE copy of the stream) into out (DEVICE, out_cap
  * bytes) at its output offset, checking ISIZE and CRC-32; index is the DEVICE
- * copy of the index; members must produce <= 64 KiB each (OFL_EFORMAT
- * otherwise); ws: DEVICE, >= 256 bytes.  Synchronous; OFL_EINVAL for corrupt
+ * copy of the index (any member size); ws: DEVICE, >= 256 bytes.  Synchronous; OFL_EINVAL for corrupt
  * data (what gzip.decompress would raise on). */
 int ofl_gzip_member_index(const uint8_t* src, size_t n, int64_t* index, int64_t cap_members, int64_t* nmembers,
                           size_t* out_len, uint32_t* max_isize);
