@@ -149,3 +149,25 @@ def test_host_copy_many_and_serial_sums_many():
         ref = _serial_sum(f)
         assert g == ref and type(g) is type(ref)
     assert _lib.lib().ofl_host_copy_many(0, None, None, None, 4) == 0
+
+
+def test_one_call_host_entry_points_check_their_block_layout():
+    """ofl_eden_encode_host / _decode_host validate the caller's pinned / device
+    block layout against the plan before touching the GPU (OFL_EINVAL)."""
+    import ctypes
+    from openfl_amd import _lib
+    from openfl_amd.codec import EdenPlan
+    L = _lib.lib()
+    p = EdenPlan([1000], n_bits=8)
+    buf = ctypes.create_string_buffer(1 << 16)
+    a = ctypes.addressof(buf)
+    pb, ns = p.planes_bytes, p.n_slices
+    # encode: seeds must sit after the x arena, scales after the planes
+    assert L.ofl_eden_encode_host(p.handle, a, a, 8192, 4 * 1000 - 4, a, a, 8192, 1024, None, 0, None) == _lib.OFL_EINVAL
+    assert L.ofl_eden_encode_host(p.handle, a, a, 8192, 4096, a, a, pb + 4 * ns, pb - 1, None, 0, None) == _lib.OFL_EINVAL
+    assert L.ofl_eden_encode_host(p.handle, a, a, 4096, 4096, a, a, 8192, 1024, None, 0, None) == _lib.OFL_EINVAL
+    # decode: scales after the planes, seeds after the scales, y no longer than the arena
+    assert L.ofl_eden_decode_host(p.handle, a, a, 8192, pb - 1, 4096, a, a, 4000, None, 0, None) == _lib.OFL_EINVAL
+    assert L.ofl_eden_decode_host(p.handle, a, a, 8192, 256, 256, a, a, 4000, None, 0, None) == _lib.OFL_EINVAL
+    assert L.ofl_eden_decode_host(p.handle, a, a, 8192, 256, 1024, a, a, 4004, None, 0, None) == _lib.OFL_EINVAL
+    assert L.ofl_eden_encode_host(None, a, a, 8192, 4096, a, a, 8192, 1024, None, 0, None) == _lib.OFL_EINVAL
