@@ -358,8 +358,13 @@ def gunzip_device(data, out):
     L = _lib.lib()
     src = np.frombuffer(data, np.uint8)
     nm, tot, mx = ctypes.c_int64(), ctypes.c_size_t(), ctypes.c_uint32()
-    rc = L.ofl_gzip_member_index(src.ctypes.data if src.size else None, src.size, None, 0, ctypes.byref(nm),
-                                 ctypes.byref(tot), ctypes.byref(mx)) if src.size else _lib.OFL_EFORMAT
+    # one pass over the headers: a member takes >= 26 bytes, so n // 26 + 1
+    # entries always suffice (untouched pages of the array cost nothing)
+    cap = src.size // 26 + 1
+    idx = np.empty((cap, 4), np.int64)
+    rc = L.ofl_gzip_member_index(src.ctypes.data if src.size else None, src.size, idx.ctypes.data, cap,
+                                 ctypes.byref(nm), ctypes.byref(tot), ctypes.byref(mx)) if src.size \
+        else _lib.OFL_EFORMAT
     if rc == _lib.OFL_EFORMAT:
         raw = np.frombuffer(gzip.decompress(bytes(data)), np.uint8)
         if raw.size > out.numel():
@@ -370,9 +375,7 @@ def gunzip_device(data, out):
     _lib.check_gzip(rc)
     if tot.value > out.numel():
         raise _lib.CodecError("gunzip_device: output buffer too small")
-    idx = np.empty((nm.value, 4), np.int64)
-    _lib.check_gzip(L.ofl_gzip_member_index(src.ctypes.data, src.size, idx.ctypes.data, nm.value, ctypes.byref(nm),
-                                            ctypes.byref(tot), ctypes.byref(mx)))
+    idx = idx[:nm.value]
     dev = out.device
     ioff = (src.size + 7) // 8 * 8  # the stream, then the index, in one H2D
     need = ioff + idx.nbytes
