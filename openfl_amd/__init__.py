@@ -10,3 +10,10 @@ select it with
       settings: {n_bits: 8, dim_threshold: 100, device: cuda:0}
 """
 __version__ = "0.1.0"
+
+import os as _os
+
+if _os.environ.get("OFL_HOST_KEEP_LARGE_BLOCKS") == "1":  # opt-in host-memory policy (openfl_amd/hostmem.py)
+    from openfl_amd.hostmem import keep_large_blocks as _keep
+
+    _keep()
