@@ -97,15 +97,10 @@ struct KArgs {
     const float* yadd;      // decode: nullable, y = yadd + decoded (apply_delta, float32 add)
 };
 
-// Eden tables in global memory (copied to LDS per workgroup)
+// Eden centroids in global memory (copied to LDS per workgroup); the
+// bucketize boundaries live in the quantiser table below
 __device__ const float g_centroids[8][256] = {
 #include "eden_centroids.inc"
-};
-__device__ const unsigned char g_grid[8][EDEN_GRID_CELLS] = {
-#include "eden_grid.inc"
-};
-__device__ const float g_bounds[8][256] = {
-#include "eden_bounds.inc"
 };
 
 // ---------------------------------------------------------------------------
@@ -271,16 +266,41 @@ DEVI float block_sum(float v, float* red) {
 struct QEnt { float b64; int lo; float clo; float chi; };
 struct QTab { QEnt grid[EDEN_GRID_CELLS]; };
 
+// The entries are built at compile time from the same generated tables, so a
+// workgroup's copy into LDS is independent 16-byte loads (one memory latency)
+// instead of a grid -> bounds/centroids chain of dependent loads per entry.
+namespace qtab_gen {
+constexpr float centroids[8][256] = {
+#include "eden_centroids.inc"
+};
+constexpr unsigned char grid[8][EDEN_GRID_CELLS] = {
+#include "eden_grid.inc"
+};
+constexpr float bounds[8][256] = {
+#include "eden_bounds.inc"
+};
+struct QTabs { QTab t[8]; };
+constexpr QTabs make() {
+    QTabs r{};
+    for (int n = 0; n < 8; ++n) {
+        const int nb = (1 << (n + 1)) - 1;
+        for (int k = 0; k < EDEN_GRID_CELLS; ++k) {
+            const int lo = grid[n][k];
+            const bool top = lo >= nb;
+            r.t[n].grid[k] = QEnt{top ? __builtin_huge_valf() : bounds[n][lo] * 64.0f, lo, centroids[n][lo],
+                                  top ? centroids[n][lo] : centroids[n][lo + 1]};
+        }
+    }
+    return r;
+}
+}  // namespace qtab_gen
+__device__ const qtab_gen::QTabs g_qtabs = qtab_gen::make();
+
 template <int NT>
 DEVI void load_qtable(QTab* q, int nbits) {
-    const int nb = (1 << nbits) - 1;
-    const float* cen = g_centroids[nbits - 1];
-    for (int k = threadIdx.x; k < EDEN_GRID_CELLS; k += NT) {
-        const int lo = g_grid[nbits - 1][k];
-        const bool top = lo >= nb;
-        q->grid[k] = QEnt{top ? __int_as_float(0x7f800000) : g_bounds[nbits - 1][lo] * 64.0f, lo, cen[lo],
-                          top ? cen[lo] : cen[lo + 1]};
-    }
+    const float4* src = reinterpret_cast<const float4*>(&g_qtabs.t[nbits - 1]);
+    float4* dst = reinterpret_cast<float4*>(q);
+    for (int k = threadIdx.x; k < EDEN_GRID_CELLS; k += NT) dst[k] = src[k];
 }
 
 // bucketize + centroid (exact, one compare): returns bin, writes centroid.
