@@ -1907,6 +1907,16 @@ bool use_small_stream() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_SMALLSTREAM"); return !(s && s[0] == '0'); }();
     return on;
 }
+// OFL_EDEN_SPLIT_MIB=m: two-stream plans split their large slices into two
+// waves only above m MiB of intermediates; unset (-1): see build_schedule
+int64_t split_min_bytes() {
+    static const int64_t b = [] {
+        const char* s = getenv("OFL_EDEN_SPLIT_MIB");
+        const int64_t m = (s && *s) ? strtoll(s, nullptr, 10) : -1;
+        return m < 0 ? -1 : m << 20;
+    }();
+    return b;
+}
 // one k_col_multi launch per wave for the single-level heights 1..5
 bool use_colmulti() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_COLMULTI"); return !(s && s[0] == '0'); }();
@@ -2132,9 +2142,16 @@ void build_schedule(ofl_eden_plan* pl) {
     for (auto& D : pl->slices) D.perm = 0;
     std::vector<std::vector<int32_t>> waves;
     int64_t cap = pl->wave_bytes > 0 ? pl->wave_bytes / 4 : INT64_MAX;
-    if (pl->nstreams == 2) {  // at least two waves, so both streams have work
-        int64_t tot = 0;
-        for (int32_t si : large) tot += 1ll << pl->slices[si].logp;
+    int64_t tot = 0;
+    for (int32_t si : large) tot += 1ll << pl->slices[si].logp;
+    // two streams: at least two waves, so both streams have work -- unless
+    // every large slice fits one wave and no small-slice launches could use
+    // the second stream (the 1 GiB set: one wave on one stream, 2.24 vs
+    // 2.29 ms; ResNet-50 keeps its two waves beside the small slices: 360
+    // vs 369 us with one wave; OFL_EDEN_SPLIT_MIB=m splits above m MiB)
+    const int64_t split_min = split_min_bytes();
+    const bool split = split_min >= 0 ? 4 * tot > split_min : (!common.empty() || tot > cap);
+    if (pl->nstreams == 2 && split) {
         cap = std::min(cap, std::max<int64_t>(1, (tot + 1) / 2));
     }
     int64_t acc = 0, wmax = 0;
@@ -2150,20 +2167,27 @@ void build_schedule(ofl_eden_plan* pl) {
     // the tiny / small slices are independent of the waves: with two wave
     // streams they get a third (or, OFL_EDEN_SMALLSTREAM=0, the wave stream
     // with fewer large-slice elements)
+    bool small_own = false;
     if (nbuf == 2) {
         if (use_small_stream()) {  // their own stream: latency-bound, they fill CUs beside both waves
             for (Launch& l : common) l.stream = 2;
+            small_own = true;
         } else {
             int64_t load[2] = {0, 0};
             for (size_t w = 0; w < waves.size(); ++w)
                 for (int32_t si : waves[w]) load[w % 2] += 1ll << pl->slices[si].logp;
             for (Launch& l : common) l.stream = load[1] < load[0] ? 1 : 0;
         }
+    } else if (pl->nstreams == 2 && !waves.empty() && use_small_stream()) {
+        // one wave (too few tiles to split): the small slices run beside it
+        // on the side stream
+        for (Launch& l : common) l.stream = 1;
+        small_own = true;
     }
     // on their own stream the small-slice launches are enqueued after the
     // waves' (the critical path reaches the GPU first; each host enqueue costs
     // microseconds); on a shared stream they go first as before
-    const bool small_last = !common.empty() && common[0].stream == 2;
+    const bool small_last = !common.empty() && small_own;
     pl->enc = small_last ? std::vector<Launch>{} : common;
     pl->dec = small_last ? std::vector<Launch>{} : common;
     pl->ws_floats = nbuf * wmax;
