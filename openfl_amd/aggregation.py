@@ -27,7 +27,7 @@ GPU every call raises CodecError.
 import numpy as np
 import torch
 
-from openfl_amd import _lib
+from openfl_amd import _lib, hostmem
 from openfl_amd.codec import EdenPlan, resolve_device
 from openfl_amd.pipelines.eden_pipeline import _FAST_SEED_PREFIX
 
@@ -278,7 +278,7 @@ class RoundEnd:
                         for k, (s, d) in enumerate(zip(sn[fs:fs + len(p.dims[t])], p.dims[t])):
                             md[2 + 2 * k] = float(s)
                             md[3 + 2 * k] = float(d)
-                        result[i] = (pn[po:po + pb].tobytes(), [{"int_list": list(self.shapes[i]), "int_to_float": md}])
+                        result[i] = (hostmem.bytes_from(pn.ctypes.data + po, pb), [{"int_list": list(self.shapes[i]), "int_to_float": md}])
                 if base_arena is not None:  # decode + apply_delta fused: out = base + decoded
                     if out is None:
                         out = torch.empty(self.arena_numel, dtype=torch.float32, device=dev)
@@ -291,7 +291,7 @@ class RoundEnd:
                     dh = torch.cat([delta[self.offsets[i]:self.offsets[i] + self.numels[i]] for i in small]).cpu().numpy()
                     o = 0
                     for i in small:
-                        result[i] = (dh[o:o + self.numels[i]].tobytes(), [{"int_list": list(self.shapes[i])}])
+                        result[i] = (hostmem.bytes_from(dh.ctypes.data + 4 * o, 4 * self.numels[i]), [{"int_list": list(self.shapes[i])}])
                         o += self.numels[i]
             if out is None:
                 out = torch.empty(self.arena_numel, dtype=torch.float32, device=dev)

@@ -14,7 +14,56 @@ the OS.  OFL_HOST_KEEP_LARGE_BLOCKS=1 in the environment applies it at import.
 import ctypes
 import ctypes.util
 
+import numpy as np
+
 _M_TRIM_THRESHOLD, _M_MMAP_THRESHOLD = -1, -3
+_MADV_HUGEPAGE = 14
+_HUGE = 2 << 20
+_libc = None
+
+_new_bytes = ctypes.pythonapi.PyBytes_FromStringAndSize
+_new_bytes.argtypes = [ctypes.c_void_p, ctypes.c_ssize_t]
+_new_bytes.restype = ctypes.py_object
+_bytes_addr = ctypes.pythonapi.PyBytes_AsString
+_bytes_addr.argtypes = [ctypes.py_object]
+_bytes_addr.restype = ctypes.c_void_p
+
+
+def _c():
+    global _libc
+    if _libc is None:
+        _libc = ctypes.CDLL(ctypes.util.find_library("c") or "libc.so.6", use_errno=True)
+        _libc.madvise.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    return _libc
+
+
+def bytes_from(src_addr, n, threads=8, huge_min=8 << 20):
+    """A new `bytes` of the n bytes at host address src_addr (pinned staging).
+
+    The object is created uninitialised (PyBytes_FromStringAndSize(NULL, n),
+    the CPython idiom for filling a bytes before anyone else holds it); above
+    huge_min its 2 MiB-aligned interior is marked MADV_HUGEPAGE (transparent
+    huge pages in 'madvise' mode), so first touch costs one fault per 2 MiB
+    instead of per 4 KiB; the copy runs on native threads, so those faults are
+    taken in parallel.  Same bytes as bytes(memoryview) of the source."""
+    from openfl_amd import _lib
+    n = int(n)
+    if n < huge_min:
+        return ctypes.string_at(src_addr, n) if n else b""
+    b = _new_bytes(None, n)
+    dst = _bytes_addr(b)
+    lo = (dst + _HUGE - 1) // _HUGE * _HUGE
+    hi = (dst + n) // _HUGE * _HUGE
+    if hi > lo:
+        _c().madvise(lo, hi - lo, _MADV_HUGEPAGE)  # advisory: a refusal only costs speed
+    piece = 4 << 20
+    offs = np.arange(0, n, piece, dtype=np.uint64)
+    sizes = np.minimum(np.uint64(piece), np.uint64(n) - offs).astype(np.int64)
+    d = np.uint64(dst) + offs
+    s = np.uint64(src_addr) + offs
+    _lib.check(_lib.lib().ofl_host_copy_many(offs.size, d.ctypes.data, s.ctypes.data, sizes.ctypes.data,
+                                             int(threads)))
+    return b
 
 
 def keep_large_blocks(threshold=1 << 30):

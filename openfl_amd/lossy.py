@@ -12,7 +12,7 @@ from concurrent.futures import ThreadPoolExecutor
 import numpy as np
 import torch
 
-from openfl_amd import _lib
+from openfl_amd import _lib, hostmem
 
 _tls = threading.local()
 GZIP_CHUNK = 8 << 20
@@ -273,7 +273,7 @@ def gzip_ranks(x):
         if rc != _lib.OFL_ESPACE or cap == bound:
             break
     _lib.check_gzip(rc)
-    payload = out[:ln.value].numpy().tobytes()
+    payload = hostmem.bytes_from(out.data_ptr(), ln.value)
     _trim_bufs()
     return payload
 
