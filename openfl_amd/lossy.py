@@ -336,10 +336,15 @@ def _buf(device, name, nbytes, pinned=False):
     key = (str(device), name)
     b = bufs.get(key)
     if b is None or b.numel() < nbytes:
+        # 1/8 headroom: payload sizes wander from call to call (a compressed
+        # stream's length), and each regrowth of a pinned buffer costs a
+        # fresh pinned allocation
+        nbytes = max(nbytes, 1)
+        nbytes = (nbytes + (nbytes >> 3) + (2 << 20) - 1) // (2 << 20) * (2 << 20) if nbytes > (1 << 20) else nbytes
         if pinned:
-            b = torch.empty(max(nbytes, 1), dtype=torch.uint8).pin_memory()
+            b = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
         else:
-            b = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+            b = torch.empty(nbytes, dtype=torch.uint8, device=device)
         bufs[key] = b
     return b
 
