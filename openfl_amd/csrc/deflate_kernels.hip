@@ -846,8 +846,18 @@ constexpr int kRing = 512;                 // compressed-input ring per wave (by
 constexpr int kFastBits = 9;               // first-level decode table: codes of <= 9 bits
 constexpr int kFast = 1 << kFastBits;
 
+// A first-level table entry says what the symbol means, so the serial decode
+// (scalar-unit bound: one SALU pipe per CU serves all its waves) needs no
+// per-symbol branching on the symbol value:
+//   bits 0..3   code length (0: the code is longer than kFastBits, or unused)
+//   bits 4..7   extra bits that follow the code (length / distance codes)
+//   bits 8..9   kind: 0 literal (or plain symbol), 1 length / distance, 2 end
+//               of block, 3 not a valid symbol here
+//   bits 16..31 value: literal byte / symbol, length base, distance base
+enum { kKindLit = 0, kKindCopy = 1, kKindEnd = 2, kKindBad = 3 };
+enum { kAlphaLit = 0, kAlphaDist = 1, kAlphaPlain = 2 };
 struct InfCode {                           // one canonical Huffman code
-    uint16_t fast[kFast];                  // (symbol << 4) | length; 0: longer (or unused) code
+    uint32_t fast[kFast];                  // entries as above (code length in bits 0..3)
     uint16_t cnt[16];                      // codes per length
     uint16_t sorted[288];                  // symbols ordered by (length, symbol)
 };
@@ -882,10 +892,25 @@ DEVI uint32_t dist_base(int c, int& ext) {
     ext = (c >> 1) - 1;
     return ((2u + (uint32_t)(c & 1)) << ext) + 1u;
 }
+// the table entry of symbol s of an alphabet (code length not included)
+DEVI uint32_t inf_entry(int s, int alpha) {
+    int ext = 0;
+    if (alpha == kAlphaPlain) return (uint32_t)s << 16;
+    if (alpha == kAlphaDist) {
+        if (s > 29) return (uint32_t)kKindBad << 8;
+        const uint32_t b = dist_base(s, ext);
+        return (b << 16) | ((uint32_t)kKindCopy << 8) | ((uint32_t)ext << 4);
+    }
+    if (s < 256) return (uint32_t)s << 16;
+    if (s == 256) return (uint32_t)kKindEnd << 8;
+    if (s > 285) return (uint32_t)kKindBad << 8;
+    const uint32_t b = len_base(s - 257, ext);
+    return (b << 16) | ((uint32_t)kKindCopy << 8) | ((uint32_t)ext << 4);
+}
 
 // canonical code from lengths (wave-parallel): counts and ranks by ballots,
 // the fast table filled by the symbols' lanes.  false: over-subscribed.
-DEVI bool inf_build(InfCode& c, const uint8_t* lens, int n) {
+DEVI bool inf_build(InfCode& c, const uint8_t* lens, int n, int alpha) {
     const int lane = (int)(threadIdx.x & 63u);
     const uint64_t below = (1ull << lane) - 1ull;
     for (int k = lane; k < kFast; k += 64) c.fast[k] = 0;
@@ -928,9 +953,10 @@ DEVI bool inf_build(InfCode& c, const uint8_t* lens, int n) {
         }
         if (L) {
             c.sorted[my_off] = (uint16_t)s;
-            if (L <= kFastBits)
-                for (uint32_t k = rev_bits(my_code, L); k < (uint32_t)kFast; k += 1u << L)
-                    c.fast[k] = (uint16_t)((s << 4) | L);
+            if (L <= kFastBits) {
+                const uint32_t e = inf_entry(s, alpha) | (uint32_t)L;
+                for (uint32_t k = rev_bits(my_code, L); k < (uint32_t)kFast; k += 1u << L) c.fast[k] = e;
+            }
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -942,28 +968,35 @@ DEVI bool inf_build(InfCode& c, const uint8_t* lens, int n) {
 // VALU op per step of the serial decode would cost 4+ cycles each)
 DEVI uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
-// one symbol (needs >= 15 bits in bb); -1 if the bits are no code
-DEVI int inf_decode(const InfCode& c, uint64_t& bb, int& bc) {
-    const uint32_t e = uni(c.fast[bb & (uint64_t)(kFast - 1)]);
-    if (e & 15u) {
-        const int l = (int)(e & 15u);
-        bb >>= l;
-        bc -= l;
-        return (int)(e >> 4);
-    }
-    // canonical walk: codes are sent most significant bit first
+// codes longer than the first-level table: canonical walk, most significant
+// bit first (rare: the slow path of inf_decode)
+DEVI uint32_t inf_decode_long(const InfCode& c, uint64_t& bb, int& bc, int alpha) {
     int code = 0, first = 0, index = 0;
+#pragma unroll 1
     for (int len = 1; len <= 15; ++len) {
         code |= (int)(bb & 1u);
         bb >>= 1;
         --bc;
         const int n = (int)uni(c.cnt[len]);
-        if (code - first < n) return (int)uni(c.sorted[index + code - first]);
+        if (code - first < n) return inf_entry((int)uni(c.sorted[index + code - first]), alpha);
         index += n;
         first = (first + n) << 1;
         code <<= 1;
     }
-    return -1;
+    return (uint32_t)kKindBad << 8;
+}
+
+// one symbol's table entry (needs >= 15 bits in bb), its code consumed;
+// kKindBad if the bits are no code
+DEVI uint32_t inf_decode(const InfCode& c, uint64_t& bb, int& bc, int alpha) {
+    const uint32_t e = uni(c.fast[bb & (uint64_t)(kFast - 1)]);
+    const int l = (int)(e & 15u);
+    if (l) {
+        bb >>= l;
+        bc -= l;
+        return e;
+    }
+    return inf_decode_long(c, bb, bc, alpha);
 }
 
 // RING = false: the member's whole output stays in the WIN-byte LDS window
@@ -1057,8 +1090,8 @@ __global__ __launch_bounds__(64) void k_inflate_members(InfArgs a) {
             for (int i = lane; i < 320; i += 64)
                 S.lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : i < 288 ? 8 : 5;
             __builtin_amdgcn_wave_barrier();
-            inf_build(S.lit, S.lens, 288);
-            inf_build(S.dist, S.lens + 288, 30);
+            inf_build(S.lit, S.lens, 288, kAlphaLit);
+            inf_build(S.dist, S.lens + 288, 30, kAlphaDist);
         } else {  // dynamic: code-length code, then the literal/length and distance lengths
             topup();
             const int nlit = (int)bits(5) + 257, ndist = (int)bits(5) + 1, ncl = (int)bits(4) + 4;
@@ -1071,13 +1104,14 @@ __global__ __launch_bounds__(64) void k_inflate_members(InfArgs a) {
                 if (lane == 0) S.lens[c_clord[i]] = (uint8_t)v;
             }
             __builtin_amdgcn_wave_barrier();
-            if (!inf_build(S.lit, S.lens, 19)) { err = kInfCorrupt; break; }
+            if (!inf_build(S.lit, S.lens, 19, kAlphaPlain)) { err = kInfCorrupt; break; }
             const int total = nlit + ndist;
             int i = 0;
             while (i < total) {
                 topup();
-                const int sy = inf_decode(S.lit, bb, bc);
-                if (sy < 0) { err = kInfCorrupt; break; }
+                const uint32_t ce = inf_decode(S.lit, bb, bc, kAlphaPlain);
+                if (ce & 0x300u) { err = kInfCorrupt; break; }
+                const int sy = (int)(ce >> 16);
                 if (sy < 16) {
                     if (lane == 0) S.lens[i] = (uint8_t)sy;
                     ++i;
@@ -1109,34 +1143,43 @@ __global__ __launch_bounds__(64) void k_inflate_members(InfArgs a) {
             __builtin_amdgcn_wave_barrier();
             if (lane < 32) S.lens[288 + lane] = lane < ndist ? dl : 0;
             __builtin_amdgcn_wave_barrier();
-            if (!inf_build(S.lit, S.lens, nlit) || !inf_build(S.dist, S.lens + 288, ndist)) { err = kInfCorrupt; break; }
+            if (!inf_build(S.lit, S.lens, nlit, kAlphaLit) || !inf_build(S.dist, S.lens + 288, ndist, kAlphaDist)) {
+                err = kInfCorrupt;
+                break;
+            }
         }
         // symbols of the block
         for (;;) {
             topup();
-            const int sy = inf_decode(S.lit, bb, bc);
-            if (sy < 0) { err = kInfCorrupt; break; }
-            if (sy < 256) {
+            const uint32_t e = inf_decode(S.lit, bb, bc, kAlphaLit);
+            const uint32_t kind = (e >> 8) & 3u;
+            if (kind == kKindLit) {
                 if (p >= isize) { err = kInfSize; break; }
                 if (lane == 0) {
-                    S.win[p & M] = (uint8_t)sy;
-                    if (RING) dst[p] = (uint8_t)sy;
+                    S.win[p & M] = (uint8_t)(e >> 16);
+                    if (RING) dst[p] = (uint8_t)(e >> 16);
                 }
                 ++p;
-            } else if (sy == 256) {
+            } else if (kind == kKindEnd) {
                 break;
             } else {
-                if (sy > 285) { err = kInfCorrupt; break; }
-                int le, de;
-                const uint32_t len = len_base(sy - 257, le) + bits(le);
+                if (kind == kKindBad) { err = kInfCorrupt; break; }
+                const uint32_t len = (e >> 16) + bits((int)((e >> 4) & 15u));
                 topup();
-                const int ds = inf_decode(S.dist, bb, bc);
-                if (ds < 0 || ds > 29) { err = kInfCorrupt; break; }
-                const uint32_t d = dist_base(ds, de) + bits(de);
+                const uint32_t f = inf_decode(S.dist, bb, bc, kAlphaDist);
+                if (((f >> 8) & 3u) != kKindCopy) { err = kInfCorrupt; break; }
+                const uint32_t d = (f >> 16) + bits((int)((f >> 4) & 15u));
                 if (d > p) { err = kInfCorrupt; break; }
                 if (p + len > isize) { err = kInfSize; break; }
                 __builtin_amdgcn_wave_barrier();
-                if (!RING || d + len <= (uint32_t)WIN) {  // the source is in the window
+                if ((!RING || d + len <= (uint32_t)WIN) && len <= 64u) {  // one lane per byte, no loop
+                    if ((uint32_t)lane < len) {
+                        const uint32_t k = (uint32_t)lane;
+                        const uint8_t v = S.win[(p - d + (d >= len ? k : k % d)) & M];
+                        S.win[(p + k) & M] = v;
+                        if (RING) dst[p + k] = v;
+                    }
+                } else if (!RING || d + len <= (uint32_t)WIN) {  // the source is in the window
                     if (d >= len) {
                         for (uint32_t k = lane; k < len; k += 64) {
                             const uint8_t v = S.win[(p - d + k) & M];
