@@ -357,6 +357,9 @@ int ofl_inflate_members(const uint8_t* src, const int64_t* index, int64_t nmembe
  * (eden_pipeline.py:771, NumPy scalar arithmetic).  Host pointers. */
 float ofl_serial_sum_f32(const float* x, int64_t n);
 double ofl_serial_sum_f64(const double* x, int64_t n);
+/* ofl_serial_sum_f32 of x while copying x to dst (the pinned staging block
+ * of a one-tensor encode): the copy rides in the add chain's latency. */
+float ofl_serial_sum_copy_f32(const float* x, float* dst, int64_t n);
 /* ofl_serial_sum_* of n host arrays (f32 or, if f64, double) on up to
  * nthreads native threads, largest first; out[i] as double (exact for f32). */
 int ofl_serial_sums_many(int n, const void* const* ptrs, const int64_t* lens, int f64, double* out, int nthreads);

@@ -2694,6 +2694,22 @@ float ofl_serial_sum_f32(const float* x, int64_t n) {
     return s;
 }
 
+float ofl_serial_sum_copy_f32(const float* x, float* dst, int64_t n) {
+    float s = 0.0f;
+    int64_t i = 0;
+    for (; i + 8 <= n; i += 8) {  // the 8-element block copy issues beside the serial adds
+        float v[8];
+        memcpy(v, x + i, sizeof(v));
+        memcpy(dst + i, v, sizeof(v));
+        for (int k = 0; k < 8; ++k) s = s + v[k];
+    }
+    for (; i < n; ++i) {
+        dst[i] = x[i];
+        s = s + x[i];
+    }
+    return s;
+}
+
 double ofl_serial_sum_f64(const double* x, int64_t n) {
     double s = 0.0;
     for (int64_t i = 0; i < n; ++i) s = s + x[i];

@@ -51,6 +51,21 @@ def test_serial_sums_are_left_to_right():
         assert _serial_sum(x) == s and type(_serial_sum(x)) is dt
 
 
+@pytest.mark.parametrize("n", [0, 1, 7, 8, 9, 5003])
+def test_serial_sum_copy_is_left_to_right_and_copies(n):
+    """ofl_serial_sum_copy_f32 (the one-tensor encode's staging fill): the
+    reference seed's float32 sum(data.flatten()) (:771) and an exact copy."""
+    from openfl_amd import _lib
+    x = (np.random.default_rng(n).standard_normal(n) * 1e3).astype(np.float32)
+    s = np.float32(0)
+    for v in x:
+        s = s + v
+    dst = np.full(n + 1, 7.0, np.float32)
+    got = _lib.lib().ofl_serial_sum_copy_f32(x.ctypes.data, dst.ctypes.data, n)
+    assert np.float32(got) == s
+    assert np.array_equal(dst[:n], x) and dst[n] == 7.0
+
+
 def test_host_plan_layout():
     from openfl_amd.codec import EdenPlan, slice_plan
     numels = [1000, 300000, 5, 4096 * 1024]
