@@ -7,6 +7,7 @@ semantics are cited per function (paths relative to /root/reference).
 import ctypes
 import gzip
 import threading
+import warnings
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -382,14 +383,16 @@ def gunzip_device(data, out):
         raise _lib.CodecError("gunzip_device: output buffer too small")
     idx = idx[:nm.value]
     dev = out.device
-    ioff = (src.size + 7) // 8 * 8  # the stream, then the index, in one H2D
+    ioff = (src.size + 7) // 8 * 8  # the stream, then the index
     need = ioff + idx.nbytes
-    stage = _buf("host", "gz_in", need, pinned=True)
-    sn = stage.numpy()
-    _parallel_copy(sn.ctypes.data, src.ctypes.data, src.size)
-    sn[ioff:need] = idx.view(np.uint8).reshape(-1)
     d_in = _buf(dev, "gz_in", need)
-    d_in[:need].copy_(stage[:need], non_blocking=True)
+    # the stream goes H2D straight from the payload (pageable: the runtime
+    # streams it at the pinned rate, 2.7 ms for 144 MiB on this box,
+    # profiles/r02_hostcopy_probe.json) -- no staging copy
+    with warnings.catch_warnings():  # a read-only view of the immutable payload: torch only reads it
+        warnings.simplefilter("ignore", UserWarning)
+        d_in[:src.size].copy_(torch.from_numpy(src))
+    d_in[ioff:need].copy_(torch.from_numpy(idx.view(np.uint8).reshape(-1)))
     ws = _buf(dev, "gz_status", 256)
     _lib.check_gzip(L.ofl_inflate_members(d_in.data_ptr(), d_in.data_ptr() + ioff, nm.value, mx.value, out.data_ptr(),
                                           out.numel(), ws.data_ptr(), ws.numel(), _stream(dev)))
