@@ -1907,6 +1907,13 @@ bool use_small_stream() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_SMALLSTREAM"); return !(s && s[0] == '0'); }();
     return on;
 }
+// two-stream plans whose large slices fit one wave split them into exactly
+// two balanced waves (OFL_EDEN_TWOWAVES=0: in-order packing against half the
+// total)
+bool use_two_waves() {
+    static const bool on = [] { const char* s = getenv("OFL_EDEN_TWOWAVES"); return !(s && s[0] == '0'); }();
+    return on;
+}
 // OFL_EDEN_SPLIT_MIB=m: two-stream plans split their large slices into two
 // waves only above m MiB of intermediates; unset (-1): see build_schedule
 int64_t split_min_bytes() {
@@ -2151,13 +2158,26 @@ void build_schedule(ofl_eden_plan* pl) {
     // vs 369 us with one wave; OFL_EDEN_SPLIT_MIB=m splits above m MiB)
     const int64_t split_min = split_min_bytes();
     const bool split = split_min >= 0 ? 4 * tot > split_min : (!common.empty() || tot > cap);
-    if (pl->nstreams == 2 && split) {
+    // the split only feeds the second stream (everything fits one wave):
+    // exactly two waves, cut where the halves are closest (in-order packing
+    // against a half-total cap can leave a third wave behind the first on the
+    // same stream -- ResNet-50: 417 vs 353 tiles per stream)
+    int64_t cut = -1;
+    if (pl->nstreams == 2 && split && tot <= cap && large.size() > 1 && use_two_waves()) {
+        int64_t pre = 0, best = INT64_MAX;
+        for (size_t k = 0; k + 1 < large.size(); ++k) {
+            pre += 1ll << pl->slices[large[k]].logp;
+            const int64_t d = std::llabs(2 * pre - tot);
+            if (d < best) { best = d; cut = (int64_t)k + 1; }
+        }
+    } else if (pl->nstreams == 2 && split) {
         cap = std::min(cap, std::max<int64_t>(1, (tot + 1) / 2));
     }
     int64_t acc = 0, wmax = 0;
-    for (int32_t si : large) {
+    for (size_t k = 0; k < large.size(); ++k) {
+        const int32_t si = large[k];
         const int64_t P = 1ll << pl->slices[si].logp;
-        if (waves.empty() || acc + P > cap) { waves.emplace_back(); acc = 0; }
+        if (waves.empty() || (cut >= 0 ? (int64_t)k == cut : acc + P > cap)) { waves.emplace_back(); acc = 0; }
         waves.back().push_back(si);
         acc += P;
         wmax = std::max(wmax, acc);

@@ -47,6 +47,9 @@ def main():
     numels = [numel(s) for _, s in WORKLOADS["resnet50_fp32"]()]
     big = [n for n in numels if n > 36045]       # every slice > 2^15 (greedy slicing, 10 % pad rule)
     small = [n for n in numels if n <= 36045]
+    if len(sys.argv) > 2 and sys.argv[2] == "large":  # one eager run of the large tensors (for a kernel trace)
+        print(json.dumps({"large_only_us": round(step_time(big, steps, False), 1)}))
+        return
     out = {}
     for tag, ns in (("all", numels), ("large_only", big), ("small_only", small)):
         for graph in (False, True):
