@@ -113,6 +113,26 @@ def test_wave_schedule_layout():
         EdenPlan(numels, 8, streams=3)
 
 
+def test_two_stream_split_rules():
+    """Two-stream plans whose large slices fit one wave: with small-slice
+    launches beside them, exactly two waves cut at the closest halves (in-order
+    packing against half the total would leave a third wave behind the
+    first); large slices only, one wave on the caller's stream."""
+    from openfl_amd.codec import EdenPlan
+    from openfl_amd.workloads import WORKLOADS, numel
+    sizes = [numel(s) for _, s in WORKLOADS["resnet50_fp32"]()]
+    rn = EdenPlan(sizes, 8, streams=2)
+    assert rn.n_waves == 2
+    rows = [l["blocks"] for l in rn.launches(True) if l["name"] == "ofl::k_enc_rowA"]
+    assert len(rows) == 2 and abs(rows[0] - rows[1]) <= max(rows) // 4
+    uni = EdenPlan([numel(s) for _, s in WORKLOADS["uniform_1gib"]()], 8, streams=2)
+    assert uni.n_waves == 1
+    assert [l["name"] for l in uni.launches(True)].count("ofl::k_finalize") == 1
+    # more than one wave of large slices: waves by the wave size, as before
+    many = EdenPlan([1 << 22] * 6, 8, wave_mib=32, streams=2)
+    assert many.n_waves == 3
+
+
 def test_plan_errors():
     from openfl_amd import _lib
     from openfl_amd.codec import EdenPlan
