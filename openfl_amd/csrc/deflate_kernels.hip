@@ -70,17 +70,33 @@ struct HScratch {
     uint16_t rle_sym[kLit + kDist];
     uint16_t rle_ext[kLit + kDist];
 };
+// The member's bit buffer in LDS.  A member is at most 14.7 KiB of dynamic
+// Huffman output: its literal/length alphabet has <= 66 symbols in use (<= 36
+// literal byte values of float32 integers 0..31, end of block, <= 29 length
+// codes), so the optimal code costs at most a uniform 7-bit code, <= 7 bits
+// per literal byte (matches and one-token copies cost less than the literals
+// they replace), plus a <= 600-byte header; 17 KiB leaves margin, and a
+// member that would not fit is refused (bad flag 4), never truncated.
+constexpr int kOutCap = 4352;              // words
+constexpr int kHdrW = 160;                 // header words (<= 4642 bits)
 struct Smem {
-    uint32_t out[kOutWords];
-    uint32_t crct[256];
     union {
-        int16_t last[kNT][kTypes];         // per thread: last index of each type in its segment; then exclusive prefix max
-        uint32_t key[kTok];                // then: (3-token key << 12 | position), sorted
-        HScratch h;                        // then: Huffman scratch
-    } u;
-    alignas(16) uint8_t tk[kTok + 64];     // the member's tokens
+        struct {
+            union {
+                int16_t last[kNT][kTypes];  // per thread: last index of each type in its segment; then exclusive prefix max
+                uint32_t key[kTok];         // then: (3-token key << 12 | position), sorted
+                HScratch h;                 // then: Huffman scratch
+            } u;
+            alignas(16) uint8_t tk[kTok + 64];  // the member's tokens
+        };
+        uint32_t out[kOutCap];              // the bit buffer, once the tokens and the Huffman scratch are dead
+    };
+    uint32_t hdrw[kHdrW];                  // the member header's words (written while the scratch is live)
     uint8_t bestL[kTok];                   // longest earlier match at a position (tokens, 0 = none >= 3)
-    uint16_t bestG[kTok];                  // and its distance in tokens
+    union {
+        uint32_t crct[256];                // CRC-32 table: only while the tokens are read
+        uint16_t bestG[kTok];              // and its distance in tokens
+    };
     uint8_t op[kTok];                      // parse: 0 covered, 1 one-token op, 2 match start
     int16_t ptot[8][kTypes];
     uint32_t hl[kLit], hd[kDist], hc[kCL];
@@ -92,6 +108,8 @@ struct Smem {
     int bad;
 };
 static_assert(sizeof(HScratch) <= sizeof(int16_t) * kNT * kTypes, "Huffman scratch fits the token tables");
+static_assert(4 * kOutCap <= sizeof(int16_t) * kNT * kTypes + kTok + 64, "bit buffer overlays the token tables");
+static_assert(sizeof(Smem) <= 40 * 1024, "four member blocks per CU");
 
 DEVI void put_bits(uint32_t* out, uint32_t pos, uint32_t val, int nb) {
     if (nb == 0) return;
@@ -327,7 +345,6 @@ __global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
     const int64_t e0 = c * kTok;
     const int ntok = (int)std::min<int64_t>(kTok, a.n - e0);
     GZ_STAMP(0);
-    for (int i = tid; i < kOutWords; i += kNT) S.out[i] = 0;
     for (int i = tid; i < 256; i += kNT) {
         uint32_t r = (uint32_t)i;
         for (int k = 0; k < 8; ++k) r = (r & 1u) ? (r >> 1) ^ 0xEDB88320u : r >> 1;
@@ -660,7 +677,7 @@ __global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
             acc |= (uint64_t)v << nb;
             nb += n;
             pos += (uint32_t)n;
-            if (nb >= 32) { S.out[wi++] = (uint32_t)acc; acc >>= 32; nb -= 32; }
+            if (nb >= 32) { S.hdrw[wi++] = (uint32_t)acc; acc >>= 32; nb -= 32; }
         };
         // member header with a BGZF-style extra field (RFC 1952 FEXTRA,
         // subfield 'BC' = member size - 1, filled in at the end): a reader
@@ -680,11 +697,18 @@ __global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
             const int eb = sy == 16 ? 2 : (sy == 17 ? 3 : (sy == 18 ? 7 : 0));
             put(h.rle_ext[i], eb);
         }
-        if (nb > 0) S.out[wi] = (uint32_t)acc;
+        if (nb > 0) S.hdrw[wi] = (uint32_t)acc;
         S.hdr_bits = pos;
     }
     __syncthreads();
     GZ_STAMP(8);
+    // the tokens and the Huffman scratch are dead: the bit buffer takes their
+    // place, header words first (the ops' first word is OR-ed in after the
+    // scan's barrier)
+    {
+        const uint32_t hw = (S.hdr_bits + 31u) >> 5;
+        for (int i = tid; i < kOutCap; i += kNT) S.out[i] = (uint32_t)i < hw ? S.hdrw[i] : 0u;
+    }
     // ---- op bits: block scan of the costs, then OR into the buffer ----
     uint32_t mine = 0;
 #pragma unroll
@@ -715,10 +739,13 @@ __global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
     uint32_t pos = S.hdr_bits + inc - mine;
     for (int j = 0; j < w; ++j) pos += S.scan[j];
     if (tid == kNT - 1) S.total_bits = pos + mine;
+    // room for the ops, end of block, padding, CRC-32 and ISIZE (see kOutCap)
+    const bool fits = pos + mine + 15u + 7u + 64u <= 32u * (uint32_t)kOutCap;
+    if (!fits) atomicOr(&S.bad, 2);
     // this thread's ops are one contiguous bit range: gather them in a 64-bit
     // accumulator and store whole words; only the first and the last word
     // can be shared with a neighbour (OR-ed atomically)
-    {
+    if (fits) {
         uint64_t acc = 0;
         int nb = (int)(pos & 31u);
         uint32_t wi = pos >> 5;
@@ -766,6 +793,10 @@ __global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
     __syncthreads();
     GZ_STAMP(9);
     // ---- end of block, byte padding, CRC-32 and ISIZE ----
+    if (S.bad) {  // block-uniform: the member would not fit the bit buffer
+        if (tid == 0) { atomicOr(a.bad, 4); a.sizes[blockIdx.x] = 0; }
+        return;
+    }
     if (tid == 0) {
         uint32_t p = S.total_bits;
         put_bits(S.out, p, S.kl[256], S.ll[256]); p += S.ll[256];
@@ -1468,6 +1499,7 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
         GZHIP(hipMemcpyAsync(&badh, bad, sizeof(int), hipMemcpyDeviceToHost, st));
         GZHIP(hipStreamSynchronize(st));
         if (badh & 1) return gzfail(OFL_EINVAL, "gzip ranks: values must be float32 integers 0..31");
+        if (badh & 4) return gzfail(OFL_EHIP, "gzip ranks: a member exceeded the device bit buffer");
         if (badh & 2) return gzfail(OFL_ESPACE, "gzip ranks: output buffer too small");
         total = tot;
     }
@@ -1484,6 +1516,7 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
         GZHIP(hipMemcpyAsync(&tot, off + nb, 8, hipMemcpyDeviceToHost, st));
         GZHIP(hipMemcpyAsync(&badh, bad, sizeof(int), hipMemcpyDeviceToHost, st));
         GZHIP(hipStreamSynchronize(st));
+        if (badh & 4) return gzfail(OFL_EHIP, "gzip ranks: a member exceeded the device bit buffer");
         if (badh) return gzfail(OFL_EINVAL, "gzip ranks: values must be float32 integers 0..31");
         if (total + tot > out_cap) return gzfail(OFL_ESPACE, "gzip ranks: output buffer too small");
         GZHIP(hipMemcpyAsync(out + total, packed, tot, hipMemcpyDeviceToHost, st));
