@@ -363,14 +363,30 @@ def gunzip_device(data, out):
         raise _lib.CodecError("gunzip_device: out must be a contiguous uint8 device tensor")
     L = _lib.lib()
     src = np.frombuffer(data, np.uint8)
+    dev = out.device
     nm, tot, mx = ctypes.c_int64(), ctypes.c_size_t(), ctypes.c_uint32()
+    # the stream goes H2D straight from the payload (pageable: the runtime
+    # streams it at the pinned rate, 2.7 ms for 144 MiB on this box,
+    # profiles/r02_hostcopy_probe.json), on a pool thread while this one
+    # indexes the members (both release the GIL)
+    d_in = _buf(dev, "gz_in", max(src.size, 1))
+
+    def h2d():
+        with torch.cuda.device(dev), warnings.catch_warnings():  # a read-only view: torch only reads it
+            warnings.simplefilter("ignore", UserWarning)
+            if src.size:
+                d_in[:src.size].copy_(torch.from_numpy(src))
+    copy = _h2d_pool().submit(h2d)
     # one pass over the headers: a member takes >= 26 bytes, so n // 26 + 1
     # entries always suffice (untouched pages of the array cost nothing)
     cap = src.size // 26 + 1
     idx = np.empty((cap, 4), np.int64)
-    rc = L.ofl_gzip_member_index(src.ctypes.data if src.size else None, src.size, idx.ctypes.data, cap,
-                                 ctypes.byref(nm), ctypes.byref(tot), ctypes.byref(mx)) if src.size \
-        else _lib.OFL_EFORMAT
+    try:
+        rc = L.ofl_gzip_member_index(src.ctypes.data if src.size else None, src.size, idx.ctypes.data, cap,
+                                     ctypes.byref(nm), ctypes.byref(tot), ctypes.byref(mx)) if src.size \
+            else _lib.OFL_EFORMAT
+    finally:
+        copy.result()
     if rc == _lib.OFL_EFORMAT:
         raw = np.frombuffer(gzip.decompress(bytes(data)), np.uint8)
         if raw.size > out.numel():
@@ -382,22 +398,23 @@ def gunzip_device(data, out):
     if tot.value > out.numel():
         raise _lib.CodecError("gunzip_device: output buffer too small")
     idx = idx[:nm.value]
-    dev = out.device
-    ioff = (src.size + 7) // 8 * 8  # the stream, then the index
-    need = ioff + idx.nbytes
-    d_in = _buf(dev, "gz_in", need)
-    # the stream goes H2D straight from the payload (pageable: the runtime
-    # streams it at the pinned rate, 2.7 ms for 144 MiB on this box,
-    # profiles/r02_hostcopy_probe.json) -- no staging copy
-    with warnings.catch_warnings():  # a read-only view of the immutable payload: torch only reads it
-        warnings.simplefilter("ignore", UserWarning)
-        d_in[:src.size].copy_(torch.from_numpy(src))
-    d_in[ioff:need].copy_(torch.from_numpy(idx.view(np.uint8).reshape(-1)))
+    d_idx = _buf(dev, "gz_idx", max(idx.nbytes, 8))
+    d_idx[:idx.nbytes].copy_(torch.from_numpy(idx.view(np.uint8).reshape(-1)))
     ws = _buf(dev, "gz_status", 256)
-    _lib.check_gzip(L.ofl_inflate_members(d_in.data_ptr(), d_in.data_ptr() + ioff, nm.value, mx.value, out.data_ptr(),
+    _lib.check_gzip(L.ofl_inflate_members(d_in.data_ptr(), d_idx.data_ptr(), nm.value, mx.value, out.data_ptr(),
                                           out.numel(), ws.data_ptr(), ws.numel(), _stream(dev)))
     _trim_bufs()
     return out[:tot.value]
+
+
+_h2d_executor = None
+
+
+def _h2d_pool():
+    global _h2d_executor
+    if _h2d_executor is None:
+        _h2d_executor = ThreadPoolExecutor(max_workers=1)
+    return _h2d_executor
 
 
 def rank_map(values):
