@@ -150,6 +150,20 @@ DEVI uint32_t crc_adv_pow2(uint32_t v, int k) {
     for (int i = 0; i < 32; ++i) r ^= ((v >> i) & 1u) ? c_adv[k][i] : 0u;
     return r;
 }
+// raw (zero-initialised, reflected) CRC-32 steps, bitwise: a byte, a
+// little-endian word
+DEVI uint32_t crc_byte(uint32_t r, uint32_t b) {
+    r ^= b;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r = (r >> 1) ^ (0xEDB88320u & (0u - (r & 1u)));
+    return r;
+}
+DEVI uint32_t crc_word(uint32_t r, uint32_t w) {
+    r ^= w;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) r = (r >> 1) ^ (0xEDB88320u & (0u - (r & 1u)));
+    return r;
+}
 DEVI uint32_t crc_adv(uint32_t v, uint32_t len) {
     for (int k = 0; k < 32; ++k)
         if ((len >> k) & 1u) {
@@ -872,7 +886,7 @@ __global__ __launch_bounds__(256) void k_gzip_pack(const uint8_t* slots, const u
 // members: 8 members decode per CU at once, the decode being latency-bound;
 // 64 KiB otherwise); the compressed bytes stream through a small LDS ring.
 // Any valid deflate data decodes (stored, fixed and dynamic blocks, RFC 1951).
-// ISIZE is checked here, the CRC-32 by k_crc_members over the stored output.
+// ISIZE and the CRC-32 (over the member's output, wave-parallel) are checked here.
 constexpr int kRing = 512;                 // compressed-input ring per wave (bytes)
 constexpr int kFastBits = 9;               // first-level decode table: codes of <= 9 bits
 constexpr int kFast = 1 << kFastBits;
@@ -1048,7 +1062,6 @@ __global__ __launch_bounds__(64) void k_inflate_members(InfArgs a) {
     const uint32_t in_len = (uint32_t)ix[1];
     const int64_t out_off = ix[2];
     const uint32_t isize = (uint32_t)((uint64_t)ix[3] & 0xffffffffu), want_crc = (uint32_t)((uint64_t)ix[3] >> 32);
-    (void)want_crc;
     if ((!RING && isize > (uint32_t)WIN) || out_off < 0 || (uint64_t)out_off + isize > a.out_cap) {
         if (lane == 0) atomicOr(a.status, kInfRange);
         return;
@@ -1243,6 +1256,43 @@ __global__ __launch_bounds__(64) void k_inflate_members(InfArgs a) {
         if (lane == 0) atomicOr(a.status, err);
         return;
     }
+    __builtin_amdgcn_wave_barrier();
+    // CRC-32 of the output, checked here: lane l takes bytes [l sg, (l+1) sg)
+    // of the output seen as the tail of 64 sg bytes (leading zeros leave a
+    // zero-initialised CRC unchanged), bitwise (vector work beside the other
+    // waves' scalar-bound decode), then a tree over the lanes whose level-l
+    // shift (sg 2^l bytes) is the same for every lane.  The ring decoder
+    // reads its own stores back (same-address order within a wavefront).
+    {
+        int lg = 0;
+        while ((64ull << lg) < (uint64_t)isize) ++lg;
+        const int64_t sg = 1ll << lg;
+        const int64_t b0 = (int64_t)lane * sg - (int64_t)((64ull << lg) - isize);
+        uint32_t r = 0;
+        const bool vec = RING && sg >= 16 && ((reinterpret_cast<uintptr_t>(dst) | isize) & 15u) == 0;
+        if (vec) {  // b0 is a multiple of 16 here
+            for (int64_t i = b0 < 0 ? 0 : b0; i < b0 + sg; i += 64) {
+                uint4 w[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) w[k] = i + 16 * k < b0 + sg ? reinterpret_cast<const uint4*>(dst + i)[k] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (i + 16 * k < b0 + sg) {
+                        r = crc_word(r, w[k].x); r = crc_word(r, w[k].y);
+                        r = crc_word(r, w[k].z); r = crc_word(r, w[k].w);
+                    }
+            }
+        } else {
+            for (int64_t i = b0 < 0 ? 0 : b0; i < b0 + sg; ++i) r = crc_byte(r, RING ? dst[i] : S.win[i]);
+        }
+#pragma unroll
+        for (int l = 0; l < 6; ++l) {
+            const uint32_t x = (uint32_t)__shfl_xor((int)r, 1 << l, 64);
+            const uint32_t sh = crc_adv_pow2(r, lg + l);
+            r = (lane & (1 << l)) ? r : (sh ^ x);
+        }
+        if (lane == 0 && (crc_adv(0xffffffffu, isize) ^ r ^ 0xffffffffu) != want_crc) atomicOr(a.status, kInfCrc);
+    }
     if (RING) return;  // already stored as produced
     __builtin_amdgcn_wave_barrier();
     if (((reinterpret_cast<uintptr_t>(dst) | isize) & 15u) == 0) {
@@ -1253,47 +1303,6 @@ __global__ __launch_bounds__(64) void k_inflate_members(InfArgs a) {
     }
 }
 
-// CRC-32 of every member's output (after k_inflate_members), one 256-thread
-// block per member: the output seen as the tail of 256 * sg bytes (leading
-// zeros do not change a zero-initialised CRC), thread t takes bytes
-// [t sg, (t+1) sg) of that, then a tree whose level-l shift (sg 2^l bytes) is
-// the same for every thread
-__global__ __launch_bounds__(256) void k_crc_members(InfArgs a) {
-    __shared__ uint32_t crct[256];
-    __shared__ uint32_t part[4];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int64_t m = blockIdx.x;
-    if (m >= a.nmem) return;
-    const int64_t* ix = a.idx + 4 * m;
-    const int64_t out_off = ix[2];
-    const uint32_t isize = (uint32_t)((uint64_t)ix[3] & 0xffffffffu), want = (uint32_t)((uint64_t)ix[3] >> 32);
-    if (out_off < 0 || (uint64_t)out_off + isize > a.out_cap) return;  // reported by the inflate
-    {
-        uint32_t r = (uint32_t)tid;
-        for (int k = 0; k < 8; ++k) r = (r & 1u) ? (r >> 1) ^ 0xEDB88320u : r >> 1;
-        crct[tid] = r;
-    }
-    __syncthreads();
-    int lg = 0;
-    while ((256ull << lg) < isize) ++lg;
-    const int64_t sg = 1ll << lg;
-    const int64_t b0 = (int64_t)tid * sg - (int64_t)((256ull << lg) - isize);
-    const uint8_t* o = a.out + out_off;
-    uint32_t r = 0;
-    for (int64_t i = b0 < 0 ? 0 : b0; i < b0 + sg; ++i) r = crct[(r ^ o[i]) & 0xffu] ^ (r >> 8);
-    for (int l = 0; l < 6; ++l) {
-        const uint32_t x = (uint32_t)__shfl_xor((int)r, 1 << l, 64);
-        const uint32_t sh = crc_adv_pow2(r, lg + l);
-        r = (lane & (1 << l)) ? r : (sh ^ x);
-    }
-    if (lane == 0) part[tid >> 6] = r;
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t raw = 0;
-        for (int w = 0; w < 4; ++w) raw = crc_adv(raw, (uint32_t)(64ull * sg)) ^ part[w];
-        if ((crc_adv(0xffffffffu, isize) ^ raw ^ 0xffffffffu) != want) atomicOr(a.status, kInfCrc);
-    }
-}
 }  // namespace gz
 
 namespace {
@@ -1636,7 +1645,6 @@ int ofl_inflate_members(const uint8_t* src, const int64_t* index, int64_t nmembe
     else
         hipLaunchKernelGGL((gz::k_inflate_members<65536, false>), dim3((unsigned)nmembers), dim3(64),
                            sizeof(gz::InfSmem<65536>), st, a);
-    hipLaunchKernelGGL(gz::k_crc_members, dim3((unsigned)nmembers), dim3(256), 0, st, a);
     GZHIP(hipGetLastError());
     int h = 0;
     GZHIP(hipMemcpyAsync(&h, status, sizeof(int), hipMemcpyDeviceToHost, st));
