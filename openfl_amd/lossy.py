@@ -413,7 +413,7 @@ _h2d_executor = None
 def _h2d_pool():
     global _h2d_executor
     if _h2d_executor is None:
-        _h2d_executor = ThreadPoolExecutor(max_workers=1)
+        _h2d_executor = ThreadPoolExecutor(max_workers=4)  # concurrent callers do not queue behind one copy
     return _h2d_executor
 
 
