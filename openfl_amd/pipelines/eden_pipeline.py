@@ -169,9 +169,10 @@ class Eden:
         """(planes uint8 ndarray, scales list[float], dims list[int], total_dim) (:555-611).
         One tensor in one native call (ofl_eden_encode_host): pinned input
         block [x | seed] -> one H2D, the launches, one D2H of [planes |
-        scales], one sync.  seed_of_sum (float32 input only): the seed is
-        seed_of_sum(serial float32 sum of vec), the sum taken while vec is
-        copied into the pinned block (ofl_serial_sum_copy_f32); seed unused."""
+        scales], one sync.  With seed_of_sum the seed is seed_of_sum(the
+        reference's serial sum of vec) -- for float32 input taken while vec is
+        copied into the pinned block (ofl_serial_sum_copy_f32) -- the seed
+        argument is unused, and the result is (the tuple above, seed)."""
         src = np.asarray(vec).reshape(-1)
         fuse = seed_of_sum is not None and src.dtype == np.float32
         if seed_of_sum is not None and not fuse:
