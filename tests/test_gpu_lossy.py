@@ -471,6 +471,30 @@ def test_inflate_members_foreign_streams(kind):
     assert got.cpu().numpy().tobytes() == data
 
 
+def test_gzip_roundtrip_concurrent_threads():
+    """Device gzip + device inflate from several threads at once (gRPC worker
+    threads call the plugin concurrently): each thread's payload decodes to its
+    own ranks; payloads of different lengths exercise the scratch regrowth and
+    the shared H2D pool."""
+    from concurrent.futures import ThreadPoolExecutor
+    from openfl_amd import lossy
+
+    def one(k):
+        g = torch.Generator(device=DEV).manual_seed(100 + k)
+        n = (1 << 20) + 4096 * k + 123 * k
+        p = torch.tensor([0.1, 0.2, 0.4, 0.2, 0.1], device=DEV)
+        x = torch.multinomial(p, n, replacement=True, generator=g).to(torch.float32)
+        z = lossy.gzip_ranks(x)
+        assert np.array_equal(np.frombuffer(gzip.decompress(z), np.float32), x.cpu().numpy())
+        out = torch.empty(4 * n + 64, dtype=torch.uint8, device=DEV)
+        got = lossy.gunzip_device(z, out)
+        torch.cuda.current_stream().synchronize()
+        return torch.equal(got.view(torch.float32), x)
+
+    with ThreadPoolExecutor(max_workers=4) as ex:
+        assert all(ex.map(one, range(8)))
+
+
 def test_inflate_members_rejects_corrupt_streams():
     """Corrupt data fails loudly (gzip.decompress raises on the same bytes),
     a stream without the 'BC' field decodes on the host, output too small is
