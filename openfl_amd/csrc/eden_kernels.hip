@@ -95,6 +95,7 @@ struct KArgs {
     float* part;            // partial sums
     float* nu;              // per-slice norms (large)
     const float* yadd;      // decode: nullable, y = yadd + decoded (apply_delta, float32 add)
+    const int32_t* btab;    // column launches: per block {slice, tile << 3 | group} (nullable)
 };
 
 // Eden centroids in global memory (copied to LDS per workgroup); the
@@ -538,6 +539,11 @@ DEVI float add_rn(float b, float d) {
 
 // block-uniform slice lookup for multi-tile launches (tile b of the launch)
 DEVI void find_tile_at(const KArgs& a, int b, int& slice, uint32_t& tile) {
+    if (a.btab) {  // one load instead of a search over the launch's tile prefix
+        slice = a.btab[2 * b];
+        tile = (uint32_t)a.btab[2 * b + 1] >> 3;
+        return;
+    }
     int lo = 0, hi = a.count - 1;
     while (lo < hi) {
         int mid = (lo + hi + 1) >> 1;
@@ -548,6 +554,11 @@ DEVI void find_tile_at(const KArgs& a, int b, int& slice, uint32_t& tile) {
 }
 DEVI void find_tile(const KArgs& a, int& slice, uint32_t& tile) {
     const int b = (int)blockIdx.x;
+    if (a.btab) {
+        slice = a.btab[2 * b];
+        tile = (uint32_t)a.btab[2 * b + 1] >> 3;
+        return;
+    }
     int lo = 0, hi = a.count - 1;
     while (lo < hi) {
         int mid = (lo + hi + 1) >> 1;
@@ -1416,12 +1427,17 @@ constexpr int kColGroup = 5;
 __global__ __launch_bounds__(kColNT) void k_col_multi(KArgs a) {
     const int b = (int)blockIdx.x;
     int g = 0;
-    while (g + 1 < a.count && a.list[kColGroup * (g + 1) + 4] <= b) ++g;
+    if (a.btab) {
+        g = a.btab[2 * b + 1] & 7;
+    } else {
+        while (g + 1 < a.count && a.list[kColGroup * (g + 1) + 4] <= b) ++g;
+    }
     const int32_t* G = a.list + kColGroup * g;
     KArgs a2 = a;
     a2.list = a.list + G[1];
     a2.tstart = a.list + G[2];
     a2.count = G[3];
+    if (a.btab) a2.btab = a.btab + 2 * G[4];  // the group's blocks, indexed from its first
     const int lb = b - G[4];
     switch (G[0]) {
     case 1: col_body<1, true>(a2, lb); break;
@@ -1771,6 +1787,7 @@ struct Launch {
     int stream = 0;  // 0: the caller's stream, 1: the plan's side stream, 2: its small-slice stream
     int join = 0;    // the caller's stream waits for the side stream before this launch
     int tl = 15;     // column: log2 of the tile (16: k_col6 with 1024 threads)
+    int btab_off = -1;  // column: per-block {slice, tile << 3 | group} table in ints
     int64_t bytes_moved = 0;  // fp32/plane bytes this launch reads + writes (intermediates included)
     int64_t bytes_alg = 0;    // its share of the SURVEY 8(d) algorithmic bytes (x/y fp32 + planes only)
 };
@@ -1914,6 +1931,12 @@ bool use_two_waves() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_TWOWAVES"); return !(s && s[0] == '0'); }();
     return on;
 }
+// column launches find their tile in a per-block table (OFL_EDEN_BTAB=0:
+// binary search over the launch's tile prefix, as before)
+bool use_btab() {
+    static const bool on = [] { const char* s = getenv("OFL_EDEN_BTAB"); return !(s && s[0] == '0'); }();
+    return on;
+}
 // OFL_EDEN_SPLIT_MIB=m: two-stream plans split their large slices into two
 // waves only above m MiB of intermediates; unset (-1): see build_schedule
 int64_t split_min_bytes() {
@@ -1996,6 +2019,7 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
         ofl::KArgs a = base;
         a.list = pl->d_ints + l.list_off;
         a.tstart = l.tstart_off >= 0 ? pl->d_ints + l.tstart_off : nullptr;
+        a.btab = l.btab_off >= 0 && use_btab() ? pl->d_ints + l.btab_off : nullptr;
         a.count = l.count;
         a.lo = l.lo;
         a.do_nu = l.nu;
@@ -2314,6 +2338,42 @@ void build_schedule(ofl_eden_plan* pl) {
         Launch f{K_FINAL, 0, 0, 0, add_list(fl), -1, (int)fl.size(), (int64_t)fl.size()};
         f.stream = s;
         pl->enc.push_back(f);
+    }
+    // column launches: a per-block {slice, tile << 3 | group} table, so a
+    // block finds its tile with one load (a launch of few tiles per CU is
+    // latency-bound, and the prefix search is a chain of dependent loads);
+    // encode and decode share the table of the same list
+    {
+        std::map<std::pair<int, int>, int> made;
+        auto table = [&](Launch& l) {
+            const auto key = std::make_pair(l.list_off, l.tstart_off);
+            auto it = made.find(key);
+            if (it != made.end()) { l.btab_off = it->second; return; }
+            std::vector<int32_t> t;
+            t.reserve(2 * (size_t)l.blocks);
+            auto add_group = [&](int list_off, int pre_off, int count, int g) {
+                for (int i = 0; i < count; ++i)
+                    for (int32_t k = 0; k < ints[pre_off + i + 1] - ints[pre_off + i]; ++k) {
+                        t.push_back(ints[list_off + i]);
+                        t.push_back((k << 3) | g);
+                    }
+            };
+            if (l.kind == K_COL) {
+                add_group(l.list_off, l.tstart_off, l.count, 0);
+            } else {  // K_COLM: l.count groups {M, list, tstart (relative), count, first block}
+                for (int g = 0; g < l.count; ++g) {
+                    const int32_t* G = &ints[l.list_off + ofl::kColGroup * g];
+                    add_group(l.list_off + G[1], l.list_off + G[2], G[3], g);
+                }
+            }
+            if ((int64_t)t.size() != 2 * l.blocks) return;  // inconsistent: keep the search
+            l.btab_off = (int)ints.size();
+            made[key] = l.btab_off;
+            ints.insert(ints.end(), t.begin(), t.end());
+        };
+        for (auto* L : {&pl->enc, &pl->dec})
+            for (Launch& l : *L)
+                if (l.kind == K_COL || l.kind == K_COLM) table(l);
     }
     // per-launch byte accounting (bench / DESIGN.md roofline)
     const int64_t n_bits = pl->nbits;
