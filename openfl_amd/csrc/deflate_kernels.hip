@@ -1634,11 +1634,13 @@ int ofl_inflate_members(const uint8_t* src, const int64_t* index, int64_t nmembe
     GZHIP(hipMemsetAsync(status, 0, sizeof(int), st));
     gz::InfArgs a{src, index, nmembers, out, (uint64_t)out_cap, status};
     // OFL_GZ_INFLATE=window: whole-member LDS windows (A/B); default: a
-    // 2 KiB LDS ring per member, output stored as produced
-    // (1, 2 and 4 KiB rings measured the same: 24.4-25.0 ms for the 1 GiB set)
+    // 1 KiB LDS ring per member, output stored as produced
+    // 1 KiB ring: with the table-driven decode the kernel is scalar-unit
+    // bound and more members per CU pay (1 / 2 KiB / 512 B: 12.4 / 13.1 /
+    // 12.8 ms for the 1 GiB set; before, 1, 2 and 4 KiB measured the same)
     if (!window)
-        hipLaunchKernelGGL((gz::k_inflate_members<2048, true>), dim3((unsigned)nmembers), dim3(64),
-                           sizeof(gz::InfSmem<2048>), st, a);
+        hipLaunchKernelGGL((gz::k_inflate_members<1024, true>), dim3((unsigned)nmembers), dim3(64),
+                           sizeof(gz::InfSmem<1024>), st, a);
     else if (max_isize <= 16384u)
         hipLaunchKernelGGL((gz::k_inflate_members<16384, false>), dim3((unsigned)nmembers), dim3(64),
                            sizeof(gz::InfSmem<16384>), st, a);
