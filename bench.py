@@ -208,7 +208,10 @@ def secondary(name, n_bits, steps, warmup, dev, wave_mib, streams, cpu=False, gr
     return out
 
 
-def kc_pipeline(steps, warmup, dev):
+KC_TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r03_kc_pipeline_hbm_traffic.json")
+
+
+def kc_pipeline(steps, warmup, dev, extras=True):
     """KCPipeline (keras_cnn_with_compression, BASELINE config 3: k-means k=6
     + GZIPTransformer, kc_pipeline.py:36-63, :128-156, :160-181) on the 1 GiB
     set, gzip INCLUDED.  encode: batched device k-means -> float32 ranks ->
@@ -216,7 +219,9 @@ def kc_pipeline(steps, warmup, dev):
     H2D of the compressed bytes -> device inflate straight into the rank
     array -> batched device LUT.  Also: the device part alone, the host
     inflate (16 native threads + H2D of the ranks) and the host gzip -9
-    compressor (the reference's GZIPTransformer.forward) timed on a sample."""
+    compressor (the reference's GZIPTransformer.forward) timed on a sample.
+    extras=False: the pipeline steps only (tools/kc_bench.py, the PMC passes:
+    every step launches the same kernels, so dispatches per step are exact)."""
     import torch
     from oracle import eden as O  # host_cores only
     from openfl_amd import lossy
@@ -271,6 +276,30 @@ def kc_pipeline(steps, warmup, dev):
     wall = (time.perf_counter() - t0) / steps
     phases = {k: round(1e3 * v / steps, 3) for k, v in ph.items()}
     nbytes = 4 * sum(numels)
+    # roofline of the pipeline step: its minimum I/O, the Eden line's
+    # definition carried over -- read x (4n), write the gzip
+    # stream, read it back, write y (4n); k-means passes, the rank arrays and
+    # the inflate's output are intermediates and not counted
+    alg = 2 * nbytes + 2 * len(z)
+    roof = {"bound": "hbm", "achieved": round(alg / wall / 1e9, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+            "frac": round(alg / wall / 1e9 / PEAK_HBM_GBPS, 5), "alg_bytes_per_step": alg, "traffic": None,
+            "scope": "KC step = forward + backward of the set (wall time, gzip and inflate included); "
+                     "algorithmic bytes = 4n x read + stream write + stream read + 4n y write"}
+    if os.path.exists(KC_TRAFFIC_JSON):
+        with open(KC_TRAFFIC_JSON) as f:
+            tj = json.load(f)
+        roof["traffic"] = tj.get("hbm_bytes_per_step")
+        roof["traffic_unit"] = "HBM bytes per step (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction)"
+        roof["traffic_source"] = (os.path.relpath(KC_TRAFFIC_JSON, ROOT)
+                                  + " (rocprofv3 --pmc passes of tools/kc_bench.py, KC kernels only, not this run)")
+        if tj.get("kernels"):
+            name, k = max(tj["kernels"].items(),
+                          key=lambda kv: kv[1].get("avg_us", 0.0) * kv[1]["dispatches_per_step"])
+            roof["dominant_kernel"] = dict(k, name=name)
+    if not extras:
+        return {"value": round(nbytes / wall / 2 ** 30, 3), "unit": "GiB/s", "ms_per_step": round(1e3 * wall, 3),
+                "phases_ms": phases, "wire_ratio": round(len(z) / nbytes, 4), "roofline": roof,
+                "tensors": len(numels), "bytes": nbytes, "steps": steps, "warmup": warmup}
     # device part alone (k-means + ranks, LUT decode; the previous KC line)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -288,20 +317,9 @@ def kc_pipeline(steps, warmup, dev):
     t_h = time.perf_counter() - t0
     host_gz_gibs = len(sample) / t_h / 2 ** 30
     t_host_pipe = wall - ph["gzip"] / steps + nbytes / (host_gz_gibs * 2 ** 30)
-    # the same pipeline with the opt-in host-memory policy (openfl_amd.hostmem:
-    # large blocks kept in the heap, so each payload `bytes` reuses faulted
-    # pages); applied last, it is process-wide
-    from openfl_amd.hostmem import keep_large_blocks
-    tuned = None
-    if keep_large_blocks():
-        for _ in range(warmup + 1):
-            decode(*encode())
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            z, maps = encode()
-            decode(z, maps)
-        tuned = (time.perf_counter() - t0) / steps
+    # (the opt-in host-memory policy, openfl_amd.hostmem.keep_large_blocks,
+    # is process-wide, so it is not applied here: tools/kc_bench.py --hostmem
+    # times it in a process of its own)
     # host inflate variant (native threads into pinned staging, then H2D of the ranks)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -310,7 +328,7 @@ def kc_pipeline(steps, warmup, dev):
     torch.cuda.synchronize()
     t_host_inflate = time.perf_counter() - t0
     return {"value": round(nbytes / wall / 2 ** 30, 3), "unit": "GiB/s", "ms_per_step": round(1e3 * wall, 3),
-            "phases_ms": phases,
+            "phases_ms": phases, "roofline": roof,
             "wire_ratio": round(len(z) / nbytes, 4), "check_rel_l2": round(rel, 5),
             "device_only": {"value": round(nbytes / dev_only / 2 ** 30, 2), "ms_per_step": round(1e3 * dev_only, 3),
                             "scope": "batched k-means fit + ranks and LUT decode, no gzip"},
@@ -318,10 +336,6 @@ def kc_pipeline(steps, warmup, dev):
                                    "gzip9_GiBps": round(host_gz_gibs, 4), "ratio": round(len(zh) / len(sample), 4),
                                    "sample": f"gzip -9 of 4 tensors' ranks (64 MiB) on {cores} threads, "
                                              "extrapolated to the set in place of the device gzip"},
-            "host_malloc_keep_variant": None if tuned is None else {
-                "value": round(nbytes / tuned / 2 ** 30, 3), "ms_per_step": round(1e3 * tuned, 3),
-                "scope": "the same pipeline after openfl_amd.hostmem.keep_large_blocks() (opt-in, process-wide: "
-                         "payload bytes reuse heap pages instead of fresh mappings)"},
             "host_inflate_variant": {"inflate_h2d_ms": round(1e3 * t_host_inflate, 3),
                                      "scope": f"ofl_gunzip_members on {cores} host threads + H2D of the ranks, "
                                               "in place of the device inflate"},
@@ -541,7 +555,7 @@ def main(argv=None):
     if world == 1 and args.also:
         for name in [a for a in args.also.split(",") if a]:
             if name == "kc_uniform_1gib":
-                also[name] = kc_pipeline(max(2, args.also_steps // 10), 1, dev)
+                also[name] = kc_pipeline(max(10, args.also_steps // 2), 2, dev)
             else:
                 # a ResNet-50 step is ~0.35 ms: more steps for a stable rate
                 st = max(args.also_steps, 200) if name == "resnet50_fp32" else args.also_steps

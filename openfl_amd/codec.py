@@ -230,6 +230,75 @@ def resolve_device(device):
     return d if d.index is not None else torch.device("cuda", torch.cuda.current_device())
 
 
+def resolve_devices(device):
+    """A plugin `device` setting -> the list of ROCm devices it names.
+
+    One device: "cpu" / None (the current GPU, the reference's default),
+    "cuda:N".  Several (calls from different threads spread over them,
+    ThreadDevices): "cuda" (every visible GPU), "cuda:0,cuda:2" or a list /
+    tuple of single-device settings.  The reference has one device per
+    pipeline (eden_pipeline.py:738); its callers reach several GPUs only
+    through the gRPC server's concurrent worker threads
+    (transport/grpc/aggregator_server.py:305, component/aggregator/
+    aggregator.py:643-646), which is what the per-thread mapping serves."""
+    if isinstance(device, (list, tuple)):
+        devs = [resolve_device(d) for d in device]
+    elif isinstance(device, str) and "," in device:
+        devs = [resolve_device(d.strip()) for d in device.split(",") if d.strip()]
+    elif isinstance(device, str) and device.strip() in ("cuda", "cuda:all"):
+        if not torch.cuda.is_available():
+            raise _lib.CodecError("openfl_amd codecs need a ROCm GPU (no CPU fallback)")
+        devs = [torch.device("cuda", i) for i in range(torch.cuda.device_count())]
+    else:
+        devs = [resolve_device(device)]
+    if not devs:
+        raise _lib.CodecError(f"device setting {device!r} names no GPU")
+    return devs
+
+
+class ThreadDevices:
+    """Which of a plugin's devices a calling thread uses: the first call from
+    a thread takes the next slot round-robin, and the thread keeps it (its
+    streams, staging and device buffers are thread-local too).  Pure Python:
+    no device is touched here."""
+
+    def __init__(self, n):
+        if n < 1:
+            raise ValueError("ThreadDevices needs at least one device")
+        self.n = int(n)
+        self._tls = threading.local()
+        self._next = 0
+        self._lock = threading.Lock()
+
+    def slot(self):
+        s = getattr(self._tls, "slot", None)
+        if s is None:
+            with self._lock:
+                s = self._next % self.n
+                self._next += 1
+            self._tls.slot = s
+        return s
+
+
+class PerThreadDevice:
+    """Mixin: `self.device` is the calling thread's device among
+    `self.devices` (set up by _init_devices from a plugin device setting)."""
+
+    def _init_devices(self, device, share=None):
+        """share: another PerThreadDevice whose thread -> device mapping this
+        one follows (the transformers of one pipeline stay on one GPU per
+        thread)."""
+        if share is not None:
+            self.devices, self._thread_devices = share.devices, share._thread_devices
+            return
+        self.devices = resolve_devices(device)
+        self._thread_devices = ThreadDevices(len(self.devices))
+
+    @property
+    def device(self):
+        return self.devices[self._thread_devices.slot()]
+
+
 class EdenCodec:
     """Batch Eden codec on one device with a plan cache.
 

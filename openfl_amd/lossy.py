@@ -18,6 +18,11 @@ from openfl_amd import _lib, hostmem
 _tls = threading.local()
 GZIP_CHUNK = 8 << 20
 _pool = None
+_pool_lock = threading.Lock()
+# gunzip_device hands torch a read-only view of the payload (torch only reads
+# it for the H2D); one narrow process-wide filter instead of per-call
+# catch_warnings(), which is not thread-safe on the copy pool's threads
+warnings.filterwarnings("ignore", message="The given NumPy array is not writable", category=UserWarning)
 
 
 def _on_device(fn):
@@ -370,10 +375,12 @@ def gunzip_device(data, out):
     # profiles/r02_hostcopy_probe.json), on a pool thread while this one
     # indexes the members (both release the GIL)
     d_in = _buf(dev, "gz_in", max(src.size, 1))
+    # d_in belongs to the caller's current stream, and the inflate runs there:
+    # the pool thread enqueues the copy on that same stream
+    caller_stream = torch.cuda.current_stream(dev)
 
     def h2d():
-        with torch.cuda.device(dev), warnings.catch_warnings():  # a read-only view: torch only reads it
-            warnings.simplefilter("ignore", UserWarning)
+        with torch.cuda.device(dev), torch.cuda.stream(caller_stream):
             if src.size:
                 d_in[:src.size].copy_(torch.from_numpy(src))
     copy = _h2d_pool().submit(h2d)
@@ -412,9 +419,10 @@ _h2d_executor = None
 
 def _h2d_pool():
     global _h2d_executor
-    if _h2d_executor is None:
-        _h2d_executor = ThreadPoolExecutor(max_workers=4)  # concurrent callers do not queue behind one copy
-    return _h2d_executor
+    with _pool_lock:
+        if _h2d_executor is None:
+            _h2d_executor = ThreadPoolExecutor(max_workers=4)  # concurrent callers do not queue behind one copy
+        return _h2d_executor
 
 
 def rank_map(values):
@@ -433,7 +441,8 @@ def gzip_compress(data_bytes, level=9, threads=8):
     mv = memoryview(data_bytes)
     if len(mv) <= GZIP_CHUNK or threads <= 1:
         return gzip.compress(bytes(mv), compresslevel=level)
-    if _pool is None:
-        _pool = ThreadPoolExecutor(max_workers=threads)
+    with _pool_lock:
+        if _pool is None:
+            _pool = ThreadPoolExecutor(max_workers=threads)
     parts = [mv[i:i + GZIP_CHUNK] for i in range(0, len(mv), GZIP_CHUNK)]
     return b"".join(_pool.map(lambda p: gzip.compress(bytes(p), compresslevel=level), parts))

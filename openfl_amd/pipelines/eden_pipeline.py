@@ -31,7 +31,7 @@ import numpy as np
 import torch
 
 from openfl_amd import _lib, hostmem
-from openfl_amd.codec import EdenCodec, resolve_device
+from openfl_amd.codec import EdenCodec, PerThreadDevice
 from openfl_amd.pipelines.pipeline import Float32NumpyArrayToBytes, TransformationPipeline, Transformer
 
 _FAST_SEED_PREFIX = 4096
@@ -98,6 +98,7 @@ def eden_seeds(totals):
 
 
 _pool = None
+_pool_lock = threading.Lock()
 
 
 def _copy_many(dst, src, nbytes, threads=8):
@@ -113,23 +114,36 @@ def _copy_many(dst, src, nbytes, threads=8):
 
 def _threads():
     global _pool
-    if _pool is None:
-        _pool = ThreadPoolExecutor(max_workers=8)
-    return _pool
+    with _pool_lock:
+        if _pool is None:
+            _pool = ThreadPoolExecutor(max_workers=8)
+        return _pool
 
 
-class Eden:
-    """Device Eden codec with the reference Eden class's method surface."""
+class Eden(PerThreadDevice):
+    """Device Eden codec with the reference Eden class's method surface.
+
+    device: one GPU ("cpu" = the current one, "cuda:N"), or several ("cuda" =
+    all visible, "cuda:0,cuda:1", a list): each calling thread is bound to one
+    of them round-robin on its first call (codec.ThreadDevices), so the gRPC
+    server's concurrent compress / decompress calls spread over the GPUs with
+    the plugin surface unchanged.  Plans, workspaces, streams and staging are
+    per device and per thread."""
 
     def __init__(self, nbits=8, device="cpu"):
         if nbits not in [1, 2, 3, 4, 5, 6, 7, 8]:
             raise Exception("nbits value is not supported")  # :389-390
         self.nbits = int(nbits)
-        self.device = resolve_device(device)
+        self._init_devices(device)
         self.num_hadamard = 2           # :394
         self.max_padding_overhead = 0.1  # :397
-        self.codec = EdenCodec(self.nbits, self.device)
+        self._codecs = [EdenCodec(self.nbits, d) for d in self.devices]
         self._tls = threading.local()
+
+    @property
+    def codec(self):
+        """The calling thread's device codec (plan cache + workspaces)."""
+        return self._codecs[self._thread_devices.slot()]
 
     def _stream(self):
         st = getattr(self._tls, "stream", None)
@@ -318,7 +332,8 @@ def _batch_stage(eden, arrays):
     st = eden._stream()
     xh = eden._staging().get("x", plan.arena_numel, torch.float32)
     base = xh.data_ptr()
-    x = torch.empty(max(plan.arena_numel, 1), dtype=torch.float32, device=eden.device)
+    with torch.cuda.stream(st):  # allocated on the stream that fills and reads it
+        x = torch.empty(max(plan.arena_numel, 1), dtype=torch.float32, device=eden.device)
     offs = plan.elem_offsets
     for lo, hi in _pieces(offs, [f.size for f in flats], _CHUNKS):
         _copy_many([base + 4 * offs[i] for i in range(lo, hi)], [flats[i].ctypes.data for i in range(lo, hi)],

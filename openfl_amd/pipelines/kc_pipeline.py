@@ -10,17 +10,17 @@ is exact (sequential key->value replacement emulated per element).
 import numpy as np
 
 from openfl_amd.pipelines.lossy_common import (GZIPTransformer, float_to_int, gzip_lut_backward_device,
-                                               kmeans_ranks, lut_backward, resolve_device, to_device)
+                                               kmeans_ranks, lut_backward, PerThreadDevice, to_device)
 from openfl_amd.pipelines.pipeline import TransformationPipeline, Transformer
 
 
-class KmeansTransformer(Transformer):
+class KmeansTransformer(PerThreadDevice, Transformer):
     """Quantise to n_cluster k-means centres; int32 ranks + {rank: centre}."""
 
     def __init__(self, n_cluster=6, device="cpu"):
         self.lossy = True
         self.n_cluster = n_cluster
-        self.device = resolve_device(device)
+        self._init_devices(device)
 
     def _ranks(self, data):
         """-> (float32 rank device tensor or None, int_to_float); None = tiny path."""

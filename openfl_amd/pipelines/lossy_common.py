@@ -12,7 +12,7 @@ import numpy as np
 import torch
 
 from openfl_amd import lossy
-from openfl_amd.codec import resolve_device
+from openfl_amd.codec import PerThreadDevice, resolve_device
 from openfl_amd.pipelines.pipeline import Transformer
 
 
@@ -104,5 +104,5 @@ def lut_backward(data, int2float_map, device):
     return out.cpu().numpy().reshape(arr.shape)
 
 
-__all__ = ["GZIPTransformer", "float_to_int", "gzip_lut_backward_device", "kmeans_ranks", "lut_backward",
+__all__ = ["GZIPTransformer", "PerThreadDevice", "float_to_int", "gzip_lut_backward_device", "kmeans_ranks", "lut_backward",
            "resolve_device", "to_device"]

@@ -7,18 +7,18 @@ on the GPU (see stc_pipeline / kc_pipeline for the parity notes).
 import numpy as np
 
 from openfl_amd.pipelines.lossy_common import (GZIPTransformer, float_to_int, gzip_lut_backward_device,
-                                               kmeans_ranks, lut_backward, resolve_device, to_device)
+                                               kmeans_ranks, lut_backward, PerThreadDevice, to_device)
 from openfl_amd.pipelines.pipeline import TransformationPipeline, Transformer
 from openfl_amd.pipelines.stc_pipeline import SparsityTransformer
 
 
-class KmeansTransformer(Transformer):
+class KmeansTransformer(PerThreadDevice, Transformer):
     """k-means on a flattened (sparse, float64) vector; {"int_to_float"} only."""
 
-    def __init__(self, n_cluster=6, device="cpu"):
+    def __init__(self, n_cluster=6, device="cpu", share=None):
         self.n_cluster = n_cluster
         self.lossy = True
-        self.device = resolve_device(device)
+        self._init_devices(device, share)
 
     def forward(self, data, **kwargs):
         data = np.asarray(data)
@@ -40,7 +40,8 @@ class SKCPipeline(TransformationPipeline):
     def __init__(self, p_sparsity=0.1, n_clusters=6, device="cpu", gzip_level=9, gzip_backend="host", **kwargs):
         self.p = p_sparsity
         self.n_cluster = n_clusters
-        super().__init__(transformers=[SparsityTransformer(self.p, device), KmeansTransformer(n_clusters, device),
+        sp = SparsityTransformer(self.p, device)
+        super().__init__(transformers=[sp, KmeansTransformer(n_clusters, device, share=sp),
                                        GZIPTransformer(gzip_level, backend=gzip_backend)], **kwargs)
 
     def forward(self, data, **kwargs):

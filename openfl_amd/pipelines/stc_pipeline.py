@@ -10,7 +10,7 @@ import numpy as np
 
 from openfl_amd import lossy
 from openfl_amd.pipelines.lossy_common import (GZIPTransformer, float_to_int, gzip_lut_backward_device, lut_backward,
-                                               resolve_device, to_device)
+                                               PerThreadDevice, to_device)
 from openfl_amd.pipelines.pipeline import TransformationPipeline, Transformer
 
 
@@ -18,13 +18,13 @@ def _topk_count(n, p):
     return int(np.ceil(n * p))  # :40 / skc :45
 
 
-class SparsityTransformer(Transformer):
+class SparsityTransformer(PerThreadDevice, Transformer):
     """Keep the ceil(n*p) largest |x|; dense float64 output (:30-51)."""
 
     def __init__(self, p=0.01, device="cpu"):
         self.lossy = True
         self.p = p
-        self.device = resolve_device(device)
+        self._init_devices(device)
 
     def sparse_device(self, data):
         x = to_device(data.astype(np.float32), self.device)
@@ -52,12 +52,12 @@ def ternary_map(n, n_pos, n_neg, abs_sum):
             (ranks.get("neg", 0.0), ranks.get("zero", 0.0), ranks.get("pos", 0.0)))
 
 
-class TernaryTransformer(Transformer):
+class TernaryTransformer(PerThreadDevice, Transformer):
     """x > 0 -> +mean|x|, x < 0 -> -mean|x|, else 0; int32 ranks (:105-130)."""
 
-    def __init__(self, device="cpu"):
+    def __init__(self, device="cpu", share=None):
         self.lossy = True
-        self.device = resolve_device(device)
+        self._init_devices(device, share)
 
     def forward(self, data, **kwargs):
         x = to_device(data, self.device)
@@ -76,7 +76,8 @@ class STCPipeline(TransformationPipeline):
 
     def __init__(self, p_sparsity=0.1, n_clusters=6, device="cpu", gzip_level=9, gzip_backend="host", **kwargs):
         self.p = p_sparsity
-        super().__init__(transformers=[SparsityTransformer(self.p, device), TernaryTransformer(device),
+        sp = SparsityTransformer(self.p, device)
+        super().__init__(transformers=[sp, TernaryTransformer(device, share=sp),
                                        GZIPTransformer(gzip_level, backend=gzip_backend)], **kwargs)
 
     def forward(self, data, **kwargs):

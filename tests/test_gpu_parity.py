@@ -478,3 +478,51 @@ def test_step_graph_replay_bit_identical():
     gr.replay()
     torch.cuda.synchronize()
     assert torch.equal(p0, p1) and torch.equal(s0, s1) and torch.equal(y0, y1)
+
+
+@pytest.mark.parametrize("setting", ["cuda", "two_slots_one_gpu"])
+def test_pipeline_multi_device_threads(setting):
+    """device naming several GPUs: each calling thread is bound to one of them
+    round-robin (codec.ThreadDevices) -- concurrent forward and backward calls
+    from unchanged callers (the gRPC pool, aggregator_server.py:305) give the
+    bytes, metadata and values of the single-device path.  "cuda" = every
+    visible GPU; on a one-GPU box the same device is also listed twice, so two
+    slots (separate codecs, plans, workspaces) share it."""
+    from openfl_amd.pipelines import EdenPipeline
+    dev = "cuda" if setting == "cuda" else [DEV, DEV]
+    multi = EdenPipeline(n_bits=8, device=dev)
+    single = EdenPipeline(n_bits=8, device=DEV)
+    eden = multi.transformers[0].eden
+    assert len(eden.devices) == (torch.cuda.device_count() if setting == "cuda" else 2)
+    rng = np.random.default_rng(19)
+    xs = [rng.standard_normal(int(n)).astype(np.float32) for n in rng.integers(200, 600_000, 16)]
+    seeds = rng.integers(1, 2 ** 16, len(xs))
+    ref, ref_out = [], []
+    for x, s in zip(xs, seeds):
+        planes, scales, dims, tot = single.transformers[0].eden.compress(x, int(s))
+        ref.append((planes.tobytes(), scales, dims, tot))
+    for (b, sc, dims, tot), s in zip(ref, seeds):
+        md = {0: float(s), 1: float(tot)}
+        for k, (a, d) in enumerate(zip(sc, dims)):
+            md[2 + 2 * k], md[3 + 2 * k] = a, float(d)
+        ref_out.append(single.transformers[0].eden.decompress(np.frombuffer(b, np.uint8), md))
+    enc, dec, slots = [None] * len(xs), [None] * len(xs), [None] * len(xs)
+
+    def work(i):
+        planes, scales, dims, tot = eden.compress(xs[i], int(seeds[i]))
+        enc[i] = (planes.tobytes(), scales, dims, tot)
+        md = {0: float(seeds[i]), 1: float(tot)}
+        for k, (a, d) in enumerate(zip(scales, dims)):
+            md[2 + 2 * k], md[3 + 2 * k] = a, float(d)
+        dec[i] = eden.decompress(np.frombuffer(enc[i][0], np.uint8), md)
+        slots[i] = eden._thread_devices.slot()
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(len(xs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for i in range(len(xs)):
+        assert enc[i][0] == ref[i][0] and enc[i][1:] == ref[i][1:]
+        np.testing.assert_array_equal(dec[i], ref_out[i])
+    assert sorted(set(slots)) == list(range(len(eden.devices)))  # every device got threads
