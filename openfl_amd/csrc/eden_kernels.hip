@@ -985,6 +985,18 @@ __device__ uint8_t raw_load_u8(rsrc_t r, int voff, int soff, int aux) __asm("llv
 __device__ void raw_store_f32x4(f32x4 v, rsrc_t r, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.store.v4f32");
 __device__ void raw_store_f32(float v, rsrc_t r, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.store.f32");
 
+// Cache policy of the large-slice passes' streaming buffer accesses (aux
+// operand: bit 1 = nt on gfx950).  Tuning constants for A/B builds
+// (tools/build_variant.sh ... -DOFL_LD_AUX=2), not a platform switch.
+#ifndef OFL_LD_AUX
+#define OFL_LD_AUX 0
+#endif
+#ifndef OFL_ST_AUX
+#define OFL_ST_AUX 0
+#endif
+constexpr int kLdAux = OFL_LD_AUX;
+constexpr int kStAux = OFL_ST_AUX;
+
 // word 3 = 0x00020000: 32-bit data format, as the gfx9 family expects
 DEVI rsrc_t mk_rsrc(const void* p, uint32_t bytes) {
     const uint64_t a = reinterpret_cast<uint64_t>(p);
@@ -999,14 +1011,14 @@ DEVI uint32_t tile_valid(int64_t len) {
     return len <= 0 ? 0u : (len >= (1 << kRowLog) ? (1u << kRowLog) : (uint32_t)len);
 }
 DEVI float4 bload4(rsrc_t r, uint32_t e, uint32_t k) {
-    const f32x4 q = raw_load_f32x4(r, (int)(e * 4u), (int)(k * 4u), 0);
+    const f32x4 q = raw_load_f32x4(r, (int)(e * 4u), (int)(k * 4u), kLdAux);
     return make_float4(q.x, q.y, q.z, q.w);
 }
-DEVI float bload1(rsrc_t r, uint32_t e, uint32_t k) { return raw_load_f32(r, (int)(e * 4u), (int)(k * 4u), 0); }
-DEVI void bstore1(rsrc_t r, uint32_t e, uint32_t k, float v) { raw_store_f32(v, r, (int)(e * 4u), (int)(k * 4u), 0); }
+DEVI float bload1(rsrc_t r, uint32_t e, uint32_t k) { return raw_load_f32(r, (int)(e * 4u), (int)(k * 4u), kLdAux); }
+DEVI void bstore1(rsrc_t r, uint32_t e, uint32_t k, float v) { raw_store_f32(v, r, (int)(e * 4u), (int)(k * 4u), kStAux); }
 DEVI void bstore4(rsrc_t r, uint32_t e, uint32_t k, const float* v) {
     const f32x4 q = {v[0], v[1], v[2], v[3]};
-    raw_store_f32x4(q, r, (int)(e * 4u), (int)(k * 4u), 0);
+    raw_store_f32x4(q, r, (int)(e * 4u), (int)(k * 4u), kStAux);
 }
 
 // x tile (L1 layout, float4 per register quad); live = false reads nothing
@@ -1111,7 +1123,7 @@ DEVI void fetch_planes(const KArgs& a, const SliceDesc& D, uint32_t tile, bool l
     for (int i = 0; i < 8; ++i) {
         const rsrc_t r = mk_rsrc(p0 + (int64_t)i * D.pl_stride, (live && i < a.nbits) ? (1u << (kRowLog - 3)) : 0u);
         if (A8) {
-            const i32x2 q = raw_load_i32x2(r, (int)(base5 >> 3), 0, 0);
+            const i32x2 q = raw_load_i32x2(r, (int)(base5 >> 3), 0, kLdAux);
             w[i] = (uint64_t)(uint32_t)q.x | ((uint64_t)(uint32_t)q.y << 32);
         } else {
             uint64_t x = 0;
@@ -1533,12 +1545,12 @@ __global__ __launch_bounds__(col6_nt<TL>(), 4) void k_col6(KArgs a) {
         const uint32_t vo = opaque(ws_pos(map(base1)) * 4u);
 #pragma unroll
         for (int r = 0; r < 64; ++r)
-            v[r] = raw_load_f32(rw, (int)vo, (int)ws_pos((LT<CS::L1>::off(r) >> K) << 15) * 4, 0);
+            v[r] = raw_load_f32(rw, (int)vo, (int)ws_pos((LT<CS::L1>::off(r) >> K) << 15) * 4, kLdAux);
     } else {
         const uint32_t vo = opaque(map(base1) * 4u);
 #pragma unroll
         for (int r = 0; r < 64; ++r)
-            v[r] = raw_load_f32(rw, (int)vo, (int)uu((LT<CS::L1>::off(r) >> K) << lo) * 4, 0);
+            v[r] = raw_load_f32(rw, (int)vo, (int)uu((LT<CS::L1>::off(r) >> K) << lo) * 4, kLdAux);
     }
     stages<CS::L1, CS::A1>(v);
     if constexpr (EXCH) {
@@ -1568,14 +1580,14 @@ __global__ __launch_bounds__(col6_nt<TL>(), 4) void k_col6(KArgs a) {
             const uint32_t vo = opaque(ws_pos(map(base1)) * 4u);
 #pragma unroll
             for (int r = 0; r < 64; ++r)
-                raw_store_f32(v[r], rw, (int)vo, (int)ws_pos((LT<CS::L1>::off(r) >> K) << 15) * 4, 0);
+                raw_store_f32(v[r], rw, (int)vo, (int)ws_pos((LT<CS::L1>::off(r) >> K) << 15) * 4, kStAux);
         } else {
             const uint32_t vo = opaque(map(base1) * 4u);
             int los = lo;
             asm volatile("" : "+s"(los));  // recompute the row offsets: 64 SGPRs kept live would spill
 #pragma unroll
             for (int r = 0; r < 64; ++r)
-                raw_store_f32(v[r], rw, (int)vo, (int)uu((LT<CS::L1>::off(r) >> K) << los) * 4, 0);
+                raw_store_f32(v[r], rw, (int)vo, (int)uu((LT<CS::L1>::off(r) >> K) << los) * 4, kStAux);
         }
     } else {
         const uint32_t bcw = LT<LC>::base(tid);
@@ -1584,7 +1596,7 @@ __global__ __launch_bounds__(col6_nt<TL>(), 4) void k_col6(KArgs a) {
         asm volatile("" : "+s"(los));
 #pragma unroll
         for (int r = 0; r < 64; ++r)
-            raw_store_f32(v[r], rw, (int)vo, (int)uu((LT<LC>::off(r) >> K) << los) * 4, 0);
+            raw_store_f32(v[r], rw, (int)vo, (int)uu((LT<LC>::off(r) >> K) << los) * 4, kStAux);
     }
     if (a.do_nu && tile == 0) {  // slice norm, as in k_col
         __shared__ float nred[NT / 64];

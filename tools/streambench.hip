@@ -158,6 +158,10 @@ int main() {
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
     CHECK(hipEventCreate(&e1));
+    // bytes per element moved (read + write): 8 for the copies, 7 for the
+    // 4 B <-> 3 B pack / unpack kernels (round 2 printed every line at 8, which
+    // overstated the pack rows by 8/7: pack_l3_lds is 5.45 TB/s, not 6.23)
+    double bpe = 8.0;
     auto run = [&](const char* name, auto launch) {
         launch();
         CHECK(hipDeviceSynchronize());
@@ -167,7 +171,7 @@ int main() {
         CHECK(hipEventSynchronize(e1));
         float ms = 0;
         CHECK(hipEventElapsedTime(&ms, e0, e1));
-        printf("%-28s %8.1f us  %6.2f TB/s (read+write)\n", name, 1e3 * ms / 10, 2.0 * n * 4 / (ms / 10 * 1e-3) / 1e12);
+        printf("%-28s %8.1f us  %6.2f TB/s (read+write)\n", name, 1e3 * ms / 10, bpe * n / (ms / 10 * 1e-3) / 1e12);
     };
     for (int g : {1, 2, 4, 8}) {
         char nm[64];
@@ -186,6 +190,7 @@ int main() {
     uint8_t* pk;
     CHECK(hipMalloc(&pk, n * 3));
     hipLaunchKernelGGL(fill, dim3(cus * 4), dim3(256), 0, 0, a, n);
+    bpe = 7.0;
     run("pack_l3 (4 B in, 3 B out)", [&] { hipLaunchKernelGGL(pack_l3, dim3(cus), dim3(512), 0, 0, a, pk, n >> 15); });
     run("store34_l3 (no math)", [&] { hipLaunchKernelGGL(store34_l3, dim3(cus), dim3(512), 0, 0, a, pk, n >> 15); });
     run("pack_l3_lds (LDS-staged)", [&] { hipLaunchKernelGGL(pack_l3_lds, dim3(cus), dim3(512), 0, 0, a, pk, n >> 15); });
