@@ -94,6 +94,12 @@ void ofl_eden_plan_destroy(ofl_eden_plan_t plan);
 int ofl_eden_plan_set_schedule(ofl_eden_plan_t plan, int64_t wave_bytes, int streams);
 int ofl_eden_plan_get_schedule(ofl_eden_plan_t plan, int64_t* wave_bytes, int* streams);
 int ofl_eden_plan_num_waves(ofl_eden_plan_t plan);
+/* Kernel choice for the large slices' row passes (no reference counterpart;
+ * outputs bit-identical either way): -1 auto (launches of fewer than 4 tiles
+ * per CU use the two-blocks-per-CU kernels, the rest the persistent
+ * prefetching ones; env OFL_EDEN_ROW2 / OFL_EDEN_ROW2_TPC override the auto
+ * rule), 0 always persistent, 1 always two blocks per CU. */
+int ofl_eden_plan_set_row2(ofl_eden_plan_t plan, int mode);
 
 /* Totals: slices (= length of the scales array), planes-arena bytes,
  * workspace bytes needed by encode and decode. */

@@ -20,7 +20,7 @@ OFL_EINVAL, OFL_EHIP, OFL_ESPACE, OFL_EFORMAT = -1, -2, -3, -4
 EXPORTS = (
     "ofl_version", "ofl_last_error", "ofl_eden_slice_plan", "ofl_eden_plan_create",
     "ofl_eden_plan_destroy", "ofl_eden_plan_set_schedule", "ofl_eden_plan_num_waves",
-    "ofl_eden_plan_get_schedule", "ofl_eden_plan_num_slices", "ofl_eden_plan_planes_bytes",
+    "ofl_eden_plan_get_schedule", "ofl_eden_plan_set_row2", "ofl_eden_plan_num_slices", "ofl_eden_plan_planes_bytes",
     "ofl_eden_plan_workspace_bytes", "ofl_eden_plan_tensor_info", "ofl_eden_plan_tensor_dims",
     "ofl_eden_encode", "ofl_eden_decode", "ofl_eden_decode_add", "ofl_eden_encode_host", "ofl_eden_decode_host", "ofl_eden_plan_profile", "ofl_eden_plan_num_launches",
     "ofl_eden_plan_launch_info", "ofl_eden_plan_profile_collect", "ofl_serial_sum_f32", "ofl_serial_sum_copy_f32",
@@ -56,6 +56,8 @@ def _bind(L):
     L.ofl_eden_plan_destroy.restype = None
     L.ofl_eden_plan_set_schedule.argtypes = [vp, i64, i32]
     L.ofl_eden_plan_set_schedule.restype = i32
+    L.ofl_eden_plan_set_row2.argtypes = [vp, i32]
+    L.ofl_eden_plan_set_row2.restype = i32
     L.ofl_eden_plan_num_waves.argtypes = [vp]
     L.ofl_eden_plan_num_waves.restype = i32
     L.ofl_eden_plan_get_schedule.argtypes = [vp, vp, vp]

@@ -881,10 +881,14 @@ __global__ __launch_bounds__(256) void k_gzip_pack(const uint8_t* slots, const u
 // Huffman decode is inherently serial, so every lane runs it on the same
 // (wave-uniform) values and the lanes split the work that is parallel: table
 // construction, each copy's bytes (an overlapping copy d < L is the periodic
-// extension out[p + i] = out[p - d + i % d]) and the store.  The member's
-// output stays in LDS until it is complete (WIN = 16 KiB for the device gzip's
-// members: 8 members decode per CU at once, the decode being latency-bound;
-// 64 KiB otherwise); the compressed bytes stream through a small LDS ring.
+// extension out[p + i] = out[p - d + i % d]) and the store.  Default (RING):
+// only the last WIN = 1 KiB of a member's output stays in LDS, every byte is
+// also stored to global memory as it is produced, and the rare copy reaching
+// further back than the ring reads those global bytes back (stored earlier by
+// the same wavefront; a wavefront-scope acquire/release fence orders them);
+// the window decoder (RING = false, OFL_GZ_INFLATE=window) keeps the whole
+// output in a 16 / 64 KiB LDS window instead.  The compressed bytes stream
+// through a small LDS ring.
 // Any valid deflate data decodes (stored, fixed and dynamic blocks, RFC 1951).
 // ISIZE and the CRC-32 (over the member's output, wave-parallel) are checked here.
 constexpr int kRing = 512;                 // compressed-input ring per wave (bytes)
@@ -1238,6 +1242,8 @@ __global__ __launch_bounds__(64) void k_inflate_members(InfArgs a) {
                         }
                     }
                 } else {  // ring only: further back than the ring (d > WIN - len >= len)
+                    // the source bytes are this wavefront's earlier global stores
+                    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
                     for (uint32_t k = lane; k < len; k += 64) {
                         const uint8_t v = dst[p - d + k];
                         S.win[(p + k) & M] = v;
@@ -1257,6 +1263,7 @@ __global__ __launch_bounds__(64) void k_inflate_members(InfArgs a) {
         return;
     }
     __builtin_amdgcn_wave_barrier();
+    if (RING) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the CRC reads the stores back
     // CRC-32 of the output, checked here: lane l takes bytes [l sg, (l+1) sg)
     // of the output seen as the tail of 64 sg bytes (leading zeros leave a
     // zero-initialised CRC unchanged), bitwise (vector work beside the other

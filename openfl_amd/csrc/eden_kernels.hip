@@ -37,6 +37,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -1014,7 +1015,8 @@ DEVI float4 bload4(rsrc_t r, uint32_t e, uint32_t k) {
     const f32x4 q = raw_load_f32x4(r, (int)(e * 4u), (int)(k * 4u), kLdAux);
     return make_float4(q.x, q.y, q.z, q.w);
 }
-DEVI float bload1(rsrc_t r, uint32_t e, uint32_t k) { return raw_load_f32(r, (int)(e * 4u), (int)(k * 4u), kLdAux); }
+template <int AUX = kLdAux>
+DEVI float bload1(rsrc_t r, uint32_t e, uint32_t k) { return raw_load_f32(r, (int)(e * 4u), (int)(k * 4u), AUX); }
 DEVI void bstore1(rsrc_t r, uint32_t e, uint32_t k, float v) { raw_store_f32(v, r, (int)(e * 4u), (int)(k * 4u), kStAux); }
 DEVI void bstore4(rsrc_t r, uint32_t e, uint32_t k, const float* v) {
     const f32x4 q = {v[0], v[1], v[2], v[3]};
@@ -1033,19 +1035,23 @@ DEVI void fetch_x(const KArgs& a, const SliceDesc& D, uint32_t tile, bool live, 
     }
 }
 // the valid head of a float4 that straddles the slice's input length
+// (branch-free per lane: the <= 3 values are block-uniform loads and each
+// register takes them by a select, so no register copies or spills)
 DEVI void fix_x(const KArgs& a, const SliceDesc& D, uint32_t tile, uint32_t base1, float (&v)[64]) {
     const uint32_t e0 = tile << kRowLog;
     const uint32_t nv = tile_valid(D.len - (int64_t)e0);
-    if (nv & 3u) {
+    const uint32_t rem = nv & 3u;
+    if (rem) {
         const uint32_t eb = nv & ~3u;
         const float* x = a.xin + D.x_off + e0 + eb;
+        const float x0 = x[0], x1 = rem > 1u ? x[1] : 0.0f, x2 = rem > 2u ? x[2] : 0.0f;
 #pragma unroll
-        for (int k = 0; k < 64; k += 4)
-            if (base1 + LT<RS::L1>::off(k) == eb) {
-#pragma unroll
-                for (int q = 0; q < 3; ++q)
-                    if ((uint32_t)q < (nv & 3u)) v[k + q] = x[q];
-            }
+        for (int k = 0; k < 64; k += 4) {
+            const bool hit = base1 + LT<RS::L1>::off(k) == eb;
+            v[k] = hit ? x0 : v[k];
+            v[k + 1] = hit ? x1 : v[k + 1];
+            v[k + 2] = hit ? x2 : v[k + 2];
+        }
     }
 }
 DEVI void store_y(const KArgs& a, const SliceDesc& D, uint32_t tile, uint32_t base1, const float (&v)[64]) {
@@ -1090,16 +1096,17 @@ DEVI float* ws_row_base(const KArgs& a, const SliceDesc& D, uint32_t tile) {
     return D.perm ? a.ws + D.ws_off + ((size_t)(tile >> 1) << (kRowLog + 1)) + ((tile & 1u) << 5)
                   : a.ws + D.ws_off + ((size_t)tile << kRowLog);
 }
+template <int AUX = kLdAux>
 DEVI void fetch_ws(const KArgs& a, const SliceDesc& D, uint32_t tile, bool live, uint32_t base3, float (&v)[64]) {
     if (D.perm) {
         const rsrc_t r = mk_rsrc(ws_row_base(a, D, tile), live ? (4u << (kRowLog + 1)) - 128u : 0u);
         const uint32_t b = ws_row_idx(base3);
 #pragma unroll
-        for (int k = 0; k < 64; ++k) v[k] = bload1(r, b, LT<RS::L3>::off(k) << 1);
+        for (int k = 0; k < 64; ++k) v[k] = bload1<AUX>(r, b, LT<RS::L3>::off(k) << 1);
     } else {
         const rsrc_t r = mk_rsrc(ws_row_base(a, D, tile), live ? (4u << kRowLog) : 0u);
 #pragma unroll
-        for (int k = 0; k < 64; ++k) v[k] = bload1(r, base3, LT<RS::L3>::off(k));
+        for (int k = 0; k < 64; ++k) v[k] = bload1<AUX>(r, base3, LT<RS::L3>::off(k));
     }
 }
 DEVI void store_ws(const KArgs& a, const SliceDesc& D, uint32_t tile, uint32_t base3, const float (&v)[64]) {
@@ -1647,18 +1654,18 @@ DEVI void exchange_half_pad(float (&v)[64], float* s, uint32_t tid) {
 }
 
 // registers [32 h, 32 h + 32) of a ws tile (L3 layout), as fetch_ws
-template <int H>
+template <int H, int AUX = kLdAux>
 DEVI void fetch_ws_half(const KArgs& a, const SliceDesc& D, uint32_t tile, bool live, uint32_t base3,
                         float (&v)[64]) {
     if (D.perm) {
         const rsrc_t r = mk_rsrc(ws_row_base(a, D, tile), live ? (4u << (kRowLog + 1)) - 128u : 0u);
         const uint32_t b = ws_row_idx(base3);
 #pragma unroll
-        for (int k = 32 * H; k < 32 * H + 32; ++k) v[k] = bload1(r, b, LT<RS::L3>::off(k) << 1);
+        for (int k = 32 * H; k < 32 * H + 32; ++k) v[k] = bload1<AUX>(r, b, LT<RS::L3>::off(k) << 1);
     } else {
         const rsrc_t r = mk_rsrc(ws_row_base(a, D, tile), live ? (4u << kRowLog) : 0u);
 #pragma unroll
-        for (int k = 32 * H; k < 32 * H + 32; ++k) v[k] = bload1(r, base3, LT<RS::L3>::off(k));
+        for (int k = 32 * H; k < 32 * H + 32; ++k) v[k] = bload1<AUX>(r, base3, LT<RS::L3>::off(k));
     }
 }
 
@@ -1673,6 +1680,10 @@ DEVI void fetch_ws_half(const KArgs& a, const SliceDesc& D, uint32_t tile, bool 
 #define OFL_DIAG_ROWC2 0
 #endif
 constexpr int kDiagRowC2 = OFL_DIAG_ROWC2;
+#ifndef OFL_ROWC2_LD_AUX
+#define OFL_ROWC2_LD_AUX 2
+#endif
+constexpr int kRowC2LdAux = OFL_ROWC2_LD_AUX;  // nt (A/B: -DOFL_ROWC2_LD_AUX=0)
 template <bool ROLL>
 __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowC2(KArgs a) {
     using R = RowC2Set;
@@ -1699,14 +1710,17 @@ __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowC2(KArgs a) {
     int si; uint32_t tile;
     locate(t, si, tile);
     float v[64];
-    if (ROLL) fetch_ws(a, udesc(a.d, si), tile, true, base3, v);
+    // the intermediate is read once: nt loads (r03 A/B, profiles/r03_nt_ab.txt:
+    // 597 -> 572 us per 2 GiB wave; the same policy slows k_enc_rowA and
+    // k_dec_rowC by 8-14 %, so only this kernel uses it)
+    if (ROLL) fetch_ws<kRowC2LdAux>(a, udesc(a.d, si), tile, true, base3, v);
     for (;;) {
         const SliceDesc D = udesc(a.d, si);
         const int tn = t + (int)gridDim.x;
         const bool more = tn < total;
         int sn; uint32_t tln;
         locate(more ? tn : t, sn, tln);
-        if (!ROLL) fetch_ws(a, D, tile, true, base3, v);
+        if (!ROLL) fetch_ws<kRowC2LdAux>(a, D, tile, true, base3, v);
         stages<R::L3, R::F2c>(v);
         if (!(kDiagRowC2 & 1)) exchange_half_pad<R::L3, R::L4, R::HB>(v, s, tid);
         stages<R::L4, R::F2d>(v);
@@ -1733,8 +1747,8 @@ __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowC2(KArgs a) {
                 for (int i = 0; i < 8; ++i) w[i] = 0;
             }
             if (ROLL) {  // this half's registers are free: start the next tile's
-                if (g == 0) fetch_ws_half<0>(a, udesc(a.d, sn), tln, more, base3, v);
-                else fetch_ws_half<1>(a, udesc(a.d, sn), tln, more, base3, v);
+                if (g == 0) fetch_ws_half<0, kRowC2LdAux>(a, udesc(a.d, sn), tln, more, base3, v);
+                else fetch_ws_half<1, kRowC2LdAux>(a, udesc(a.d, sn), tln, more, base3, v);
             }
             store_planes(a.pout + D.pl_off, (tile << kRowLog) + base5 + ((uint32_t)g << R::HB), D.pl_stride,
                          a.nbits, w);
@@ -1744,6 +1758,207 @@ __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowC2(KArgs a) {
         if (tid == 0) a.part[D.part_off + tile] = dot;
         if (!more) break;
         t = tn; si = sn; tile = tln;
+    }
+}
+
+// ===========================================================================
+// Row passes with two blocks per CU, for waves of few tiles per CU (the
+// ResNet-50 class: ~1.5 tiles per CU per pass, where the persistent one-block
+// kernels' register prefetch never overlaps anything and half the CUs sit in
+// a second-tile tail).  No prefetch: the other block on the CU hides the
+// loads.  Every layout keeps one element bit at register index 5 (the half
+// bit), so each LDS exchange runs in two halves through a padded 2^14-float
+// buffer (68 KiB per block).  The sequence of index bits butterflied is the
+// persistent kernel's (an extra layout where needed), and the loads, sums and
+// stores are the same, so the outputs are bit-identical to k_enc_rowA /
+// k_dec_rowA / k_dec_rowC (tests/test_gpu_parity.py::test_row2_variants_bit_identical).
+// ===========================================================================
+struct RowA2Set {  // encode pass A, half bit 14: 0,1,11,12,13,14 | 2..6 | 10,7,8,9
+    static constexpr Lay A1 = RS::L1, A2{15, 2, 3, 4, 5, 6, 14}, A3{15, 10, 7, 8, 9, 6, 14};
+    static constexpr uint32_t F1a = RS::F1a, F1b = bits_mask({2, 3, 4, 5, 6}), F1c = bits_mask({10, 7, 8, 9});
+};
+struct DecA2Set {  // decode pass A, half bit 5: 0..4 | 11,12,13,14,5 | 6..10
+    static constexpr Lay C1 = RS::L5, C2{15, 11, 12, 13, 14, 9, 5}, C3{15, 6, 7, 8, 9, 10, 5};
+    static constexpr uint32_t G1 = RS::F2e, G2 = bits_mask({11, 12, 13, 14, 5}), G3 = bits_mask({6, 7, 8, 9, 10});
+};
+struct DecC2Set {  // decode pass C, half bit 10: 7,8,9 | 2..6,10 | 0,1,11,12,13 | 14
+    static constexpr Lay B1 = RS::L3, B2 = RS::L2, B3{15, 0, 1, 11, 12, 13, 10}, B4{15, 0, 1, 14, 11, 12, 10};
+    static constexpr uint32_t H1 = RS::F1c, H2 = RS::F1b, H3 = bits_mask({0, 1, 11, 12, 13}), H4 = bits_mask({14});
+};
+// apply_signs_direct in groups of 8 registers whose results are pinned before
+// the next group starts: at the 128-VGPR cap of two blocks per CU the
+// scheduler would otherwise overlap all 64 hash chains and spill
+template <Lay L>
+DEVI void apply_signs_grouped(float (&v)[64], uint32_t ebase, uint32_t base, int p, uint32_t b, float mul) {
+    // one code path for every p (the general per-element form of
+    // sgn_elem; no branch whose two sides the register allocator must both
+    // fit), the 64 sign bits first in two mask registers pinned per group of
+    // 8 hashes, then the flips: few live temporaries at the 128-VGPR cap
+    const uint32_t jm = (1u << (p - 3)) - 1u;
+    const uint32_t ps = (uint32_t)(p - 3);
+    uint32_t m[2] = {0u, 0u};
+#pragma unroll
+    for (int g = 0; g < 64; g += 8) {
+#pragma unroll
+        for (int r = g; r < g + 8; ++r) {
+            const uint32_t e = ebase + (base | LT<L>::off(r));
+            m[r >> 5] |= ((rd_word(e & jm, b) >> (4u * (e >> ps) + 3u)) & 1u) << (r & 31);
+        }
+        asm volatile("" : "+v"(m[0]), "+v"(m[1]));
+    }
+#pragma unroll
+    for (int r = 0; r < 64; ++r) v[r] = flip_unless(v[r] * mul, (m[r >> 5] >> (r & 31)) & 1u);
+}
+constexpr size_t kRow2Smem = kRowC2Ex + 64;     // half-exchange buffer + 8 wave partials
+constexpr size_t kRow2SmemC = kRowC2Ex + 1024;  // half-exchange buffer + 256 centroids
+
+// ws tile store / y tile store in any layout (as store_ws / store_y)
+template <Lay L>
+DEVI void store_ws_l(const KArgs& a, const SliceDesc& D, uint32_t tile, uint32_t base, const float (&v)[64]) {
+    if (D.perm) {
+        const rsrc_t r = mk_rsrc(ws_row_base(a, D, tile), (4u << (kRowLog + 1)) - 128u);
+        const uint32_t b = ws_row_idx(base);
+#pragma unroll
+        for (int k = 0; k < 64; ++k) bstore1(r, b, LT<L>::off(k) << 1, v[k]);
+    } else {
+        const rsrc_t r = mk_rsrc(ws_row_base(a, D, tile), 4u << kRowLog);
+#pragma unroll
+        for (int k = 0; k < 64; ++k) bstore1(r, base, LT<L>::off(k), v[k]);
+    }
+}
+template <Lay L>
+DEVI void store_y_l(const KArgs& a, const SliceDesc& D, uint32_t tile, uint32_t base, const float (&v)[64]) {
+    static_assert(LT<L>::rb(0) == 0 && LT<L>::rb(1) == 1, "float4 stores need element bits 0, 1 in registers 0, 1");
+    const uint32_t e0 = tile << kRowLog;
+    const uint32_t nv = tile_valid(D.ylen - (int64_t)e0);
+    const rsrc_t r = mk_rsrc(a.xout + D.y_off + e0, (nv & ~3u) * 4u);
+    if (a.yadd) {
+        const rsrc_t rb = mk_rsrc(a.yadd + D.y_off + e0, (nv & ~3u) * 4u);
+#pragma unroll
+        for (int k = 0; k < 64; k += 4) {
+            const float4 b = bload4(rb, base, LT<L>::off(k));
+            const float o[4] = {add_rn(b.x, v[k]), add_rn(b.y, v[k + 1]), add_rn(b.z, v[k + 2]), add_rn(b.w, v[k + 3])};
+            bstore4(r, base, LT<L>::off(k), o);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 64; k += 4) bstore4(r, base, LT<L>::off(k), &v[k]);
+    }
+    if (nv & 3u) {
+        const uint32_t eb = nv & ~3u;
+        float* y = a.xout + D.y_off + e0 + eb;
+        const float* yb = a.yadd ? a.yadd + D.y_off + e0 + eb : nullptr;
+#pragma unroll
+        for (int k = 0; k < 64; k += 4)
+            if (base + LT<L>::off(k) == eb) {
+#pragma unroll
+                for (int q = 0; q < 3; ++q)
+                    if ((uint32_t)q < (nv & 3u)) y[q] = yb ? add_rn(yb[q], v[k + q]) : v[k + q];
+            }
+    }
+}
+// block-uniform tile lookup of the non-persistent row launches (scalar loads)
+DEVI void row_locate(const KArgs& a, int t, int& si, uint32_t& tile) {
+    int lo = 0, hi = a.count - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((int)sld(a.tstart, mid) <= t) lo = mid; else hi = mid - 1;
+    }
+    si = (int)sld(a.list, lo);
+    tile = (uint32_t)(t - (int)sld(a.tstart, lo));
+}
+
+// encode pass A (as k_enc_rowA)
+__global__ __launch_bounds__(kRowNT, 4) void k_enc_rowA2(KArgs a) {
+    using R = RowA2Set;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float* s = reinterpret_cast<float*>(smem);
+    float* red = reinterpret_cast<float*>(smem + kRowC2Ex);
+    const int total = (int)sld(a.tstart, a.count);
+    for (int t = (int)blockIdx.x; t < total; t += (int)gridDim.x) {
+        // thread-derived addresses are recomputed every tile (an opaque tid):
+        // hoisted out of the loop they stay live across it and spill
+        const uint32_t tid = opaque(threadIdx.x);
+        const uint32_t base1 = LT<R::A1>::base(tid), base3 = LT<R::A3>::base(tid);
+        int si; uint32_t tile;
+        row_locate(a, t, si, tile);
+        const SliceDesc D = udesc(a.d, si);
+        float v[64];
+        fetch_x(a, D, tile, true, base1, v);
+        fix_x(a, D, tile, base1, v);
+        const uint32_t b1 = seed_b(sld(a.seeds, D.tensor));
+        float ss = 0.f;
+#pragma unroll
+        for (int r = 0; r < 64; ++r) ss += v[r] * v[r];
+        // the sum is taken here, not sunk past the sign flips (which would keep
+        // the 64 unflipped values live through the butterflies and spill them)
+        asm volatile("" : "+v"(ss));
+        apply_signs_grouped<R::A1>(v, tile << kRowLog, base1, D.logp, b1, 1.0f);
+        stages<R::A1, R::F1a>(v);
+        exchange_half_pad<R::A1, R::A2, 14>(v, s, tid);
+        stages<R::A2, R::F1b>(v);
+        exchange_half_pad<R::A2, R::A3, 14>(v, s, tid);
+        stages<R::A3, R::F1c>(v);
+        store_ws_l<R::A3>(a, D, tile, base3, v);
+        ss = block_sum<kRowNT>(ss, red);
+        if (tid == 0) a.part[D.part_off + tile] = ss;
+    }
+}
+
+// decode pass A (as k_dec_rowA)
+template <bool A8>
+__global__ __launch_bounds__(kRowNT, 4) void k_dec_rowA2(KArgs a) {
+    using R = DecA2Set;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float* s = reinterpret_cast<float*>(smem);
+    float* cen = reinterpret_cast<float*>(smem + kRowC2Ex);
+    if (threadIdx.x < 256) cen[threadIdx.x] = g_centroids[a.nbits - 1][threadIdx.x];
+    __syncthreads();
+    const int total = (int)sld(a.tstart, a.count);
+    for (int t = (int)blockIdx.x; t < total; t += (int)gridDim.x) {
+        const uint32_t tid = opaque(threadIdx.x);  // as in k_enc_rowA2
+        const uint32_t base1 = LT<R::C1>::base(tid), base3 = LT<R::C3>::base(tid);
+        int si; uint32_t tile;
+        row_locate(a, t, si, tile);
+        const SliceDesc D = udesc(a.d, si);
+        uint64_t w[8];
+        fetch_planes<A8>(a, D, tile, true, base1, w);
+        float v[64];
+        unpack_centroids64(w, cen, v);
+        stages<R::C1, R::G1>(v);
+        exchange_half_pad<R::C1, R::C2, 5>(v, s, tid);
+        stages<R::C2, R::G2>(v);
+        exchange_half_pad<R::C2, R::C3, 5>(v, s, tid);
+        stages<R::C3, R::G3>(v);
+        store_ws_l<R::C3>(a, D, tile, base3, v);
+    }
+}
+
+// decode pass C (as k_dec_rowC)
+__global__ __launch_bounds__(kRowNT, 4) void k_dec_rowC2(KArgs a) {
+    using R = DecC2Set;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float* s = reinterpret_cast<float*>(smem);
+    const int total = (int)sld(a.tstart, a.count);
+    for (int t = (int)blockIdx.x; t < total; t += (int)gridDim.x) {
+        const uint32_t tid = opaque(threadIdx.x);  // as in k_enc_rowA2
+        const uint32_t base1 = LT<R::B1>::base(tid), base4 = LT<R::B4>::base(tid);
+        int si; uint32_t tile;
+        row_locate(a, t, si, tile);
+        const SliceDesc D = udesc(a.d, si);
+        float v[64];
+        fetch_ws(a, D, tile, true, base1, v);
+        const uint32_t b1 = seed_b(sld(a.seeds, D.tensor));
+        stages<R::B1, R::H1>(v);
+        exchange_half_pad<R::B1, R::B2, 10>(v, s, tid);
+        stages<R::B2, R::H2>(v);
+        exchange_half_pad<R::B2, R::B3, 10>(v, s, tid);
+        stages<R::B3, R::H3>(v);
+        exchange_half_pad<R::B3, R::B4, 10>(v, s, tid);
+        stages<R::B4, R::H4>(v);
+        const float sc = sldf(a.scales_in, D.scale_idx);
+        apply_signs_grouped<R::B4>(v, tile << kRowLog, base4, D.logp, b1, sc * pow2i(-((D.logp + 1) / 2)));
+        store_y_l<R::B4>(a, D, tile, base4, v);
     }
 }
 
@@ -1796,7 +2011,7 @@ struct Launch {
     int count;       // list entries
     int64_t blocks;  // grid size
     int nu = 0;      // column: tile 0 of each slice writes the slice norm
-    int stream = 0;  // 0: the caller's stream, 1: the plan's side stream, 2: its small-slice stream
+    int stream = 0;  // 0: the caller's stream, 1: the plan's side stream, 2 / 3: its small-slice streams
     int join = 0;    // the caller's stream waits for the side stream before this launch
     int tl = 15;     // column: log2 of the tile (16: k_col6 with 1024 threads)
     int btab_off = -1;  // column: per-block {slice, tile << 3 | group} table in ints
@@ -1824,6 +2039,7 @@ struct ofl_eden_plan {
     int64_t wave_bytes = 0;     // intermediate bytes per wave of large slices; 0: one wave
     int nstreams = 1;           // 2: waves alternate between the caller's and a side stream
     int nwaves = 0;
+    int row2 = -1;              // row launches on the two-blocks-per-CU kernels: -1 auto, 0 never, 1 always
     std::vector<Launch> enc, dec;
     std::vector<int32_t> ints;  // launch lists and tile prefixes (host copy)
     // profiling: events around every launch of every call while enabled
@@ -1838,7 +2054,8 @@ struct ofl_eden_plan {
     std::mutex mu;
     hipStream_t side = nullptr;  // nstreams == 2: the device's shared side streams (shared_side_streams)
     hipStream_t side2 = nullptr; // the tiny / small slices, beside both wave streams
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr;
+    hipStream_t side3 = nullptr; // half of the tiny / small launches (use_small_split)
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr, ev_join3 = nullptr;
     std::mutex run_mu;          // serialises runs that use the side stream
 };
 
@@ -1919,6 +2136,23 @@ bool use_roll() {
     return on;
 }
 
+// Row launches of fewer than row2_max_tiles_per_cu() tiles per CU use the
+// two-blocks-per-CU kernels (k_enc_rowA2 / k_dec_rowA2 / k_dec_rowC2; outputs
+// bit-identical).  OFL_EDEN_ROW2=0: never, =1: always, unset: below the
+// threshold (OFL_EDEN_ROW2_TPC tiles per CU, default 4).
+int row2_mode() {
+    static const int m = [] { const char* s = getenv("OFL_EDEN_ROW2"); return (s && *s) ? (s[0] == '1' ? 1 : 0) : -1; }();
+    return m;
+}
+int64_t row2_max_tiles_per_cu() {
+    static const int64_t v = [] { const char* s = getenv("OFL_EDEN_ROW2_TPC"); return (s && *s) ? strtoll(s, nullptr, 10) : 4ll; }();
+    return v;
+}
+bool use_row2(int64_t tiles, int ncu, int plan_mode) {
+    const int m = plan_mode >= 0 ? plan_mode : row2_mode();
+    return m >= 0 ? m == 1 : tiles < row2_max_tiles_per_cu() * (int64_t)ncu;
+}
+
 // column passes with M >= 8 rows, or a middle pass with M >= 6, use k_col6
 // (measured: the 1024-thread k_col is ~4 % faster on the plain M = 7 pass);
 // OFL_EDEN_COL6=0 forces k_col everywhere (A/B)
@@ -1929,6 +2163,12 @@ bool use_col6() {
 // interleaved ws layout for 2^25 slices (256-B segments in the middle pass)
 bool use_perm25() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_PERM25"); return !(s && s[0] == '0'); }();
+    return on;
+}
+// the tiny / small launches (latency-bound, independent of each other) split
+// over two streams instead of one (OFL_EDEN_SMALL2=0: one stream, A/B)
+bool use_small_split() {
+    static const bool on = [] { const char* s = getenv("OFL_EDEN_SMALL2"); return !(s && s[0] == '0'); }();
     return on;
 }
 // tiny / small slices on a third stream when the waves use two
@@ -1979,6 +2219,10 @@ hipError_t set_all_attrs() {
     if ((e = set_lds((const void*)ofl::k_dec_rowA<true>, ofl::kRowSmemC)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_dec_rowA<false>, ofl::kRowSmemC)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_dec_rowC, ofl::kRowSmemA)) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_enc_rowA2, ofl::kRow2Smem)) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_dec_rowA2<true>, ofl::kRow2SmemC)) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_dec_rowA2<false>, ofl::kRow2SmemC)) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_dec_rowC2, ofl::kRow2Smem)) != hipSuccess) return e;
     if ((e = set_col_attr<6>()) != hipSuccess) return e;
     if ((e = set_col_attr<7>()) != hipSuccess) return e;
     if ((e = set_col_attr<8>()) != hipSuccess) return e;
@@ -2005,8 +2249,10 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
         HIP_TRY(hipEventRecord(pl->ev_fork, caller));
         HIP_TRY(hipStreamWaitEvent(pl->side, pl->ev_fork, 0));
         if (pl->side2) HIP_TRY(hipStreamWaitEvent(pl->side2, pl->ev_fork, 0));
+        if (pl->side3) HIP_TRY(hipStreamWaitEvent(pl->side3, pl->ev_fork, 0));
     }
-    const hipStream_t streams[3] = {caller, two ? pl->side : caller, pl->side2 ? pl->side2 : caller};
+    const hipStream_t streams[4] = {caller, two ? pl->side : caller, pl->side2 ? pl->side2 : caller,
+                                    pl->side3 ? pl->side3 : (pl->side2 ? pl->side2 : caller)};
     bool joined = !two;
     std::vector<hipEvent_t>* evs = nullptr;
     if (pl->prof) {  // one event before and one after every launch, on its stream
@@ -2059,10 +2305,18 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
             break;
         }
         case K_ROWA: {
+            const bool a8 = l.mid && (reinterpret_cast<uintptr_t>(base.pin) & 7u) == 0;
+            if (use_row2(l.blocks, pl->ncu, pl->row2)) {
+                const int64_t g2 = std::min<int64_t>(l.blocks, 2 * pl->ncu);
+                e = enc ? launch(ofl::k_enc_rowA2, g2, ofl::kRowNT, ofl::kRow2Smem, st, a)
+                        : a8 ? launch(ofl::k_dec_rowA2<true>, g2, ofl::kRowNT, ofl::kRow2SmemC, st, a)
+                             : launch(ofl::k_dec_rowA2<false>, g2, ofl::kRowNT, ofl::kRow2SmemC, st, a);
+                break;
+            }
             const int64_t g = std::min<int64_t>(l.blocks, pl->ncu);
             e = enc ? launch(ofl::k_enc_rowA, g, ofl::kRowNT, ofl::kRowSmemA, st, a)
-                    : (l.mid && (reinterpret_cast<uintptr_t>(base.pin) & 7u) == 0) ? launch(ofl::k_dec_rowA<true>, g, ofl::kRowNT, ofl::kRowSmemC, st, a)
-                           : launch(ofl::k_dec_rowA<false>, g, ofl::kRowNT, ofl::kRowSmemC, st, a);
+                    : a8 ? launch(ofl::k_dec_rowA<true>, g, ofl::kRowNT, ofl::kRowSmemC, st, a)
+                         : launch(ofl::k_dec_rowA<false>, g, ofl::kRowNT, ofl::kRowSmemC, st, a);
             break;
         }
         case K_ROWC: {
@@ -2072,6 +2326,8 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
                                         ofl::kRowC2Smem, st, a)
                                : launch(ofl::k_enc_rowC2<false>, std::min<int64_t>(l.blocks, 2 * pl->ncu), ofl::kRowNT,
                                         ofl::kRowC2Smem, st, a);
+            else if (!enc && use_row2(l.blocks, pl->ncu, pl->row2))
+                e = launch(ofl::k_dec_rowC2, std::min<int64_t>(l.blocks, 2 * pl->ncu), ofl::kRowNT, ofl::kRow2Smem, st, a);
             else
                 e = enc ? launch(ofl::k_enc_rowC, g, ofl::kRowNT, ofl::kRowSmemQ, st, a)
                         : launch(ofl::k_dec_rowC, g, ofl::kRowNT, ofl::kRowSmemA, st, a);
@@ -2128,17 +2384,22 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
         HIP_TRY(hipEventRecord(pl->ev_join2, pl->side2));
         HIP_TRY(hipStreamWaitEvent(caller, pl->ev_join2, 0));
     }
+    if (two && pl->side3) {
+        HIP_TRY(hipEventRecord(pl->ev_join3, pl->side3));
+        HIP_TRY(hipStreamWaitEvent(caller, pl->ev_join3, 0));
+    }
     return OFL_OK;
 }
 
-std::string launch_name(const Launch& l, bool enc) {
+std::string launch_name(const Launch& l, bool enc, int ncu, int row2) {
     const char* d = enc ? "enc" : "dec";
     switch (l.kind) {
     case K_TINY: return std::string("ofl::k_") + d + "_tiny";
     case K_SMALL: return std::string("ofl::k_") + d + "_small<" + std::to_string(l.param) + ">";
-    case K_ROWA: return std::string("ofl::k_") + d + "_rowA";
+    case K_ROWA: return std::string("ofl::k_") + d + (use_row2(l.blocks, ncu, row2) ? "_rowA2" : "_rowA");
     case K_ROWC:
         if (enc && use_rowc2()) return std::string("ofl::k_enc_rowC2<") + (use_roll() ? "true" : "false") + ">";
+        if (!enc && use_row2(l.blocks, ncu, row2)) return "ofl::k_dec_rowC2";
         return std::string("ofl::k_") + d + "_rowC";
     case K_COL:
         if (l.tl == 16) return "ofl::k_col6<" + std::to_string(l.param) + ", " + (l.mid ? "true" : "false") + ", 16>";
@@ -2225,8 +2486,9 @@ void build_schedule(ofl_eden_plan* pl) {
     // with fewer large-slice elements)
     bool small_own = false;
     if (nbuf == 2) {
-        if (use_small_stream()) {  // their own stream: latency-bound, they fill CUs beside both waves
-            for (Launch& l : common) l.stream = 2;
+        if (use_small_stream()) {  // their own stream(s): latency-bound, they fill CUs beside both waves
+            int k = 0;
+            for (Launch& l : common) l.stream = use_small_split() && common.size() > 1 ? 2 + (k++ & 1) : 2;
             small_own = true;
         } else {
             int64_t load[2] = {0, 0};
@@ -2540,15 +2802,17 @@ int ofl_eden_plan_create(int ntensors, const int64_t* numel, const int64_t* elem
 // stream then waits behind a wave stream.  Runs of different plans on the
 // shared streams stay correct (fork/join events per plan); they may wait for
 // each other's work enqueued in between.
-static int shared_side_streams(int dev, bool two, hipStream_t& s1, hipStream_t& s2) {
+static int shared_side_streams(int dev, bool two, bool three, hipStream_t& s1, hipStream_t& s2, hipStream_t& s3) {
     static std::mutex mu;
-    static std::map<int, std::pair<hipStream_t, hipStream_t>> pool;
+    static std::map<int, std::array<hipStream_t, 3>> pool;
     std::lock_guard<std::mutex> g(mu);
     auto& e = pool[dev];
-    if (!e.first) HIP_TRY(hipStreamCreateWithFlags(&e.first, hipStreamNonBlocking));
-    if (two && !e.second) HIP_TRY(hipStreamCreateWithFlags(&e.second, hipStreamNonBlocking));
-    s1 = e.first;
-    s2 = two ? e.second : nullptr;
+    if (!e[0]) HIP_TRY(hipStreamCreateWithFlags(&e[0], hipStreamNonBlocking));
+    if (two && !e[1]) HIP_TRY(hipStreamCreateWithFlags(&e[1], hipStreamNonBlocking));
+    if (three && !e[2]) HIP_TRY(hipStreamCreateWithFlags(&e[2], hipStreamNonBlocking));
+    s1 = e[0];
+    s2 = two ? e[1] : nullptr;
+    s3 = three ? e[2] : nullptr;
     return OFL_OK;
 }
 
@@ -2569,14 +2833,15 @@ static int ensure_device(ofl_eden_plan_t pl) {
     bool side = false;
     for (const Launch& l : pl->enc) side |= l.stream != 0;
     for (const Launch& l : pl->dec) side |= l.stream != 0;
-    bool side3 = false;
-    for (const Launch& l : pl->enc) side3 |= l.stream == 2;
-    for (const Launch& l : pl->dec) side3 |= l.stream == 2;
+    bool side3 = false, side4 = false;
+    for (const Launch& l : pl->enc) { side3 |= l.stream >= 2; side4 |= l.stream == 3; }
+    for (const Launch& l : pl->dec) { side3 |= l.stream >= 2; side4 |= l.stream == 3; }
     if (side) {
-        if (int rc = shared_side_streams(pl->device, side3, pl->side, pl->side2)) return rc;
+        if (int rc = shared_side_streams(pl->device, side3, side4, pl->side, pl->side2, pl->side3)) return rc;
         HIP_TRY(hipEventCreateWithFlags(&pl->ev_fork, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&pl->ev_join, hipEventDisableTiming));
         if (side3) HIP_TRY(hipEventCreateWithFlags(&pl->ev_join2, hipEventDisableTiming));
+        if (side4) HIP_TRY(hipEventCreateWithFlags(&pl->ev_join3, hipEventDisableTiming));
     }
     pl->uploaded = true;
     return OFL_OK;
@@ -2589,6 +2854,7 @@ void ofl_eden_plan_destroy(ofl_eden_plan_t pl) {
     if (pl->d_slices) (void)hipFree(pl->d_slices);
     if (pl->d_ints) (void)hipFree(pl->d_ints);
     if (pl->ev_join2) (void)hipEventDestroy(pl->ev_join2);
+    if (pl->ev_join3) (void)hipEventDestroy(pl->ev_join3);
     if (pl->ev_fork) (void)hipEventDestroy(pl->ev_fork);
     if (pl->ev_join) (void)hipEventDestroy(pl->ev_join);
     delete pl;
@@ -2602,6 +2868,14 @@ int ofl_eden_plan_set_schedule(ofl_eden_plan_t pl, int64_t wave_bytes, int strea
     if (wave_bytes >= 0) pl->wave_bytes = wave_bytes;
     if (streams > 0) pl->nstreams = streams;
     build_schedule(pl);
+    return OFL_OK;
+}
+
+int ofl_eden_plan_set_row2(ofl_eden_plan_t pl, int mode) {
+    if (!pl) return fail(OFL_EINVAL, "null plan");
+    if (mode < -1 || mode > 1) return fail(OFL_EINVAL, "row2 mode must be -1 (auto), 0 or 1");
+    std::lock_guard<std::mutex> g(pl->mu);
+    pl->row2 = mode;
     return OFL_OK;
 }
 
@@ -2749,7 +3023,7 @@ int ofl_eden_plan_launch_info(ofl_eden_plan_t pl, int encode, int idx, char* nam
     const std::vector<Launch>& L = encode ? pl->enc : pl->dec;
     if (idx < 0 || idx >= (int)L.size()) return fail(OFL_EINVAL, "launch index out of range");
     if (name && cap > 0) {
-        const std::string s = launch_name(L[idx], encode != 0);
+        const std::string s = launch_name(L[idx], encode != 0, pl->ncu, pl->row2);
         snprintf(name, (size_t)cap, "%s", s.c_str());
     }
     if (blocks) *blocks = L[idx].blocks;

@@ -526,3 +526,57 @@ def test_pipeline_multi_device_threads(setting):
         assert enc[i][0] == ref[i][0] and enc[i][1:] == ref[i][1:]
         np.testing.assert_array_equal(dec[i], ref_out[i])
     assert sorted(set(slots)) == list(range(len(eden.devices)))  # every device got threads
+
+
+def test_row2_variants_bit_identical():
+    """The two-blocks-per-CU row kernels (k_enc_rowA2 / k_dec_rowA2 /
+    k_dec_rowC2, ofl_eden_plan_set_row2) butterfly the index bits in the same
+    order as the persistent ones and load, sum and store the same values: planes,
+    scales and decoded values are bit-identical, for 3-pass (incl. the
+    interleaved 2^25 layout) and 5-pass slices, ragged tails and decode_add."""
+    from openfl_amd.codec import EdenPlan
+    numels = [(1 << 26) + 777, 1 << 25, (1 << 22) + 12345, (1 << 16) + 5, 3000]
+    g = torch.Generator(device=DEV).manual_seed(21)
+    outs = []
+    for row2 in (0, 1):
+        plan = EdenPlan(numels, 8, wave_mib=4096, streams=1, row2=row2)
+        x = torch.empty(plan.arena_numel, device=DEV).normal_(0, 0.01, generator=g.manual_seed(21))
+        base = torch.empty(plan.arena_numel, device=DEV).normal_(0, 1.0, generator=g.manual_seed(22))
+        seeds = torch.tensor([5, 6, 7, 8, 9], dtype=torch.int32, device=DEV)
+        ws = torch.empty(max(plan.ws_bytes, 256), dtype=torch.uint8, device=DEV)
+        p = torch.full((plan.planes_bytes,), 0x5A, dtype=torch.uint8, device=DEV)
+        s = torch.zeros(plan.n_slices, dtype=torch.float32, device=DEV)
+        y = torch.zeros_like(x)
+        y2 = torch.zeros_like(x)
+        plan.encode(x, seeds, p, s, ws)
+        plan.decode(p, seeds, s, y, ws)
+        plan.decode(p, seeds, s, y2, ws, base=base)
+        torch.cuda.synchronize()
+        outs.append((p.cpu(), s.cpu(), y.cpu(), y2.cpu()))
+        del x, base, ws, p, s, y, y2
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+def test_small_launch_split_bit_identical():
+    """Tiny / small slices on two side streams (OFL_EDEN_SMALL2 default) give
+    the same bytes as one stream: a mixed set through the default two-stream
+    schedule vs the single-stream schedule."""
+    from openfl_amd.codec import EdenPlan
+    numels = [300, 2000, 5000, 9000, 17000, 33000, 70000, 1 << 20, (1 << 21) + 99, 150]
+    res = []
+    for streams in (1, 2):
+        plan = EdenPlan(numels, 8, streams=streams)
+        g = torch.Generator(device=DEV).manual_seed(31)
+        x = torch.empty(plan.arena_numel, device=DEV).normal_(0, 0.01, generator=g)
+        seeds = torch.arange(1, len(numels) + 1, dtype=torch.int32, device=DEV)
+        ws = torch.empty(max(plan.ws_bytes, 256), dtype=torch.uint8, device=DEV)
+        p = torch.zeros(plan.planes_bytes, dtype=torch.uint8, device=DEV)
+        s = torch.zeros(plan.n_slices, dtype=torch.float32, device=DEV)
+        y = torch.zeros_like(x)
+        plan.encode(x, seeds, p, s, ws)
+        plan.decode(p, seeds, s, y, ws)
+        torch.cuda.synchronize()
+        res.append((p.cpu(), s.cpu(), y.cpu()))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)

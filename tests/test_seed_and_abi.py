@@ -98,7 +98,8 @@ def test_wave_schedule_layout():
     for enc in (True, False):
         names = [l["name"] for l in w2.launches(enc)]
         d = "enc" if enc else "dec"
-        assert names.count(f"ofl::k_{d}_rowA") == 4
+        # small waves (< 4 tiles per CU) take the two-blocks-per-CU row kernels
+        assert sum(n in (f"ofl::k_{d}_rowA", f"ofl::k_{d}_rowA2") for n in names) == 4
         assert sum(n.startswith(f"ofl::k_{d}_rowC") for n in names) == 4
         # one k_finalize per wave stream (no mid-call join)
         assert names.count("ofl::k_finalize") == (2 if enc else 0)
@@ -107,6 +108,13 @@ def test_wave_schedule_layout():
     w1 = EdenPlan(numels, 8, wave_mib=32, streams=1)
     assert w1.n_waves == 4 and w1.ws_bytes < w2.ws_bytes
     assert [l["name"] for l in w1.launches(True)].count("ofl::k_finalize") == 1
+    # kernel choice for the row passes: auto / forced (outputs identical, GPU test)
+    names0 = [l["name"] for l in EdenPlan(numels, 8, wave_mib=32, streams=1, row2=0).launches(False)]
+    names1 = [l["name"] for l in EdenPlan(numels, 8, wave_mib=32, streams=1, row2=1).launches(False)]
+    assert "ofl::k_dec_rowA2" not in names0 and names0.count("ofl::k_dec_rowC") == 4
+    assert names1.count("ofl::k_dec_rowA2") == 4 and names1.count("ofl::k_dec_rowC2") == 4
+    with pytest.raises(_lib.CodecError, match="row2"):
+        EdenPlan(numels, 8, row2=2)
     big = EdenPlan([1 << 25, 1 << 22], 8, wave_mib=16, streams=1)   # a slice above the wave size
     assert big.n_waves == 2
     with pytest.raises(_lib.CodecError, match="streams"):
@@ -123,7 +131,7 @@ def test_two_stream_split_rules():
     sizes = [numel(s) for _, s in WORKLOADS["resnet50_fp32"]()]
     rn = EdenPlan(sizes, 8, streams=2)
     assert rn.n_waves == 2
-    rows = [l["blocks"] for l in rn.launches(True) if l["name"] == "ofl::k_enc_rowA"]
+    rows = [l["blocks"] for l in rn.launches(True) if l["name"] in ("ofl::k_enc_rowA", "ofl::k_enc_rowA2")]
     assert len(rows) == 2 and abs(rows[0] - rows[1]) <= max(rows) // 4
     uni = EdenPlan([numel(s) for _, s in WORKLOADS["uniform_1gib"]()], 8, streams=2)
     assert uni.n_waves == 1

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round 3, GPU call B: the -m gpu suite (incl. the two-block row kernels and
+# the split small-slice streams), ResNet-50 A/B of those two schedule
+# changes, the default bench, and the KC pipeline's rocprofv3 evidence
+# (kernel trace + FETCH_SIZE / WRITE_SIZE passes of tools/kc_bench.py alone).
+set -uo pipefail
+R=$PWD
+O=$R/gpurun_out/r3b
+mkdir -p $O
+T() { timeout -k 10 "$@"; }
+T 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || exit 13
+i=0
+for v in "auto" "row2off:OFL_EDEN_ROW2=0" "small1:OFL_EDEN_SMALL2=0" "both_off:OFL_EDEN_ROW2=0 OFL_EDEN_SMALL2=0" "auto" "row2on:OFL_EDEN_ROW2=1"; do
+  i=$((i+1)); n=${v%%:*}; e=""; [ "$n" != "$v" ] && e=${v#*:}
+  T 200 env $e python -u bench.py --workload resnet50_fp32 --steps 300 --warmup 20 --also '' --no-cpu-baseline > $O/resnet_${i}_$n.json 2> $O/resnet_${i}_$n.err || exit 14
+done
+T 200 python -u bench.py --workload uniform_1gib --steps 50 --warmup 5 --also '' --no-cpu-baseline > $O/uniform_auto.json 2> $O/uniform_auto.err || exit 15
+T 400 python -u bench.py > $O/bench_default.json 2> $O/bench_default.err || exit 16
+cd /tmp && export TMPDIR=/tmp
+T 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kc_trace -o k -- python $R/tools/kc_bench.py --steps 3 --warmup 1 > $O/kc_trace.log 2>&1 || exit 17
+T 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/kc_pmc/pass1 -o p -- python $R/tools/kc_bench.py --steps 3 --warmup 1 > $O/kc_pmc1.log 2>&1 || exit 18
+T 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/kc_pmc/pass2 -o p -- python $R/tools/kc_bench.py --steps 3 --warmup 1 > $O/kc_pmc2.log 2>&1 || exit 19
+T 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/rn_trace -o k -- python $R/bench.py --workload resnet50_fp32 --steps 100 --warmup 10 --also '' --no-cpu-baseline --no-kernel-events > $O/rn_trace.log 2>&1 || exit 20
