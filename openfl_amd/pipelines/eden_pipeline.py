@@ -24,6 +24,8 @@ Deliberate differences (DESIGN.md "Reference quirks"):
   * device="cpu" (the reference default) selects the current GPU.
 """
 import contextlib
+import ctypes
+import os
 import threading
 from concurrent.futures import ThreadPoolExecutor
 
@@ -179,6 +181,26 @@ class Eden(PerThreadDevice):
             sg.trim(_RETAIN_BYTES)
         self.codec.ws.trim(self.device, _RETAIN_BYTES)
 
+    def _ctx(self, key, make):
+        """Per-thread call context of one tensor shape (small calls only)."""
+        cache = getattr(self._tls, "ctx", None)
+        if cache is None:
+            cache = self._tls.ctx = {}
+        c = cache.get(key)
+        if c is None:
+            if len(cache) >= _CTX_MAX:
+                cache.clear()
+            c = cache[key] = make()
+        return c
+
+    def _enc_ctx(self, n):
+        plan = self.codec.plan([n], streams=1)
+        return _CallCtx(plan, self.device, self._stream(), enc=True)
+
+    def _dec_ctx(self, total_dim, dims):
+        plan = self.codec.plan([total_dim], dims=[list(dims)], streams=1)
+        return _CallCtx(plan, self.device, self._stream(), enc=False, total_dim=total_dim)
+
     def compress(self, vec, seed, seed_of_sum=None):
         """(planes uint8 ndarray, scales list[float], dims list[int], total_dim) (:555-611).
         One tensor in one native call (ofl_eden_encode_host): pinned input
@@ -193,6 +215,19 @@ class Eden(PerThreadDevice):
             seed = seed_of_sum(_serial_sum(src))
         flat = np.ascontiguousarray(src, dtype=np.float32)
         n = flat.size
+        if 0 < n <= _CTX_NUMEL and _USE_CTX:
+            # small tensors: a cached per-shape context (own pinned / device
+            # buffers and the native call's arguments prepared once) -- the
+            # call is latency-bound and its Python work was most of it
+            c = self._ctx(("e", n), lambda: self._enc_ctx(n))
+            if fuse:
+                seed = seed_of_sum(np.float32(_lib.lib().ofl_serial_sum_copy_f32(flat.ctypes.data, c.in_ptr, n)))
+            else:
+                c.x_view[:] = flat
+            c.seed_view[0] = int(seed) & 0xFFFFFFFF
+            c.run()
+            out = (np.frombuffer(ctypes.string_at(c.out_ptr, c.pb), np.uint8), c.scales_view.tolist(), list(c.dims), n)
+            return out if seed_of_sum is None else (out, int(seed))
         plan = self.codec.plan([n], streams=_one_tensor_streams(n))
         pb, ns = plan.planes_bytes, plan.n_slices
         off_seeds = _al256(4 * plan.arena_numel)
@@ -237,6 +272,16 @@ class Eden(PerThreadDevice):
             raise ValueError(f"Eden metadata: total_dim {total_dim} exceeds the slices ({sum(dims)})")
         planes_h = np.frombuffer(bins, dtype=np.uint8) if isinstance(bins, (bytes, bytearray, memoryview)) \
             else np.asarray(bins, dtype=np.uint8).reshape(-1)
+        if 0 < total_dim <= _CTX_NUMEL and sum(dims) <= 2 * _CTX_NUMEL and _USE_CTX:
+            c = self._ctx(("d", total_dim, tuple(dims)), lambda: self._dec_ctx(total_dim, dims))
+            if planes_h.size < c.pb:
+                raise ValueError(f"Eden payload has {planes_h.size} bytes, expected {c.pb}")
+            c.planes_view[:] = planes_h[:c.pb]
+            c.scales_view[:] = scales
+            c.seed_view[0] = seed & 0xFFFFFFFF
+            y = np.empty(total_dim, np.float32)
+            c.run(y.ctypes.data)
+            return y
         plan = self.codec.plan([total_dim], dims=[dims], streams=_one_tensor_streams(sum(dims)))
         if planes_h.size < plan.planes_bytes:
             raise ValueError(f"Eden payload has {planes_h.size} bytes, expected {plan.planes_bytes}")
@@ -263,6 +308,71 @@ class Eden(PerThreadDevice):
                 y.ctypes.data, out_bytes, ws.data_ptr(), ws.numel(), self._stream().cuda_stream))
         self._trim()
         return y[:total_dim]
+
+
+# one-tensor calls of at most this many elements use cached per-shape call
+# contexts (_CallCtx); OFL_PLUGIN_CTX=0 turns them off (A/B)
+_CTX_NUMEL = 1 << 16
+_CTX_MAX = 256
+_USE_CTX = os.environ.get("OFL_PLUGIN_CTX", "1") != "0"
+
+
+class _CallCtx:
+    """One tensor shape's one-call encode or decode, prepared once per thread:
+    the plan (single stream), pinned in/out blocks and device buffers of
+    exactly its size, numpy views into the pinned blocks, and the native
+    call's argument list (ofl_eden_encode_host / ofl_eden_decode_host)."""
+
+    def __init__(self, plan, device, stream, enc, total_dim=0):
+        self.plan = plan
+        self.pb, ns = plan.planes_bytes, plan.n_slices
+        self.dims = plan.dims[0]
+        self.dev_index = device.index
+        self.stream = stream
+        ws = torch.empty(max(plan.ws_bytes, 256), dtype=torch.uint8, device=device)
+        L = _lib.lib()
+        if enc:
+            off_seeds = _al256(4 * plan.arena_numel)
+            in_bytes = off_seeds + 4
+            off_scales = _al256(self.pb)
+            out_bytes = off_scales + 4 * ns
+            ih = torch.empty(in_bytes, dtype=torch.uint8).pin_memory()
+            oh = torch.empty(out_bytes, dtype=torch.uint8).pin_memory()
+            ia, oa = ih.numpy(), oh.numpy()
+            self.x_view = ia[:4 * plan.numels[0]].view(np.float32)
+            self.seed_view = ia[off_seeds:off_seeds + 4].view(np.uint32)
+            self.scales_view = oa[off_scales:off_scales + 4 * ns].view(np.float32)
+            idev = torch.empty(in_bytes, dtype=torch.uint8, device=device)
+            odev = torch.empty(out_bytes, dtype=torch.uint8, device=device)
+            self.in_ptr, self.out_ptr = ih.data_ptr(), oh.data_ptr()
+            self._fn = L.ofl_eden_encode_host
+            self._args = [plan.handle, ih.data_ptr(), idev.data_ptr(), in_bytes, off_seeds, odev.data_ptr(),
+                          oh.data_ptr(), out_bytes, off_scales, ws.data_ptr(), ws.numel(), stream.cuda_stream]
+            self._keep = (ih, oh, idev, odev, ws)
+        else:
+            off_scales = _al256(self.pb)
+            off_seeds = _al256(off_scales + 4 * ns)
+            in_bytes = off_seeds + 4
+            ih = torch.empty(in_bytes, dtype=torch.uint8).pin_memory()
+            ia = ih.numpy()
+            self.planes_view = ia[:self.pb]
+            self.scales_view = ia[off_scales:off_scales + 4 * ns].view(np.float32)
+            self.seed_view = ia[off_seeds:off_seeds + 4].view(np.uint32)
+            idev = torch.empty(in_bytes, dtype=torch.uint8, device=device)
+            ydev = torch.empty(max(plan.arena_numel, 1), dtype=torch.float32, device=device)
+            self._fn = L.ofl_eden_decode_host
+            self._args = [plan.handle, ih.data_ptr(), idev.data_ptr(), in_bytes, off_scales, off_seeds, ydev.data_ptr(),
+                          None, 4 * total_dim, ws.data_ptr(), ws.numel(), stream.cuda_stream]
+            self._keep = (ih, idev, ydev, ws)
+
+    def run(self, y_ptr=None):
+        if y_ptr is not None:
+            self._args[7] = y_ptr
+        if self.dev_index is not None and self.dev_index != torch.cuda.current_device():
+            with torch.cuda.device(self.dev_index):
+                _lib.check(self._fn(*self._args))
+        else:
+            _lib.check(self._fn(*self._args))
 
 
 def _one_tensor_streams(n):

@@ -580,3 +580,26 @@ def test_small_launch_split_bit_identical():
         res.append((p.cpu(), s.cpu(), y.cpu()))
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+def test_plugin_call_contexts_identical(monkeypatch):
+    """Small one-tensor calls go through cached per-shape call contexts
+    (eden_pipeline._CallCtx): bytes, scales, seeds and decoded values equal
+    the uncached path's, including repeated and interleaved shapes."""
+    from openfl_amd.pipelines import eden_pipeline as E
+    sizes = [101, 777, 2048, 2049, 40000, 1 << 16, 777, 101]
+    rng = np.random.default_rng(5)
+    xs = [rng.standard_normal(n).astype(np.float32) for n in sizes]
+
+    def run(use):
+        monkeypatch.setattr(E, "_USE_CTX", use)
+        pipe = E.EdenPipeline(n_bits=8, device=DEV)
+        np.random.seed(11)
+        enc = [pipe.forward(x) for x in xs]
+        dec = [pipe.backward(d, [dict(m[0])]) for d, m in enc]
+        return enc, dec
+
+    (e1, d1), (e0, d0) = run(True), run(False)
+    for (b1, m1), (b0, m0), y1, y0 in zip(e1, e0, d1, d0):
+        assert b1 == b0 and m1 == m0
+        np.testing.assert_array_equal(y1, y0)

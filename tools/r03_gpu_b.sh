@@ -15,6 +15,9 @@ for v in "auto" "row2off:OFL_EDEN_ROW2=0" "small1:OFL_EDEN_SMALL2=0" "both_off:O
   T 200 env $e python -u bench.py --workload resnet50_fp32 --steps 300 --warmup 20 --also '' --no-cpu-baseline > $O/resnet_${i}_$n.json 2> $O/resnet_${i}_$n.err || exit 14
 done
 T 200 python -u bench.py --workload uniform_1gib --steps 50 --warmup 5 --also '' --no-cpu-baseline > $O/uniform_auto.json 2> $O/uniform_auto.err || exit 15
+T 300 python -u tools/call_overhead_probe.py > $O/call_overhead.json 2> $O/call_overhead.err || exit 21
+T 300 env OFL_PLUGIN_CTX=0 python -u tools/call_overhead_probe.py > $O/call_overhead_noctx.json 2> $O/call_overhead_noctx.err || exit 22
+T 300 python -u tools/e2e_bench.py --out $O/e2e_resnet50.json > $O/e2e.log 2>&1 || exit 23
 T 400 python -u bench.py > $O/bench_default.json 2> $O/bench_default.err || exit 16
 cd /tmp && export TMPDIR=/tmp
 T 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kc_trace -o k -- python $R/tools/kc_bench.py --steps 3 --warmup 1 > $O/kc_trace.log 2>&1 || exit 17
