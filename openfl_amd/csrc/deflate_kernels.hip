@@ -910,12 +910,22 @@ struct InfCode {                           // one canonical Huffman code
     uint16_t cnt[16];                      // codes per length
     uint16_t sorted[288];                  // symbols ordered by (length, symbol)
 };
-template <int WIN>
+// (length, distance) pair table: the next kPairBits bits of the stream ->
+// one whole copy when its length code, length extra bits, distance code and
+// distance extra bits all fit in them: bits 0..4 bits consumed, 5..13
+// length, 14..29 distance, bit 30 valid.  The device gzip's rank streams are
+// mostly 4-byte copies (a token's previous occurrence) with short distance
+// codes, so most copies decode with one table read instead of two decodes
+// and two extra-bit reads on the scalar unit.
+constexpr int kPairBits = 10;
+constexpr int kPair = 1 << kPairBits;
+template <int WIN, bool PAIR>
 struct InfSmem {
     alignas(16) uint8_t win[WIN];          // the member's output
     alignas(4) uint8_t ring[kRing];
     InfCode lit, dist;
     uint8_t lens[320];                     // code lengths (literal/length | distance)
+    uint32_t pair[PAIR ? kPair : 1];
 };
 
 struct InfArgs {
@@ -1012,6 +1022,32 @@ DEVI bool inf_build(InfCode& c, const uint8_t* lens, int n, int alpha) {
     return true;
 }
 
+// the pair table of a block's codes (wave-parallel, after both builds)
+template <int WIN, bool PAIR>
+DEVI void inf_build_pairs(InfSmem<WIN, PAIR>& S) {
+    if constexpr (PAIR) {
+        const int lane = (int)(threadIdx.x & 63u);
+        for (int k = lane; k < kPair; k += 64) {
+            uint32_t out = 0;
+            const uint32_t e = S.lit.fast[k & (kFast - 1)];
+            const uint32_t l = e & 15u, x = (e >> 4) & 15u;
+            if (l && ((e >> 8) & 3u) == (uint32_t)kKindCopy && l + x <= (uint32_t)kPairBits) {
+                const uint32_t len = (e >> 16) + (((uint32_t)k >> l) & ((1u << x) - 1u));
+                const uint32_t r = (uint32_t)k >> (l + x);
+                const uint32_t f = S.dist.fast[r & (kFast - 1)];
+                const uint32_t l2 = f & 15u, x2 = (f >> 4) & 15u;
+                const uint32_t nb = l + x + l2 + x2;
+                if (l2 && ((f >> 8) & 3u) == (uint32_t)kKindCopy && nb <= (uint32_t)kPairBits) {
+                    const uint32_t d = (f >> 16) + ((r >> l2) & ((1u << x2) - 1u));
+                    out = nb | (len << 5) | (d << 14) | (1u << 30);
+                }
+            }
+            S.pair[k] = out;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // wave-uniform value from LDS into a scalar register: the decode state then
 // lives in SGPRs and its arithmetic runs on the scalar unit (one wave-wide
 // VALU op per step of the serial decode would cost 4+ cycles each)
@@ -1054,10 +1090,10 @@ DEVI uint32_t inf_decode(const InfCode& c, uint64_t& bb, int& bc, int alpha) {
 // memory as it is produced; a copy reaching further back than the ring reads
 // global memory (bytes this wavefront stored earlier: same-address order
 // within a wavefront).  Less LDS per member -> more members per CU.
-template <int WIN, bool RING>
+template <int WIN, bool RING, bool PAIR>
 __global__ __launch_bounds__(64) void k_inflate_members(InfArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    InfSmem<WIN>& S = *reinterpret_cast<InfSmem<WIN>*>(smem_raw);
+    InfSmem<WIN, PAIR>& S = *reinterpret_cast<InfSmem<WIN, PAIR>*>(smem_raw);
     const int lane = threadIdx.x;
     const int64_t m = blockIdx.x;
     if (m >= a.nmem) return;
@@ -1140,6 +1176,7 @@ __global__ __launch_bounds__(64) void k_inflate_members(InfArgs a) {
             __builtin_amdgcn_wave_barrier();
             inf_build(S.lit, S.lens, 288, kAlphaLit);
             inf_build(S.dist, S.lens + 288, 30, kAlphaDist);
+            inf_build_pairs(S);
         } else {  // dynamic: code-length code, then the literal/length and distance lengths
             topup();
             const int nlit = (int)bits(5) + 257, ndist = (int)bits(5) + 1, ncl = (int)bits(4) + 4;
@@ -1195,10 +1232,46 @@ __global__ __launch_bounds__(64) void k_inflate_members(InfArgs a) {
                 err = kInfCorrupt;
                 break;
             }
+            inf_build_pairs(S);
         }
         // symbols of the block
         for (;;) {
             topup();
+            if constexpr (PAIR) {
+                const uint32_t pe = uni(S.pair[bb & (uint64_t)(kPair - 1)]);
+                if (pe >> 30) {  // a whole copy from one lookup
+                    const uint32_t nb = pe & 31u, len = (pe >> 5) & 511u, d = (pe >> 14) & 0xffffu;
+                    bb >>= nb;
+                    bc -= (int)nb;
+                    if (d > p) { err = kInfCorrupt; break; }
+                    if (p + len > isize) { err = kInfSize; break; }
+                    __builtin_amdgcn_wave_barrier();
+                    if ((!RING || d + len <= (uint32_t)WIN) && len <= 64u) {
+                        if ((uint32_t)lane < len) {
+                            const uint32_t k = (uint32_t)lane;
+                            const uint8_t v = S.win[(p - d + (d >= len ? k : k % d)) & M];
+                            S.win[(p + k) & M] = v;
+                            if (RING) dst[p + k] = v;
+                        }
+                    } else if (!RING || d + len <= (uint32_t)WIN) {
+                        for (uint32_t k = lane; k < len; k += 64) {
+                            const uint8_t v = S.win[(p - d + (d >= len ? k : k % d)) & M];
+                            S.win[(p + k) & M] = v;
+                            if (RING) dst[p + k] = v;
+                        }
+                    } else {
+                        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                        for (uint32_t k = lane; k < len; k += 64) {
+                            const uint8_t v = dst[p - d + k];
+                            S.win[(p + k) & M] = v;
+                            dst[p + k] = v;
+                        }
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    p += len;
+                    continue;
+                }
+            }
             const uint32_t e = inf_decode(S.lit, bb, bc, kAlphaLit);
             const uint32_t kind = (e >> 8) & 3u;
             if (kind == kKindLit) {
@@ -1632,8 +1705,8 @@ int ofl_inflate_members(const uint8_t* src, const int64_t* index, int64_t nmembe
         crc_matrices(m);
         hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(gz::c_adv), m, sizeof(m));
         if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)gz::k_inflate_members<65536, false>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(gz::InfSmem<65536>));
+            e = hipFuncSetAttribute((const void*)gz::k_inflate_members<65536, false, false>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(gz::InfSmem<65536, false>));
         return e;
     }));
     hipStream_t st = static_cast<hipStream_t>(stream);
@@ -1645,15 +1718,24 @@ int ofl_inflate_members(const uint8_t* src, const int64_t* index, int64_t nmembe
     // 1 KiB ring: with the table-driven decode the kernel is scalar-unit
     // bound and more members per CU pay (1 / 2 KiB / 512 B: 12.4 / 13.1 /
     // 12.8 ms for the 1 GiB set; before, 1, 2 and 4 KiB measured the same)
-    if (!window)
-        hipLaunchKernelGGL((gz::k_inflate_members<1024, true>), dim3((unsigned)nmembers), dim3(64),
-                           sizeof(gz::InfSmem<1024>), st, a);
+    // the (length, distance) pair table: opt-in (OFL_GZ_PAIR=1).  Measured
+    // slower on the 1 GiB rank set: 16.8 vs 12.4 ms per inflate launch
+    // (profiles/r03_kc_pair_ab.txt): the 4 KiB table per member cuts the
+    // members resident per CU from 26 to 15, and the decode is bound by the
+    // scalar issue of many members, not by one member's steps
+    static const bool pair = [] { const char* v = getenv("OFL_GZ_PAIR"); return v && v[0] == '1'; }();
+    if (!window && pair)
+        hipLaunchKernelGGL((gz::k_inflate_members<1024, true, true>), dim3((unsigned)nmembers), dim3(64),
+                           sizeof(gz::InfSmem<1024, true>), st, a);
+    else if (!window)
+        hipLaunchKernelGGL((gz::k_inflate_members<1024, true, false>), dim3((unsigned)nmembers), dim3(64),
+                           sizeof(gz::InfSmem<1024, false>), st, a);
     else if (max_isize <= 16384u)
-        hipLaunchKernelGGL((gz::k_inflate_members<16384, false>), dim3((unsigned)nmembers), dim3(64),
-                           sizeof(gz::InfSmem<16384>), st, a);
+        hipLaunchKernelGGL((gz::k_inflate_members<16384, false, false>), dim3((unsigned)nmembers), dim3(64),
+                           sizeof(gz::InfSmem<16384, false>), st, a);
     else
-        hipLaunchKernelGGL((gz::k_inflate_members<65536, false>), dim3((unsigned)nmembers), dim3(64),
-                           sizeof(gz::InfSmem<65536>), st, a);
+        hipLaunchKernelGGL((gz::k_inflate_members<65536, false, false>), dim3((unsigned)nmembers), dim3(64),
+                           sizeof(gz::InfSmem<65536, false>), st, a);
     GZHIP(hipGetLastError());
     int h = 0;
     GZHIP(hipMemcpyAsync(&h, status, sizeof(int), hipMemcpyDeviceToHost, st));

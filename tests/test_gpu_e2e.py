@@ -10,7 +10,9 @@ SerializeToString -> ParseFromString -> metadata as protobuf containers
 
 Checked against the CPU oracle on the WIRE contents: the Eden bins of every
 payload vs oracle.compress with the seed the metadata carries (>= 99.9 %
-equal, |dbin| <= 1), the decoded array vs oracle.decompress of the same
+equal over the update, per tensor >= the survey's 99.8 % or at most 2
+boundary flips -- a 512-element tensor with one flipped bin is 99.80 % --
+and |dbin| <= 1), the decoded array vs oracle.decompress of the same
 bytes and float32 metadata (rel-L2 and max-abs <= 2e-6), raw fp32 payloads
 of small tensors exact, and int_to_float values arriving as float32
 (base.proto:22).
@@ -57,13 +59,14 @@ def _receive(pipe, wire, batched, P):
 
 
 def _check_tensor(x, data, md, y, bits=8):
+    """-> (bins compared, bins that differ) of an Eden payload, (0, 0) else."""
     i2f = md["int_to_float"]
     assert list(md["int_list"]) == list(x.shape)
     assert y.dtype == np.float32 and y.shape == x.shape
     if not i2f:                                   # small tensor: raw float32 bytes (pipeline.py:59-77)
         assert data == x.astype(np.float32).tobytes()
         np.testing.assert_array_equal(y, x)
-        return
+        return 0, 0
     for v in i2f.values():                        # float32 on the wire (base.proto:22)
         assert np.float32(v) == v
     seed, total = int(i2f[0]), int(i2f[1])
@@ -74,13 +77,15 @@ def _check_tensor(x, data, md, y, bits=8):
     assert odims == dims and len(data) == len(op.tobytes())
     a = O.bins_of(data, sum(dims), bits)
     b = O.bins_of(op, sum(dims), bits)
-    assert np.mean(a == b) >= 0.999 and np.max(np.abs(a - b)) <= 1
+    diff = int(np.sum(a != b))
+    assert (diff <= max(0.002 * a.size, 2)) and np.max(np.abs(a - b)) <= 1
     np.testing.assert_allclose(scales, np.float32(osc), rtol=1e-3)
     yo = O.decompress(data, total, scales, dims, seed, bits).reshape(x.shape)
     ref = yo.astype(np.float64)
     err = y.astype(np.float64) - ref
     assert np.max(np.abs(err)) <= 2e-6 * max(np.max(np.abs(ref)), 1e-30)
     assert np.linalg.norm(err) <= 2e-6 * np.linalg.norm(ref)
+    return a.size, diff
 
 
 @pytest.mark.timeout(600)
@@ -99,8 +104,11 @@ def test_loopback_two_collaborators(workload, limit, batched):
         wire, _ = _send(col_pipe, sd, batched, P)
         outs, parsed = _receive(agg_pipe, wire, batched, P)
         assert len(outs) == len(sd)
+        seen = flips = 0
         for (name, x), (data, mds), y in zip(sd, parsed, outs):
-            _check_tensor(x, data, mds[0], y)
+            n, d = _check_tensor(x, data, mds[0], y)
+            seen, flips = seen + n, flips + d
+        assert flips <= 1e-3 * seen
         # Eden error band of the whole update (8-bit, Gaussian): ~6.4e-3
         num = sum(float(np.sum((o.astype(np.float64) - a) ** 2)) for (_, a), o in zip(sd, outs))
         den = sum(float(np.sum(a.astype(np.float64) ** 2)) for _, a in sd)
