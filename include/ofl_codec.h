@@ -153,6 +153,23 @@ int ofl_eden_encode_host(ofl_eden_plan_t plan, const void* in_host, void* in_dev
 int ofl_eden_decode_host(ofl_eden_plan_t plan, const void* in_host, void* in_dev, size_t in_bytes, size_t off_scales,
                          size_t off_seeds, void* out_dev, void* out_host, size_t out_bytes, void* ws, size_t ws_bytes,
                          void* stream);
+/* The same one-tensor calls for large tensors, the host buffers used where
+ * they lie (pageable is fine; the runtime streams them at the pinned rate on
+ * this box) instead of being copied into a pinned block first:
+ *   encode_host_x: x_host (x_bytes, NULL = already copied to in_dev, e.g. by
+ *     ofl_copy_h2d_async while the host computed the seed's serial sum),
+ *     the seed written to in_dev + off_seeds by a device memset;
+ *   decode_host_x: planes and scales from separate host arrays, the seed by
+ *     a device memset, y D2H into y_host.
+ * Both synchronise `stream` before returning. */
+int ofl_eden_encode_host_x(ofl_eden_plan_t plan, const void* x_host, size_t x_bytes, uint32_t seed, void* in_dev,
+                           size_t off_seeds, void* out_dev, void* out_host, size_t out_bytes, size_t off_scales,
+                           void* ws, size_t ws_bytes, void* stream);
+int ofl_eden_decode_host_x(ofl_eden_plan_t plan, const void* planes_host, size_t planes_bytes, const float* scales_host,
+                           int nscales, uint32_t seed, void* in_dev, size_t off_scales, size_t off_seeds,
+                           void* out_dev, void* y_host, size_t y_bytes, void* ws, size_t ws_bytes, void* stream);
+/* hipMemcpyAsync host -> device on `stream` (no synchronisation). */
+int ofl_copy_h2d_async(void* dst_dev, const void* src_host, size_t bytes, void* stream);
 
 /* ---- profiling (bench.py) --------------------------------------------------
  * While enabled, every encode/decode of the plan records a HIP event before

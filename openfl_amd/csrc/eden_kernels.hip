@@ -3001,6 +3001,56 @@ int ofl_eden_decode_host(ofl_eden_plan_t pl, const void* in_host, void* in_dev, 
     return OFL_OK;
 }
 
+int ofl_eden_encode_host_x(ofl_eden_plan_t pl, const void* x_host, size_t x_bytes, uint32_t seed, void* in_dev,
+                           size_t off_seeds, void* out_dev, void* out_host, size_t out_bytes, size_t off_scales,
+                           void* ws, size_t ws_bytes, void* stream) {
+    if (!pl || !in_dev || !out_dev || !out_host) return fail(OFL_EINVAL, "encode_host_x: null argument");
+    if (pl->ntensors != 1 || off_seeds < 4 * (size_t)pl->arena || (x_host && x_bytes > off_seeds) ||
+        off_scales < (size_t)pl->planes_bytes || off_scales + 4 * pl->slices.size() > out_bytes)
+        return fail(OFL_EINVAL, "encode_host_x: block layout does not fit the plan");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    char* i = static_cast<char*>(in_dev);
+    if (x_host && x_bytes) HIP_TRY(hipMemcpyAsync(i, x_host, x_bytes, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(i + off_seeds), (int)seed, 1, st));
+    char* o = static_cast<char*>(out_dev);
+    if (int rc = ofl_eden_encode(pl, reinterpret_cast<const float*>(i), reinterpret_cast<const uint32_t*>(i + off_seeds),
+                                 reinterpret_cast<uint8_t*>(o), reinterpret_cast<float*>(o + off_scales), ws, ws_bytes,
+                                 stream))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(out_host, out_dev, out_bytes, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return OFL_OK;
+}
+
+int ofl_eden_decode_host_x(ofl_eden_plan_t pl, const void* planes_host, size_t planes_bytes, const float* scales_host,
+                           int nscales, uint32_t seed, void* in_dev, size_t off_scales, size_t off_seeds,
+                           void* out_dev, void* y_host, size_t y_bytes, void* ws, size_t ws_bytes, void* stream) {
+    if (!pl || !planes_host || !scales_host || !in_dev || !out_dev || !y_host)
+        return fail(OFL_EINVAL, "decode_host_x: null argument");
+    if (pl->ntensors != 1 || planes_bytes != (size_t)pl->planes_bytes || nscales != (int)pl->slices.size() ||
+        off_scales < planes_bytes || off_seeds < off_scales + 4 * (size_t)nscales || y_bytes > 4 * (size_t)pl->arena)
+        return fail(OFL_EINVAL, "decode_host_x: block layout does not fit the plan");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    char* i = static_cast<char*>(in_dev);
+    HIP_TRY(hipMemcpyAsync(i, planes_host, planes_bytes, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(i + off_scales, scales_host, 4 * (size_t)nscales, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(i + off_seeds), (int)seed, 1, st));
+    if (int rc = ofl_eden_decode(pl, reinterpret_cast<const uint8_t*>(i), reinterpret_cast<const uint32_t*>(i + off_seeds),
+                                 reinterpret_cast<const float*>(i + off_scales), static_cast<float*>(out_dev), ws, ws_bytes,
+                                 stream))
+        return rc;
+    if (y_bytes) HIP_TRY(hipMemcpyAsync(y_host, out_dev, y_bytes, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return OFL_OK;
+}
+
+int ofl_copy_h2d_async(void* dst_dev, const void* src_host, size_t bytes, void* stream) {
+    if (!bytes) return OFL_OK;
+    if (!dst_dev || !src_host) return fail(OFL_EINVAL, "copy_h2d_async: null argument");
+    HIP_TRY(hipMemcpyAsync(dst_dev, src_host, bytes, hipMemcpyHostToDevice, static_cast<hipStream_t>(stream)));
+    return OFL_OK;
+}
+
 int ofl_eden_plan_profile(ofl_eden_plan_t pl, int enable) {
     if (!pl) return fail(OFL_EINVAL, "null plan");
     std::lock_guard<std::mutex> g(pl->mu);
