@@ -130,6 +130,20 @@ int ofl_eden_encode(ofl_eden_plan_t plan, const float* x_arena, const uint32_t* 
 int ofl_eden_decode(ofl_eden_plan_t plan, const uint8_t* planes_arena, const uint32_t* seeds,
                     const float* scales, float* y_arena, void* ws, size_t ws_bytes,
                     void* stream);
+/* encode fused with the aggregator's WeightedAverage + generate_delta
+ * (aggregator.py:780-865, weighted_average.py:14, tensor_codec.py:150-180):
+ * the large slices' row pass computes x = float32((sum_c f64(x_c) * w_c) /
+ * wsum - f64(base)) from the ncollab (1..16) collaborator arenas (device array
+ * collab_arenas of device pointers, weights a DEVICE float64 array; arenas,
+ * base_arena (nullable) and delta_arena share the plan's layout) instead of
+ * reading a delta arena -- the delta's 8 B/element round trip through HBM
+ * is not made.  Slices of at most 2^15 elements still read delta_arena, so
+ * the caller fills it for their ranges (ofl_wavg_delta_ranges32).  Outputs
+ * equal ofl_eden_encode of the delta ofl_wavg_delta would write. */
+int ofl_eden_encode_wavg(ofl_eden_plan_t plan, const float* const* collab_arenas, const double* weights,
+                         int ncollab, double wsum, const float* base_arena, const float* delta_arena,
+                         const uint32_t* seeds, uint8_t* planes_arena, float* scales, void* ws, size_t ws_bytes,
+                         void* stream);
 /* decode fused with TensorCodec.apply_delta (tensor_codec.py:182-211):
  * y = base + decoded, two float32 roundings as in NumPy (decoded delta first,
  * then the add).  base_arena has the plan's layout; y_arena may alias it. */
@@ -329,6 +343,12 @@ int ofl_apply_delta(const float* base, const float* delta, int64_t n, float* out
 int ofl_sub_f32_f64(const float* data, const double* shift, int64_t n, double* out, void* stream);
 int ofl_apply_delta_ranges(const float* base, const float* delta, float* out, int nranges, const int64_t* starts,
                            const int64_t* dst, int64_t total, void* stream);
+/* ofl_wavg_delta's float32 delta on listed ranges only (xs: host array of
+ * ncollab <= 16 device pointers; starts [nranges] / dst [nranges + 1]: DEVICE
+ * tables as ofl_apply_delta_ranges): what ofl_eden_encode_wavg reads. */
+int ofl_wavg_delta32_ranges(int ncollab, const float* const* xs, const double* weights, double wsum,
+                            const float* base, int nranges, const int64_t* starts, const int64_t* dst, int64_t total,
+                            float* delta32_out, void* stream);
 
 /* ---- gzip of rank arrays (csrc/deflate_kernels.hip) -------------------------
  * GZIPTransformer.forward (kc_pipeline.py:128-156, skc_pipeline.py:201-230,

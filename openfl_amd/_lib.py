@@ -22,7 +22,7 @@ EXPORTS = (
     "ofl_eden_plan_destroy", "ofl_eden_plan_set_schedule", "ofl_eden_plan_num_waves",
     "ofl_eden_plan_get_schedule", "ofl_eden_plan_set_row2", "ofl_eden_plan_num_slices", "ofl_eden_plan_planes_bytes",
     "ofl_eden_plan_workspace_bytes", "ofl_eden_plan_tensor_info", "ofl_eden_plan_tensor_dims",
-    "ofl_eden_encode", "ofl_eden_decode", "ofl_eden_decode_add", "ofl_eden_encode_host", "ofl_eden_decode_host", "ofl_eden_encode_host_x", "ofl_eden_decode_host_x", "ofl_copy_h2d_async", "ofl_eden_plan_profile", "ofl_eden_plan_num_launches",
+    "ofl_eden_encode", "ofl_eden_encode_wavg", "ofl_eden_decode", "ofl_eden_decode_add", "ofl_eden_encode_host", "ofl_eden_decode_host", "ofl_eden_encode_host_x", "ofl_eden_decode_host_x", "ofl_copy_h2d_async", "ofl_eden_plan_profile", "ofl_eden_plan_num_launches",
     "ofl_eden_plan_launch_info", "ofl_eden_plan_profile_collect", "ofl_serial_sum_f32", "ofl_serial_sum_copy_f32",
     "ofl_serial_sum_f64", "ofl_host_copy_many", "ofl_serial_sums_many", "ofl_lossy_last_error", "ofl_lossy_workspace_bytes", "ofl_kmeans1d_fit",
     "ofl_kmeans1d_batch_workspace_bytes", "ofl_kmeans1d_batch",
@@ -34,7 +34,7 @@ EXPORTS = (
     "ofl_wavg_range_sums_workspace_bytes", "ofl_wavg_delta_range_sums", "ofl_wavg_delta_seeds",
     "ofl_py_hash_doubles",
     "ofl_wavg_points_workspace_bytes", "ofl_wavg_delta_points", "ofl_apply_delta",
-    "ofl_apply_delta_ranges", "ofl_sub_f32_f64",
+    "ofl_apply_delta_ranges", "ofl_wavg_delta32_ranges", "ofl_sub_f32_f64",
     "ofl_gzip_last_error", "ofl_gzip_ranks_workspace_bytes", "ofl_gzip_ranks_bound", "ofl_gzip_ranks",
     "ofl_gunzip_members", "ofl_gzip_member_index", "ofl_inflate_members",
 )
@@ -70,6 +70,8 @@ def _bind(L):
     L.ofl_eden_plan_tensor_dims.argtypes = [vp, i32, vp]
     L.ofl_eden_plan_tensor_dims.restype = i32
     L.ofl_eden_encode.argtypes = [vp, vp, vp, vp, vp, vp, sz, vp]
+    L.ofl_eden_encode_wavg.argtypes = [vp, vp, vp, i32, ctypes.c_double, vp, vp, vp, vp, vp, vp, sz, vp]
+    L.ofl_eden_encode_wavg.restype = i32
     L.ofl_eden_encode.restype = i32
     L.ofl_eden_decode.argtypes = [vp, vp, vp, vp, vp, vp, sz, vp]
     L.ofl_eden_decode.restype = i32
@@ -151,6 +153,8 @@ def _bind(L):
     L.ofl_sub_f32_f64.restype = i32
     L.ofl_apply_delta_ranges.argtypes = [vp, vp, vp, i32, vp, vp, i64, vp]
     L.ofl_apply_delta_ranges.restype = i32
+    L.ofl_wavg_delta32_ranges.argtypes = [i32, vp, vp, ctypes.c_double, vp, i32, vp, vp, i64, vp, vp]
+    L.ofl_wavg_delta32_ranges.restype = i32
     L.ofl_gzip_last_error.restype = ctypes.c_char_p
     L.ofl_gzip_ranks_workspace_bytes.argtypes = [i64]
     L.ofl_gzip_ranks_workspace_bytes.restype = sz

@@ -28,10 +28,11 @@ import numpy as np
 import torch
 
 from openfl_amd import _lib, hostmem
-from openfl_amd.codec import EdenPlan, resolve_device
+from openfl_amd.codec import EdenPlan, resolve_device, slice_plan
 from openfl_amd.pipelines.eden_pipeline import _FAST_SEED_PREFIX
 
 _ALIGN = 64
+_ROW_TILE = 1 << 15  # slices above this go through the row passes (kRowLog)
 
 
 def _stream(device):
@@ -134,9 +135,13 @@ class RoundEnd:
     seed_mode apply); shapes: the model's tensor shapes in the aggregator's
     order.  Tensors live in flat float32 arenas, tensor i at offsets[i]
     (64-element aligned); arena() / pack() / view() make and read them.
+    fused (default): without agg_out and with at most 16 collaborators the
+    large slices' first encode pass computes the delta from the collaborator
+    arenas itself (ofl_eden_encode_wavg) instead of reading a delta arena
+    the averaging kernel wrote -- same bytes, 8 B/element less HBM traffic.
     """
 
-    def __init__(self, pipeline, shapes, device=None):
+    def __init__(self, pipeline, shapes, device=None, fused=True):
         tr = pipeline.transformers[0]
         self.transformer = tr
         self.device = resolve_device(device) if device is not None else tr.eden.device
@@ -176,6 +181,24 @@ class RoundEnd:
         self._seeds = torch.empty(max(T, 1), dtype=torch.int32, device=self.device)
         self._packed = torch.empty(max(self._seed_total, 1), dtype=torch.float64, device=self.device)
         self._big_idx = torch.tensor(self.big or [0], dtype=torch.int64).to(self.device)
+        # fused round-end encode (ofl_eden_encode_wavg): the large slices' row
+        # pass computes the delta from the collaborators' arenas itself, so the
+        # delta arena is written only where something else reads it -- the
+        # tensors the codec does not touch and the slices of <= 2^15 elements
+        self.fused = bool(fused) and self.plan is not None
+        fz = [(self.offsets[i], self.numels[i]) for i in rest]
+        for t, i in enumerate(self.big):
+            _, lens = slice_plan(self.numels[i])
+            xo = self.offsets[i]
+            for P, ln in zip(self.plan.dims[t], lens):
+                if P <= _ROW_TILE and ln > 0:
+                    fz.append((xo, ln))
+                xo += ln
+        fz.sort()
+        self._fz_n = len(fz)
+        self._fz_total = sum(n for _, n in fz)
+        self._fz_start = torch.tensor([o for o, _ in fz] or [0], dtype=torch.int64).to(self.device)
+        self._fz_dst = torch.from_numpy(np.cumsum([0] + [n for _, n in fz]).astype(np.int64)).to(self.device)
         self._host_args = None   # pinned [collaborator pointers | weights | draws], reused after _args_done
         self._dev_args = None
         self._args_done = None
@@ -224,12 +247,22 @@ class RoundEnd:
         w64 = _f64_weights(weights, len(xs))
         wsum = self._wsum(w64)
         L = _lib.lib()
+        fused = self.fused and agg_out is None and len(xs) <= 16
         with torch.cuda.device(dev):
             delta = torch.empty(self.arena_numel, dtype=torch.float32, device=dev)
             if agg_out is None and len(xs) > 16:  # running sums between chained launches
                 agg_out = torch.empty(self.arena_numel, dtype=torch.float64, device=dev)
-            # 1. average + delta (float64), delta rounded to float32
-            _wavg_launch(xs, w64, wsum, base_arena, self.arena_numel, agg=agg_out, delta32=delta, device=dev)
+            # 1. average + delta (float64), delta rounded to float32 -- fused:
+            # only on the ranges the large slices' encode does not compute
+            if fused:
+                ptrs = np.asarray([x.data_ptr() for x in xs], np.uint64)
+                _lib.check_agg(L.ofl_wavg_delta32_ranges(
+                    len(xs), ptrs.ctypes.data, w64.ctypes.data, wsum,
+                    base_arena.data_ptr() if base_arena is not None else None, self._fz_n,
+                    self._fz_start.data_ptr(), self._fz_dst.data_ptr(), self._fz_total, delta.data_ptr(),
+                    _stream(dev)))
+            else:
+                _wavg_launch(xs, w64, wsum, base_arena, self.arena_numel, agg=agg_out, delta32=delta, device=dev)
             if self.single:
                 _points_launch(xs, w64, wsum, base_arena, [self.offsets[i] for i in self.single], agg_out, delta,
                                dev, self._ws)
@@ -268,7 +301,13 @@ class RoundEnd:
                 scales = torch.empty(max(p.n_slices, 1), dtype=torch.float32, device=dev)
                 if self._codec_ws is None or self._codec_ws.numel() < p.ws_bytes:
                     self._codec_ws = torch.empty(max(p.ws_bytes, 256), dtype=torch.uint8, device=dev)
-                p.encode(delta, sd, planes, scales, self._codec_ws)
+                if fused:
+                    _lib.check(L.ofl_eden_encode_wavg(
+                        p.handle, dp, dp + 8 * C, C, wsum, base_arena.data_ptr() if base_arena is not None else None,
+                        delta.data_ptr(), sd.data_ptr(), planes.data_ptr(), scales.data_ptr(),
+                        self._codec_ws.data_ptr(), self._codec_ws.numel(), _stream(dev)))
+                else:
+                    p.encode(delta, sd, planes, scales, self._codec_ws)
                 if payloads:
                     pn = planes[:p.planes_bytes].cpu().numpy()
                     sn = scales[:p.n_slices].cpu().numpy()

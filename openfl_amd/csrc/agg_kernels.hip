@@ -309,6 +309,25 @@ __global__ __launch_bounds__(kNT) void k_apply_ranges(const float* base, const f
     }
 }
 
+// the float32 delta (as k_wavg_delta writes it) on listed ranges only: the
+// elements the fused round-end encode does not compute itself
+// (ofl_eden_encode_wavg: slices of <= 2^15 elements and the tensors the codec
+// does not touch)
+__global__ __launch_bounds__(kNT) void k_wavg_delta32_ranges(WavgArgs a, const int64_t* start, const int64_t* dst,
+                                                             int nr) {
+    const int64_t total = dst[nr];
+    for (int64_t j = (int64_t)blockIdx.x * kNT + threadIdx.x; j < total; j += (int64_t)gridDim.x * kNT) {
+        int lo = 0, hi = nr - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (dst[mid] <= j) lo = mid; else hi = mid - 1;
+        }
+        const int64_t i = start[lo] + (j - dst[lo]);
+        double avg;
+        a.delta32[i] = (float)wavg_delta(a, i, wavg_sum(a, i, 0.0), avg);
+    }
+}
+
 __global__ __launch_bounds__(64) void k_py_hash(const double* v, int n, int64_t* out) {
     const int i = blockIdx.x * 64 + threadIdx.x;
     if (i < n) out[i] = py_hash_double(v[i]);
@@ -543,6 +562,29 @@ int ofl_sub_f32_f64(const float* data, const double* shift, int64_t n, double* o
     if (n == 0) return OFL_OK;
     hipLaunchKernelGGL(agg::k_unshift64, dim3(grid_for(n, 16)), dim3(agg::kNT), 0, static_cast<hipStream_t>(stream),
                        data, shift, n, out);
+    AHIP(hipGetLastError());
+    return OFL_OK;
+}
+
+int ofl_wavg_delta32_ranges(int ncollab, const float* const* xs, const double* weights, double wsum,
+                            const float* base, int nranges, const int64_t* starts, const int64_t* dst, int64_t total,
+                            float* delta32_out, void* stream) {
+    if (nranges < 1 || total <= 0) return OFL_OK;
+    if (ncollab > agg::kMaxC) return afail(OFL_EINVAL, "wavg_delta32_ranges: at most 16 collaborators");
+    if (!starts || !dst || !delta32_out) return afail(OFL_EINVAL, "wavg_delta32_ranges: bad arguments");
+    agg::WavgArgs a;
+    if (int rc = fill_args(a, ncollab, xs, weights, wsum, base, total)) return rc;
+    a.nc = ncollab;
+    for (int c = 0; c < ncollab; ++c) {
+        if (!xs[c]) return afail(OFL_EINVAL, "wavg: null collaborator tensor");
+        a.x[c] = xs[c];
+        a.w[c] = weights[c];
+    }
+    a.first = 1;
+    a.last = 1;
+    a.delta32 = delta32_out;
+    hipLaunchKernelGGL(agg::k_wavg_delta32_ranges, dim3(grid_for(total, 1)), dim3(agg::kNT), 0,
+                       static_cast<hipStream_t>(stream), a, starts, dst, nranges);
     AHIP(hipGetLastError());
     return OFL_OK;
 }

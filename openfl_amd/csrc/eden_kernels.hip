@@ -97,6 +97,14 @@ struct KArgs {
     float* nu;              // per-slice norms (large)
     const float* yadd;      // decode: nullable, y = yadd + decoded (apply_delta, float32 add)
     const int32_t* btab;    // column launches: per block {slice, tile << 3 | group} (nullable)
+    // round-end fused encode (ofl_eden_encode_wavg): the large slices' x is
+    // the float32-rounded delta (sum_c f64(x_c) * w_c) / wsum - f64(base),
+    // computed from the collaborators' arenas as the row pass loads it
+    const float* const* wx; // collaborator arenas (device array of wc pointers), nullable
+    const double* ww;       // their weights (device)
+    const float* wbase;     // base model arena, nullable
+    double wsum;            // NumPy's float64 sum of the weights
+    int32_t wc;             // collaborators (1..16)
 };
 
 // Eden centroids in global memory (copied to LDS per workgroup); the
@@ -1868,7 +1876,80 @@ DEVI void row_locate(const KArgs& a, int t, int& si, uint32_t& tile) {
     tile = (uint32_t)(t - (int)sld(a.tstart, lo));
 }
 
-// encode pass A (as k_enc_rowA)
+// x tile of the fused round-end encode: per element the delta of the
+// weighted average, in k_wavg_delta's operation order (agg_kernels.hip:
+// products rounded, summed from the first collaborator on, / wsum, - base,
+// FMA contraction off), rounded to float32 -- the values Eden.compress would
+// get.  Elements past the slice's valid length are zero (padding).  Loads go
+// two float4 chunks x two collaborators at a time (the 128-VGPR budget of two
+// blocks per CU; the other block hides the round trips).
+DEVI void fetch_x_wavg(const KArgs& a, const SliceDesc& D, uint32_t tile, uint32_t base1, float (&v)[64]) {
+#pragma clang fp contract(off)
+    const uint32_t e0 = tile << kRowLog;
+    const uint32_t nv = tile_valid(D.len - (int64_t)e0);
+    const uint32_t rec = (nv & ~3u) * 4u;  // whole float4s; the straddling one below
+    const int nc = a.wc;
+#pragma unroll
+    for (int g = 0; g < 64; g += 8) {
+        double s[8];
+        for (int c = 0; c < nc; c += 2) {
+            const bool two = c + 1 < nc;
+            const rsrc_t r0 = mk_rsrc(a.wx[c] + D.x_off + e0, rec);
+            const rsrc_t r1 = mk_rsrc(a.wx[two ? c + 1 : c] + D.x_off + e0, two ? rec : 0u);
+            const float4 p0 = bload4(r0, base1, LT<RS::L1>::off(g)), p1 = bload4(r0, base1, LT<RS::L1>::off(g + 4));
+            const float4 q0 = bload4(r1, base1, LT<RS::L1>::off(g)), q1 = bload4(r1, base1, LT<RS::L1>::off(g + 4));
+            const float xp[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+            const float xq[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+            const double w0 = a.ww[c], w1 = two ? a.ww[c + 1] : 0.0;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                s[t] = c == 0 ? (double)xp[t] * w0 : s[t] + (double)xp[t] * w0;
+                if (two) s[t] = s[t] + (double)xq[t] * w1;
+            }
+        }
+        float4 b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0;
+        if (a.wbase) {
+            const rsrc_t rb = mk_rsrc(a.wbase + D.x_off + e0, rec);
+            b0 = bload4(rb, base1, LT<RS::L1>::off(g));
+            b1 = bload4(rb, base1, LT<RS::L1>::off(g + 4));
+        }
+        const float xb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const double avg = s[t] / a.wsum;
+            const double d = a.wbase ? avg - (double)xb[t] : avg;
+            const uint32_t i = base1 + LT<RS::L1>::off(g + (t & ~3)) + (uint32_t)(t & 3);
+            v[g + t] = i < (nv & ~3u) ? (float)d : 0.0f;
+        }
+        asm volatile("" : "+v"(v[g]), "+v"(v[g + 1]), "+v"(v[g + 2]), "+v"(v[g + 3]), "+v"(v[g + 4]), "+v"(v[g + 5]),
+                     "+v"(v[g + 6]), "+v"(v[g + 7]));
+    }
+    // the <= 3 valid elements of a float4 that straddles the valid length
+    const uint32_t rem = nv & 3u;
+    if (rem) {
+        const uint32_t eb = nv & ~3u;
+        float xs[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            double sq = 0.0;
+            const int64_t ei = D.x_off + e0 + eb + q;
+            for (int c = 0; c < nc; ++c) sq = c == 0 ? (double)a.wx[c][ei] * a.ww[c] : sq + (double)a.wx[c][ei] * a.ww[c];
+            const double avg = sq / a.wsum;
+            const double d = a.wbase ? avg - (double)a.wbase[ei] : avg;
+            xs[q] = (uint32_t)q < rem ? (float)d : 0.0f;
+        }
+#pragma unroll
+        for (int k = 0; k < 64; k += 4) {
+            const bool hit = base1 + LT<RS::L1>::off(k) == eb;
+            v[k] = hit ? xs[0] : v[k];
+            v[k + 1] = hit ? xs[1] : v[k + 1];
+            v[k + 2] = hit ? xs[2] : v[k + 2];
+        }
+    }
+}
+
+// encode pass A (as k_enc_rowA); WAVG: x from the collaborators' arenas
+template <bool WAVG>
 __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowA2(KArgs a) {
     using R = RowA2Set;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1884,8 +1965,16 @@ __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowA2(KArgs a) {
         row_locate(a, t, si, tile);
         const SliceDesc D = udesc(a.d, si);
         float v[64];
-        fetch_x(a, D, tile, true, base1, v);
-        fix_x(a, D, tile, base1, v);
+        if constexpr (WAVG) {
+            fetch_x_wavg(a, D, tile, base1, v);
+        } else {
+            fetch_x(a, D, tile, true, base1, v);
+            fix_x(a, D, tile, base1, v);
+#pragma unroll
+            for (int r = 0; r < 64; r += 8)
+                asm volatile("" : "+v"(v[r]), "+v"(v[r + 1]), "+v"(v[r + 2]), "+v"(v[r + 3]), "+v"(v[r + 4]),
+                             "+v"(v[r + 5]), "+v"(v[r + 6]), "+v"(v[r + 7]));
+        }
         const uint32_t b1 = seed_b(sld(a.seeds, D.tensor));
         float ss = 0.f;
 #pragma unroll
@@ -2167,8 +2256,10 @@ bool use_perm25() {
 }
 // the tiny / small launches (latency-bound, independent of each other) split
 // over two streams instead of one (OFL_EDEN_SMALL2=0: one stream, A/B)
+// (opt-in OFL_EDEN_SMALL2=1: measured slower on ResNet-50, 259-269 vs
+// 273-276 GiB/s, profiles/r03_resnet50_row2_small2_ab.txt)
 bool use_small_split() {
-    static const bool on = [] { const char* s = getenv("OFL_EDEN_SMALL2"); return !(s && s[0] == '0'); }();
+    static const bool on = [] { const char* s = getenv("OFL_EDEN_SMALL2"); return s && s[0] == '1'; }();
     return on;
 }
 // tiny / small slices on a third stream when the waves use two
@@ -2219,7 +2310,8 @@ hipError_t set_all_attrs() {
     if ((e = set_lds((const void*)ofl::k_dec_rowA<true>, ofl::kRowSmemC)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_dec_rowA<false>, ofl::kRowSmemC)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_dec_rowC, ofl::kRowSmemA)) != hipSuccess) return e;
-    if ((e = set_lds((const void*)ofl::k_enc_rowA2, ofl::kRow2Smem)) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_enc_rowA2<false>, ofl::kRow2Smem)) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_enc_rowA2<true>, ofl::kRow2Smem)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_dec_rowA2<true>, ofl::kRow2SmemC)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_dec_rowA2<false>, ofl::kRow2SmemC)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_dec_rowC2, ofl::kRow2Smem)) != hipSuccess) return e;
@@ -2306,9 +2398,14 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
         }
         case K_ROWA: {
             const bool a8 = l.mid && (reinterpret_cast<uintptr_t>(base.pin) & 7u) == 0;
+            if (enc && base.wx) {  // fused round-end encode: x = the weighted-average delta
+                e = launch(ofl::k_enc_rowA2<true>, std::min<int64_t>(l.blocks, 2 * pl->ncu), ofl::kRowNT, ofl::kRow2Smem,
+                           st, a);
+                break;
+            }
             if (use_row2(l.blocks, pl->ncu, pl->row2)) {
                 const int64_t g2 = std::min<int64_t>(l.blocks, 2 * pl->ncu);
-                e = enc ? launch(ofl::k_enc_rowA2, g2, ofl::kRowNT, ofl::kRow2Smem, st, a)
+                e = enc ? launch(ofl::k_enc_rowA2<false>, g2, ofl::kRowNT, ofl::kRow2Smem, st, a)
                         : a8 ? launch(ofl::k_dec_rowA2<true>, g2, ofl::kRowNT, ofl::kRow2SmemC, st, a)
                              : launch(ofl::k_dec_rowA2<false>, g2, ofl::kRowNT, ofl::kRow2SmemC, st, a);
                 break;
@@ -2940,6 +3037,27 @@ int ofl_eden_encode(ofl_eden_plan_t pl, const float* x_arena, const uint32_t* se
     a.pout = planes_arena;
     a.seeds = seeds;
     a.scales = scales;
+    return run(pl, true, a, static_cast<hipStream_t>(stream));
+}
+
+int ofl_eden_encode_wavg(ofl_eden_plan_t pl, const float* const* collab_arenas, const double* weights, int ncollab,
+                         double wsum, const float* base_arena, const float* delta_arena, const uint32_t* seeds,
+                         uint8_t* planes_arena, float* scales, void* ws, size_t ws_bytes, void* stream) {
+    if (!pl) return fail(OFL_EINVAL, "null plan");
+    if (!collab_arenas || !weights || ncollab < 1 || ncollab > 16 || !(wsum != 0.0))
+        return fail(OFL_EINVAL, "encode_wavg: 1..16 collaborators, their weights and a nonzero weight sum");
+    ofl::KArgs a;
+    int rc = prep_args(pl, a, ws, ws_bytes);
+    if (rc) return rc;
+    a.xin = delta_arena;
+    a.pout = planes_arena;
+    a.seeds = seeds;
+    a.scales = scales;
+    a.wx = collab_arenas;
+    a.ww = weights;
+    a.wc = ncollab;
+    a.wsum = wsum;
+    a.wbase = base_arena;
     return run(pl, true, a, static_cast<hipStream_t>(stream));
 }
 

@@ -228,9 +228,6 @@ class Eden(PerThreadDevice):
             c.run()
             out = (np.frombuffer(ctypes.string_at(c.out_ptr, c.pb), np.uint8), c.scales_view.tolist(), list(c.dims), n)
             return out if seed_of_sum is None else (out, int(seed))
-        # larger tensors: x goes H2D from where it lies (no copy into pinned
-        # staging first: a pageable source streams at the pinned rate here);
-        # with the reference seed the DMA runs beside the serial sum
         L = _lib.lib()
         plan = self.codec.plan([n], streams=_one_tensor_streams(n))
         pb, ns = plan.planes_bytes, plan.n_slices
@@ -238,20 +235,39 @@ class Eden(PerThreadDevice):
         in_bytes = off_seeds + 4
         off_scales = _al256(pb)
         out_bytes = off_scales + 4 * ns
-        oh = self._staging().get("out1", out_bytes, torch.uint8)
+        stg = self._staging()
+        oh = stg.get("out1", out_bytes, torch.uint8)
         idev = self._dev("in", in_bytes, torch.uint8)
         odev = self._dev("out", out_bytes, torch.uint8)
         ws = self.codec.ws.get(plan.ws_bytes, self.device)
         st = self._stream().cuda_stream
         with _device_guard(self.device):
-            x_ptr = flat.ctypes.data if n else None
-            if fuse:
-                _lib.check(L.ofl_copy_h2d_async(idev.data_ptr(), x_ptr, 4 * n, st))
-                x_ptr = None
-                seed = seed_of_sum(np.float32(L.ofl_serial_sum_f32(flat.ctypes.data, n)))
-            _lib.check(L.ofl_eden_encode_host_x(
-                plan.handle, x_ptr, 4 * n, int(seed) & 0xFFFFFFFF, idev.data_ptr(), off_seeds, odev.data_ptr(),
-                oh.data_ptr(), out_bytes, off_scales, ws.data_ptr(), ws.numel(), st))
+            if _PAGEABLE:
+                # x H2D from where it lies (ofl_eden_encode_host_x); with the
+                # reference seed the DMA runs beside the serial sum.  Faster
+                # on one reused array, slower over a model's many fresh ones
+                # (profiles/r03_e2e_*), hence opt-in
+                x_ptr = flat.ctypes.data if n else None
+                if fuse:
+                    _lib.check(L.ofl_copy_h2d_async(idev.data_ptr(), x_ptr, 4 * n, st))
+                    x_ptr = None
+                    seed = seed_of_sum(np.float32(L.ofl_serial_sum_f32(flat.ctypes.data, n)))
+                _lib.check(L.ofl_eden_encode_host_x(
+                    plan.handle, x_ptr, 4 * n, int(seed) & 0xFFFFFFFF, idev.data_ptr(), off_seeds, odev.data_ptr(),
+                    oh.data_ptr(), out_bytes, off_scales, ws.data_ptr(), ws.numel(), st))
+            else:
+                # pinned block [x | seed], filled while the seed's serial sum
+                # is taken (ofl_serial_sum_copy_f32), then one H2D
+                ih = stg.get("in1", in_bytes, torch.uint8)
+                ia = ih.numpy()
+                if fuse:
+                    seed = seed_of_sum(np.float32(L.ofl_serial_sum_copy_f32(flat.ctypes.data, ia.ctypes.data, n)))
+                elif n:
+                    ia[:4 * n].view(np.float32)[:] = flat
+                ia[off_seeds:off_seeds + 4].view(np.uint32)[0] = int(seed) & 0xFFFFFFFF
+                _lib.check(L.ofl_eden_encode_host(
+                    plan.handle, ih.data_ptr(), idev.data_ptr(), in_bytes, off_seeds, odev.data_ptr(),
+                    oh.data_ptr(), out_bytes, off_scales, ws.data_ptr(), ws.numel(), st))
         oa = oh.numpy()
         # one host copy, pinned -> bytes; the array is a zero-copy view of it
         out = (np.frombuffer(hostmem.bytes_from(oa.ctypes.data, pb), np.uint8),
@@ -292,17 +308,29 @@ class Eden(PerThreadDevice):
         in_bytes = off_seeds + 4
         out_bytes = 4 * total_dim
         sc = np.asarray(scales, np.float32)
-        # planes H2D from the payload itself, y D2H into the returned array
-        # (both pageable: the runtime streams them; no pinned staging copies)
+        # y D2H lands in the returned array itself (pageable: the runtime
+        # stages it), not in pinned staging followed by a host copy
         y = np.empty(max(total_dim, 1), np.float32)
         idev = self._dev("in", in_bytes, torch.uint8)
         ydev = self._dev("y", max(plan.arena_numel, 1), torch.float32)
         ws = self.codec.ws.get(plan.ws_bytes, self.device)
+        L = _lib.lib()
         with _device_guard(self.device):
-            _lib.check(_lib.lib().ofl_eden_decode_host_x(
-                plan.handle, planes_h.ctypes.data, pb, sc.ctypes.data, ns, seed & 0xFFFFFFFF, idev.data_ptr(),
-                off_scales, off_seeds, ydev.data_ptr(), y.ctypes.data, out_bytes, ws.data_ptr(), ws.numel(),
-                self._stream().cuda_stream))
+            if _PAGEABLE:
+                # planes H2D from the payload itself (opt-in, see compress)
+                _lib.check(L.ofl_eden_decode_host_x(
+                    plan.handle, planes_h.ctypes.data, pb, sc.ctypes.data, ns, seed & 0xFFFFFFFF, idev.data_ptr(),
+                    off_scales, off_seeds, ydev.data_ptr(), y.ctypes.data, out_bytes, ws.data_ptr(), ws.numel(),
+                    self._stream().cuda_stream))
+            else:
+                ih = self._staging().get("in1", in_bytes, torch.uint8)
+                ia = ih.numpy()
+                ia[:pb] = planes_h[:pb]
+                ia[off_scales:off_scales + 4 * ns].view(np.float32)[:] = sc
+                ia[off_seeds:off_seeds + 4].view(np.uint32)[0] = seed & 0xFFFFFFFF
+                _lib.check(L.ofl_eden_decode_host(
+                    plan.handle, ih.data_ptr(), idev.data_ptr(), in_bytes, off_scales, off_seeds, ydev.data_ptr(),
+                    y.ctypes.data, out_bytes, ws.data_ptr(), ws.numel(), self._stream().cuda_stream))
         self._trim()
         return y[:total_dim]
 
@@ -312,6 +340,9 @@ class Eden(PerThreadDevice):
 _CTX_NUMEL = 1 << 16
 _CTX_MAX = 256
 _USE_CTX = os.environ.get("OFL_PLUGIN_CTX", "1") != "0"
+# larger one-tensor calls: OFL_PLUGIN_PAGEABLE=1 moves x / planes straight
+# from the caller's arrays (ofl_eden_*_host_x) instead of via pinned staging
+_PAGEABLE = os.environ.get("OFL_PLUGIN_PAGEABLE", "0") == "1"
 
 
 class _CallCtx:

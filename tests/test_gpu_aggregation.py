@@ -100,6 +100,47 @@ def test_round_end_matches_per_tensor(seed_mode, with_base):
     assert y.shape == shapes[3]
 
 
+@pytest.mark.parametrize("seed_mode,with_base,C", [("fast", True, 3), ("reference", True, 1), ("fast", False, 16),
+                                                   ("reference", False, 2)])
+def test_round_end_fused_encode_matches_per_tensor(seed_mode, with_base, C):
+    """Fused round end (no agg_out, <= 16 collaborators): the large slices'
+    first encode pass computes the weighted-average delta from the
+    collaborator arenas (ofl_eden_encode_wavg); the rest of the delta arena is
+    written on ranges only.  Payloads, metadata, draws and the new model equal
+    the reference's per-tensor sequence and the unfused run, bit for bit --
+    with large slices whose valid length ends inside a float4 (60001, 60003),
+    large slices followed by small / tiny ones, tensors the codec skips and
+    1-element tensors."""
+    from openfl_amd.aggregation import RoundEnd
+    from openfl_amd.pipelines import EdenPipeline
+    rng = np.random.default_rng(17 + C)
+    shapes = [(60001,), (3, 20001), (64,), (1,), (70_000,), (1 << 20) + 333, (100,), (100_001,), (2, 2),
+              (3, 1 << 17), (5000,)]
+    shapes = [s if isinstance(s, tuple) else (s,) for s in shapes]
+    collabs = [[(rng.standard_normal(s) * 10.0 ** rng.integers(-3, 1)).astype(np.float32) for s in shapes]
+               for _ in range(C)]
+    base = [(rng.standard_normal(s) * 0.1).astype(np.float32) for s in shapes] if with_base else None
+    w = list(rng.random(C) * 3 + 0.1)
+    pipe = EdenPipeline(n_bits=8, device=DEV, seed_mode=seed_mode)
+    np.random.seed(23)
+    ref_pay, ref_models, _ = _reference_round(pipe, shapes, collabs, w, base)
+    outs = []
+    for fused in (True, False):
+        re = RoundEnd(pipe, shapes, DEV, fused=fused)
+        assert re.fused == fused
+        arenas = [re.pack(c) for c in collabs]
+        base_a = re.pack(base) if with_base else None
+        np.random.seed(23)
+        new, pay, seeds = re.run(arenas, w, base_a)
+        outs.append((new, pay, seeds, re))
+        for i, s in enumerate(shapes):
+            assert pay[i][0] == ref_pay[i][0], (fused, i)
+            assert pay[i][1] == ref_pay[i][1], (fused, i)
+            np.testing.assert_array_equal(re.view(new, i).cpu().numpy(), ref_models[i].reshape(s),
+                                          err_msg=f"{fused} {i}")
+    assert outs[0][2] == outs[1][2]
+
+
 def test_round_end_many_collaborators_chained():
     """> 16 collaborators: the running float64 sums are chained through agg_out."""
     from openfl_amd.aggregation import RoundEnd

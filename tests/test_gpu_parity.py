@@ -559,9 +559,9 @@ def test_row2_variants_bit_identical():
 
 
 def test_small_launch_split_bit_identical():
-    """Tiny / small slices on two side streams (OFL_EDEN_SMALL2 default) give
-    the same bytes as one stream: a mixed set through the default two-stream
-    schedule vs the single-stream schedule."""
+    """Tiny / small slices on the side stream(s) (two of them with
+    OFL_EDEN_SMALL2=1) give the same bytes as one stream: a mixed set through
+    the default two-stream schedule vs the single-stream schedule."""
     from openfl_amd.codec import EdenPlan
     numels = [300, 2000, 5000, 9000, 17000, 33000, 70000, 1 << 20, (1 << 21) + 99, 150]
     res = []
@@ -595,6 +595,28 @@ def test_plugin_call_contexts_identical(monkeypatch):
         monkeypatch.setattr(E, "_USE_CTX", use)
         pipe = E.EdenPipeline(n_bits=8, device=DEV)
         np.random.seed(11)
+        enc = [pipe.forward(x) for x in xs]
+        dec = [pipe.backward(d, [dict(m[0])]) for d, m in enc]
+        return enc, dec
+
+    (e1, d1), (e0, d0) = run(True), run(False)
+    for (b1, m1), (b0, m0), y1, y0 in zip(e1, e0, d1, d0):
+        assert b1 == b0 and m1 == m0
+        np.testing.assert_array_equal(y1, y0)
+
+
+def test_plugin_pageable_path_identical(monkeypatch):
+    """Larger one-tensor calls: x / planes straight from the caller's arrays
+    (OFL_PLUGIN_PAGEABLE=1, ofl_eden_*_host_x) give the same bytes, seeds and
+    decoded values as the default pinned-staging path."""
+    from openfl_amd.pipelines import eden_pipeline as E
+    sizes = [70000, 1 << 20, (1 << 21) + 5, 70000]
+    rng = np.random.default_rng(9)
+    xs = [rng.standard_normal(n).astype(np.float32) for n in sizes]
+
+    def run(pageable):
+        monkeypatch.setattr(E, "_PAGEABLE", pageable)
+        pipe = E.EdenPipeline(n_bits=8, device=DEV)
         enc = [pipe.forward(x) for x in xs]
         dec = [pipe.backward(d, [dict(m[0])]) for d, m in enc]
         return enc, dec

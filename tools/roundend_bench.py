@@ -10,7 +10,8 @@ seeds), new model = base + decoded delta.  Collaborator updates and the base
 model are resident in HBM; the new model is written to HBM.
 
 Prints one JSON line: value = model GiB per second of round-end work
-(fused, device-resident, no payload D2H); also: the same with the wire
+(fused, device-resident, no payload D2H); also: the unfused sequence
+(average kernel writes the delta, the encode reads it), the same with the wire
 payloads copied to the host, and the reference's call pattern (per tensor:
 host np.average, TensorCodec.generate_delta / compress / decompress /
 apply_delta with the openfl_amd EdenPipeline) on the same data.
@@ -75,6 +76,16 @@ def main():
     t_pay = timed(lambda: re.run(collabs, w, base, payloads=True, out=out), max(1, args.steps // 2), 1)
 
     also = {"fused_with_payload_d2h": {"value": round(nbytes / t_pay / 2 ** 30, 3), "ms_per_step": round(1e3 * t_pay, 3)}}
+    # A/B: the delta arena written by the averaging kernel and read by the
+    # encode (RoundEnd(fused=False)), interleaved with the fused run
+    re_u = RoundEnd(pipe, shapes, dev, fused=False)
+    t_u, t_f = [], []
+    for _ in range(3):
+        t_u.append(timed(lambda: re_u.run(collabs, w, base, payloads=False, out=out), args.steps, 1))
+        t_f.append(timed(lambda: re.run(collabs, w, base, payloads=False, out=out), args.steps, 1))
+    also["unfused_average_then_encode"] = {"value": round(nbytes / min(t_u) / 2 ** 30, 3),
+                                           "ms_per_step": round(1e3 * min(t_u), 3),
+                                           "fused_same_interleave_ms": round(1e3 * min(t_f), 3)}
     if args.host_steps > 0:
         from openfl_amd.tensor_codec import TensorCodec, TensorKey
         tc = TensorCodec(pipe)
