@@ -100,6 +100,11 @@ int ofl_eden_plan_num_waves(ofl_eden_plan_t plan);
  * prefetching ones; env OFL_EDEN_ROW2 / OFL_EDEN_ROW2_TPC override the auto
  * rule), 0 always persistent, 1 always two blocks per CU. */
 int ofl_eden_plan_set_row2(ofl_eden_plan_t plan, int mode);
+/* Launches of the tiny (<= 2^10) and small (2^11..2^15) slices (no reference
+ * counterpart; outputs bit-identical either way): 1 one small-set launch of
+ * 1024-thread workgroups for all of them, 0 one launch per size class, -1 the
+ * default (1; env OFL_EDEN_SSET=0 selects 0).  Before the first encode/decode. */
+int ofl_eden_plan_set_sset(ofl_eden_plan_t plan, int mode);
 
 /* Totals: slices (= length of the scales array), planes-arena bytes,
  * workspace bytes needed by encode and decode. */
@@ -161,6 +166,15 @@ int ofl_eden_decode_add(ofl_eden_plan_t plan, const uint8_t* planes_arena, const
  * slice) at off_scales >= planes bytes.  Decode input block: planes arena at
  * 0, scales at off_scales, seeds at off_seeds; output block: the y arena
  * (out_bytes <= 4 * arena length copied back). */
+/* Zero-copy variants for plans of tiny / small slices only (every slice <=
+ * 2^15 elements; else OFL_EINVAL): the same blocks, but in_host / out_host /
+ * y_host are MAPPED pinned host memory (hipHostMalloc, torch pin_memory) that
+ * the single launch reads and writes directly -- no DMA copies; y_host holds
+ * 4 * arena bytes.  Synchronous (stream synchronised).  Not mapped -> OFL_EINVAL. */
+int ofl_eden_encode_mapped(ofl_eden_plan_t plan, const void* in_host, size_t off_seeds, void* out_host,
+                           size_t off_scales, void* ws, size_t ws_bytes, void* stream);
+int ofl_eden_decode_mapped(ofl_eden_plan_t plan, const void* in_host, size_t off_scales, size_t off_seeds,
+                           void* y_host, void* ws, size_t ws_bytes, void* stream);
 int ofl_eden_encode_host(ofl_eden_plan_t plan, const void* in_host, void* in_dev, size_t in_bytes, size_t off_seeds,
                          void* out_dev, void* out_host, size_t out_bytes, size_t off_scales, void* ws, size_t ws_bytes,
                          void* stream);

@@ -37,11 +37,14 @@ def slice_plan(n):
 class EdenPlan:
     """Layout + launch plan for one batch shape (list of numels, optional dims)."""
 
-    def __init__(self, numels, n_bits=8, dims=None, elem_offsets=None, wave_mib=None, streams=None, row2=None):
+    def __init__(self, numels, n_bits=8, dims=None, elem_offsets=None, wave_mib=None, streams=None, row2=None,
+                 sset=None):
         """wave_mib / streams: large-slice schedule (ofl_eden_plan_set_schedule;
         None keeps the library default); row2: row-pass kernels
         (ofl_eden_plan_set_row2: None/-1 auto, 0 persistent, 1 two blocks per
-        CU).  Outputs do not depend on either."""
+        CU); sset: tiny / small slices in one launch (ofl_eden_plan_set_sset:
+        None/-1 default, 0 one launch per size class, 1 one launch).  Outputs
+        do not depend on any of them."""
         L = _lib.lib()
         self.n_bits = int(n_bits)
         self.numels = [int(n) for n in numels]
@@ -73,6 +76,8 @@ class EdenPlan:
                                                     0 if streams is None else int(streams)))
         if row2 is not None:
             _lib.check(L.ofl_eden_plan_set_row2(h, int(row2)))
+        if sset is not None:
+            _lib.check(L.ofl_eden_plan_set_sset(h, int(sset)))
         self.n_waves = int(L.ofl_eden_plan_num_waves(h))
         wb, ns = ctypes.c_int64(), ctypes.c_int()
         _lib.check(L.ofl_eden_plan_get_schedule(h, ctypes.byref(wb), ctypes.byref(ns)))

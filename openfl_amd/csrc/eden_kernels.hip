@@ -255,7 +255,7 @@ DEVI float wave_sum(float v) {
 template <int NT>
 DEVI float block_sum(float v, float* red) {
     v = wave_sum(v);
-    const int w = threadIdx.x >> 6;
+    const int w = (threadIdx.x >> 6) & (NT / 64 - 1);  // within an NT-thread (sub-)block
     if ((threadIdx.x & 63) == 0) red[w] = v;
     __syncthreads();
     float t = 0.f;
@@ -395,6 +395,21 @@ DEVI void pin_group(const float* v, float (&vg)[8]) {
         vg[t] = v[t];
         asm volatile("" : "+v"(vg[t]));
     }
+}
+
+// Sum of squares of a thread's values, each square rounded, then added in
+// register order: contraction off, so every kernel variant (and context the
+// body is inlined into) rounds the same way -- bit-identical partials.
+template <int N>
+DEVI float sum_sq(const float (&v)[N], float mul = 1.0f) {
+#pragma clang fp contract(off)
+    float ss = 0.f;
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+        const float y = v[r] * mul;
+        ss += y * y;
+    }
+    return ss;
 }
 
 // 32 contiguous values -> 8 plane words of 32 bits (bit t = element t)
@@ -663,26 +678,27 @@ template <int P_LOG> struct SmallSmem {
 };
 
 // ===========================================================================
-// Small slices (2^11 <= P <= 2^15): one workgroup per slice, whole codec.
+// Small slices (2^11 <= P <= 2^15): one NT = 2^(P-5)-thread group per slice,
+// whole codec.  The bodies run either as their own workgroup (k_enc_small /
+// k_dec_small) or as one of 2^(15-P) sub-blocks of a 1024-thread workgroup of
+// the small-set kernels below (every sub-block runs the same P, so they meet
+// the same barriers; tid is the thread within the sub-block, sm its LDS).
+// st = false: a padding sub-block -- computes, stores nothing.
 // ===========================================================================
 template <int P_LOG>
-__global__ __launch_bounds__(1 << (P_LOG - 5)) void k_enc_small(KArgs a) {
+DEVI void enc_small_body(const KArgs& a, int si, uint32_t tid, unsigned char* sm, const QTab* qt, float* red,
+                         bool st) {
     using S = SmallSet<P_LOG>;
     using SM = SmallSmem<P_LOG>;
     constexpr int NT = SM::NT, NS = SM::NS;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    float* s = reinterpret_cast<float*>(smem);
-    uint8_t* tab1 = smem + SM::data;
+    float* s = reinterpret_cast<float*>(sm);
+    uint8_t* tab1 = sm + SM::data;
     uint8_t* tab2 = tab1 + NS;
-    QTab* qt = reinterpret_cast<QTab*>(smem + SM::data + SM::tabs);
-    float* red = reinterpret_cast<float*>(qt + 1);
 
-    const SliceDesc D = a.d[a.list[blockIdx.x]];
-    const uint32_t tid = threadIdx.x;
+    const SliceDesc D = a.d[si];
     const uint32_t seed = a.seeds[D.tensor];
     const uint32_t b1 = seed_b(seed), b2 = seed_b(seed + 1u);
     for (int j = tid; j < NS; j += NT) { tab1[j] = (uint8_t)rd_byte(j, b1); tab2[j] = (uint8_t)rd_byte(j, b2); }
-    load_qtable<NT>(qt, a.nbits);
 
     float v[32];
     const float* x = a.xin + D.x_off;
@@ -706,9 +722,7 @@ __global__ __launch_bounds__(1 << (P_LOG - 5)) void k_enc_small(KArgs a) {
     stages<S::L5, S::F2e>(v);
 
     const float ysc = pow2i(-((P_LOG + 1) / 2));
-    float ss = 0.f;
-#pragma unroll
-    for (int r = 0; r < 32; ++r) { const float y = v[r] * ysc; ss += y * y; }
+    float ss = sum_sq(v, ysc);
     ss = block_sum<NT>(ss, red);
     const float nu = sqrtf(ss);
     const bool pos = nu > 0.0f;
@@ -724,27 +738,24 @@ __global__ __launch_bounds__(1 << (P_LOG - 5)) void k_enc_small(KArgs a) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) w[i] = 0;
     }
+    if (!st) return;
     store_planes(a.pout + D.pl_off, LT<S::L5>::base(tid), D.pl_stride, a.nbits, w);
     if (tid == 0) a.scales[D.scale_idx] = scale;
 }
 
 template <int P_LOG>
-__global__ __launch_bounds__(1 << (P_LOG - 5)) void k_dec_small(KArgs a) {
+DEVI void dec_small_body(const KArgs& a, int si, uint32_t tid, unsigned char* sm, const float* cen, bool st) {
     using S = SmallSet<P_LOG>;
     using SM = SmallSmem<P_LOG>;
     constexpr int NT = SM::NT, NS = SM::NS;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    float* s = reinterpret_cast<float*>(smem);
-    uint8_t* tab1 = smem + SM::data;
+    float* s = reinterpret_cast<float*>(sm);
+    uint8_t* tab1 = sm + SM::data;
     uint8_t* tab2 = tab1 + NS;
-    float* cen = reinterpret_cast<float*>(smem + SM::data + SM::tabs);
 
-    const SliceDesc D = a.d[a.list[blockIdx.x]];
-    const uint32_t tid = threadIdx.x;
+    const SliceDesc D = a.d[si];
     const uint32_t seed = a.seeds[D.tensor];
     const uint32_t b1 = seed_b(seed), b2 = seed_b(seed + 1u);
     for (int j = tid; j < NS; j += NT) { tab1[j] = (uint8_t)rd_byte(j, b1); tab2[j] = (uint8_t)rd_byte(j, b2); }
-    for (int j = tid; j < 256; j += NT) cen[j] = g_centroids[a.nbits - 1][j];
     float v[32];
     {
         uint32_t w[8];
@@ -763,6 +774,7 @@ __global__ __launch_bounds__(1 << (P_LOG - 5)) void k_dec_small(KArgs a) {
     stages<S::L2, S::F1b>(v);
     exchange<S::L2, S::L1>(v, s, tid);
     stages<S::L1, S::F1a>(v);
+    if (!st) return;
     const float sc = a.scales_in[D.scale_idx];
     const uint32_t base = LT<S::L1>::base(tid);
     apply_signs_tab<S::L1>(v, base, tab1, P_LOG, pow2i(-((P_LOG + 1) / 2)));
@@ -783,14 +795,34 @@ __global__ __launch_bounds__(1 << (P_LOG - 5)) void k_dec_small(KArgs a) {
     for (int r = 0; r < 32; r += 4) store4(y, base | LT<S::L1>::off(r), D.ylen, &v[r]);
 }
 
+template <int P_LOG>
+__global__ __launch_bounds__(1 << (P_LOG - 5)) void k_enc_small(KArgs a) {
+    using SM = SmallSmem<P_LOG>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    QTab* qt = reinterpret_cast<QTab*>(smem + SM::data + SM::tabs);
+    load_qtable<SM::NT>(qt, a.nbits);
+    enc_small_body<P_LOG>(a, a.list[blockIdx.x], threadIdx.x, smem, qt, reinterpret_cast<float*>(qt + 1), true);
+}
+
+template <int P_LOG>
+__global__ __launch_bounds__(1 << (P_LOG - 5)) void k_dec_small(KArgs a) {
+    using SM = SmallSmem<P_LOG>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float* cen = reinterpret_cast<float*>(smem + SM::data + SM::tabs);
+    for (int j = threadIdx.x; j < 256; j += SM::NT) cen[j] = g_centroids[a.nbits - 1][j];
+    dec_small_body<P_LOG>(a, a.list[blockIdx.x], threadIdx.x, smem, cen, true);
+}
+
 // ===========================================================================
-// Tiny slices (P <= 2^10): one 256-thread workgroup per slice, LDS-resident
-// (latency-bound: more threads per slice shorten every stage).
+// Tiny slices (P <= 2^10): one 256-thread group per slice, LDS-resident
+// (latency-bound: more threads per slice shorten every stage).  As above, a
+// body runs as its own workgroup or as one of 4 sub-blocks (all of one p) of
+// a small-set workgroup.
 // ===========================================================================
 constexpr int kTinyNT = 256;
-DEVI void fwht_lds_generic(float* s, int P) {
+DEVI void fwht_lds_generic(float* s, int P, uint32_t tid) {
     for (int h = 1; h < P; h <<= 1) {
-        for (int q = threadIdx.x; q < (P >> 1); q += kTinyNT) {
+        for (int q = tid; q < (P >> 1); q += kTinyNT) {
             const int i = ((q & ~(h - 1)) << 1) | (q & (h - 1));
             const float a = s[i], b = s[i + h];
             s[i] = a + b;
@@ -799,34 +831,37 @@ DEVI void fwht_lds_generic(float* s, int P) {
         __syncthreads();
     }
 }
+struct TinySmem { float s[1024]; unsigned char bins[1024]; };
 
-__global__ __launch_bounds__(kTinyNT) void k_enc_tiny(KArgs a) {
-    __shared__ float s[1024];
-    __shared__ unsigned char bins[1024];
-    __shared__ QTab qt[1];
-    __shared__ float red[kTinyNT / 64];
-    const SliceDesc D = a.d[a.list[blockIdx.x]];
+DEVI void enc_tiny_body(const KArgs& a, int si, uint32_t tid, TinySmem* ts, const QTab* qt, float* red, bool st) {
+    float* s = ts->s;
+    unsigned char* bins = ts->bins;
+    const SliceDesc D = a.d[si];
     const int p = D.logp, P = 1 << p;
     const uint32_t seed = a.seeds[D.tensor];
     const uint32_t b1 = seed_b(seed), b2 = seed_b(seed + 1u);
-    load_qtable<kTinyNT>(qt, a.nbits);
     const float* x = a.xin + D.x_off;
-    for (int e = threadIdx.x; e < P; e += kTinyNT) s[e] = sgn_elem(e < D.len ? x[e] : 0.0f, e, p, b1);
+    for (int e = tid; e < P; e += kTinyNT) s[e] = sgn_elem(e < D.len ? x[e] : 0.0f, e, p, b1);
     __syncthreads();
-    fwht_lds_generic(s, P);
+    fwht_lds_generic(s, P, tid);
     const float m2 = pow2i(-(p / 2));
-    for (int e = threadIdx.x; e < P; e += kTinyNT) s[e] = sgn_elem(s[e] * m2, e, p, b2);
+    for (int e = tid; e < P; e += kTinyNT) s[e] = sgn_elem(s[e] * m2, e, p, b2);
     __syncthreads();
-    fwht_lds_generic(s, P);
+    fwht_lds_generic(s, P, tid);
     const float ysc = pow2i(-((p + 1) / 2));
     float ss = 0.f;
-    for (int e = threadIdx.x; e < P; e += kTinyNT) { const float y = s[e] * ysc; s[e] = y; ss += y * y; }
+    for (int e = tid; e < P; e += kTinyNT) {
+#pragma clang fp contract(off)
+        const float y = s[e] * ysc;
+        s[e] = y;
+        ss += y * y;
+    }
     ss = block_sum<kTinyNT>(ss, red);
     const float nu = sqrtf(ss);
     const bool pos = nu > 0.0f;
     const float zm64 = 64.0f * (sqrtf((float)P) / nu);
     float dot = 0.f;
-    for (int e = threadIdx.x; e < P; e += kTinyNT) {
+    for (int e = tid; e < P; e += kTinyNT) {
         float c;
         const int b = pos ? quant(s[e] * zm64, qt, c) : 0;
         if (pos) dot += c * s[e];
@@ -837,44 +872,136 @@ __global__ __launch_bounds__(kTinyNT) void k_enc_tiny(KArgs a) {
     const bool zero = !pos || isnan(scale);
     if (zero) scale = 0.0f;
     __syncthreads();
+    if (!st) return;
     uint8_t* pl = a.pout + D.pl_off;
-    for (int q = threadIdx.x; q < (P >> 3) * a.nbits; q += kTinyNT) {
+    for (int q = tid; q < (P >> 3) * a.nbits; q += kTinyNT) {
         const int i = q / (P >> 3), j = q % (P >> 3);
         uint32_t by = 0;
         if (!zero)
             for (int t = 0; t < 8; ++t) by |= ((uint32_t)(bins[8 * j + t] >> i) & 1u) << t;
         pl[(int64_t)i * D.pl_stride + j] = (uint8_t)by;
     }
-    if (threadIdx.x == 0) a.scales[D.scale_idx] = scale;
+    if (tid == 0) a.scales[D.scale_idx] = scale;
 }
 
-__global__ __launch_bounds__(kTinyNT) void k_dec_tiny(KArgs a) {
-    __shared__ float s[1024];
-    const SliceDesc D = a.d[a.list[blockIdx.x]];
+DEVI void dec_tiny_body(const KArgs& a, int si, uint32_t tid, float* s, bool st) {
+    const SliceDesc D = a.d[si];
     const int p = D.logp, P = 1 << p;
     const uint32_t seed = a.seeds[D.tensor];
     const uint32_t b1 = seed_b(seed), b2 = seed_b(seed + 1u);
     const uint8_t* pl = a.pin + D.pl_off;
-    for (int e = threadIdx.x; e < P; e += kTinyNT) {
+    for (int e = tid; e < P; e += kTinyNT) {
         int b = 0;
         for (int i = 0; i < a.nbits; ++i) b |= ((pl[(int64_t)i * D.pl_stride + (e >> 3)] >> (e & 7)) & 1) << i;
         s[e] = g_centroids[a.nbits - 1][b];
     }
     __syncthreads();
-    fwht_lds_generic(s, P);
+    fwht_lds_generic(s, P, tid);
     const float m2 = pow2i(-(p / 2));
-    for (int e = threadIdx.x; e < P; e += kTinyNT) s[e] = sgn_elem(s[e] * m2, e, p, b2);
+    for (int e = tid; e < P; e += kTinyNT) s[e] = sgn_elem(s[e] * m2, e, p, b2);
     __syncthreads();
-    fwht_lds_generic(s, P);
+    fwht_lds_generic(s, P, tid);
+    if (!st) return;
     const float m1 = pow2i(-((p + 1) / 2));
     const float sc = a.scales_in[D.scale_idx];
     float* y = a.xout + D.y_off;
     const float* yb = a.yadd ? a.yadd + D.y_off : nullptr;
-    for (int e = threadIdx.x; e < P; e += kTinyNT)
+    for (int e = tid; e < P; e += kTinyNT)
         if (e < D.ylen) {
             const float d = sc * sgn_elem(s[e] * m1, e, p, b1);
             y[e] = yb ? add_rn(yb[e], d) : d;
         }
+}
+
+__global__ __launch_bounds__(kTinyNT) void k_enc_tiny(KArgs a) {
+    __shared__ TinySmem ts;
+    __shared__ QTab qt[1];
+    __shared__ float red[kTinyNT / 64];
+    load_qtable<kTinyNT>(qt, a.nbits);
+    enc_tiny_body(a, a.list[blockIdx.x], threadIdx.x, &ts, qt, red, true);
+}
+
+__global__ __launch_bounds__(kTinyNT) void k_dec_tiny(KArgs a) {
+    __shared__ float s[1024];
+    dec_tiny_body(a, a.list[blockIdx.x], threadIdx.x, s, true);
+}
+
+// ===========================================================================
+// Small-set kernels: every tiny and small slice of a call in ONE launch of
+// 1024-thread workgroups (instead of one latency-bound launch per size class
+// in a chain).  Workgroup b reads its group {P (0: tiny), list offset, count}
+// from a.list[3b..3b+2]; a group holds slices of one size: 2^(15-P) small
+// slices of 2^P elements, or 4 tiny slices of one p.  Sub-blocks past count
+// recompute the group's last slice without storing it.
+// ===========================================================================
+constexpr int kSetNT = 1024;
+template <int P_LOG> struct SetSmem {
+    static constexpr int SUB = kSetNT >> (P_LOG - 5);
+    static constexpr size_t per = (SmallSmem<P_LOG>::data + SmallSmem<P_LOG>::tabs + 15) & ~(size_t)15;
+    static constexpr size_t body = SUB * per;
+};
+constexpr size_t cmax(size_t a, size_t b) { return a > b ? a : b; }
+constexpr size_t kSetBody = cmax(cmax(cmax(SetSmem<11>::body, SetSmem<12>::body), cmax(SetSmem<13>::body, SetSmem<14>::body)),
+                                 cmax(SetSmem<15>::body, (kSetNT / kTinyNT) * sizeof(TinySmem)));
+constexpr size_t kSetSmemEnc = kSetBody + sizeof(QTab) + sizeof(float) * (kSetNT / 64);
+constexpr size_t kSetSmemDec = kSetBody + sizeof(float) * 256;
+
+template <int P_LOG>
+DEVI void enc_set_group(const KArgs& a, const int32_t* sl, int cnt, unsigned char* sm, const QTab* qt, float* red) {
+    constexpr int NT = SmallSmem<P_LOG>::NT;
+    const uint32_t sub = threadIdx.x / NT;
+    enc_small_body<P_LOG>(a, sl[min((int)sub, cnt - 1)], threadIdx.x % NT, sm + sub * SetSmem<P_LOG>::per, qt,
+                          red + sub * (NT / 64), (int)sub < cnt);
+}
+template <int P_LOG>
+DEVI void dec_set_group(const KArgs& a, const int32_t* sl, int cnt, unsigned char* sm, const float* cen) {
+    constexpr int NT = SmallSmem<P_LOG>::NT;
+    const uint32_t sub = threadIdx.x / NT;
+    dec_small_body<P_LOG>(a, sl[min((int)sub, cnt - 1)], threadIdx.x % NT, sm + sub * SetSmem<P_LOG>::per, cen,
+                          (int)sub < cnt);
+}
+
+__global__ __launch_bounds__(kSetNT) void k_enc_sset(KArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    QTab* qt = reinterpret_cast<QTab*>(smem + kSetBody);
+    float* red = reinterpret_cast<float*>(qt + 1);
+    const int32_t* g = a.list + 3 * blockIdx.x;
+    const int P = g[0], cnt = g[2];
+    const int32_t* sl = a.list + g[1];
+    load_qtable<kSetNT>(qt, a.nbits);  // published by the bodies' first barrier
+    switch (P) {
+    case 11: enc_set_group<11>(a, sl, cnt, smem, qt, red); break;
+    case 12: enc_set_group<12>(a, sl, cnt, smem, qt, red); break;
+    case 13: enc_set_group<13>(a, sl, cnt, smem, qt, red); break;
+    case 14: enc_set_group<14>(a, sl, cnt, smem, qt, red); break;
+    case 15: enc_set_group<15>(a, sl, cnt, smem, qt, red); break;
+    default: {
+        const uint32_t sub = threadIdx.x / kTinyNT;
+        enc_tiny_body(a, sl[min((int)sub, cnt - 1)], threadIdx.x % kTinyNT, reinterpret_cast<TinySmem*>(smem) + sub,
+                      qt, red + sub * (kTinyNT / 64), (int)sub < cnt);
+    }
+    }
+}
+
+__global__ __launch_bounds__(kSetNT) void k_dec_sset(KArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float* cen = reinterpret_cast<float*>(smem + kSetBody);
+    const int32_t* g = a.list + 3 * blockIdx.x;
+    const int P = g[0], cnt = g[2];
+    const int32_t* sl = a.list + g[1];
+    for (int j = threadIdx.x; j < 256; j += kSetNT) cen[j] = g_centroids[a.nbits - 1][j];
+    switch (P) {
+    case 11: dec_set_group<11>(a, sl, cnt, smem, cen); break;
+    case 12: dec_set_group<12>(a, sl, cnt, smem, cen); break;
+    case 13: dec_set_group<13>(a, sl, cnt, smem, cen); break;
+    case 14: dec_set_group<14>(a, sl, cnt, smem, cen); break;
+    case 15: dec_set_group<15>(a, sl, cnt, smem, cen); break;
+    default: {
+        const uint32_t sub = threadIdx.x / kTinyNT;
+        dec_tiny_body(a, sl[min((int)sub, cnt - 1)], threadIdx.x % kTinyNT,
+                      reinterpret_cast<TinySmem*>(smem)[sub].s, (int)sub < cnt);
+    }
+    }
 }
 
 // ===========================================================================
@@ -1176,9 +1303,7 @@ __global__ __launch_bounds__(kRowNT) void k_enc_rowA(KArgs a) {
         fetch_x(a, udesc(a.d, sn), tln, more, base1, nx);
         fix_x(a, D, tile, base1, v);
         const uint32_t b1 = seed_b(sld(a.seeds, D.tensor));
-        float ss = 0.f;
-#pragma unroll
-        for (int r = 0; r < 64; ++r) ss += v[r] * v[r];
+        float ss = sum_sq(v);
         apply_signs_direct<RS::L1>(v, tile << kRowLog, base1, D.logp, b1, 1.0f);
         stages<RS::L1, RS::F1a>(v);
         exchange<RS::L1, RS::L2>(v, s, tid);
@@ -1976,9 +2101,7 @@ __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowA2(KArgs a) {
                              "+v"(v[r + 5]), "+v"(v[r + 6]), "+v"(v[r + 7]));
         }
         const uint32_t b1 = seed_b(sld(a.seeds, D.tensor));
-        float ss = 0.f;
-#pragma unroll
-        for (int r = 0; r < 64; ++r) ss += v[r] * v[r];
+        float ss = sum_sq(v);
         // the sum is taken here, not sunk past the sign flips (which would keep
         // the 64 unflipped values live through the butterflies and spill them)
         asm volatile("" : "+v"(ss));
@@ -2107,7 +2230,7 @@ struct Launch {
     int64_t bytes_moved = 0;  // fp32/plane bytes this launch reads + writes (intermediates included)
     int64_t bytes_alg = 0;    // its share of the SURVEY 8(d) algorithmic bytes (x/y fp32 + planes only)
 };
-enum Kind { K_TINY, K_SMALL, K_ROWA, K_ROWC, K_COL, K_FINAL, K_COLM };
+enum Kind { K_TINY, K_SMALL, K_ROWA, K_ROWC, K_COL, K_FINAL, K_COLM, K_SSET };
 
 }  // namespace
 
@@ -2129,6 +2252,7 @@ struct ofl_eden_plan {
     int nstreams = 1;           // 2: waves alternate between the caller's and a side stream
     int nwaves = 0;
     int row2 = -1;              // row launches on the two-blocks-per-CU kernels: -1 auto, 0 never, 1 always
+    int sset = -1;              // tiny / small slices in one small-set launch: -1 env default, 0 no, 1 yes
     std::vector<Launch> enc, dec;
     std::vector<int32_t> ints;  // launch lists and tile prefixes (host copy)
     // profiling: events around every launch of every call while enabled
@@ -2262,6 +2386,12 @@ bool use_small_split() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_SMALL2"); return s && s[0] == '1'; }();
     return on;
 }
+// every tiny / small slice in one small-set launch (k_enc_sset / k_dec_sset)
+// instead of a chain of one launch per size class (OFL_EDEN_SSET=0, A/B)
+bool use_sset() {
+    static const bool on = [] { const char* s = getenv("OFL_EDEN_SSET"); return !(s && s[0] == '0'); }();
+    return on;
+}
 // tiny / small slices on a third stream when the waves use two
 bool use_small_stream() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_SMALLSTREAM"); return !(s && s[0] == '0'); }();
@@ -2303,6 +2433,8 @@ hipError_t set_all_attrs() {
     if ((e = set_small_attr<13>()) != hipSuccess) return e;
     if ((e = set_small_attr<14>()) != hipSuccess) return e;
     if ((e = set_small_attr<15>()) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_enc_sset, ofl::kSetSmemEnc)) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_dec_sset, ofl::kSetSmemDec)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_enc_rowA, ofl::kRowSmemA)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_enc_rowC, ofl::kRowSmemQ)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_enc_rowC2<true>, ofl::kRowC2Smem)) != hipSuccess) return e;
@@ -2379,6 +2511,10 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
         case K_TINY:
             e = enc ? launch(ofl::k_enc_tiny, l.blocks, ofl::kTinyNT, 0, st, a)
                     : launch(ofl::k_dec_tiny, l.blocks, ofl::kTinyNT, 0, st, a);
+            break;
+        case K_SSET:
+            e = enc ? launch(ofl::k_enc_sset, l.blocks, ofl::kSetNT, ofl::kSetSmemEnc, st, a)
+                    : launch(ofl::k_dec_sset, l.blocks, ofl::kSetNT, ofl::kSetSmemDec, st, a);
             break;
         case K_SMALL: {
             const int p = l.param;
@@ -2492,6 +2628,7 @@ std::string launch_name(const Launch& l, bool enc, int ncu, int row2) {
     const char* d = enc ? "enc" : "dec";
     switch (l.kind) {
     case K_TINY: return std::string("ofl::k_") + d + "_tiny";
+    case K_SSET: return std::string("ofl::k_") + d + "_sset";
     case K_SMALL: return std::string("ofl::k_") + d + "_small<" + std::to_string(l.param) + ">";
     case K_ROWA: return std::string("ofl::k_") + d + (use_row2(l.blocks, ncu, row2) ? "_rowA2" : "_rowA");
     case K_ROWC:
@@ -2533,12 +2670,39 @@ void build_schedule(ofl_eden_plan* pl) {
         return o;
     };
     std::vector<Launch> common;
-    if (!pl->tiny.empty())
-        common.push_back({K_TINY, 0, 0, 0, add_list(pl->tiny), -1, (int)pl->tiny.size(), (int64_t)pl->tiny.size()});
-    for (int k = 0; k < 5; ++k)
-        if (!pl->small[k].empty())
-            common.push_back({K_SMALL, 11 + k, 0, 0, add_list(pl->small[k]), -1, (int)pl->small[k].size(),
-                              (int64_t)pl->small[k].size()});
+    if (pl->sset >= 0 ? pl->sset == 1 : use_sset()) {
+        // one small-set launch: groups of one size, largest first; table of
+        // {P (0: tiny), slice-list offset (from the table), count} per block
+        std::vector<std::array<int32_t, 3>> groups;
+        std::vector<int32_t> ids;
+        auto add_groups = [&](int P, const std::vector<int32_t>& sl, int per) {
+            for (size_t i = 0; i < sl.size(); i += per) {
+                const int c = (int)std::min<size_t>(per, sl.size() - i);
+                groups.push_back({P, (int32_t)ids.size(), c});
+                ids.insert(ids.end(), sl.begin() + i, sl.begin() + i + c);
+            }
+        };
+        for (int k = 4; k >= 0; --k) add_groups(11 + k, pl->small[k], ofl::kSetNT >> (6 + k));
+        for (int p = 10; p >= 0; --p) {  // tiny slices: groups of one p (same barrier count)
+            std::vector<int32_t> sl;
+            for (int32_t si : pl->tiny) if (pl->slices[si].logp == p) sl.push_back(si);
+            add_groups(0, sl, ofl::kSetNT / ofl::kTinyNT);
+        }
+        if (!groups.empty()) {
+            const int o = (int)ints.size();
+            const int nt = 3 * (int)groups.size();
+            for (auto& g : groups) { ints.push_back(g[0]); ints.push_back(g[1] + nt); ints.push_back(g[2]); }
+            ints.insert(ints.end(), ids.begin(), ids.end());
+            common.push_back({K_SSET, 0, 0, 0, o, -1, (int)groups.size(), (int64_t)groups.size()});
+        }
+    } else {
+        if (!pl->tiny.empty())
+            common.push_back({K_TINY, 0, 0, 0, add_list(pl->tiny), -1, (int)pl->tiny.size(), (int64_t)pl->tiny.size()});
+        for (int k = 0; k < 5; ++k)
+            if (!pl->small[k].empty())
+                common.push_back({K_SMALL, 11 + k, 0, 0, add_list(pl->small[k]), -1, (int)pl->small[k].size(),
+                                  (int64_t)pl->small[k].size()});
+    }
     const std::vector<int32_t>& large = pl->large;
     for (auto& D : pl->slices) D.perm = 0;
     std::vector<std::vector<int32_t>> waves;
@@ -2753,6 +2917,16 @@ void build_schedule(ofl_eden_plan* pl) {
         for (Launch& l : enc ? pl->enc : pl->dec) {
             if (l.kind == K_COLM) continue;  // counted when built (its list is a group table)
             int64_t mv = 0, al = 0;
+            if (l.kind == K_SSET) {  // group table {P, offset, count}, then the slice ids
+                for (int g = 0; g < l.count; ++g)
+                    for (int i = 0; i < ints[l.list_off + 3 * g + 2]; ++i) {
+                        const ofl::SliceDesc& D = pl->slices[ints[l.list_off + ints[l.list_off + 3 * g + 1] + i]];
+                        const int64_t pb = n_bits * (1ll << D.logp) / 8;
+                        mv += enc ? 4 * D.len + pb : pb + 4 * D.ylen;
+                    }
+                l.bytes_moved = l.bytes_alg = mv;
+                continue;
+            }
             for (int i = 0; i < l.count; ++i) {
                 const ofl::SliceDesc& D = pl->slices[ints[l.list_off + i]];
                 const int64_t P = 1ll << D.logp, pb = n_bits * P / 8;
@@ -2976,6 +3150,16 @@ int ofl_eden_plan_set_row2(ofl_eden_plan_t pl, int mode) {
     return OFL_OK;
 }
 
+int ofl_eden_plan_set_sset(ofl_eden_plan_t pl, int mode) {
+    if (!pl) return fail(OFL_EINVAL, "null plan");
+    if (mode < -1 || mode > 1) return fail(OFL_EINVAL, "sset mode must be -1 (default), 0 or 1");
+    std::lock_guard<std::mutex> g(pl->mu);
+    if (pl->uploaded) return fail(OFL_EINVAL, "sset must be set before the plan's first encode/decode");
+    pl->sset = mode;
+    build_schedule(pl);
+    return OFL_OK;
+}
+
 int ofl_eden_plan_get_schedule(ofl_eden_plan_t pl, int64_t* wave_bytes, int* streams) {
     if (!pl) return fail(OFL_EINVAL, "null plan");
     if (wave_bytes) *wave_bytes = pl->wave_bytes;
@@ -3115,6 +3299,56 @@ int ofl_eden_decode_host(ofl_eden_plan_t pl, const void* in_host, void* in_dev, 
                                  stream))
         return rc;
     if (out_bytes) HIP_TRY(hipMemcpyAsync(out_host, out_dev, out_bytes, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return OFL_OK;
+}
+
+// Zero-copy one-tensor calls: the kernels read and write mapped pinned host
+// memory directly (no DMA copies): for plans of tiny / small slices only,
+// whose single launch moves a few KiB across the link.
+static int mapped_ptr(void* h, void** d) {
+    if (hipHostGetDevicePointer(d, h, 0) != hipSuccess || !*d) {
+        (void)hipGetLastError();
+        return fail(OFL_EINVAL, "mapped call: buffer is not mapped pinned host memory (hipHostMalloc / pin_memory)");
+    }
+    return OFL_OK;
+}
+
+int ofl_eden_encode_mapped(ofl_eden_plan_t pl, const void* in_host, size_t off_seeds, void* out_host,
+                           size_t off_scales, void* ws, size_t ws_bytes, void* stream) {
+    if (!pl || !in_host || !out_host) return fail(OFL_EINVAL, "encode_mapped: null argument");
+    if (!pl->large.empty()) return fail(OFL_EINVAL, "encode_mapped: plans of tiny / small slices (<= 2^15) only");
+    if (off_seeds < 4 * (size_t)pl->arena || off_scales < (size_t)pl->planes_bytes)
+        return fail(OFL_EINVAL, "encode_mapped: block layout does not fit the plan");
+    void *i = nullptr, *o = nullptr;
+    if (int rc = mapped_ptr(const_cast<void*>(in_host), &i)) return rc;
+    if (int rc = mapped_ptr(out_host, &o)) return rc;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    char* oc = static_cast<char*>(o);
+    const char* ic = static_cast<const char*>(i);
+    if (int rc = ofl_eden_encode(pl, reinterpret_cast<const float*>(ic), reinterpret_cast<const uint32_t*>(ic + off_seeds),
+                                 reinterpret_cast<uint8_t*>(oc), reinterpret_cast<float*>(oc + off_scales), ws, ws_bytes,
+                                 stream))
+        return rc;
+    HIP_TRY(hipStreamSynchronize(st));
+    return OFL_OK;
+}
+
+int ofl_eden_decode_mapped(ofl_eden_plan_t pl, const void* in_host, size_t off_scales, size_t off_seeds, void* y_host,
+                           void* ws, size_t ws_bytes, void* stream) {
+    if (!pl || !in_host || !y_host) return fail(OFL_EINVAL, "decode_mapped: null argument");
+    if (!pl->large.empty()) return fail(OFL_EINVAL, "decode_mapped: plans of tiny / small slices (<= 2^15) only");
+    if (off_scales < (size_t)pl->planes_bytes || off_seeds < off_scales + 4 * pl->slices.size())
+        return fail(OFL_EINVAL, "decode_mapped: block layout does not fit the plan");
+    void *i = nullptr, *y = nullptr;
+    if (int rc = mapped_ptr(const_cast<void*>(in_host), &i)) return rc;
+    if (int rc = mapped_ptr(y_host, &y)) return rc;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const char* ic = static_cast<const char*>(i);
+    if (int rc = ofl_eden_decode(pl, reinterpret_cast<const uint8_t*>(ic), reinterpret_cast<const uint32_t*>(ic + off_seeds),
+                                 reinterpret_cast<const float*>(ic + off_scales), static_cast<float*>(y), ws, ws_bytes,
+                                 stream))
+        return rc;
     HIP_TRY(hipStreamSynchronize(st));
     return OFL_OK;
 }

@@ -343,13 +343,17 @@ _USE_CTX = os.environ.get("OFL_PLUGIN_CTX", "1") != "0"
 # larger one-tensor calls: OFL_PLUGIN_PAGEABLE=1 moves x / planes straight
 # from the caller's arrays (ofl_eden_*_host_x) instead of via pinned staging
 _PAGEABLE = os.environ.get("OFL_PLUGIN_PAGEABLE", "0") == "1"
+# contexts whose slices are all <= 2^15: kernels on mapped pinned memory
+# (OFL_PLUGIN_MAPPED=0: H2D / D2H copies around the launch, A/B)
+_USE_MAPPED = os.environ.get("OFL_PLUGIN_MAPPED", "1") != "0"
 
 
 class _CallCtx:
     """One tensor shape's one-call encode or decode, prepared once per thread:
     the plan (single stream), pinned in/out blocks and device buffers of
     exactly its size, numpy views into the pinned blocks, and the native
-    call's argument list (ofl_eden_encode_host / ofl_eden_decode_host)."""
+    call's argument list (ofl_eden_encode_host / ofl_eden_decode_host, or
+    the zero-copy ofl_eden_encode_mapped / ofl_eden_decode_mapped)."""
 
     def __init__(self, plan, device, stream, enc, total_dim=0):
         self.plan = plan
@@ -357,6 +361,9 @@ class _CallCtx:
         self.dims = plan.dims[0]
         self.dev_index = device.index
         self.stream = stream
+        # slices of <= 2^15 only: one launch that reads / writes the pinned
+        # blocks directly (ofl_eden_*_mapped, no DMA copies)
+        self.mapped = _USE_MAPPED and all(d <= 1 << 15 for d in self.dims)
         ws = torch.empty(max(plan.ws_bytes, 256), dtype=torch.uint8, device=device)
         L = _lib.lib()
         if enc:
@@ -370,13 +377,21 @@ class _CallCtx:
             self.x_view = ia[:4 * plan.numels[0]].view(np.float32)
             self.seed_view = ia[off_seeds:off_seeds + 4].view(np.uint32)
             self.scales_view = oa[off_scales:off_scales + 4 * ns].view(np.float32)
-            idev = torch.empty(in_bytes, dtype=torch.uint8, device=device)
-            odev = torch.empty(out_bytes, dtype=torch.uint8, device=device)
+            idev = odev = None
+            if not self.mapped:
+                idev = torch.empty(in_bytes, dtype=torch.uint8, device=device)
+                odev = torch.empty(out_bytes, dtype=torch.uint8, device=device)
             self.in_ptr, self.out_ptr = ih.data_ptr(), oh.data_ptr()
-            self._fn = L.ofl_eden_encode_host
-            self._args = [plan.handle, ih.data_ptr(), idev.data_ptr(), in_bytes, off_seeds, odev.data_ptr(),
-                          oh.data_ptr(), out_bytes, off_scales, ws.data_ptr(), ws.numel(), stream.cuda_stream]
-            self._keep = (ih, oh, idev, odev, ws)
+            if self.mapped:
+                self._fn = L.ofl_eden_encode_mapped
+                self._args = [plan.handle, ih.data_ptr(), off_seeds, oh.data_ptr(), off_scales, ws.data_ptr(),
+                              ws.numel(), stream.cuda_stream]
+                self._keep = (ih, oh, ws)
+            else:
+                self._fn = L.ofl_eden_encode_host
+                self._args = [plan.handle, ih.data_ptr(), idev.data_ptr(), in_bytes, off_seeds, odev.data_ptr(),
+                              oh.data_ptr(), out_bytes, off_scales, ws.data_ptr(), ws.numel(), stream.cuda_stream]
+                self._keep = (ih, oh, idev, odev, ws)
         else:
             off_scales = _al256(self.pb)
             off_seeds = _al256(off_scales + 4 * ns)
@@ -386,14 +401,21 @@ class _CallCtx:
             self.planes_view = ia[:self.pb]
             self.scales_view = ia[off_scales:off_scales + 4 * ns].view(np.float32)
             self.seed_view = ia[off_seeds:off_seeds + 4].view(np.uint32)
-            idev = torch.empty(in_bytes, dtype=torch.uint8, device=device)
-            ydev = torch.empty(max(plan.arena_numel, 1), dtype=torch.float32, device=device)
-            yh = torch.empty(max(total_dim, 1), dtype=torch.float32).pin_memory()
+            yh = torch.empty(max(plan.arena_numel, 1), dtype=torch.float32).pin_memory()
             self.y_view = yh.numpy()[:total_dim]
-            self._fn = L.ofl_eden_decode_host
-            self._args = [plan.handle, ih.data_ptr(), idev.data_ptr(), in_bytes, off_scales, off_seeds, ydev.data_ptr(),
-                          yh.data_ptr(), 4 * total_dim, ws.data_ptr(), ws.numel(), stream.cuda_stream]
-            self._keep = (ih, idev, ydev, yh, ws)
+            if self.mapped:
+                self._fn = L.ofl_eden_decode_mapped
+                self._args = [plan.handle, ih.data_ptr(), off_scales, off_seeds, yh.data_ptr(), ws.data_ptr(),
+                              ws.numel(), stream.cuda_stream]
+                self._keep = (ih, yh, ws)
+            else:
+                idev = torch.empty(in_bytes, dtype=torch.uint8, device=device)
+                ydev = torch.empty(max(plan.arena_numel, 1), dtype=torch.float32, device=device)
+                self._fn = L.ofl_eden_decode_host
+                self._args = [plan.handle, ih.data_ptr(), idev.data_ptr(), in_bytes, off_scales, off_seeds,
+                              ydev.data_ptr(), yh.data_ptr(), 4 * total_dim, ws.data_ptr(), ws.numel(),
+                              stream.cuda_stream]
+                self._keep = (ih, idev, ydev, yh, ws)
 
     def run(self):
         if self.dev_index is not None and self.dev_index != torch.cuda.current_device():

@@ -585,24 +585,28 @@ def test_small_launch_split_bit_identical():
 def test_plugin_call_contexts_identical(monkeypatch):
     """Small one-tensor calls go through cached per-shape call contexts
     (eden_pipeline._CallCtx): bytes, scales, seeds and decoded values equal
-    the uncached path's, including repeated and interleaved shapes."""
+    the uncached path's, including repeated and interleaved shapes -- with
+    the zero-copy mapped calls (slices <= 2^15) and with DMA copies."""
     from openfl_amd.pipelines import eden_pipeline as E
-    sizes = [101, 777, 2048, 2049, 40000, 1 << 16, 777, 101]
+    sizes = [101, 777, 2048, 2049, 40000, 1 << 16, 777, 101, 32768, 32769, 5000]
     rng = np.random.default_rng(5)
     xs = [rng.standard_normal(n).astype(np.float32) for n in sizes]
 
-    def run(use):
+    def run(use, mapped):
         monkeypatch.setattr(E, "_USE_CTX", use)
+        monkeypatch.setattr(E, "_USE_MAPPED", mapped)
         pipe = E.EdenPipeline(n_bits=8, device=DEV)
         np.random.seed(11)
         enc = [pipe.forward(x) for x in xs]
         dec = [pipe.backward(d, [dict(m[0])]) for d, m in enc]
         return enc, dec
 
-    (e1, d1), (e0, d0) = run(True), run(False)
-    for (b1, m1), (b0, m0), y1, y0 in zip(e1, e0, d1, d0):
-        assert b1 == b0 and m1 == m0
-        np.testing.assert_array_equal(y1, y0)
+    (e0, d0) = run(False, False)
+    for use, mapped in ((True, True), (True, False)):
+        e1, d1 = run(use, mapped)
+        for (b1, m1), (b0, m0), y1, y0 in zip(e1, e0, d1, d0):
+            assert b1 == b0 and m1 == m0
+            np.testing.assert_array_equal(y1, y0)
 
 
 def test_plugin_pageable_path_identical(monkeypatch):
@@ -617,6 +621,7 @@ def test_plugin_pageable_path_identical(monkeypatch):
     def run(pageable):
         monkeypatch.setattr(E, "_PAGEABLE", pageable)
         pipe = E.EdenPipeline(n_bits=8, device=DEV)
+        np.random.seed(13)
         enc = [pipe.forward(x) for x in xs]
         dec = [pipe.backward(d, [dict(m[0])]) for d, m in enc]
         return enc, dec
@@ -625,3 +630,35 @@ def test_plugin_pageable_path_identical(monkeypatch):
     for (b1, m1), (b0, m0), y1, y0 in zip(e1, e0, d1, d0):
         assert b1 == b0 and m1 == m0
         np.testing.assert_array_equal(y1, y0)
+
+
+@pytest.mark.parametrize("nbits", [1, 4, 8])
+def test_small_set_bit_identical(nbits):
+    """All tiny / small slices in one small-set launch (sset=1: 2^(15-P)
+    slices of 2^P per 1024-thread workgroup, 4 tiny slices of one p, padding
+    sub-blocks that store nothing) vs one launch per size class (sset=0):
+    planes, scales, decoded values and the fused apply_delta are identical."""
+    from openfl_amd.codec import EdenPlan
+    rng = np.random.default_rng(nbits)
+    numels = ([int(v) for v in rng.integers(9, 1024, 23)] + [2048] * 17 + [3000, 4096, 4100] * 3 + [8192] * 3 +
+              [9000, 16384, 16385, 20000] + [32768] * 3 + [1 << 16, (1 << 17) + 7])
+    rng.shuffle(numels)
+    outs = []
+    for sset in (0, 1):
+        plan = EdenPlan(numels, nbits, sset=sset)
+        g = torch.Generator(device=DEV).manual_seed(5)
+        x = torch.empty(plan.arena_numel, device=DEV).normal_(0, 0.05, generator=g)
+        base = torch.empty(plan.arena_numel, device=DEV).normal_(0, 1.0, generator=g)
+        seeds = torch.arange(3, 3 + len(numels), dtype=torch.int32, device=DEV)
+        ws = torch.empty(max(plan.ws_bytes, 256), dtype=torch.uint8, device=DEV)
+        p = torch.zeros(plan.planes_bytes, dtype=torch.uint8, device=DEV)
+        s = torch.zeros(plan.n_slices, dtype=torch.float32, device=DEV)
+        y = torch.zeros_like(x)
+        y2 = torch.zeros_like(x)
+        plan.encode(x, seeds, p, s, ws)
+        plan.decode(p, seeds, s, y, ws)
+        plan.decode(p, seeds, s, y2, ws, base=base)
+        torch.cuda.synchronize()
+        outs.append((p.cpu(), s.cpu(), y.cpu(), y2.cpu()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

@@ -141,6 +141,31 @@ def test_two_stream_split_rules():
     assert many.n_waves == 3
 
 
+def test_small_set_launch():
+    """Tiny and small slices go out as ONE small-set launch per direction
+    (k_enc_sset / k_dec_sset: groups of one size per 1024-thread workgroup),
+    or with sset=0 as one launch per size class.  Same algorithmic bytes."""
+    from openfl_amd import _lib
+    from openfl_amd.codec import EdenPlan
+    from openfl_amd.workloads import WORKLOADS, numel
+    sizes = [numel(s) for _, s in WORKLOADS["resnet50_fp32"]()]
+    on, off = EdenPlan(sizes, 8, sset=1), EdenPlan(sizes, 8, sset=0)
+    for enc in (True, False):
+        d = "enc" if enc else "dec"
+        n1 = [l["name"] for l in on.launches(enc)]
+        n0 = [l["name"] for l in off.launches(enc)]
+        assert n1.count(f"ofl::k_{d}_sset") == 1
+        assert not any(n.startswith(f"ofl::k_{d}_small") or n == f"ofl::k_{d}_tiny" for n in n1)
+        assert "ofl::k_enc_sset" not in n0 and f"ofl::k_{d}_tiny" in n0
+        assert len(n0) - len(n1) == sum(n.startswith(f"ofl::k_{d}_small") for n in n0)
+        assert sum(l["bytes_alg"] for l in on.launches(enc)) == sum(l["bytes_alg"] for l in off.launches(enc))
+        # one 1024-thread group per 2^15 elements of one size, tiny ones 4 of one p per group
+        sset = [l for l in on.launches(enc) if l["name"].endswith("_sset")][0]
+        assert sset["blocks"] < sum(1 for n in sizes if 100 < n <= 1 << 15)
+    with pytest.raises(_lib.CodecError, match="sset"):
+        EdenPlan(sizes, 8, sset=3)
+
+
 def test_plan_errors():
     from openfl_amd import _lib
     from openfl_amd.codec import EdenPlan

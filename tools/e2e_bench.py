@@ -32,17 +32,36 @@ def state_dict(shapes, seed):
     return [(n, (rng.standard_normal(s, dtype=np.float32) * np.float32(0.01))) for n, s in shapes]
 
 
-def run_plugin(sd, pipe, P):
+def _bucket(n):
+    return "<=100" if n <= 100 else "<=2^15" if n <= 1 << 15 else "<=2^18" if n <= 1 << 18 else ">2^18"
+
+
+def run_plugin(sd, pipe, P, phases=None):
+    """phases: dict to accumulate seconds per (phase, size bucket) into."""
+    clk = time.perf_counter
     wire = []
     for name, arr in sd:
+        t0 = clk()
         data, md = pipe.forward(arr)
+        t1 = clk()
         wire.append(P.construct_named_tensor((name, "col", 1, False, ("trained",)), data, md,
                                              False).SerializeToString())
+        if phases is not None:
+            k = _bucket(arr.size)
+            phases["forward " + k] = phases.get("forward " + k, 0.0) + t1 - t0
+            phases["protobuf build"] = phases.get("protobuf build", 0.0) + clk() - t1
     out = []
-    for b in wire:
+    for b, (_, arr) in zip(wire, sd):
+        t0 = clk()
         nt = P.NamedTensor()
         nt.ParseFromString(b)
-        out.append(pipe.backward(nt.data_bytes, P.transformer_metadata_of(nt)))
+        md = P.transformer_metadata_of(nt)
+        t1 = clk()
+        out.append(pipe.backward(nt.data_bytes, md))
+        if phases is not None:
+            k = _bucket(arr.size)
+            phases["protobuf parse"] = phases.get("protobuf parse", 0.0) + t1 - t0
+            phases["backward " + k] = phases.get("backward " + k, 0.0) + clk() - t1
     return out, sum(len(b) for b in wire)
 
 
@@ -134,6 +153,16 @@ def main():
             dt = time.perf_counter() - t0
         res["plugin"] = {"s": round(dt, 4), "GiB_s": round(in_bytes / dt / 2 ** 30, 3),
                          "wire_bytes": sum(o[1] for o in outs), "rel_err": round(rel_err(sds[0], outs[0][0]), 6)}
+        # where a round's time goes (a third, instrumented round)
+        ph = {}
+        torch.cuda.synchronize()
+        for sd in sds:
+            run_plugin(sd, pipe, P, ph)
+        res["plugin"]["phases_ms"] = {k: round(1e3 * v, 2) for k, v in sorted(ph.items())}
+        cnt = {}
+        for _, a in sds[0]:
+            cnt[_bucket(a.size)] = cnt.get(_bucket(a.size), 0) + len(sds)
+        res["plugin"]["tensors_per_bucket"] = cnt
     if "batched" in modes:
         for mode in ("reference", "fast"):
             pipe = EdenPipeline(n_bits=8, dim_threshold=100, device="cuda:0", seed_mode=mode)
