@@ -171,6 +171,12 @@ int ofl_eden_decode_add(ofl_eden_plan_t plan, const uint8_t* planes_arena, const
  * y_host are MAPPED pinned host memory (hipHostMalloc, torch pin_memory) that
  * the single launch reads and writes directly -- no DMA copies; y_host holds
  * 4 * arena bytes.  Synchronous (stream synchronised).  Not mapped -> OFL_EINVAL. */
+/* Second half of a one-tensor encode whose x is already on (or on its way
+ * to) the device, e.g. by ofl_copy_h2d_chunked on the same stream: the seed
+ * written into in_dev + off_seeds, the launches, one D2H of [planes | scales]
+ * into out_host (pinned), stream synchronised. */
+int ofl_eden_encode_seeded(ofl_eden_plan_t plan, void* in_dev, size_t off_seeds, uint32_t seed, void* out_dev,
+                           void* out_host, size_t out_bytes, size_t off_scales, void* ws, size_t ws_bytes, void* stream);
 int ofl_eden_encode_mapped(ofl_eden_plan_t plan, const void* in_host, size_t off_seeds, void* out_host,
                            size_t off_scales, void* ws, size_t ws_bytes, void* stream);
 int ofl_eden_decode_mapped(ofl_eden_plan_t plan, const void* in_host, size_t off_scales, size_t off_seeds,
@@ -417,6 +423,14 @@ double ofl_serial_sum_f64(const double* x, int64_t n);
 /* ofl_serial_sum_f32 of x while copying x to dst (the pinned staging block
  * of a one-tensor encode): the copy rides in the add chain's latency. */
 float ofl_serial_sum_copy_f32(const float* x, float* dst, int64_t n);
+/* x (pageable host float32[n]) -> pinned staging -> device, in chunks of
+ * `chunk` elements: each chunk's async H2D on `stream` is issued as soon as it
+ * sits in the pinned buffer, so the DMA runs beside the copy of the next one
+ * (and, want_sum != 0, beside the reference seed's serial float32 sum, one
+ * dependent chain over all chunks: *sum_out = ofl_serial_sum_f32(x, n)).
+ * The caller keeps `pinned` alive until the stream has passed the copies. */
+int ofl_copy_h2d_chunked(const float* x, float* pinned, void* dev, int64_t n, int64_t chunk, int want_sum,
+                         float* sum_out, void* stream);
 /* ofl_serial_sum_* of n host arrays (f32 or, if f64, double) on up to
  * nthreads native threads, largest first; out[i] as double (exact for f32). */
 int ofl_serial_sums_many(int n, const void* const* ptrs, const int64_t* lens, int f64, double* out, int nthreads);

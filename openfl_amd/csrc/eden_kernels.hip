@@ -3353,6 +3353,25 @@ int ofl_eden_decode_mapped(ofl_eden_plan_t pl, const void* in_host, size_t off_s
     return OFL_OK;
 }
 
+int ofl_eden_encode_seeded(ofl_eden_plan_t pl, void* in_dev, size_t off_seeds, uint32_t seed, void* out_dev,
+                           void* out_host, size_t out_bytes, size_t off_scales, void* ws, size_t ws_bytes, void* stream) {
+    if (!pl || !in_dev || !out_dev || !out_host) return fail(OFL_EINVAL, "encode_seeded: null argument");
+    if (pl->ntensors != 1 || off_seeds < 4 * (size_t)pl->arena || off_scales < (size_t)pl->planes_bytes ||
+        off_scales + 4 * pl->slices.size() > out_bytes)
+        return fail(OFL_EINVAL, "encode_seeded: one-tensor plans; block layout does not fit the plan");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    char* i = static_cast<char*>(in_dev);
+    HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(i + off_seeds), (int)seed, 1, st));
+    char* o = static_cast<char*>(out_dev);
+    if (int rc = ofl_eden_encode(pl, reinterpret_cast<const float*>(i), reinterpret_cast<const uint32_t*>(i + off_seeds),
+                                 reinterpret_cast<uint8_t*>(o), reinterpret_cast<float*>(o + off_scales), ws, ws_bytes,
+                                 stream))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(out_host, out_dev, out_bytes, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return OFL_OK;
+}
+
 int ofl_eden_encode_host_x(ofl_eden_plan_t pl, const void* x_host, size_t x_bytes, uint32_t seed, void* in_dev,
                            size_t off_seeds, void* out_dev, void* out_host, size_t out_bytes, size_t off_scales,
                            void* ws, size_t ws_bytes, void* stream) {
@@ -3476,6 +3495,37 @@ float ofl_serial_sum_copy_f32(const float* x, float* dst, int64_t n) {
         s = s + x[i];
     }
     return s;
+}
+
+int ofl_copy_h2d_chunked(const float* x, float* pinned, void* dev, int64_t n, int64_t chunk, int want_sum,
+                         float* sum_out, void* stream) {
+    if (n < 0 || (n && (!x || !pinned || !dev)) || chunk <= 0) return fail(OFL_EINVAL, "copy_h2d_chunked: bad arguments");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    float s = 0.0f;
+    for (int64_t o = 0; o < n; o += chunk) {
+        const int64_t c = std::min(chunk, n - o);
+        if (want_sum) {
+            // the serial sum continues from the previous chunk: one dependent chain
+            int64_t i = 0;
+            const float* xs = x + o;
+            float* d = pinned + o;
+            for (; i + 8 <= c; i += 8) {
+                float v[8];
+                memcpy(v, xs + i, sizeof(v));
+                memcpy(d + i, v, sizeof(v));
+                for (int k = 0; k < 8; ++k) s = s + v[k];
+            }
+            for (; i < c; ++i) {
+                d[i] = xs[i];
+                s = s + xs[i];
+            }
+        } else {
+            memcpy(pinned + o, x + o, 4 * c);
+        }
+        HIP_TRY(hipMemcpyAsync(static_cast<float*>(dev) + o, pinned + o, 4 * c, hipMemcpyHostToDevice, st));
+    }
+    if (sum_out) *sum_out = s;
+    return OFL_OK;
 }
 
 double ofl_serial_sum_f64(const double* x, int64_t n) {

@@ -256,17 +256,18 @@ class Eden(PerThreadDevice):
                     plan.handle, x_ptr, 4 * n, int(seed) & 0xFFFFFFFF, idev.data_ptr(), off_seeds, odev.data_ptr(),
                     oh.data_ptr(), out_bytes, off_scales, ws.data_ptr(), ws.numel(), st))
             else:
-                # pinned block [x | seed], filled while the seed's serial sum
-                # is taken (ofl_serial_sum_copy_f32), then one H2D
+                # x into pinned staging in chunks, each chunk's H2D issued as
+                # soon as it is there (ofl_copy_h2d_chunked): the DMA runs
+                # beside the copy and the reference seed's serial sum; then the
+                # seed, the launches and one D2H (ofl_eden_encode_seeded)
                 ih = stg.get("in1", in_bytes, torch.uint8)
-                ia = ih.numpy()
+                sm = ctypes.c_float(0.0)
+                _lib.check(L.ofl_copy_h2d_chunked(flat.ctypes.data if n else None, ih.data_ptr(), idev.data_ptr(), n,
+                                                  _H2D_CHUNK, 1 if fuse else 0, ctypes.byref(sm), st))
                 if fuse:
-                    seed = seed_of_sum(np.float32(L.ofl_serial_sum_copy_f32(flat.ctypes.data, ia.ctypes.data, n)))
-                elif n:
-                    ia[:4 * n].view(np.float32)[:] = flat
-                ia[off_seeds:off_seeds + 4].view(np.uint32)[0] = int(seed) & 0xFFFFFFFF
-                _lib.check(L.ofl_eden_encode_host(
-                    plan.handle, ih.data_ptr(), idev.data_ptr(), in_bytes, off_seeds, odev.data_ptr(),
+                    seed = seed_of_sum(np.float32(sm.value))
+                _lib.check(L.ofl_eden_encode_seeded(
+                    plan.handle, idev.data_ptr(), off_seeds, int(seed) & 0xFFFFFFFF, odev.data_ptr(),
                     oh.data_ptr(), out_bytes, off_scales, ws.data_ptr(), ws.numel(), st))
         oa = oh.numpy()
         # one host copy, pinned -> bytes; the array is a zero-copy view of it
@@ -343,6 +344,8 @@ _USE_CTX = os.environ.get("OFL_PLUGIN_CTX", "1") != "0"
 # larger one-tensor calls: OFL_PLUGIN_PAGEABLE=1 moves x / planes straight
 # from the caller's arrays (ofl_eden_*_host_x) instead of via pinned staging
 _PAGEABLE = os.environ.get("OFL_PLUGIN_PAGEABLE", "0") == "1"
+# larger one-tensor encodes: x goes H2D in chunks of this many elements
+_H2D_CHUNK = 1 << 18
 # contexts whose slices are all <= 2^15: kernels on mapped pinned memory
 # (OFL_PLUGIN_MAPPED=0: H2D / D2H copies around the launch, A/B)
 _USE_MAPPED = os.environ.get("OFL_PLUGIN_MAPPED", "1") != "0"

@@ -12,7 +12,7 @@ T 700 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread 
 rc=$?; echo "pytest rc=$rc" >> $O/pytest_gpu.log
 [ $rc -le 1 ] || exit 13
 for rep in 1 2 3; do
-  for v in "sset" "nosset:OFL_EDEN_SSET=0"; do
+  for v in "sset" "nosset:OFL_EDEN_SSET=0" "onewave:OFL_EDEN_SPLIT_MIB=100000"; do
     n=${v%%:*}; e=""; [ "$n" != "$v" ] && e=${v#*:}
     T 200 env $e python -u bench.py --workload resnet50_fp32 --steps 400 --warmup 30 --also '' --no-cpu-baseline --no-kernel-events > $O/rn_${rep}_$n.json 2> $O/rn_${rep}_$n.err || exit 16
   done
