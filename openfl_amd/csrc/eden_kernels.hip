@@ -930,9 +930,9 @@ __global__ __launch_bounds__(kTinyNT) void k_dec_tiny(KArgs a) {
 // Small-set kernels: every tiny and small slice of a call in ONE launch of
 // 1024-thread workgroups (instead of one latency-bound launch per size class
 // in a chain).  Workgroup b reads its group {P (0: tiny), list offset, count}
-// from a.list[3b..3b+2]; a group holds slices of one size: 2^(15-P) small
-// slices of 2^P elements, or 4 tiny slices of one p.  Sub-blocks past count
-// recompute the group's last slice without storing it.
+// from a.list[3b..3b+2]; a group holds slices of one size: up to 2^(15-P)
+// small slices of 2^P elements, or up to 4 tiny slices of one p.  The waves of
+// sub-blocks past count end at once.
 // ===========================================================================
 constexpr int kSetNT = 1024;
 template <int P_LOG> struct SetSmem {
@@ -947,19 +947,20 @@ constexpr size_t kSetSmemEnc = kSetBody + sizeof(QTab) + sizeof(float) * (kSetNT
 constexpr size_t kSetSmemDec = kSetBody + sizeof(float) * 256;
 
 template <int P_LOG>
-DEVI void enc_set_group(const KArgs& a, const int32_t* sl, int cnt, unsigned char* sm, const QTab* qt, float* red) {
+DEVI void enc_set_group(const KArgs& a, const int32_t* sl, unsigned char* sm, const QTab* qt, float* red) {
     constexpr int NT = SmallSmem<P_LOG>::NT;
     const uint32_t sub = threadIdx.x / NT;
-    enc_small_body<P_LOG>(a, sl[min((int)sub, cnt - 1)], threadIdx.x % NT, sm + sub * SetSmem<P_LOG>::per, qt,
-                          red + sub * (NT / 64), (int)sub < cnt);
+    enc_small_body<P_LOG>(a, sl[sub], threadIdx.x % NT, sm + sub * SetSmem<P_LOG>::per, qt, red + sub * (NT / 64),
+                          true);
 }
 template <int P_LOG>
-DEVI void dec_set_group(const KArgs& a, const int32_t* sl, int cnt, unsigned char* sm, const float* cen) {
+DEVI void dec_set_group(const KArgs& a, const int32_t* sl, unsigned char* sm, const float* cen) {
     constexpr int NT = SmallSmem<P_LOG>::NT;
     const uint32_t sub = threadIdx.x / NT;
-    dec_small_body<P_LOG>(a, sl[min((int)sub, cnt - 1)], threadIdx.x % NT, sm + sub * SetSmem<P_LOG>::per, cen,
-                          (int)sub < cnt);
+    dec_small_body<P_LOG>(a, sl[sub], threadIdx.x % NT, sm + sub * SetSmem<P_LOG>::per, cen, true);
 }
+// threads of a group's sub-blocks (whole waves: every NT >= 64)
+DEVI int set_active(int P, int cnt) { return cnt * (P ? (1 << (P - 5)) : kTinyNT); }
 
 __global__ __launch_bounds__(kSetNT) void k_enc_sset(KArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -968,17 +969,25 @@ __global__ __launch_bounds__(kSetNT) void k_enc_sset(KArgs a) {
     const int32_t* g = a.list + 3 * blockIdx.x;
     const int P = g[0], cnt = g[2];
     const int32_t* sl = a.list + g[1];
-    load_qtable<kSetNT>(qt, a.nbits);  // published by the bodies' first barrier
+    // waves past the group's sub-blocks end here: a workgroup barrier waits
+    // for the waves that have not ended only
+    const int act = set_active(P, cnt);
+    if ((int)threadIdx.x >= act) return;
+    {  // the quantiser table, by the active threads (published by the bodies' first barrier)
+        const float4* src = reinterpret_cast<const float4*>(&g_qtabs.t[a.nbits - 1]);
+        float4* dst = reinterpret_cast<float4*>(qt);
+        for (int k = threadIdx.x; k < EDEN_GRID_CELLS; k += act) dst[k] = src[k];
+    }
     switch (P) {
-    case 11: enc_set_group<11>(a, sl, cnt, smem, qt, red); break;
-    case 12: enc_set_group<12>(a, sl, cnt, smem, qt, red); break;
-    case 13: enc_set_group<13>(a, sl, cnt, smem, qt, red); break;
-    case 14: enc_set_group<14>(a, sl, cnt, smem, qt, red); break;
-    case 15: enc_set_group<15>(a, sl, cnt, smem, qt, red); break;
+    case 11: enc_set_group<11>(a, sl, smem, qt, red); break;
+    case 12: enc_set_group<12>(a, sl, smem, qt, red); break;
+    case 13: enc_set_group<13>(a, sl, smem, qt, red); break;
+    case 14: enc_set_group<14>(a, sl, smem, qt, red); break;
+    case 15: enc_set_group<15>(a, sl, smem, qt, red); break;
     default: {
         const uint32_t sub = threadIdx.x / kTinyNT;
-        enc_tiny_body(a, sl[min((int)sub, cnt - 1)], threadIdx.x % kTinyNT, reinterpret_cast<TinySmem*>(smem) + sub,
-                      qt, red + sub * (kTinyNT / 64), (int)sub < cnt);
+        enc_tiny_body(a, sl[sub], threadIdx.x % kTinyNT, reinterpret_cast<TinySmem*>(smem) + sub, qt,
+                      red + sub * (kTinyNT / 64), true);
     }
     }
 }
@@ -989,17 +998,18 @@ __global__ __launch_bounds__(kSetNT) void k_dec_sset(KArgs a) {
     const int32_t* g = a.list + 3 * blockIdx.x;
     const int P = g[0], cnt = g[2];
     const int32_t* sl = a.list + g[1];
-    for (int j = threadIdx.x; j < 256; j += kSetNT) cen[j] = g_centroids[a.nbits - 1][j];
+    const int act = set_active(P, cnt);
+    if ((int)threadIdx.x >= act) return;  // as in k_enc_sset
+    for (int j = threadIdx.x; j < 256; j += act) cen[j] = g_centroids[a.nbits - 1][j];
     switch (P) {
-    case 11: dec_set_group<11>(a, sl, cnt, smem, cen); break;
-    case 12: dec_set_group<12>(a, sl, cnt, smem, cen); break;
-    case 13: dec_set_group<13>(a, sl, cnt, smem, cen); break;
-    case 14: dec_set_group<14>(a, sl, cnt, smem, cen); break;
-    case 15: dec_set_group<15>(a, sl, cnt, smem, cen); break;
+    case 11: dec_set_group<11>(a, sl, smem, cen); break;
+    case 12: dec_set_group<12>(a, sl, smem, cen); break;
+    case 13: dec_set_group<13>(a, sl, smem, cen); break;
+    case 14: dec_set_group<14>(a, sl, smem, cen); break;
+    case 15: dec_set_group<15>(a, sl, smem, cen); break;
     default: {
         const uint32_t sub = threadIdx.x / kTinyNT;
-        dec_tiny_body(a, sl[min((int)sub, cnt - 1)], threadIdx.x % kTinyNT,
-                      reinterpret_cast<TinySmem*>(smem)[sub].s, (int)sub < cnt);
+        dec_tiny_body(a, sl[sub], threadIdx.x % kTinyNT, reinterpret_cast<TinySmem*>(smem)[sub].s, true);
     }
     }
 }
@@ -2670,7 +2680,8 @@ void build_schedule(ofl_eden_plan* pl) {
         return o;
     };
     std::vector<Launch> common;
-    if (pl->sset >= 0 ? pl->sset == 1 : use_sset()) {
+    const bool sset = pl->sset >= 0 ? pl->sset == 1 : use_sset();
+    if (sset) {
         // one small-set launch: groups of one size, largest first; table of
         // {P (0: tiny), slice-list offset (from the table), count} per block
         std::vector<std::array<int32_t, 3>> groups;
@@ -2714,8 +2725,11 @@ void build_schedule(ofl_eden_plan* pl) {
     // the second stream (the 1 GiB set: one wave on one stream, 2.24 vs
     // 2.29 ms; ResNet-50 keeps its two waves beside the small slices: 360
     // vs 369 us with one wave; OFL_EDEN_SPLIT_MIB=m splits above m MiB)
+    // With the small-set launch a plan that fits one wave keeps it whole: the
+    // one small-set launch runs beside it on the side stream (ResNet-50 0.288
+    // vs 0.309 ms with two waves, profiles/r03_resnet50_sset_onewave_ab.txt)
     const int64_t split_min = split_min_bytes();
-    const bool split = split_min >= 0 ? 4 * tot > split_min : (!common.empty() || tot > cap);
+    const bool split = split_min >= 0 ? 4 * tot > split_min : ((!common.empty() && !sset) || tot > cap);
     // the split only feeds the second stream (everything fits one wave):
     // exactly two waves, cut where the halves are closest (in-order packing
     // against a half-total cap can leave a third wave behind the first on the

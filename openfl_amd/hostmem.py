@@ -37,33 +37,55 @@ def _c():
     return _libc
 
 
-def bytes_from(src_addr, n, threads=8, huge_min=8 << 20):
+def bytes_from(src_addr, n, threads=8, huge_min=8 << 20, par_min=1 << 20):
     """A new `bytes` of the n bytes at host address src_addr (pinned staging).
 
     The object is created uninitialised (PyBytes_FromStringAndSize(NULL, n),
     the CPython idiom for filling a bytes before anyone else holds it); above
     huge_min its 2 MiB-aligned interior is marked MADV_HUGEPAGE (transparent
     huge pages in 'madvise' mode), so first touch costs one fault per 2 MiB
-    instead of per 4 KiB; the copy runs on native threads, so those faults are
-    taken in parallel.  Same bytes as bytes(memoryview) of the source."""
-    from openfl_amd import _lib
+    instead of per 4 KiB; above par_min the copy runs on native threads, so
+    those faults are taken in parallel.  Same bytes as bytes(memoryview) of
+    the source."""
     n = int(n)
-    if n < huge_min:
+    if n < par_min:
         return ctypes.string_at(src_addr, n) if n else b""
     b = _new_bytes(None, n)
-    dst = _bytes_addr(b)
-    lo = (dst + _HUGE - 1) // _HUGE * _HUGE
-    hi = (dst + n) // _HUGE * _HUGE
-    if hi > lo:
-        _c().madvise(lo, hi - lo, _MADV_HUGEPAGE)  # advisory: a refusal only costs speed
-    piece = 4 << 20
+    _fill(_bytes_addr(b), src_addr, n, threads, huge_min, 4 << 20 if n >= huge_min else
+          max(256 << 10, -(-n // (2 * threads)) // 4096 * 4096))
+    return b
+
+
+def _fill(dst, src_addr, n, threads, huge_min, piece):
+    if n >= huge_min:
+        lo = (dst + _HUGE - 1) // _HUGE * _HUGE
+        hi = (dst + n) // _HUGE * _HUGE
+        if hi > lo:
+            _c().madvise(lo, hi - lo, _MADV_HUGEPAGE)  # advisory: a refusal only costs speed
+    from openfl_amd import _lib
     offs = np.arange(0, n, piece, dtype=np.uint64)
     sizes = np.minimum(np.uint64(piece), np.uint64(n) - offs).astype(np.int64)
     d = np.uint64(dst) + offs
     s = np.uint64(src_addr) + offs
     _lib.check(_lib.lib().ofl_host_copy_many(offs.size, d.ctypes.data, s.ctypes.data, sizes.ctypes.data,
                                              int(threads)))
-    return b
+
+
+def array_from(src_addr, count, dtype=np.float32, threads=8, par_min=1 << 20, huge_min=4 << 20):
+    """A new ndarray of `count` elements copied from host address src_addr
+    (pinned staging): a fresh array's first touch is page faults, so above
+    par_min bytes the copy runs in pieces on native threads (the faults taken
+    in parallel) and above huge_min the array's 2 MiB-aligned interior is
+    marked MADV_HUGEPAGE first."""
+    dt = np.dtype(dtype)
+    out = np.empty(int(count), dt)
+    n = out.nbytes
+    if n < par_min:
+        if n:
+            ctypes.memmove(out.ctypes.data, src_addr, n)
+        return out
+    _fill(out.ctypes.data, src_addr, n, threads, huge_min, max(256 << 10, -(-n // (2 * threads)) // 4096 * 4096))
+    return out
 
 
 def keep_large_blocks(threshold=1 << 30):

@@ -309,9 +309,7 @@ class Eden(PerThreadDevice):
         in_bytes = off_seeds + 4
         out_bytes = 4 * total_dim
         sc = np.asarray(scales, np.float32)
-        # y D2H lands in the returned array itself (pageable: the runtime
-        # stages it), not in pinned staging followed by a host copy
-        y = np.empty(max(total_dim, 1), np.float32)
+        y = np.empty(max(total_dim, 1), np.float32) if _PAGEABLE else None
         idev = self._dev("in", in_bytes, torch.uint8)
         ydev = self._dev("y", max(plan.arena_numel, 1), torch.float32)
         ws = self.codec.ws.get(plan.ws_bytes, self.device)
@@ -324,14 +322,21 @@ class Eden(PerThreadDevice):
                     off_scales, off_seeds, ydev.data_ptr(), y.ctypes.data, out_bytes, ws.data_ptr(), ws.numel(),
                     self._stream().cuda_stream))
             else:
-                ih = self._staging().get("in1", in_bytes, torch.uint8)
+                # y D2H into pinned staging, then a threaded copy into the
+                # fresh array (its first-touch faults taken in parallel, huge
+                # pages above 4 MiB): a pageable D2H into fresh memory ran at
+                # ~3 GB/s in the end-to-end loop (profiles/r03_e2e_*)
+                stg = self._staging()
+                ih = stg.get("in1", in_bytes, torch.uint8)
                 ia = ih.numpy()
                 ia[:pb] = planes_h[:pb]
                 ia[off_scales:off_scales + 4 * ns].view(np.float32)[:] = sc
                 ia[off_seeds:off_seeds + 4].view(np.uint32)[0] = seed & 0xFFFFFFFF
+                yh = stg.get("out1", max(out_bytes, 4), torch.uint8)
                 _lib.check(L.ofl_eden_decode_host(
                     plan.handle, ih.data_ptr(), idev.data_ptr(), in_bytes, off_scales, off_seeds, ydev.data_ptr(),
-                    y.ctypes.data, out_bytes, ws.data_ptr(), ws.numel(), self._stream().cuda_stream))
+                    yh.data_ptr(), out_bytes, ws.data_ptr(), ws.numel(), self._stream().cuda_stream))
+                y = hostmem.array_from(yh.data_ptr(), max(total_dim, 1), np.float32)
         self._trim()
         return y[:total_dim]
 
