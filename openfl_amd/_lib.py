@@ -23,7 +23,7 @@ EXPORTS = (
     "ofl_eden_plan_get_schedule", "ofl_eden_plan_set_row2", "ofl_eden_plan_set_sset", "ofl_eden_plan_num_slices", "ofl_eden_plan_planes_bytes",
     "ofl_eden_plan_workspace_bytes", "ofl_eden_plan_tensor_info", "ofl_eden_plan_tensor_dims",
     "ofl_eden_encode", "ofl_eden_encode_wavg", "ofl_eden_decode", "ofl_eden_decode_add", "ofl_eden_encode_host", "ofl_eden_decode_host", "ofl_eden_encode_mapped", "ofl_eden_decode_mapped", "ofl_eden_encode_seeded", "ofl_copy_h2d_chunked", "ofl_eden_encode_host_x", "ofl_eden_decode_host_x", "ofl_copy_h2d_async", "ofl_eden_plan_profile", "ofl_eden_plan_num_launches",
-    "ofl_eden_plan_launch_info", "ofl_eden_plan_profile_collect", "ofl_serial_sum_f32", "ofl_serial_sum_copy_f32",
+    "ofl_eden_plan_launch_info", "ofl_eden_plan_profile_collect", "ofl_serial_sum_f32", "ofl_serial_sum_f32_mt", "ofl_serial_sum_copy_f32",
     "ofl_serial_sum_f64", "ofl_host_copy_many", "ofl_serial_sums_many", "ofl_lossy_last_error", "ofl_lossy_workspace_bytes", "ofl_kmeans1d_fit",
     "ofl_kmeans1d_batch_workspace_bytes", "ofl_kmeans1d_batch",
     "ofl_kmeans1d_label", "ofl_sparsify_topk", "ofl_ternary_stats", "ofl_ternary_ranks", "ofl_lut_decode",
@@ -180,6 +180,8 @@ def _bind(L):
     L.ofl_inflate_members.restype = i32
     L.ofl_serial_sum_f32.argtypes = [vp, i64]
     L.ofl_serial_sum_f32.restype = ctypes.c_float
+    L.ofl_serial_sum_f32_mt.argtypes = [vp, i64, vp, i32]
+    L.ofl_serial_sum_f32_mt.restype = ctypes.c_float
     L.ofl_serial_sum_copy_f32.argtypes = [vp, vp, i64]
     L.ofl_serial_sum_copy_f32.restype = ctypes.c_float
     L.ofl_serial_sum_f64.argtypes = [vp, i64]

@@ -14,7 +14,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libofl_codec.so")
-SOURCES = ["eden_kernels.hip", "lossy_kernels.hip", "agg_kernels.hip", "deflate_kernels.hip"]
+SOURCES = ["eden_kernels.hip", "lossy_kernels.hip", "agg_kernels.hip", "deflate_kernels.hip", "serial_sum.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-std=c++20", "-O3", "-fPIC", "-shared",
          "-Wall", "-Wno-unused-function", "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]

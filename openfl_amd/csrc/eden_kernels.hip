@@ -3488,14 +3488,23 @@ int ofl_eden_plan_profile_collect(ofl_eden_plan_t pl, int encode, double* ms_sum
 }
 
 // strict IEEE order: the library is built without fast-math/reassociation,
-// so the compiler keeps the dependent add chain (no vectorised partial sums)
-float ofl_serial_sum_f32(const float* x, int64_t n) {
+// so the compiler keeps the dependent add chain (no vectorised partial sums).
+// Arrays of 2^16 elements and more go to the exact multi-threaded evaluation
+// of the same chain (csrc/serial_sum.cpp: binade-wise integer prefix sums).
+static float serial_sum_f32_loop(const float* x, int64_t n) {
     float s = 0.0f;
     for (int64_t i = 0; i < n; ++i) s = s + x[i];
     return s;
 }
+constexpr int64_t kSumMtMin = 1 << 16;
+
+float ofl_serial_sum_f32(const float* x, int64_t n) {
+    if (n >= kSumMtMin) return ofl::serial_sum_f32_mt_cb(x, n, nullptr, 0, nullptr, nullptr);
+    return serial_sum_f32_loop(x, n);
+}
 
 float ofl_serial_sum_copy_f32(const float* x, float* dst, int64_t n) {
+    if (n >= kSumMtMin) return ofl::serial_sum_f32_mt_cb(x, n, dst, 0, nullptr, nullptr);
     float s = 0.0f;
     int64_t i = 0;
     for (; i + 8 <= n; i += 8) {  // the 8-element block copy issues beside the serial adds
@@ -3515,6 +3524,18 @@ int ofl_copy_h2d_chunked(const float* x, float* pinned, void* dev, int64_t n, in
                          float* sum_out, void* stream) {
     if (n < 0 || (n && (!x || !pinned || !dev)) || chunk <= 0) return fail(OFL_EINVAL, "copy_h2d_chunked: bad arguments");
     hipStream_t st = static_cast<hipStream_t>(stream);
+    if (want_sum && n >= kSumMtMin) {
+        // the copy into pinned staging runs on the sum's threads (its first
+        // phase); the one H2D is issued right after it, beside the rest
+        struct Ctx { const float* pinned; void* dev; int64_t n; hipStream_t st; hipError_t err; } c{pinned, dev, n, st, hipSuccess};
+        const float s = ofl::serial_sum_f32_mt_cb(x, n, pinned, 0, [](void* p) {
+            Ctx& c = *static_cast<Ctx*>(p);
+            c.err = hipMemcpyAsync(c.dev, c.pinned, 4 * c.n, hipMemcpyHostToDevice, c.st);
+        }, &c);
+        HIP_TRY(c.err);
+        if (sum_out) *sum_out = s;
+        return OFL_OK;
+    }
     float s = 0.0f;
     for (int64_t o = 0; o < n; o += chunk) {
         const int64_t c = std::min(chunk, n - o);
@@ -3554,15 +3575,23 @@ int ofl_serial_sums_many(int n, const void* const* ptrs, const int64_t* lens, in
     std::vector<int> order(n);
     for (int i = 0; i < n; ++i) order[i] = i;
     std::sort(order.begin(), order.end(), [&](int a, int b) { return lens[a] > lens[b]; });  // largest first
-    std::atomic<int> next{0};
+    // float32 arrays of 2^22 elements and more: one at a time on all threads
+    // (the exact multi-threaded chain); the rest: one array per thread
+    int first = 0;
+    while (!f64 && first < n && lens[order[first]] >= (1 << 22)) {
+        const int i = order[first++];
+        out[i] = (double)ofl::serial_sum_f32_mt_cb(static_cast<const float*>(ptrs[i]), lens[i], nullptr, nthreads,
+                                                   nullptr, nullptr);
+    }
+    std::atomic<int> next{first};
     auto work = [&] {
         for (int k = next++; k < n; k = next++) {
             const int i = order[k];
             out[i] = f64 ? ofl_serial_sum_f64(static_cast<const double*>(ptrs[i]), lens[i])
-                         : (double)ofl_serial_sum_f32(static_cast<const float*>(ptrs[i]), lens[i]);
+                         : (double)serial_sum_f32_loop(static_cast<const float*>(ptrs[i]), lens[i]);
         }
     };
-    const int nt = std::max(1, std::min(nthreads, n));
+    const int nt = std::max(1, std::min(nthreads, n - first));
     std::vector<std::thread> th;
     for (int t = 1; t < nt; ++t) th.emplace_back(work);
     work();

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
 #include <map>
 #include <mutex>
 
@@ -26,3 +27,11 @@ hipError_t per_device_once(F f) {
 }
 
 }  // namespace ofl_util
+
+namespace ofl {
+// exact serial float32 sum (csrc/serial_sum.cpp): s <- fl(s + x[i]) left to
+// right, evaluated on up to nthreads threads (<= 0: the default); dst (or
+// NULL) receives a copy of x, after which after_copy(ctx) (or NULL) runs on
+// the calling thread while the sum goes on
+float serial_sum_f32_mt_cb(const float* x, int64_t n, float* dst, int nthreads, void (*after_copy)(void*), void* ctx);
+}  // namespace ofl

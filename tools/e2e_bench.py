@@ -126,7 +126,13 @@ def main():
     ap.add_argument("--collaborators", type=int, default=2)
     ap.add_argument("--modes", default="plugin,batched,cpu")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--heap-policy", action="store_true",
+                    help="hostmem.keep_large_blocks() first (the opt-in deployment setting: large host "
+                         "blocks stay in the heap, so protobuf copies and fresh arrays do not page-fault)")
     args = ap.parse_args()
+    if args.heap_policy:
+        from openfl_amd import hostmem
+        hostmem.keep_large_blocks()
     import torch
     from openfl_amd import protocols as P
     from openfl_amd.pipelines import EdenPipeline
@@ -136,7 +142,7 @@ def main():
     sds = [state_dict(shapes, 100 + c) for c in range(args.collaborators)]
     in_bytes = sum(a.nbytes for sd in sds for _, a in sd)
     res = {"workload": args.workload, "collaborators": args.collaborators, "input_bytes": in_bytes,
-           "tensors_per_collaborator": len(shapes)}
+           "tensors_per_collaborator": len(shapes), "hostmem_policy": bool(args.heap_policy)}
 
     def rel_err(sd, out):
         num = sum(float(np.sum((o.astype(np.float64) - a) ** 2)) for (_, a), o in zip(sd, out))
