@@ -423,7 +423,8 @@ double ofl_serial_sum_f64(const double* x, int64_t n);
 /* The same float32 chain, exact, on up to nthreads threads (<= 0: env
  * OFL_SUM_THREADS, default 8) -- binade-wise integer prefix sums stitched in
  * order (csrc/serial_sum.cpp); dst (or NULL) receives a copy of x.
- * ofl_serial_sum_f32 and ofl_serial_sum_copy_f32 use it from 2^16 elements. */
+ * ofl_serial_sum_f32, ofl_serial_sum_copy_f32 and ofl_copy_h2d_chunked use it
+ * from 2^20 elements. */
 float ofl_serial_sum_f32_mt(const float* x, int64_t n, float* dst, int nthreads);
 /* ofl_serial_sum_f32 of x while copying x to dst (the pinned staging block
  * of a one-tensor encode): the copy rides in the add chain's latency. */

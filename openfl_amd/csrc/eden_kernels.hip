@@ -1023,6 +1023,10 @@ __global__ __launch_bounds__(kSetNT) void k_dec_sset(KArgs a) {
 struct RowSet6 {
     static constexpr Lay L1{15, 0, 1, 11, 12, 13, 14}, L2{15, 2, 3, 4, 5, 6, 10}, L3{15, 5, 6, 7, 8, 9, 10},
                          L4{15, 11, 12, 13, 14, 9, 10}, L5{15, 0, 1, 2, 3, 4, 5};
+    // F1c's layout with element bits 0, 1 in registers: the ws tile moves as
+    // float4s (k_enc_rowA's stores, k_dec_rowC's loads); lanes vary bits 2..6,
+    // a conflict-free pattern of pad().  Same stages in the same order as L3.
+    static constexpr Lay L3F{15, 0, 1, 7, 8, 9, 10};
     static constexpr uint32_t F1a = bits_mask({0, 1, 11, 12, 13, 14}), F1b = bits_mask({2, 3, 4, 5, 6, 10}),
                               F1c = bits_mask({7, 8, 9}), F2c = bits_mask({5, 6, 7, 8, 9, 10}),
                               F2d = bits_mask({11, 12, 13, 14}), F2e = bits_mask({0, 1, 2, 3, 4});
@@ -1266,6 +1270,37 @@ DEVI void store_ws(const KArgs& a, const SliceDesc& D, uint32_t tile, uint32_t b
         for (int k = 0; k < 64; ++k) bstore1(r, base3, LT<RS::L3>::off(k), v[k]);
     }
 }
+// ws tile in layout L (element bits 0, 1 in registers 0, 1) as float4s
+#ifndef OFL_ROW_WS4
+#define OFL_ROW_WS4 1  // A/B builds: 0 = the dword L3 tile I/O in k_enc_rowA / k_dec_rowC
+#endif
+constexpr bool kRowWs4 = OFL_ROW_WS4 != 0;
+template <Lay L>
+DEVI void fetch_ws4(const KArgs& a, const SliceDesc& D, uint32_t tile, bool live, uint32_t base, float (&v)[64]) {
+    static_assert(LT<L>::rb(0) == 0 && LT<L>::rb(1) == 1, "float4 loads need element bits 0, 1 in registers 0, 1");
+    const bool perm = D.perm;
+    const rsrc_t r = mk_rsrc(ws_row_base(a, D, tile), live ? (perm ? (4u << (kRowLog + 1)) - 128u : 4u << kRowLog) : 0u);
+    const uint32_t b = perm ? ws_row_idx(base) : base;
+#pragma unroll
+    for (int k = 0; k < 64; k += 4) {
+        const uint32_t o = LT<L>::off(k);
+        const float4 f = bload4(r, b, perm ? ws_row_idx(o) : o);
+        v[k] = f.x; v[k + 1] = f.y; v[k + 2] = f.z; v[k + 3] = f.w;
+    }
+}
+template <Lay L>
+DEVI void store_ws4(const KArgs& a, const SliceDesc& D, uint32_t tile, uint32_t base, const float (&v)[64]) {
+    static_assert(LT<L>::rb(0) == 0 && LT<L>::rb(1) == 1, "float4 stores need element bits 0, 1 in registers 0, 1");
+    const bool perm = D.perm;
+    const rsrc_t r = mk_rsrc(ws_row_base(a, D, tile), perm ? (4u << (kRowLog + 1)) - 128u : 4u << kRowLog);
+    const uint32_t b = perm ? ws_row_idx(base) : base;
+#pragma unroll
+    for (int k = 0; k < 64; k += 4) {
+        const uint32_t o = LT<L>::off(k);
+        bstore4(r, b, perm ? ws_row_idx(o) : o, &v[k]);
+    }
+}
+
 // the tile's 8-byte word of every plane (planes >= nbits read as 0).  A8: the
 // launch's plane rows are 8-byte aligned; otherwise bytes.
 template <bool A8>
@@ -1296,7 +1331,7 @@ __global__ __launch_bounds__(kRowNT) void k_enc_rowA(KArgs a) {
     const TileWalk tw(a, reinterpret_cast<TileTab*>(smem + kRowTab), tid);
     int t = (int)blockIdx.x;
     if (t >= tw.total) return;
-    const uint32_t base1 = LT<RS::L1>::base(tid), base3 = LT<RS::L3>::base(tid);
+    const uint32_t base1 = LT<RS::L1>::base(tid), base3 = LT<kRowWs4 ? RS::L3F : RS::L3>::base(tid);
     int si; uint32_t tile;
     tw.at(t, si, tile);
     float nx[64];
@@ -1318,9 +1353,15 @@ __global__ __launch_bounds__(kRowNT) void k_enc_rowA(KArgs a) {
         stages<RS::L1, RS::F1a>(v);
         exchange<RS::L1, RS::L2>(v, s, tid);
         stages<RS::L2, RS::F1b>(v);
-        exchange<RS::L2, RS::L3>(v, s, tid);
-        stages<RS::L3, RS::F1c>(v);
-        store_ws(a, D, tile, base3, v);
+        if constexpr (kRowWs4) {
+            exchange<RS::L2, RS::L3F>(v, s, tid);
+            stages<RS::L3F, RS::F1c>(v);
+            store_ws4<RS::L3F>(a, D, tile, base3, v);
+        } else {
+            exchange<RS::L2, RS::L3>(v, s, tid);
+            stages<RS::L3, RS::F1c>(v);
+            store_ws(a, D, tile, base3, v);
+        }
         ss = block_sum<kRowNT>(ss, red);
         if (tid == 0) a.part[D.part_off + tile] = ss;
         if (!more) break;
@@ -1425,11 +1466,12 @@ __global__ __launch_bounds__(kRowNT) void k_dec_rowC(KArgs a) {
     const TileWalk tw(a, reinterpret_cast<TileTab*>(smem + kRowTab), tid);
     int t = (int)blockIdx.x;
     if (t >= tw.total) return;
-    const uint32_t base1 = LT<RS::L1>::base(tid), base3 = LT<RS::L3>::base(tid);
+    const uint32_t base1 = LT<RS::L1>::base(tid), base3 = LT<kRowWs4 ? RS::L3F : RS::L3>::base(tid);
     int si; uint32_t tile;
     tw.at(t, si, tile);
     float nx[64];
-    fetch_ws(a, udesc(a.d, si), tile, true, base3, nx);
+    if constexpr (kRowWs4) fetch_ws4<RS::L3F>(a, udesc(a.d, si), tile, true, base3, nx);
+    else fetch_ws(a, udesc(a.d, si), tile, true, base3, nx);
     for (;;) {
         float v[64];
 #pragma unroll
@@ -1439,10 +1481,16 @@ __global__ __launch_bounds__(kRowNT) void k_dec_rowC(KArgs a) {
         const bool more = tn < tw.total;
         int sn; uint32_t tln;
         tw.at(more ? tn : t, sn, tln);
-        fetch_ws(a, udesc(a.d, sn), tln, more, base3, nx);
+        if constexpr (kRowWs4) fetch_ws4<RS::L3F>(a, udesc(a.d, sn), tln, more, base3, nx);
+        else fetch_ws(a, udesc(a.d, sn), tln, more, base3, nx);
         const uint32_t b1 = seed_b(sld(a.seeds, D.tensor));
-        stages<RS::L3, RS::F1c>(v);
-        exchange<RS::L3, RS::L2>(v, s, tid);
+        if constexpr (kRowWs4) {
+            stages<RS::L3F, RS::F1c>(v);
+            exchange<RS::L3F, RS::L2>(v, s, tid);
+        } else {
+            stages<RS::L3, RS::F1c>(v);
+            exchange<RS::L3, RS::L2>(v, s, tid);
+        }
         stages<RS::L2, RS::F1b>(v);
         exchange<RS::L2, RS::L1>(v, s, tid);
         stages<RS::L1, RS::F1a>(v);
@@ -1925,7 +1973,7 @@ struct DecA2Set {  // decode pass A, half bit 5: 0..4 | 11,12,13,14,5 | 6..10
     static constexpr uint32_t G1 = RS::F2e, G2 = bits_mask({11, 12, 13, 14, 5}), G3 = bits_mask({6, 7, 8, 9, 10});
 };
 struct DecC2Set {  // decode pass C, half bit 10: 7,8,9 | 2..6,10 | 0,1,11,12,13 | 14
-    static constexpr Lay B1 = RS::L3, B2 = RS::L2, B3{15, 0, 1, 11, 12, 13, 10}, B4{15, 0, 1, 14, 11, 12, 10};
+    static constexpr Lay B1 = kRowWs4 ? RS::L3F : RS::L3, B2 = RS::L2, B3{15, 0, 1, 11, 12, 13, 10}, B4{15, 0, 1, 14, 11, 12, 10};
     static constexpr uint32_t H1 = RS::F1c, H2 = RS::F1b, H3 = bits_mask({0, 1, 11, 12, 13}), H4 = bits_mask({14});
 };
 // apply_signs_direct in groups of 8 registers whose results are pinned before
@@ -2169,7 +2217,8 @@ __global__ __launch_bounds__(kRowNT, 4) void k_dec_rowC2(KArgs a) {
         row_locate(a, t, si, tile);
         const SliceDesc D = udesc(a.d, si);
         float v[64];
-        fetch_ws(a, D, tile, true, base1, v);
+        if constexpr (kRowWs4) fetch_ws4<R::B1>(a, D, tile, true, base1, v);
+        else fetch_ws(a, D, tile, true, base1, v);
         const uint32_t b1 = seed_b(sld(a.seeds, D.tensor));
         stages<R::B1, R::H1>(v);
         exchange_half_pad<R::B1, R::B2, 10>(v, s, tid);
@@ -3489,14 +3538,14 @@ int ofl_eden_plan_profile_collect(ofl_eden_plan_t pl, int encode, double* ms_sum
 
 // strict IEEE order: the library is built without fast-math/reassociation,
 // so the compiler keeps the dependent add chain (no vectorised partial sums).
-// Arrays of 2^16 elements and more go to the exact multi-threaded evaluation
+// Arrays of 2^20 elements and more go to the exact multi-threaded evaluation
 // of the same chain (csrc/serial_sum.cpp: binade-wise integer prefix sums).
 static float serial_sum_f32_loop(const float* x, int64_t n) {
     float s = 0.0f;
     for (int64_t i = 0; i < n; ++i) s = s + x[i];
     return s;
 }
-constexpr int64_t kSumMtMin = 1 << 16;
+constexpr int64_t kSumMtMin = 1 << 20;
 
 float ofl_serial_sum_f32(const float* x, int64_t n) {
     if (n >= kSumMtMin) return ofl::serial_sum_f32_mt_cb(x, n, nullptr, 0, nullptr, nullptr);

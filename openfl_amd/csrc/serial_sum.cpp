@@ -35,6 +35,8 @@
 // inputs: ties, binade crossings, zeros, subnormals, Inf / NaN).
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <cmath>
 #include <condition_variable>
 #include <cstdint>
@@ -59,8 +61,21 @@ struct Sub {
     int8_t tdel[kTieCap];
     int16_t ntie;
     int16_t e;   // guessed binade; kNoBinade: none (phase C runs the serial loop)
+    float up, down;  // 2^(23 - e), 2^(e - 23)
     double dsum;
 };
+// biased exponent field of a float (1..254: normal)
+inline int expo(float f) {
+    uint32_t b;
+    std::memcpy(&b, &f, 4);
+    return (int)((b >> 23) & 0xffu);
+}
+inline float pow2f(int k) {  // 2^k, -126 <= k <= 127
+    const uint32_t b = (uint32_t)(k + 127) << 23;
+    float f;
+    std::memcpy(&f, &b, 4);
+    return f;
+}
 constexpr int16_t kNoBinade = -32768;
 
 // A small persistent pool: try_run(n, w, f) calls f(0..n-1) on the caller and
@@ -131,48 +146,77 @@ float serial_loop(const float* x, int64_t n, float s) {
 void phase_b(const float* x, int len, Sub& b) {
     const float f = (float)b.dsum;  // estimate of the serial sum at the sub-chunk start
     b.e = kNoBinade;
-    if (!std::isnormal(f)) return;
-    const int e = std::ilogb(f);
+    const int be = expo(f);
+    if (be == 0 || be == 255) return;  // zero / subnormal / non-finite: serial loop
+    const int e = be - 127;
     if (e < -103) return;  // u = 2^(e-23) must be a normal float
-    const float scale = std::ldexp(1.0f, 23 - e);
-    int64_t p = 0, lo = INT64_MAX, hi = INT64_MIN;
-    int nt = 0;
-    bool nan = false;
+    const float scale = pow2f(23 - e);
+    // R and the tie flags: a branch-free loop the compiler vectorises.  An
+    // element with |x/u| > 2^22 (a step of more than a quarter of the sum)
+    // sends the sub-chunk to the serial loop, so the relative prefix fits
+    // int32 (|prefix| <= 256 * 2^22).
+    alignas(64) int32_t R[kG + 4];
+    alignas(64) int32_t tie[kG + 4];
+    int bad = 0;
     for (int j = 0; j < len; ++j) {
-        float q = x[j] * scale;  // exact (power-of-two scaling)
-        nan |= q != q;
-        // |R| >= 2^25 leaves the range whatever S0 is; the clamp keeps R in int range
-        q = q > 0x1p25f ? 0x1p25f : q;
-        q = q < -0x1p25f ? -0x1p25f : q;
-        // round half even: the 1.5 * 2^23 shift rounds in the FPU's default mode;
-        // |q| >= 2^23 is an integer already
-        const float m = (q + 0x1.8p23f) - 0x1.8p23f;
-        const float r = std::fabs(q) < 0x1p23f ? m : q;
-        if (std::fabs(q - r) == 0.5f) {
-            if (nt < kTieCap) {
-                b.tpre[nt] = p;
-                b.tdel[nt] = q > r ? 1 : -1;
-            }
-            ++nt;
-        }
-        p += (int64_t)r;
-        lo = p < lo ? p : lo;
-        hi = p > hi ? p : hi;
+        const float q = x[j] * scale;  // exact (power-of-two scaling)
+        bad |= !(std::fabs(q) <= 0x1p22f);  // also NaN
+        // round half even: the 1.5 * 2^23 shift rounds in the FPU's default mode
+        const float qc = std::fabs(q) <= 0x1p22f ? q : 0.0f;
+        const float r = (qc + 0x1.8p23f) - 0x1.8p23f;
+        // a tie's other candidate: +1 if q lies above r, -1 below (0: no tie)
+        tie[j] = std::fabs(qc - r) == 0.5f ? (qc > r ? 1 : -1) : 0;
+        R[j] = (int32_t)r;
     }
-    if (nan) return;
+    if (bad) return;
+    for (int j = len; j < ((len + 3) & ~3); ++j) R[j] = tie[j] = 0;  // ragged tail: zero steps
+    // the inclusive prefix, four lanes at a time, and its envelope
+    typedef int32_t i4 __attribute__((ext_vector_type(4)));
+    const i4 z = {0, 0, 0, 0};
+    i4 carry = z, mn = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX}, mx = {INT32_MIN, INT32_MIN, INT32_MIN, INT32_MIN};
+    int anytie = 0;
+    alignas(64) int32_t P[kG + 4];
+    for (int j = 0; j < len; j += 4) {
+        i4 v = *reinterpret_cast<const i4*>(R + j);
+        v += __builtin_shufflevector(z, v, 0, 4, 5, 6);
+        v += __builtin_shufflevector(z, v, 0, 1, 4, 5);
+        v += carry;
+        *reinterpret_cast<i4*>(P + j) = v;
+        carry = __builtin_shufflevector(v, v, 3, 3, 3, 3);
+        mn = v < mn ? v : mn;
+        mx = v > mx ? v : mx;
+        const i4 t = *reinterpret_cast<const i4*>(tie + j);
+        anytie |= (t.x | t.y | t.z | t.w);
+    }
+    // (lanes past len in a ragged last group hold P[len - 1]: a real partial sum)
+    int64_t lo = std::min(std::min(mn.x, mn.y), std::min(mn.z, mn.w));
+    int64_t hi = std::max(std::max(mx.x, mx.y), std::max(mx.z, mx.w));
+    const int64_t p = P[len - 1];
+    int nt = 0;
+    if (anytie)
+        for (int j = 0; j < len; ++j)
+            if (tie[j]) {
+                if (nt < kTieCap) {
+                    b.tpre[nt] = P[j] - R[j];  // the prefix before element j
+                    b.tdel[nt] = (int8_t)tie[j];
+                }
+                ++nt;
+            }
     if (nt > kTieCap) return;
     b.pre_end = p;
     b.lo = lo;
     b.hi = hi;
     b.ntie = (int16_t)nt;
+    b.up = scale;
+    b.down = pow2f(e - 23);
     b.e = (int16_t)e;
 }
 
 // exact continuation of s over one sub-chunk through its phase-B summary;
 // false: the summary does not apply (the caller runs the serial loop)
 bool phase_c(const Sub& b, float& s) {
-    if (b.e == kNoBinade || !std::isnormal(s) || std::ilogb(s) != b.e) return false;
-    const int64_t S0 = (int64_t)std::ldexp(s, 23 - b.e);  // exact integer in [2^23, 2^24)
+    if (b.e == kNoBinade || expo(s) - 127 != b.e) return false;  // also rejects 0 / subnormal / Inf / NaN
+    const int64_t S0 = (int64_t)(s * b.up);  // exact integer in [2^23, 2^24) in magnitude
     const int64_t nt = b.ntie;
     if (S0 > 0 ? !(S0 + b.lo - nt >= kLo && S0 + b.hi + nt <= kHi)
                : !(S0 + b.hi + nt <= -kLo && S0 + b.lo - nt >= -kHi))
@@ -180,8 +224,16 @@ bool phase_c(const Sub& b, float& s) {
     int64_t c = 0;
     for (int t = 0; t < nt; ++t)
         if ((S0 + b.tpre[t] + c) & 1) c += b.tdel[t];
-    s = std::ldexp((float)(S0 + b.pre_end + c), b.e - 23);  // |S| < 2^24: exact
+    s = (float)(S0 + b.pre_end + c) * b.down;  // |S| < 2^24, a power-of-two scale: exact
     return true;
+}
+
+double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+bool debug_on() {
+    static const bool on = [] { const char* v = std::getenv("OFL_SUM_DEBUG"); return v && v[0] == '1'; }();
+    return on;
 }
 
 int default_threads() {
@@ -208,6 +260,7 @@ float serial_sum_f32_mt_cb(const float* x, int64_t n, float* dst, int nthreads, 
         return serial_loop(x, n, 0.0f);
     };
     if (nthreads <= 1 || K < 64) return plain();
+    const double t0 = debug_on() ? now_s() : 0.0;
     std::vector<Sub> subs(K);
     const int parts = (int)std::min<int64_t>(nthreads * 4, K);
     auto range = [&](int i, int64_t& k0, int64_t& k1) {
@@ -236,6 +289,7 @@ float serial_sum_f32_mt_cb(const float* x, int64_t n, float* dst, int nthreads, 
     };
     if (!Pool::get().try_run(parts, nthreads - 1, fa)) return plain();
     if (after_copy) after_copy(ctx);
+    const double t1 = debug_on() ? now_s() : 0.0;
     double run = 0.0;  // dsum -> the estimate at each sub-chunk's start
     for (int64_t k = 0; k < K; ++k) {
         const double d = subs[k].dsum;
@@ -251,9 +305,18 @@ float serial_sum_f32_mt_cb(const float* x, int64_t n, float* dst, int nthreads, 
     if (!Pool::get().try_run(parts, nthreads - 1, fb))
         for (int i = 0; i < parts; ++i) fb(i);
     // phase C: in order, exact
+    const double t2 = debug_on() ? now_s() : 0.0;
     float s = 0.0f;
+    int64_t serial = 0;
     for (int64_t k = 0; k < K; ++k)
-        if (!phase_c(subs[k], s)) s = serial_loop(x + k * kG, std::min<int64_t>(kG, n - k * kG), s);
+        if (!phase_c(subs[k], s)) {
+            s = serial_loop(x + k * kG, std::min<int64_t>(kG, n - k * kG), s);
+            ++serial;
+        }
+    if (debug_on())
+        std::fprintf(stderr, "[ofl sum] n=%lld threads=%d A %.1f us B %.1f us C %.1f us serial sub-chunks %lld/%lld\n",
+                     (long long)n, nthreads, 1e6 * (t1 - t0), 1e6 * (t2 - t1), 1e6 * (now_s() - t2),
+                     (long long)serial, (long long)K);
     return s;
 }
 

@@ -9,4 +9,4 @@ C=$R/openfl_amd/csrc
 mkdir -p "$(dirname "$OUT")"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -std=c++20 -O3 -fPIC -shared -Wno-unused-function "$@" \
     -I"$R"/include -I"$C" -o "$OUT" "$C"/eden_kernels.hip "$C"/lossy_kernels.hip "$C"/agg_kernels.hip \
-    "$C"/deflate_kernels.hip -lz
+    "$C"/deflate_kernels.hip "$C"/serial_sum.cpp -lz
