@@ -97,7 +97,7 @@ class Pool {
             njob_ = n;
             next_.store(1);
             pending_ = (int)th_.size();  // every worker checks in once per job
-            ++gen_;
+            gen_.fetch_add(1, std::memory_order_release);
         }
         cv_.notify_all();
         f(0);
@@ -115,12 +115,15 @@ class Pool {
     void loop() {
         int seen = 0;
         for (;;) {
+            // a plugin call's phases come back to back: spin briefly (~2000 pauses)
+            // before sleeping, so a wake-up does not cost a futex round trip
+            for (int i = 0; i < 2000 && gen_.load(std::memory_order_acquire) == seen; ++i) __builtin_ia32_pause();
             const std::function<void(int)>* f;
             int n;
             {
                 std::unique_lock<std::mutex> g(m_);
-                cv_.wait(g, [&] { return gen_ != seen; });
-                seen = gen_;
+                cv_.wait(g, [&] { return gen_.load(std::memory_order_relaxed) != seen; });
+                seen = gen_.load(std::memory_order_relaxed);
                 f = job_;
                 n = njob_;
             }
@@ -134,7 +137,8 @@ class Pool {
     std::condition_variable cv_, done_;
     std::vector<std::thread> th_;
     const std::function<void(int)>* job_ = nullptr;
-    int njob_ = 0, pending_ = 0, gen_ = 0;
+    int njob_ = 0, pending_ = 0;
+    std::atomic<int> gen_{0};
     std::atomic<int> next_{0};
 };
 
