@@ -1452,6 +1452,8 @@ __global__ __launch_bounds__(kRowNT) void k_dec_rowA(KArgs a) {
         stages<RS::L4, RS::F2d>(v);
         exchange<RS::L4, RS::L3>(v, s, tid);
         stages<RS::L3, RS::F2c>(v);
+        // (one more exchange to L3F for float4 stores: 494 -> 533 us per wave,
+        // profiles/r03_deca_ws4_ab.txt)
         store_ws(a, D, tile, base3, v);
         if (!more) break;
         t = tn; si = sn; tile = tln;
