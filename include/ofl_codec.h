@@ -105,6 +105,13 @@ int ofl_eden_plan_set_row2(ofl_eden_plan_t plan, int mode);
  * 1024-thread workgroups for all of them, 0 one launch per size class, -1 the
  * default (1; env OFL_EDEN_SSET=0 selects 0).  Before the first encode/decode. */
 int ofl_eden_plan_set_sset(ofl_eden_plan_t plan, int mode);
+/* A plan whose large slices fit one wave and whose single-level middle passes
+ * share one k_col_multi launch runs its small-set groups inside that launch,
+ * on the caller's stream (no side stream, no fork / join): 1 yes, 0 the
+ * small-set launch on the side stream, -1 the default (1; env
+ * OFL_EDEN_FUSESET=0 selects 0).  Outputs bit-identical either way.  Before
+ * the first encode/decode. */
+int ofl_eden_plan_set_fuse(ofl_eden_plan_t plan, int mode);
 
 /* Totals: slices (= length of the scales array), planes-arena bytes,
  * workspace bytes needed by encode and decode. */

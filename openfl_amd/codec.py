@@ -38,13 +38,15 @@ class EdenPlan:
     """Layout + launch plan for one batch shape (list of numels, optional dims)."""
 
     def __init__(self, numels, n_bits=8, dims=None, elem_offsets=None, wave_mib=None, streams=None, row2=None,
-                 sset=None):
+                 sset=None, fuse=None):
         """wave_mib / streams: large-slice schedule (ofl_eden_plan_set_schedule;
         None keeps the library default); row2: row-pass kernels
         (ofl_eden_plan_set_row2: None/-1 auto, 0 persistent, 1 two blocks per
         CU); sset: tiny / small slices in one launch (ofl_eden_plan_set_sset:
-        None/-1 default, 0 one launch per size class, 1 one launch).  Outputs
-        do not depend on any of them."""
+        None/-1 default, 0 one launch per size class, 1 one launch); fuse:
+        that launch inside a one-wave plan's column launch on the caller's
+        stream (ofl_eden_plan_set_fuse: None/-1 default, 0 no, 1 yes).
+        Outputs do not depend on any of them."""
         L = _lib.lib()
         self.n_bits = int(n_bits)
         self.numels = [int(n) for n in numels]
@@ -78,6 +80,8 @@ class EdenPlan:
             _lib.check(L.ofl_eden_plan_set_row2(h, int(row2)))
         if sset is not None:
             _lib.check(L.ofl_eden_plan_set_sset(h, int(sset)))
+        if fuse is not None:
+            _lib.check(L.ofl_eden_plan_set_fuse(h, int(fuse)))
         self.n_waves = int(L.ofl_eden_plan_num_waves(h))
         wb, ns = ctypes.c_int64(), ctypes.c_int()
         _lib.check(L.ofl_eden_plan_get_schedule(h, ctypes.byref(wb), ctypes.byref(ns)))

@@ -44,6 +44,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <set>
 #include <atomic>
 #include <mutex>
 #include <thread>
@@ -105,6 +106,10 @@ struct KArgs {
     const float* wbase;     // base model arena, nullable
     double wsum;            // NumPy's float64 sum of the weights
     int32_t wc;             // collaborators (1..16)
+    // fused column + small-set launches (k_enc_colm_set / k_dec_colm_set):
+    // blocks < sset_first run the small-set groups of table sset
+    const int32_t* sset;
+    int32_t sset_first;
 };
 
 // Eden centroids in global memory (copied to LDS per workgroup); the
@@ -962,11 +967,12 @@ DEVI void dec_set_group(const KArgs& a, const int32_t* sl, unsigned char* sm, co
 // threads of a group's sub-blocks (whole waves: every NT >= 64)
 DEVI int set_active(int P, int cnt) { return cnt * (P ? (1 << (P - 5)) : kTinyNT); }
 
-__global__ __launch_bounds__(kSetNT) void k_enc_sset(KArgs a) {
+// workgroup b of a small-set launch (a.list: its group table)
+DEVI void enc_sset_block(const KArgs& a, int b) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     QTab* qt = reinterpret_cast<QTab*>(smem + kSetBody);
     float* red = reinterpret_cast<float*>(qt + 1);
-    const int32_t* g = a.list + 3 * blockIdx.x;
+    const int32_t* g = a.list + 3 * b;
     const int P = g[0], cnt = g[2];
     const int32_t* sl = a.list + g[1];
     // waves past the group's sub-blocks end here: a workgroup barrier waits
@@ -991,11 +997,12 @@ __global__ __launch_bounds__(kSetNT) void k_enc_sset(KArgs a) {
     }
     }
 }
+__global__ __launch_bounds__(kSetNT) void k_enc_sset(KArgs a) { enc_sset_block(a, (int)blockIdx.x); }
 
-__global__ __launch_bounds__(kSetNT) void k_dec_sset(KArgs a) {
+DEVI void dec_sset_block(const KArgs& a, int b) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float* cen = reinterpret_cast<float*>(smem + kSetBody);
-    const int32_t* g = a.list + 3 * blockIdx.x;
+    const int32_t* g = a.list + 3 * b;
     const int P = g[0], cnt = g[2];
     const int32_t* sl = a.list + g[1];
     const int act = set_active(P, cnt);
@@ -1013,6 +1020,7 @@ __global__ __launch_bounds__(kSetNT) void k_dec_sset(KArgs a) {
     }
     }
 }
+__global__ __launch_bounds__(kSetNT) void k_dec_sset(KArgs a) { dec_sset_block(a, (int)blockIdx.x); }
 
 // ===========================================================================
 // Large slices (P >= 2^16): row passes over contiguous 2^15-element rows,
@@ -1636,8 +1644,7 @@ __global__ __launch_bounds__(kColNT) void k_col(KArgs a) {
 // {M, list, tstart (both relative to the table), count, first block};
 // a.count = groups.
 constexpr int kColGroup = 5;
-__global__ __launch_bounds__(kColNT) void k_col_multi(KArgs a) {
-    const int b = (int)blockIdx.x;
+DEVI void col_multi_block(const KArgs& a, int b) {
     int g = 0;
     if (a.btab) {
         g = a.btab[2 * b + 1] & 7;
@@ -1658,6 +1665,35 @@ __global__ __launch_bounds__(kColNT) void k_col_multi(KArgs a) {
     case 4: col_body<4, true>(a2, lb); break;
     default: col_body<5, true>(a2, lb); break;
     }
+}
+__global__ __launch_bounds__(kColNT) void k_col_multi(KArgs a) { col_multi_block(a, (int)blockIdx.x); }
+
+// One launch for a one-wave plan's small-set groups (blocks < a.sset_first,
+// dispatched first: each is longer than a column tile) AND its single-level
+// middle passes: the small slices share the CUs with the column tiles, in the
+// caller's stream, so the call needs no side
+// stream and no cross-queue fork / join (each join cost ~10 us of the caller's
+// queue).  Both parts are the bodies of k_col_multi and
+// k_enc_sset / k_dec_sset: outputs identical to those launches.
+__global__ __launch_bounds__(kColNT) void k_enc_colm_set(KArgs a) {
+    const int b = (int)blockIdx.x;
+    if (b < a.sset_first) {
+        KArgs s = a;
+        s.list = a.sset;
+        enc_sset_block(s, b);
+        return;
+    }
+    col_multi_block(a, b - a.sset_first);
+}
+__global__ __launch_bounds__(kColNT) void k_dec_colm_set(KArgs a) {
+    const int b = (int)blockIdx.x;
+    if (b < a.sset_first) {
+        KArgs s = a;
+        s.list = a.sset;
+        dec_sset_block(s, b);
+        return;
+    }
+    col_multi_block(a, b - a.sset_first);
 }
 
 // ===========================================================================
@@ -2288,10 +2324,12 @@ struct Launch {
     int join = 0;    // the caller's stream waits for the side stream before this launch
     int tl = 15;     // column: log2 of the tile (16: k_col6 with 1024 threads)
     int btab_off = -1;  // column: per-block {slice, tile << 3 | group} table in ints
+    int sset_off = -1;  // K_COLMSET: the small-set group table in ints
+    int sset_groups = 0;  // K_COLMSET: its groups (the launch's first blocks)
     int64_t bytes_moved = 0;  // fp32/plane bytes this launch reads + writes (intermediates included)
     int64_t bytes_alg = 0;    // its share of the SURVEY 8(d) algorithmic bytes (x/y fp32 + planes only)
 };
-enum Kind { K_TINY, K_SMALL, K_ROWA, K_ROWC, K_COL, K_FINAL, K_COLM, K_SSET };
+enum Kind { K_TINY, K_SMALL, K_ROWA, K_ROWC, K_COL, K_FINAL, K_COLM, K_SSET, K_COLMSET };
 
 }  // namespace
 
@@ -2314,6 +2352,8 @@ struct ofl_eden_plan {
     int nwaves = 0;
     int row2 = -1;              // row launches on the two-blocks-per-CU kernels: -1 auto, 0 never, 1 always
     int sset = -1;              // tiny / small slices in one small-set launch: -1 env default, 0 no, 1 yes
+    int fuse = -1;              // small-set groups fused into the column launch: -1 env default, 0 no, 1 yes
+    bool single = false;        // every launch on the caller's stream (no fork / join) -- K_COLMSET plans
     std::vector<Launch> enc, dec;
     std::vector<int32_t> ints;  // launch lists and tile prefixes (host copy)
     // profiling: events around every launch of every call while enabled
@@ -2481,6 +2521,13 @@ int64_t split_min_bytes() {
     }();
     return b;
 }
+// one-wave plans with a k_col_multi launch and a small-set launch fuse the
+// two into one launch on the caller's stream (OFL_EDEN_FUSESET=0: the
+// small-set launch beside the wave on the side stream)
+bool use_fuse_sset() {
+    static const bool on = [] { const char* s = getenv("OFL_EDEN_FUSESET"); return !(s && s[0] == '0'); }();
+    return on;
+}
 // one k_col_multi launch per wave for the single-level heights 1..5
 bool use_colmulti() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_COLMULTI"); return !(s && s[0] == '0'); }();
@@ -2496,6 +2543,8 @@ hipError_t set_all_attrs() {
     if ((e = set_small_attr<15>()) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_enc_sset, ofl::kSetSmemEnc)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_dec_sset, ofl::kSetSmemDec)) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_enc_colm_set, ofl::kSetSmemEnc)) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_dec_colm_set, ofl::kSetSmemDec)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_enc_rowA, ofl::kRowSmemA)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_enc_rowC, ofl::kRowSmemQ)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_enc_rowC2<true>, ofl::kRowC2Smem)) != hipSuccess) return e;
@@ -2527,7 +2576,7 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
     if (attrs_err != hipSuccess) return fail(OFL_EHIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(attrs_err));
     const std::vector<Launch>& L = enc ? pl->enc : pl->dec;
     // waves on the side stream fork from and join back into the caller's stream
-    const bool two = pl->side != nullptr;
+    const bool two = pl->side != nullptr && !pl->single;
     std::unique_lock<std::mutex> lk(pl->run_mu, std::defer_lock);
     if (two) {
         lk.lock();
@@ -2666,6 +2715,12 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
         }
         case K_FINAL: e = launch(ofl::k_finalize, l.blocks, 256, 0, st, a); break;
         case K_COLM: e = launch(ofl::k_col_multi, l.blocks, ofl::kColNT, ofl::kColTab, st, a); break;
+        case K_COLMSET:
+            a.sset = pl->d_ints + l.sset_off;
+            a.sset_first = (int32_t)l.sset_groups;
+            e = enc ? launch(ofl::k_enc_colm_set, l.blocks, ofl::kColNT, ofl::kSetSmemEnc, st, a)
+                    : launch(ofl::k_dec_colm_set, l.blocks, ofl::kColNT, ofl::kSetSmemDec, st, a);
+            break;
         }
         if (e != hipSuccess) return fail(OFL_EHIP, std::string("kernel launch failed: ") + hipGetErrorString(e));
         if (evs) HIP_TRY(hipEventRecord((*evs)[2 * li + 1], st));
@@ -2702,6 +2757,7 @@ std::string launch_name(const Launch& l, bool enc, int ncu, int row2) {
                std::to_string(l.param) + ", " + (l.mid ? "true" : "false") +
                ((l.param >= 8 || (l.param >= 6 && l.mid)) && use_col6() ? ", 15>" : ">");
     case K_COLM: return "ofl::k_col_multi";
+    case K_COLMSET: return std::string("ofl::k_") + d + "_colm_set";
     default: return "ofl::k_finalize";
     }
 }
@@ -2842,6 +2898,23 @@ void build_schedule(ofl_eden_plan* pl) {
     // decode row A reads 8-byte plane words when every plane row is 8-byte aligned
     int a8 = 1;
     for (int32_t si : large) a8 &= (pl->slices[si].pl_off % 8 == 0) && (pl->slices[si].pl_stride % 8 == 0);
+    // one wave with a k_col_multi launch and one small-set launch: fused
+    // (k_*_colm_set), everything on the caller's stream
+    bool fuse = false;
+    if ((pl->fuse >= 0 ? pl->fuse == 1 : use_fuse_sset()) && use_colmulti() && waves.size() == 1 && common.size() == 1 && common[0].kind == K_SSET) {
+        std::set<int> hs;
+        for (int32_t si : waves[0]) {
+            const int r = pl->slices[si].logp - ofl::kRowLog;
+            if (r >= 1 && r <= 5) hs.insert(r);
+        }
+        fuse = hs.size() >= 2;  // the condition for the k_col_multi launch below
+    }
+    pl->single = fuse;
+    if (fuse) {
+        pl->enc.clear();
+        pl->dec.clear();
+        for (Launch& l : common) l.stream = 0;
+    }
     for (size_t w = 0; w < waves.size(); ++w) {
         const std::vector<int32_t>& wl = waves[w];
         const int s = (int)(w % nbuf);
@@ -2877,6 +2950,12 @@ void build_schedule(ofl_eden_plan* pl) {
             Launch l{K_COLM, 0, ofl::kRowLog, 1, gt, -1, (int)mg.size(), blk};
             l.stream = s;
             l.bytes_moved = mv;
+            if (fuse) {  // the small-set groups ride in this launch (its first blocks)
+                l.kind = K_COLMSET;
+                l.sset_off = common[0].list_off;
+                l.sset_groups = common[0].count;
+                l.blocks += common[0].count;
+            }
             cd.push_back(l);
             l.nu = 1;  // encode: every group is a slice's first (only) column launch
             ce.push_back(l);
@@ -2923,7 +3002,7 @@ void build_schedule(ofl_eden_plan* pl) {
         pl->dec.insert(pl->dec.end(), cd.begin(), cd.end());
         pl->dec.push_back(rc);
     }
-    if (small_last) {
+    if (small_last && !fuse) {
         pl->enc.insert(pl->enc.end(), common.begin(), common.end());
         pl->dec.insert(pl->dec.end(), common.begin(), common.end());
     }
@@ -2960,20 +3039,20 @@ void build_schedule(ofl_eden_plan* pl) {
             };
             if (l.kind == K_COL) {
                 add_group(l.list_off, l.tstart_off, l.count, 0);
-            } else {  // K_COLM: l.count groups {M, list, tstart (relative), count, first block}
+            } else {  // K_COLM / K_COLMSET: l.count groups {M, list, tstart (relative), count, first block}
                 for (int g = 0; g < l.count; ++g) {
                     const int32_t* G = &ints[l.list_off + ofl::kColGroup * g];
                     add_group(l.list_off + G[1], l.list_off + G[2], G[3], g);
                 }
             }
-            if ((int64_t)t.size() != 2 * l.blocks) return;  // inconsistent: keep the search
+            if ((int64_t)t.size() != 2 * (l.blocks - l.sset_groups)) return;  // inconsistent: keep the search
             l.btab_off = (int)ints.size();
             made[key] = l.btab_off;
             ints.insert(ints.end(), t.begin(), t.end());
         };
         for (auto* L : {&pl->enc, &pl->dec})
             for (Launch& l : *L)
-                if (l.kind == K_COL || l.kind == K_COLM) table(l);
+                if (l.kind == K_COL || l.kind == K_COLM || l.kind == K_COLMSET) table(l);
     }
     // per-launch byte accounting (bench / DESIGN.md roofline)
     const int64_t n_bits = pl->nbits;
@@ -2982,14 +3061,18 @@ void build_schedule(ofl_eden_plan* pl) {
         for (Launch& l : enc ? pl->enc : pl->dec) {
             if (l.kind == K_COLM) continue;  // counted when built (its list is a group table)
             int64_t mv = 0, al = 0;
-            if (l.kind == K_SSET) {  // group table {P, offset, count}, then the slice ids
-                for (int g = 0; g < l.count; ++g)
-                    for (int i = 0; i < ints[l.list_off + 3 * g + 2]; ++i) {
-                        const ofl::SliceDesc& D = pl->slices[ints[l.list_off + ints[l.list_off + 3 * g + 1] + i]];
+            if (l.kind == K_SSET || l.kind == K_COLMSET) {  // group table {P, offset, count}, then the slice ids
+                const int to = l.kind == K_SSET ? l.list_off : l.sset_off;
+                const int ng = l.kind == K_SSET ? l.count : l.sset_groups;
+                for (int g = 0; g < ng; ++g)
+                    for (int i = 0; i < ints[to + 3 * g + 2]; ++i) {
+                        const ofl::SliceDesc& D = pl->slices[ints[to + ints[to + 3 * g + 1] + i]];
                         const int64_t pb = n_bits * (1ll << D.logp) / 8;
                         mv += enc ? 4 * D.len + pb : pb + 4 * D.ylen;
                     }
-                l.bytes_moved = l.bytes_alg = mv;
+                if (l.kind == K_SSET) l.bytes_moved = mv;
+                else l.bytes_moved += mv;  // + the column part, counted when built
+                l.bytes_alg = mv;
                 continue;
             }
             for (int i = 0; i < l.count; ++i) {
@@ -3221,6 +3304,16 @@ int ofl_eden_plan_set_sset(ofl_eden_plan_t pl, int mode) {
     std::lock_guard<std::mutex> g(pl->mu);
     if (pl->uploaded) return fail(OFL_EINVAL, "sset must be set before the plan's first encode/decode");
     pl->sset = mode;
+    build_schedule(pl);
+    return OFL_OK;
+}
+
+int ofl_eden_plan_set_fuse(ofl_eden_plan_t pl, int mode) {
+    if (!pl) return fail(OFL_EINVAL, "null plan");
+    if (mode < -1 || mode > 1) return fail(OFL_EINVAL, "fuse mode must be -1 (default), 0 or 1");
+    std::lock_guard<std::mutex> g(pl->mu);
+    if (pl->uploaded) return fail(OFL_EINVAL, "fuse must be set before the plan's first encode/decode");
+    pl->fuse = mode;
     build_schedule(pl);
     return OFL_OK;
 }

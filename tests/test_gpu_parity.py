@@ -360,6 +360,36 @@ def test_schedules_bit_identical():
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("streams", [1, 2])
+def test_fused_small_set_bit_identical(streams):
+    """The small-set groups inside a one-wave plan's k_col_multi launch
+    (k_*_colm_set, every launch on the caller's stream) give the same planes,
+    scales and decoded values as the small-set launch on its own (ResNet-50's
+    slice sizes: tiny, small, heights 1..6)."""
+    from openfl_amd.codec import EdenPlan
+    from openfl_amd.workloads import WORKLOADS, numel
+    numels = [numel(s) for _, s in WORKLOADS["resnet50_fp32"]() if numel(s) > 100]
+    g = torch.Generator(device=DEV).manual_seed(5)
+    sd = torch.tensor([(31 * t + 7) % 65536 for t in range(len(numels))], dtype=torch.int32, device=DEV)
+    c = _codec(8)
+    outs = {}
+    arena = None
+    for fuse in (1, 0):
+        plan = EdenPlan(numels, 8, streams=streams, fuse=fuse)
+        names = [l["name"] for l in plan.launches(True)]
+        assert ("ofl::k_enc_colm_set" in names) == (fuse == 1), names
+        if arena is None:
+            arena = torch.empty(plan.arena_numel, device=DEV).normal_(0, 0.01, generator=g)
+        planes, scales = c.encode_arena(plan, arena, sd)
+        y = c.decode_arena(plan, planes, scales, sd)
+        torch.cuda.synchronize()
+        outs[fuse] = (torch.cat([planes[o:o + b] for o, b in zip(plan.planes_offsets, plan.planes_nbytes)]),
+                      scales[:plan.n_slices].clone(),
+                      torch.cat([y[o:o + n] for o, n in zip(plan.elem_offsets, numels)]))
+    for a, b in zip(outs[1], outs[0]):
+        assert torch.equal(a, b)
+
+
 # --------------------------------------------------------- plugin surface ---
 @pytest.mark.parametrize("rec", IDX["forward"], ids=lambda r: r["tag"])
 def test_pipeline_forward_backward_vs_reference(rec):
