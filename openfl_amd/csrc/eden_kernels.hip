@@ -1638,12 +1638,14 @@ __global__ __launch_bounds__(kColNT) void k_col(KArgs a) {
     col_body<M, MID>(a, (int)blockIdx.x);
 }
 
-// Several single-level middle passes (heights M = 1..5) in one launch: a
+// Several single-level middle passes (heights M = 1..6) in one launch: a
 // wave's slices of different sizes share the grid instead of running one
 // short launch per height.  a.list -> table of kColGroup ints per group
 // {M, list, tstart (both relative to the table), count, first block};
-// a.count = groups.
+// a.count = groups.  Height 6 needs col_body's exchange buffer: the launch
+// takes kColMultiSmem.
 constexpr int kColGroup = 5;
+constexpr size_t kColMultiSmem = kColSmem + kColTab;
 DEVI void col_multi_block(const KArgs& a, int b) {
     int g = 0;
     if (a.btab) {
@@ -1663,7 +1665,8 @@ DEVI void col_multi_block(const KArgs& a, int b) {
     case 2: col_body<2, true>(a2, lb); break;
     case 3: col_body<3, true>(a2, lb); break;
     case 4: col_body<4, true>(a2, lb); break;
-    default: col_body<5, true>(a2, lb); break;
+    case 5: col_body<5, true>(a2, lb); break;
+    default: col_body<6, true>(a2, lb); break;
     }
 }
 __global__ __launch_bounds__(kColNT) void k_col_multi(KArgs a) { col_multi_block(a, (int)blockIdx.x); }
@@ -2528,7 +2531,19 @@ bool use_fuse_sset() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_FUSESET"); return !(s && s[0] == '0'); }();
     return on;
 }
-// one k_col_multi launch per wave for the single-level heights 1..5
+// height-6 middle passes (2^21 slices) run col_body<6> (1024 threads, the
+// k_col arithmetic) and join the k_col_multi launch of the smaller heights;
+// OFL_EDEN_COLM6=0: their own k_col6<6, true, 15> launch after it (A/B; the
+// two differ in the order of the row butterflies after D2, so their bytes
+// differ slightly -- every schedule of one setting is bit-identical)
+bool use_colm6() {
+    static const bool on = [] { const char* s = getenv("OFL_EDEN_COLM6"); return !(s && s[0] == '0'); }();
+    return on;
+}
+// lowest middle-pass height that runs k_col6 (7 when height 6 runs col_body<6>:
+// a standalone height-6 launch then uses k_col<6, true> too)
+int col6_mid_min() { return use_colm6() ? 7 : 6; }
+// one k_col_multi launch per wave for the single-level heights 1..5 (6)
 bool use_colmulti() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_COLMULTI"); return !(s && s[0] == '0'); }();
     return on;
@@ -2543,8 +2558,9 @@ hipError_t set_all_attrs() {
     if ((e = set_small_attr<15>()) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_enc_sset, ofl::kSetSmemEnc)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_dec_sset, ofl::kSetSmemDec)) != hipSuccess) return e;
-    if ((e = set_lds((const void*)ofl::k_enc_colm_set, ofl::kSetSmemEnc)) != hipSuccess) return e;
-    if ((e = set_lds((const void*)ofl::k_dec_colm_set, ofl::kSetSmemDec)) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_enc_colm_set, std::max(ofl::kSetSmemEnc, ofl::kColMultiSmem))) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_dec_colm_set, std::max(ofl::kSetSmemDec, ofl::kColMultiSmem))) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_col_multi, ofl::kColMultiSmem)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_enc_rowA, ofl::kRowSmemA)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_enc_rowC, ofl::kRowSmemQ)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_enc_rowC2<true>, ofl::kRowC2Smem)) != hipSuccess) return e;
@@ -2685,7 +2701,7 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
                                           : launch(ofl::k_col6<10, false, 16>, l.blocks, 1024, sm, st, a));
                 break;
             }
-            if ((l.param >= 8 || (l.param >= 6 && l.mid)) && use_col6()) {
+            if ((l.param >= 8 || (l.param >= col6_mid_min() && l.mid)) && use_col6()) {
                 const size_t sm = col6_smem(l.param, l.mid != 0, 15);
 #define COL6CASE(MM)                                                                                 \
     case MM:                                                                                         \
@@ -2714,12 +2730,12 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
             break;
         }
         case K_FINAL: e = launch(ofl::k_finalize, l.blocks, 256, 0, st, a); break;
-        case K_COLM: e = launch(ofl::k_col_multi, l.blocks, ofl::kColNT, ofl::kColTab, st, a); break;
+        case K_COLM: e = launch(ofl::k_col_multi, l.blocks, ofl::kColNT, ofl::kColMultiSmem, st, a); break;
         case K_COLMSET:
             a.sset = pl->d_ints + l.sset_off;
             a.sset_first = (int32_t)l.sset_groups;
-            e = enc ? launch(ofl::k_enc_colm_set, l.blocks, ofl::kColNT, ofl::kSetSmemEnc, st, a)
-                    : launch(ofl::k_dec_colm_set, l.blocks, ofl::kColNT, ofl::kSetSmemDec, st, a);
+            e = enc ? launch(ofl::k_enc_colm_set, l.blocks, ofl::kColNT, std::max(ofl::kSetSmemEnc, ofl::kColMultiSmem), st, a)
+                    : launch(ofl::k_dec_colm_set, l.blocks, ofl::kColNT, std::max(ofl::kSetSmemDec, ofl::kColMultiSmem), st, a);
             break;
         }
         if (e != hipSuccess) return fail(OFL_EHIP, std::string("kernel launch failed: ") + hipGetErrorString(e));
@@ -2753,9 +2769,9 @@ std::string launch_name(const Launch& l, bool enc, int ncu, int row2) {
         return std::string("ofl::k_") + d + "_rowC";
     case K_COL:
         if (l.tl == 16) return "ofl::k_col6<" + std::to_string(l.param) + ", " + (l.mid ? "true" : "false") + ", 16>";
-        return std::string((l.param >= 8 || (l.param >= 6 && l.mid)) && use_col6() ? "ofl::k_col6<" : "ofl::k_col<") +
+        return std::string((l.param >= 8 || (l.param >= col6_mid_min() && l.mid)) && use_col6() ? "ofl::k_col6<" : "ofl::k_col<") +
                std::to_string(l.param) + ", " + (l.mid ? "true" : "false") +
-               ((l.param >= 8 || (l.param >= 6 && l.mid)) && use_col6() ? ", 15>" : ">");
+               ((l.param >= 8 || (l.param >= col6_mid_min() && l.mid)) && use_col6() ? ", 15>" : ">");
     case K_COLM: return "ofl::k_col_multi";
     case K_COLMSET: return std::string("ofl::k_") + d + "_colm_set";
     default: return "ofl::k_finalize";
@@ -2900,12 +2916,13 @@ void build_schedule(ofl_eden_plan* pl) {
     for (int32_t si : large) a8 &= (pl->slices[si].pl_off % 8 == 0) && (pl->slices[si].pl_stride % 8 == 0);
     // one wave with a k_col_multi launch and one small-set launch: fused
     // (k_*_colm_set), everything on the caller's stream
+    const int mmax = use_colm6() ? 6 : 5;
     bool fuse = false;
     if ((pl->fuse >= 0 ? pl->fuse == 1 : use_fuse_sset()) && use_colmulti() && waves.size() == 1 && common.size() == 1 && common[0].kind == K_SSET) {
         std::set<int> hs;
         for (int32_t si : waves[0]) {
             const int r = pl->slices[si].logp - ofl::kRowLog;
-            if (r >= 1 && r <= 5) hs.insert(r);
+            if (r >= 1 && r <= mmax) hs.insert(r);
         }
         fuse = hs.size() >= 2;  // the condition for the k_col_multi launch below
     }
@@ -2924,10 +2941,11 @@ void build_schedule(ofl_eden_plan* pl) {
         std::map<int, std::vector<int32_t>> byp;  // column launches grouped by p
         for (int32_t si : wl) byp[pl->slices[si].logp].push_back(si);
         std::vector<Launch> ce, cd;
-        std::vector<std::pair<int, const std::vector<int32_t>*>> mg;  // heights 1..5 -> one k_col_multi
+        // heights 1..5 (6) -> one k_col_multi
+        std::vector<std::pair<int, const std::vector<int32_t>*>> mg;
         if (use_colmulti()) {
             for (auto& kv : byp)
-                if (kv.first - ofl::kRowLog >= 1 && kv.first - ofl::kRowLog <= 5) mg.push_back({kv.first - ofl::kRowLog, &kv.second});
+                if (kv.first - ofl::kRowLog >= 1 && kv.first - ofl::kRowLog <= mmax) mg.push_back({kv.first - ofl::kRowLog, &kv.second});
             if (mg.size() < 2) mg.clear();
         }
         if (!mg.empty()) {
@@ -2962,7 +2980,7 @@ void build_schedule(ofl_eden_plan* pl) {
         }
         for (auto& kv : byp) {
             const int r = kv.first - ofl::kRowLog;
-            if (!mg.empty() && r >= 1 && r <= 5) continue;  // in the k_col_multi launch
+            if (!mg.empty() && r >= 1 && r <= mmax) continue;  // in the k_col_multi launch
             int64_t tiles = 0;
             const int lo_c = add_list(kv.second);
             const int tp = add_prefix(kv.second, ofl::kColLog, tiles);
