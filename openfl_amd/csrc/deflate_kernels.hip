@@ -905,11 +905,19 @@ constexpr int kFast = 1 << kFastBits;
 //   bits 16..31 value: literal byte / symbol, length base, distance base
 enum { kKindLit = 0, kKindCopy = 1, kKindEnd = 2, kKindBad = 3 };
 enum { kAlphaLit = 0, kAlphaDist = 1, kAlphaPlain = 2 };
-struct InfCode {                           // one canonical Huffman code
-    uint32_t fast[kFast];                  // entries as above (code length in bits 0..3)
+template <int FB, int NS>
+struct InfCodeT {                          // one canonical Huffman code
+    static constexpr int kFB = FB, kSize = 1 << FB;
+    uint32_t fast[kSize];                  // entries as above (code length in bits 0..3)
     uint16_t cnt[16];                      // codes per length
-    uint16_t sorted[288];                  // symbols ordered by (length, symbol)
+    uint16_t sorted[NS];                   // symbols ordered by (length, symbol)
 };
+// literal / length (and code-length) codes: 9-bit first level, 288 symbols;
+// distance codes: 8-bit first level, 30 symbols -- 1.5 KiB less LDS per
+// member (more members resident per CU for the scalar-bound decode; a
+// distance code longer than 8 bits takes the canonical walk)
+using InfCode = InfCodeT<kFastBits, 288>;
+using InfDistCode = InfCodeT<8, 32>;
 // (length, distance) pair table: the next kPairBits bits of the stream ->
 // one whole copy when its length code, length extra bits, distance code and
 // distance extra bits all fit in them: bits 0..4 bits consumed, 5..13
@@ -923,7 +931,8 @@ template <int WIN, bool PAIR>
 struct InfSmem {
     alignas(16) uint8_t win[WIN];          // the member's output
     alignas(4) uint8_t ring[kRing];
-    InfCode lit, dist;
+    InfCode lit;
+    InfDistCode dist;
     uint8_t lens[320];                     // code lengths (literal/length | distance)
     uint32_t pair[PAIR ? kPair : 1];
 };
@@ -969,10 +978,11 @@ DEVI uint32_t inf_entry(int s, int alpha) {
 
 // canonical code from lengths (wave-parallel): counts and ranks by ballots,
 // the fast table filled by the symbols' lanes.  false: over-subscribed.
-DEVI bool inf_build(InfCode& c, const uint8_t* lens, int n, int alpha) {
+template <typename C>
+DEVI bool inf_build(C& c, const uint8_t* lens, int n, int alpha) {
     const int lane = (int)(threadIdx.x & 63u);
     const uint64_t below = (1ull << lane) - 1ull;
-    for (int k = lane; k < kFast; k += 64) c.fast[k] = 0;
+    for (int k = lane; k < C::kSize; k += 64) c.fast[k] = 0;
     uint32_t cnt[16];
 #pragma unroll
     for (int b = 0; b < 16; ++b) cnt[b] = 0;
@@ -1012,9 +1022,9 @@ DEVI bool inf_build(InfCode& c, const uint8_t* lens, int n, int alpha) {
         }
         if (L) {
             c.sorted[my_off] = (uint16_t)s;
-            if (L <= kFastBits) {
+            if (L <= C::kFB) {
                 const uint32_t e = inf_entry(s, alpha) | (uint32_t)L;
-                for (uint32_t k = rev_bits(my_code, L); k < (uint32_t)kFast; k += 1u << L) c.fast[k] = e;
+                for (uint32_t k = rev_bits(my_code, L); k < (uint32_t)C::kSize; k += 1u << L) c.fast[k] = e;
             }
         }
     }
@@ -1029,12 +1039,12 @@ DEVI void inf_build_pairs(InfSmem<WIN, PAIR>& S) {
         const int lane = (int)(threadIdx.x & 63u);
         for (int k = lane; k < kPair; k += 64) {
             uint32_t out = 0;
-            const uint32_t e = S.lit.fast[k & (kFast - 1)];
+            const uint32_t e = S.lit.fast[k & (InfCode::kSize - 1)];
             const uint32_t l = e & 15u, x = (e >> 4) & 15u;
             if (l && ((e >> 8) & 3u) == (uint32_t)kKindCopy && l + x <= (uint32_t)kPairBits) {
                 const uint32_t len = (e >> 16) + (((uint32_t)k >> l) & ((1u << x) - 1u));
                 const uint32_t r = (uint32_t)k >> (l + x);
-                const uint32_t f = S.dist.fast[r & (kFast - 1)];
+                const uint32_t f = S.dist.fast[r & (InfDistCode::kSize - 1)];
                 const uint32_t l2 = f & 15u, x2 = (f >> 4) & 15u;
                 const uint32_t nb = l + x + l2 + x2;
                 if (l2 && ((f >> 8) & 3u) == (uint32_t)kKindCopy && nb <= (uint32_t)kPairBits) {
@@ -1055,7 +1065,8 @@ DEVI uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(
 
 // codes longer than the first-level table: canonical walk, most significant
 // bit first (rare: the slow path of inf_decode)
-DEVI uint32_t inf_decode_long(const InfCode& c, uint64_t& bb, int& bc, int alpha) {
+template <typename C>
+DEVI uint32_t inf_decode_long(const C& c, uint64_t& bb, int& bc, int alpha) {
     int code = 0, first = 0, index = 0;
 #pragma unroll 1
     for (int len = 1; len <= 15; ++len) {
@@ -1073,8 +1084,9 @@ DEVI uint32_t inf_decode_long(const InfCode& c, uint64_t& bb, int& bc, int alpha
 
 // one symbol's table entry (needs >= 15 bits in bb), its code consumed;
 // kKindBad if the bits are no code
-DEVI uint32_t inf_decode(const InfCode& c, uint64_t& bb, int& bc, int alpha) {
-    const uint32_t e = uni(c.fast[bb & (uint64_t)(kFast - 1)]);
+template <typename C>
+DEVI uint32_t inf_decode(const C& c, uint64_t& bb, int& bc, int alpha) {
+    const uint32_t e = uni(c.fast[bb & (uint64_t)(C::kSize - 1)]);
     const int l = (int)(e & 15u);
     if (l) {
         bb >>= l;
