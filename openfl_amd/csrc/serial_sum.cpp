@@ -255,72 +255,91 @@ int default_threads() {
 
 namespace ofl {
 float serial_sum_f32_mt_cb(const float* x, int64_t n, float* dst, int nthreads, void (*after_copy)(void*),
-                               void* ctx) {
+                           void* ctx) {
     if (nthreads <= 0) nthreads = default_threads();
-    const int64_t K = (n + kG - 1) / kG;
     auto plain = [&] {
         if (dst && n) std::memcpy(dst, x, sizeof(float) * n);
         if (after_copy) after_copy(ctx);
         return serial_loop(x, n, 0.0f);
     };
-    if (nthreads <= 1 || K < 64) return plain();
-    const double t0 = debug_on() ? now_s() : 0.0;
-    std::vector<Sub> subs(K);
-    const int parts = (int)std::min<int64_t>(nthreads * 4, K);
-    auto range = [&](int i, int64_t& k0, int64_t& k1) {
-        k0 = K * i / parts;
-        k1 = K * (i + 1) / parts;
-    };
-    // phase A: float64 sums of the sub-chunks (and the copy)
-    const std::function<void(int)> fa = [&](int i) {
-        int64_t k0, k1;
-        range(i, k0, k1);
-        if (dst) std::memcpy(dst + k0 * kG, x + k0 * kG, sizeof(float) * (std::min(n, k1 * kG) - k0 * kG));
-        for (int64_t k = k0; k < k1; ++k) {
-            const float* xs = x + k * kG;
-            const int len = (int)std::min<int64_t>(kG, n - k * kG);
-            double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-            int j = 0;
-            for (; j + 4 <= len; j += 4) {
-                a0 += xs[j];
-                a1 += xs[j + 1];
-                a2 += xs[j + 2];
-                a3 += xs[j + 3];
-            }
-            for (; j < len; ++j) a0 += xs[j];
-            subs[k].dsum = (a0 + a1) + (a2 + a3);
-        }
-    };
-    if (!Pool::get().try_run(parts, nthreads - 1, fa)) return plain();
-    if (after_copy) after_copy(ctx);
-    const double t1 = debug_on() ? now_s() : 0.0;
-    double run = 0.0;  // dsum -> the estimate at each sub-chunk's start
-    for (int64_t k = 0; k < K; ++k) {
-        const double d = subs[k].dsum;
-        subs[k].dsum = run;
-        run += d;
-    }
-    // phase B: integer prefix summaries in the estimated binades
-    const std::function<void(int)> fb = [&](int i) {
-        int64_t k0, k1;
-        range(i, k0, k1);
-        for (int64_t k = k0; k < k1; ++k) phase_b(x + k * kG, (int)std::min<int64_t>(kG, n - k * kG), subs[k]);
-    };
-    if (!Pool::get().try_run(parts, nthreads - 1, fb))
-        for (int i = 0; i < parts; ++i) fb(i);
-    // phase C: in order, exact
-    const double t2 = debug_on() ? now_s() : 0.0;
-    float s = 0.0f;
+    if (nthreads <= 1 || (n + kG - 1) / kG < 64) return plain();
+    // chunks of kChunk elements (the sub-chunk summaries stay a few MB for
+    // any n); the estimate and the exact sum carry over from chunk to chunk
+    constexpr int64_t kChunk = (int64_t)1 << 24;
+    const int64_t Kmax = (std::min(n, kChunk) + kG - 1) / kG;
+    std::vector<Sub> subs(Kmax);
+    double run = 0.0;  // float64 running sum: the estimate at each sub-chunk's start
+    float s = 0.0f;    // the exact serial sum so far
     int64_t serial = 0;
-    for (int64_t k = 0; k < K; ++k)
-        if (!phase_c(subs[k], s)) {
-            s = serial_loop(x + k * kG, std::min<int64_t>(kG, n - k * kG), s);
-            ++serial;
+    double ta = 0, tb = 0, tc = 0;
+    for (int64_t c0 = 0; c0 < n; c0 += kChunk) {
+        const float* xc = x + c0;
+        const int64_t nc = std::min(kChunk, n - c0);
+        const int64_t K = (nc + kG - 1) / kG;
+        const int parts = (int)std::min<int64_t>(nthreads * 4, K);
+        auto range = [&](int i, int64_t& k0, int64_t& k1) {
+            k0 = K * i / parts;
+            k1 = K * (i + 1) / parts;
+        };
+        const double t0 = debug_on() ? now_s() : 0.0;
+        // phase A: float64 sums of the sub-chunks (and the copy)
+        const std::function<void(int)> fa = [&](int i) {
+            int64_t k0, k1;
+            range(i, k0, k1);
+            if (dst) std::memcpy(dst + c0 + k0 * kG, xc + k0 * kG, sizeof(float) * (std::min(nc, k1 * kG) - k0 * kG));
+            for (int64_t k = k0; k < k1; ++k) {
+                const float* xs = xc + k * kG;
+                const int len = (int)std::min<int64_t>(kG, nc - k * kG);
+                double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+                int j = 0;
+                for (; j + 4 <= len; j += 4) {
+                    a0 += xs[j];
+                    a1 += xs[j + 1];
+                    a2 += xs[j + 2];
+                    a3 += xs[j + 3];
+                }
+                for (; j < len; ++j) a0 += xs[j];
+                subs[k].dsum = (a0 + a1) + (a2 + a3);
+            }
+        };
+        if (!Pool::get().try_run(parts, nthreads - 1, fa)) {
+            // the pool is busy (another caller): the plain chain for the rest
+            if (dst) std::memcpy(dst + c0, xc, sizeof(float) * (n - c0));
+            if (after_copy) after_copy(ctx);
+            return serial_loop(xc, n - c0, s);
         }
+        if (after_copy && c0 + nc == n) after_copy(ctx);
+        const double t1 = debug_on() ? now_s() : 0.0;
+        for (int64_t k = 0; k < K; ++k) {
+            const double d = subs[k].dsum;
+            subs[k].dsum = run;
+            run += d;
+        }
+        // phase B: integer prefix summaries in the estimated binades
+        const std::function<void(int)> fb = [&](int i) {
+            int64_t k0, k1;
+            range(i, k0, k1);
+            for (int64_t k = k0; k < k1; ++k) phase_b(xc + k * kG, (int)std::min<int64_t>(kG, nc - k * kG), subs[k]);
+        };
+        if (!Pool::get().try_run(parts, nthreads - 1, fb))
+            for (int i = 0; i < parts; ++i) fb(i);
+        // phase C: in order, exact
+        const double t2 = debug_on() ? now_s() : 0.0;
+        for (int64_t k = 0; k < K; ++k)
+            if (!phase_c(subs[k], s)) {
+                s = serial_loop(xc + k * kG, std::min<int64_t>(kG, nc - k * kG), s);
+                ++serial;
+            }
+        if (debug_on()) {
+            ta += t1 - t0;
+            tb += t2 - t1;
+            tc += now_s() - t2;
+        }
+    }
     if (debug_on())
         std::fprintf(stderr, "[ofl sum] n=%lld threads=%d A %.1f us B %.1f us C %.1f us serial sub-chunks %lld/%lld\n",
-                     (long long)n, nthreads, 1e6 * (t1 - t0), 1e6 * (t2 - t1), 1e6 * (now_s() - t2),
-                     (long long)serial, (long long)K);
+                     (long long)n, nthreads, 1e6 * ta, 1e6 * tb, 1e6 * tc, (long long)serial,
+                     (long long)((n + kG - 1) / kG));
     return s;
 }
 

@@ -29,6 +29,7 @@ def _cases():
         "zeros": np.zeros(n, np.float32),
         "subnormal": (rng.standard_normal(n) * 1e-42).astype(np.float32),
         "ones (saturates at 2^24)": np.ones(1 << 25, np.float32),
+        "two chunks N(.002,.01)": (rng.standard_normal((1 << 24) + 777_777) * 0.01 + 0.002).astype(np.float32),
         "alternating big/small": (np.where(idx % 2 == 0, 1e8, 1e-3) * np.where(idx % 4 < 2, 1, -1)).astype(np.float32),
         "nan": np.where(idx == 500_000, np.nan, rng.standard_normal(n)).astype(np.float32),
         "inf": np.where(idx == 7777, np.inf, rng.standard_normal(n)).astype(np.float32),
