@@ -10,9 +10,24 @@ heap and freed ones stay there for the next call: the same copy then runs at
 ~30 GB/s (tools/bytes_copy_probe.py, profiles/r02_bytes_copy_probe_mallopt.txt).
 The cost: memory freed by the process is kept by it rather than returned to
 the OS.  OFL_HOST_KEEP_LARGE_BLOCKS=1 in the environment applies it at import.
+
+Independently of that policy, bytes_from recycles its own large payloads
+(module-local, on by default): a `bytes` of >= 8 MiB it made is kept in a
+small pool, and once the caller has dropped it (the pool holds the only
+reference) the next payload of a size that fits is written into it.  Freeing
+a 144 MiB payload is an munmap of ~37k pages, ~8.7 ms single-threaded on the
+GPU box, and its successor's first touch faults them in again; a recycled one
+pays neither (KC step 43-51 -> 34.3 ms, profiles/r03_kc_step_gap.json,
+profiles/r03_kc_recycle_ab.txt).  A
+payload any caller still references -- directly, through a memoryview or
+through an ndarray over it -- is never touched.  OFL_HOST_RECYCLE=0 turns
+it off; OFL_HOST_RECYCLE_MIB caps the pooled capacity (default 2048 MiB).
 """
 import ctypes
 import ctypes.util
+import os
+import sys
+import threading
 
 import numpy as np
 
@@ -37,6 +52,72 @@ def _c():
     return _libc
 
 
+_RECYCLE = os.environ.get("OFL_HOST_RECYCLE", "1") != "0"
+_RECYCLE_MIN = 8 << 20
+_RECYCLE_CAP = int(os.environ.get("OFL_HOST_RECYCLE_MIB", "2048")) << 20
+_pool = []  # [[bytes, capacity]]: payloads this module made, newest last
+_pool_lock = threading.Lock()
+_layout_ok = None
+
+
+def _bytes_layout_ok():
+    """CPython 3.x PyBytesObject: {refcnt, type, ob_size, ob_shash, ob_sval[]}.
+    Checked once on live objects before any in-place reuse."""
+    global _layout_ok
+    if _layout_ok is None:
+        ok = sys.implementation.name == "cpython" and ctypes.sizeof(ctypes.c_void_p) == 8
+        if ok:
+            b = _new_bytes(None, 100)
+            a = id(b)
+            ok = (_bytes_addr(b) == a + 32 and ctypes.c_ssize_t.from_address(a + 16).value == 100
+                  and ctypes.c_ssize_t.from_address(a).value >= 1)
+            if ok:
+                h = hash(b)
+                ok = ctypes.c_ssize_t.from_address(a + 24).value == h
+        _layout_ok = bool(ok)
+    return _layout_ok
+
+
+def _recycled(n):
+    """A pooled payload of capacity >= n that nobody else references, resized
+    to n bytes (hash reset), or None.  The pool keeps the caller's reference
+    out of the count: the object is claimed under the lock and only reached
+    through the pool, so no other thread can obtain it meanwhile."""
+    with _pool_lock:
+        best = -1
+        # the refcount is read by address with no local bound to the object
+        # (a loop variable holding it would count too): 1 = the pool's entry
+        for i in range(len(_pool)):
+            ent = _pool[i]
+            cap = ent[1]
+            if cap < n or cap > 2 * n + (64 << 20):
+                continue
+            if ctypes.c_ssize_t.from_address(id(ent[0])).value != 1:
+                continue
+            if best < 0 or cap < _pool[best][1]:
+                best = i
+        if best < 0:
+            return None
+        ent = _pool.pop(best)
+        b = ent[0]
+        a = id(b)
+        ctypes.c_ssize_t.from_address(a + 16).value = n   # ob_size (the allocation stays cap + 1 bytes)
+        ctypes.c_ssize_t.from_address(a + 24).value = -1  # ob_shash: not computed
+        ctypes.c_char.from_address(a + 32 + n).value = b"\0"
+        _pool.append(ent)  # newest last; the caller's reference keeps it from reuse
+        return b
+
+
+def _remember(b, cap):
+    with _pool_lock:
+        _pool.append([b, cap])
+        tot = sum(c for _, c in _pool)
+        i = 0
+        while tot > _RECYCLE_CAP and i < len(_pool):  # oldest first
+            tot -= _pool[i][1]
+            _pool.pop(i)
+
+
 def bytes_from(src_addr, n, threads=8, huge_min=8 << 20, par_min=1 << 20):
     """A new `bytes` of the n bytes at host address src_addr (pinned staging).
 
@@ -50,9 +131,24 @@ def bytes_from(src_addr, n, threads=8, huge_min=8 << 20, par_min=1 << 20):
     n = int(n)
     if n < par_min:
         return ctypes.string_at(src_addr, n) if n else b""
+    piece = 4 << 20 if n >= huge_min else max(256 << 10, -(-n // (2 * threads)) // 4096 * 4096)
+    if _RECYCLE and n >= _RECYCLE_MIN and _bytes_layout_ok():
+        b = _recycled(n)
+        if b is not None:
+            _fill(_bytes_addr(b), src_addr, n, threads, 1 << 62, piece)  # pages already resident
+            return b
+        # a fresh one with 1/8 headroom (untouched pages cost nothing), so the
+        # next payload of a slightly larger size still fits
+        cap = n + (n >> 3)
+        b = _new_bytes(None, cap)
+        _fill(_bytes_addr(b), src_addr, n, threads, huge_min, piece)
+        a = id(b)
+        ctypes.c_ssize_t.from_address(a + 16).value = n
+        ctypes.c_char.from_address(a + 32 + n).value = b"\0"
+        _remember(b, cap)
+        return b
     b = _new_bytes(None, n)
-    _fill(_bytes_addr(b), src_addr, n, threads, huge_min, 4 << 20 if n >= huge_min else
-          max(256 << 10, -(-n // (2 * threads)) // 4096 * 4096))
+    _fill(_bytes_addr(b), src_addr, n, threads, huge_min, piece)
     return b
 
 
