@@ -1,4 +1,5 @@
-"""Host-memory policy for the payload path (opt-in, process-wide).
+"""Host memory of the payload path: payload bytes made from pinned staging
+(recycled above 8 MiB) and the opt-in, process-wide heap policy.
 
 Every payload crosses the plugin boundary as a fresh Python `bytes` (the
 reference API; protobuf's data_bytes takes nothing else) and every decoded
@@ -127,7 +128,8 @@ def bytes_from(src_addr, n, threads=8, huge_min=8 << 20, par_min=1 << 20):
     huge pages in 'madvise' mode), so first touch costs one fault per 2 MiB
     instead of per 4 KiB; above par_min the copy runs on native threads, so
     those faults are taken in parallel.  Same bytes as bytes(memoryview) of
-    the source."""
+    the source.  From 8 MiB on, a payload this function made earlier and
+    nobody references any more is refilled instead (module docstring)."""
     n = int(n)
     if n < par_min:
         return ctypes.string_at(src_addr, n) if n else b""
