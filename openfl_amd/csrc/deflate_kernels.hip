@@ -892,7 +892,13 @@ __global__ __launch_bounds__(256) void k_gzip_pack(const uint8_t* slots, const u
 // Any valid deflate data decodes (stored, fixed and dynamic blocks, RFC 1951).
 // ISIZE and the CRC-32 (over the member's output, wave-parallel) are checked here.
 constexpr int kRing = 512;                 // compressed-input ring per wave (bytes)
-constexpr int kFastBits = 9;               // first-level decode table: codes of <= 9 bits
+#ifndef OFL_INF_FASTBITS
+#define OFL_INF_FASTBITS 9
+#endif
+#ifndef OFL_INF_WAVES
+#define OFL_INF_WAVES 1
+#endif
+constexpr int kFastBits = OFL_INF_FASTBITS; // first-level decode table: codes of <= 9 bits
 constexpr int kFast = 1 << kFastBits;
 
 // A first-level table entry says what the symbol means, so the serial decode
@@ -1103,7 +1109,7 @@ DEVI uint32_t inf_decode(const C& c, uint64_t& bb, int& bc, int alpha) {
 // global memory (bytes this wavefront stored earlier: same-address order
 // within a wavefront).  Less LDS per member -> more members per CU.
 template <int WIN, bool RING, bool PAIR>
-__global__ __launch_bounds__(64) void k_inflate_members(InfArgs a) {
+__global__ __launch_bounds__(64, OFL_INF_WAVES) void k_inflate_members(InfArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     InfSmem<WIN, PAIR>& S = *reinterpret_cast<InfSmem<WIN, PAIR>*>(smem_raw);
     const int lane = threadIdx.x;
