@@ -155,6 +155,12 @@ class RoundEnd:
             self.offsets.append(acc)
             acc += (n + _ALIGN - 1) // _ALIGN * _ALIGN
         self.arena_numel = max(acc, 1)
+        # the alignment padding between tensors (and the arena's tail): zeroed
+        # in every output arena, so it is the same whichever path ran
+        gaps = [np.arange(o + n, o + (n + _ALIGN - 1) // _ALIGN * _ALIGN) for o, n in zip(self.offsets, self.numels)]
+        gaps.append(np.arange(acc, self.arena_numel))
+        gap_idx = np.concatenate(gaps).astype(np.int64) if gaps else np.zeros(0, np.int64)
+        self._gap_idx = torch.from_numpy(gap_idx).to(self.device) if gap_idx.size else None
         self.big = [i for i, n in enumerate(self.numels) if n > self.dim_threshold]
         self.single = [i for i, n in enumerate(self.numels) if n == 1]
         self.plan = EdenPlan([self.numels[i] for i in self.big], self.n_bits,
@@ -344,4 +350,6 @@ class RoundEnd:
                                                      out.data_ptr(), _stream(dev)))
             else:
                 out.copy_(delta)
+            if self._gap_idx is not None:
+                out.index_fill_(0, self._gap_idx, 0.0)
         return out, result, (seeds if payloads else self._seeds[:len(self.numels)])

@@ -246,19 +246,21 @@ def resolve_device(device):
 def resolve_devices(device):
     """A plugin `device` setting -> the list of ROCm devices it names.
 
-    One device: "cpu" / None (the current GPU, the reference's default),
-    "cuda:N".  Several (calls from different threads spread over them,
-    ThreadDevices): "cuda" (every visible GPU), "cuda:0,cuda:2" or a list /
-    tuple of single-device settings.  The reference has one device per
-    pipeline (eden_pipeline.py:738); its callers reach several GPUs only
-    through the gRPC server's concurrent worker threads
+    One device: "cpu" / None / "cuda" (the current GPU, as torch and the
+    reference mean it), "cuda:N".  Several (calls from different threads
+    spread over them, ThreadDevices): "cuda:all" (every visible GPU),
+    "cuda:0,cuda:2" or a list / tuple of single-device settings -- only ever
+    named explicitly, so a process-per-GPU deployment that calls
+    torch.cuda.set_device(k) and passes "cuda" stays on GPU k.  The reference
+    has one device per pipeline (eden_pipeline.py:738); its callers reach
+    several GPUs only through the gRPC server's concurrent worker threads
     (transport/grpc/aggregator_server.py:305, component/aggregator/
     aggregator.py:643-646), which is what the per-thread mapping serves."""
     if isinstance(device, (list, tuple)):
         devs = [resolve_device(d) for d in device]
     elif isinstance(device, str) and "," in device:
         devs = [resolve_device(d.strip()) for d in device.split(",") if d.strip()]
-    elif isinstance(device, str) and device.strip() in ("cuda", "cuda:all"):
+    elif isinstance(device, str) and device.strip() == "cuda:all":
         if not torch.cuda.is_available():
             raise _lib.CodecError("openfl_amd codecs need a ROCm GPU (no CPU fallback)")
         devs = [torch.device("cuda", i) for i in range(torch.cuda.device_count())]

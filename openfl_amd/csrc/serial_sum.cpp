@@ -45,6 +45,8 @@
 #include <functional>
 #include <mutex>
 #include <thread>
+
+#include <unistd.h>
 #include <vector>
 
 #include "ofl_util.h"
@@ -81,6 +83,9 @@ constexpr int16_t kNoBinade = -32768;
 // A small persistent pool: try_run(n, w, f) calls f(0..n-1) on the caller and
 // (at least) w workers.  One job at a time; a caller that finds the pool busy
 // gets false and runs serially (concurrent plugin calls keep their own core).
+// Fork-safe: a fork()ed child inherits the pool's state but none of its
+// threads, so a pool created in another process (pid recorded at creation)
+// always reports busy and the caller runs serially.
 class Pool {
    public:
     static Pool& get() {
@@ -88,6 +93,7 @@ class Pool {
         return *p;
     }
     bool try_run(int n, int workers, const std::function<void(int)>& f) {
+        if (getpid() != pid_) return false;
         std::unique_lock<std::mutex> busy(run_m_, std::try_to_lock);
         if (!busy.owns_lock()) return false;
         ensure(workers);
@@ -133,6 +139,7 @@ class Pool {
             if (f && --pending_ == 0) done_.notify_all();
         }
     }
+    const pid_t pid_ = getpid();
     std::mutex run_m_, m_;
     std::condition_variable cv_, done_;
     std::vector<std::thread> th_;

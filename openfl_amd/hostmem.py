@@ -12,17 +12,24 @@ heap and freed ones stay there for the next call: the same copy then runs at
 The cost: memory freed by the process is kept by it rather than returned to
 the OS.  OFL_HOST_KEEP_LARGE_BLOCKS=1 in the environment applies it at import.
 
-Independently of that policy, bytes_from recycles its own large payloads
-(module-local, on by default): a `bytes` of >= 8 MiB it made is kept in a
-small pool, and once the caller has dropped it (the pool holds the only
-reference) the next payload of a size that fits is written into it.  Freeing
-a 144 MiB payload is an munmap of ~37k pages, ~8.7 ms single-threaded on the
-GPU box, and its successor's first touch faults them in again; a recycled one
-pays neither (KC step 43-51 -> 34.3 ms, profiles/r03_kc_step_gap.json,
-profiles/r03_kc_recycle_ab.txt).  A
-payload any caller still references -- directly, through a memoryview or
-through an ndarray over it -- is never touched.  OFL_HOST_RECYCLE=0 turns
-it off; OFL_HOST_RECYCLE_MIB caps the pooled capacity (default 2048 MiB).
+Large payloads (>= 8 MiB) that bytes_from made are tracked in a small pool
+for one purpose by default: when the caller has dropped one (the pool holds
+the only reference), the pool hands its last reference to a background
+thread, so the munmap of the dead payload (~37k pages for a 144 MiB stream,
+~8.7 ms on the GPU box) is not paid on the caller's thread.  Nothing is ever
+written into a `bytes` in this default mode; hostmem.release_pool() drops
+every tracked reference at once, and tracked payloads older than
+OFL_HOST_POOL_IDLE_S seconds (default 30) are dropped at the next call.
+
+Opt-in (OFL_HOST_RECYCLE=1): instead of being released, a dead payload is
+refilled in place for the next payload of a size that fits (its ob_size /
+ob_shash reset; the CPython layout is checked once on a live object), which
+also saves the successor's first-touch faults (KC step 43-51 -> 34.3 ms,
+profiles/r03_kc_recycle_ab.txt).  The invariant this mode relies on: every
+consumer of a payload holds a real reference while it uses the buffer (a
+memoryview, an ndarray or protobuf's own copy all do, tests/test_hostmem.py);
+C code that keeps a borrowed char* past its last reference would see the
+bytes change.  OFL_HOST_RECYCLE_MIB caps the pooled capacity (default 2048).
 """
 import ctypes
 import ctypes.util
@@ -53,12 +60,54 @@ def _c():
     return _libc
 
 
-_RECYCLE = os.environ.get("OFL_HOST_RECYCLE", "1") != "0"
+_RECYCLE = os.environ.get("OFL_HOST_RECYCLE", "0") == "1"
 _RECYCLE_MIN = 8 << 20
 _RECYCLE_CAP = int(os.environ.get("OFL_HOST_RECYCLE_MIB", "2048")) << 20
-_pool = []  # [[bytes, capacity]]: payloads this module made, newest last
+_POOL_IDLE_S = float(os.environ.get("OFL_HOST_POOL_IDLE_S", "30"))
+_pool = []  # [[bytes, capacity, made_at]]: payloads this module made, newest last
 _pool_lock = threading.Lock()
 _layout_ok = None
+_reaper = None
+
+
+def _refcount_is_pool_only(ent):
+    # read by address with no local bound to the object (a loop variable
+    # holding it would count too): 1 = the pool's entry
+    return ctypes.c_ssize_t.from_address(id(ent[0])).value == 1
+
+
+def _drop_later(objs):
+    """Release the last references to dead payloads on a background thread
+    (their munmap off the caller's thread).  Nothing is written into them."""
+    global _reaper
+    if not objs:
+        return
+    if _reaper is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _reaper = ThreadPoolExecutor(max_workers=1, thread_name_prefix="ofl-hostmem-release")
+    _reaper.submit(objs.clear)
+
+
+def _release_dead():
+    """Default mode: hand tracked payloads nobody else references (and those
+    tracked longer than _POOL_IDLE_S) to the release thread."""
+    import time
+    now = time.monotonic()
+    with _pool_lock:
+        dead = [e[0] for e in _pool if _refcount_is_pool_only(e) or now - e[2] > _POOL_IDLE_S]
+        if dead:
+            keep = [e for e in _pool if not any(e[0] is d for d in dead)]
+            _pool[:] = keep
+    _drop_later(dead)
+
+
+def release_pool():
+    """Drop every payload reference the pool holds (e.g. at round end); the
+    payloads still referenced elsewhere live on, the rest are freed."""
+    with _pool_lock:
+        objs = [e[0] for e in _pool]
+        _pool.clear()
+    objs.clear()
 
 
 def _bytes_layout_ok():
@@ -86,14 +135,12 @@ def _recycled(n):
     through the pool, so no other thread can obtain it meanwhile."""
     with _pool_lock:
         best = -1
-        # the refcount is read by address with no local bound to the object
-        # (a loop variable holding it would count too): 1 = the pool's entry
         for i in range(len(_pool)):
             ent = _pool[i]
             cap = ent[1]
             if cap < n or cap > 2 * n + (64 << 20):
                 continue
-            if ctypes.c_ssize_t.from_address(id(ent[0])).value != 1:
+            if not _refcount_is_pool_only(ent):
                 continue
             if best < 0 or cap < _pool[best][1]:
                 best = i
@@ -110,9 +157,10 @@ def _recycled(n):
 
 
 def _remember(b, cap):
+    import time
     with _pool_lock:
-        _pool.append([b, cap])
-        tot = sum(c for _, c in _pool)
+        _pool.append([b, cap, time.monotonic()])
+        tot = sum(e[1] for e in _pool)
         i = 0
         while tot > _RECYCLE_CAP and i < len(_pool):  # oldest first
             tot -= _pool[i][1]
@@ -128,8 +176,10 @@ def bytes_from(src_addr, n, threads=8, huge_min=8 << 20, par_min=1 << 20):
     huge pages in 'madvise' mode), so first touch costs one fault per 2 MiB
     instead of per 4 KiB; above par_min the copy runs on native threads, so
     those faults are taken in parallel.  Same bytes as bytes(memoryview) of
-    the source.  From 8 MiB on, a payload this function made earlier and
-    nobody references any more is refilled instead (module docstring)."""
+    the source.  From 8 MiB on the payload is tracked so its release happens
+    off the caller's thread; with OFL_HOST_RECYCLE=1 a payload this function
+    made earlier and nobody references any more is refilled instead (module
+    docstring)."""
     n = int(n)
     if n < par_min:
         return ctypes.string_at(src_addr, n) if n else b""
@@ -151,6 +201,9 @@ def bytes_from(src_addr, n, threads=8, huge_min=8 << 20, par_min=1 << 20):
         return b
     b = _new_bytes(None, n)
     _fill(_bytes_addr(b), src_addr, n, threads, huge_min, piece)
+    if n >= _RECYCLE_MIN:
+        _release_dead()
+        _remember(b, n)
     return b
 
 

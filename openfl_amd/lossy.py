@@ -7,7 +7,6 @@ semantics are cited per function (paths relative to /root/reference).
 import ctypes
 import gzip
 import threading
-import warnings
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -19,10 +18,6 @@ _tls = threading.local()
 GZIP_CHUNK = 8 << 20
 _pool = None
 _pool_lock = threading.Lock()
-# gunzip_device hands torch a read-only view of the payload (torch only reads
-# it for the H2D); one narrow process-wide filter instead of per-call
-# catch_warnings(), which is not thread-safe on the copy pool's threads
-warnings.filterwarnings("ignore", message="The given NumPy array is not writable", category=UserWarning)
 
 
 def _on_device(fn):
@@ -380,9 +375,12 @@ def gunzip_device(data, out):
     caller_stream = torch.cuda.current_stream(dev)
 
     def h2d():
-        with torch.cuda.device(dev), torch.cuda.stream(caller_stream):
-            if src.size:
-                d_in[:src.size].copy_(torch.from_numpy(src))
+        # straight from the immutable payload through the C ABI (no torch
+        # wrapper of a read-only buffer); the caller's stream orders it
+        if src.size:
+            with torch.cuda.device(dev):
+                _lib.check(L.ofl_copy_h2d_async(d_in.data_ptr(), src.ctypes.data, src.size,
+                                                caller_stream.cuda_stream))
     copy = _h2d_pool().submit(h2d)
     # one pass over the headers: a member takes >= 26 bytes, so n // 26 + 1
     # entries always suffice (untouched pages of the array cost nothing)

@@ -139,6 +139,12 @@ def test_round_end_fused_encode_matches_per_tensor(seed_mode, with_base, C):
             np.testing.assert_array_equal(re.view(new, i).cpu().numpy(), ref_models[i].reshape(s),
                                           err_msg=f"{fused} {i}")
     assert outs[0][2] == outs[1][2]
+    # whole arenas, alignment padding included, are the same for both paths
+    # (the padding is zeroed whichever path ran)
+    assert torch.equal(outs[0][0], outs[1][0])
+    re = outs[0][3]
+    if re._gap_idx is not None:
+        assert not outs[0][0].index_select(0, re._gap_idx).any()
 
 
 def test_round_end_many_collaborators_chained():

@@ -510,20 +510,21 @@ def test_step_graph_replay_bit_identical():
     assert torch.equal(p0, p1) and torch.equal(s0, s1) and torch.equal(y0, y1)
 
 
-@pytest.mark.parametrize("setting", ["cuda", "two_slots_one_gpu"])
+@pytest.mark.parametrize("setting", ["cuda:all", "two_slots_one_gpu"])
 def test_pipeline_multi_device_threads(setting):
     """device naming several GPUs: each calling thread is bound to one of them
     round-robin (codec.ThreadDevices) -- concurrent forward and backward calls
     from unchanged callers (the gRPC pool, aggregator_server.py:305) give the
-    bytes, metadata and values of the single-device path.  "cuda" = every
-    visible GPU; on a one-GPU box the same device is also listed twice, so two
+    bytes, metadata and values of the single-device path.  "cuda:all" = every
+    visible GPU (plain "cuda" is the current device only); on a one-GPU box the same device is also listed twice, so two
     slots (separate codecs, plans, workspaces) share it."""
     from openfl_amd.pipelines import EdenPipeline
-    dev = "cuda" if setting == "cuda" else [DEV, DEV]
+    dev = "cuda:all" if setting == "cuda:all" else [DEV, DEV]
     multi = EdenPipeline(n_bits=8, device=dev)
     single = EdenPipeline(n_bits=8, device=DEV)
     eden = multi.transformers[0].eden
-    assert len(eden.devices) == (torch.cuda.device_count() if setting == "cuda" else 2)
+    assert len(eden.devices) == (torch.cuda.device_count() if setting == "cuda:all" else 2)
+    assert len(EdenPipeline(n_bits=8, device="cuda").transformers[0].eden.devices) == 1
     rng = np.random.default_rng(19)
     xs = [rng.standard_normal(int(n)).astype(np.float32) for n in rng.integers(200, 600_000, 16)]
     seeds = rng.integers(1, 2 ** 16, len(xs))

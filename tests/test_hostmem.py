@@ -17,7 +17,8 @@ def test_bytes_from_equals_tobytes(n):
     if n > 1:  # b"" and 1-byte bytes are interned singletons
         # no leaked reference from the C-API call (payloads >= 8 MiB: plus the
         # recycling pool's own)
-        pooled = hostmem._RECYCLE and n >= hostmem._RECYCLE_MIN and hostmem._bytes_layout_ok()
+        # (payloads >= 8 MiB: plus the pool's own, recycling or not)
+        pooled = n >= hostmem._RECYCLE_MIN and (hostmem._bytes_layout_ok() or not hostmem._RECYCLE)
         assert sys.getrefcount(b) == (3 if pooled else 2)
     assert len(b) == n and hash(b) == hash(src[:n].tobytes())
 
@@ -32,10 +33,22 @@ def _src(seed, n):
     return np.random.default_rng(seed).integers(0, 256, size=n, dtype=np.uint8)
 
 
-needs_recycle = pytest.mark.skipif(not (hostmem._RECYCLE and hostmem._bytes_layout_ok()),
-                                   reason="payload recycling off (OFL_HOST_RECYCLE=0 or another Python layout)")
+needs_layout = pytest.mark.skipif(not hostmem._bytes_layout_ok(), reason="another Python object layout")
 
 
+@pytest.fixture
+def recycle_on(monkeypatch):
+    """The opt-in in-place recycling (OFL_HOST_RECYCLE=1) for one test."""
+    hostmem.release_pool()
+    monkeypatch.setattr(hostmem, "_RECYCLE", True)
+    yield
+    hostmem.release_pool()
+
+
+needs_recycle = pytest.mark.usefixtures("recycle_on")
+
+
+@needs_layout
 @needs_recycle
 def test_recycled_payload_is_reused_only_when_released():
     n = 9 << 20
@@ -54,6 +67,7 @@ def test_recycled_payload_is_reused_only_when_released():
     assert b3[-1:] == want[-1:] and bytes(memoryview(b3)[-3:]) == want[-3:]
 
 
+@needs_layout
 @needs_recycle
 @pytest.mark.parametrize("hold", ["memoryview", "ndarray", "slice_view"])
 def test_referenced_payload_is_never_rewritten(hold):
@@ -71,6 +85,7 @@ def test_referenced_payload_is_never_rewritten(hold):
     assert bytes(keep) == (a.tobytes() if hold != "slice_view" else a[10:20].tobytes())
 
 
+@needs_layout
 @needs_recycle
 def test_recycling_under_threads():
     from concurrent.futures import ThreadPoolExecutor
@@ -89,10 +104,55 @@ def test_recycling_under_threads():
         assert all(ex.map(job, range(8)))
 
 
+@needs_layout
 @needs_recycle
 def test_pool_capacity_is_bounded():
     n = 8 << 20
     a = _src(5, n)
     held = [hostmem.bytes_from(a.ctypes.data, n) for _ in range(4)]
-    assert sum(c for _, c in hostmem._pool) <= hostmem._RECYCLE_CAP
+    assert sum(e[1] for e in hostmem._pool) <= hostmem._RECYCLE_CAP
     assert all(h == a.tobytes() for h in held)
+
+
+def test_default_mode_never_rewrites_a_payload(monkeypatch):
+    """Default (OFL_HOST_RECYCLE unset): a dropped payload is only released
+    (off the caller's thread), never refilled; a payload held by a protobuf
+    NamedTensor built from it, by a serialized gRPC-style copy of that message
+    or by nothing at all keeps its bytes while later payloads are made."""
+    from openfl_amd import protocols
+    monkeypatch.setattr(hostmem, "_RECYCLE", False)
+    hostmem.release_pool()
+    n = 9 << 20
+    srcs = [_src(10 + k, n) for k in range(4)]
+    b1 = hostmem.bytes_from(srcs[0].ctypes.data, n)
+    k1, want1 = id(b1), srcs[0].tobytes()
+    nt = protocols.NamedTensor(name="w", round_number=1, lossless=False, report=False,
+                               data_bytes=b1)
+    wire = nt.SerializeToString()
+    del b1
+    b2 = hostmem.bytes_from(srcs[1].ctypes.data, n)
+    b3 = hostmem.bytes_from(srcs[2].ctypes.data, n - 5)
+    assert nt.data_bytes == want1
+    back = protocols.NamedTensor()
+    back.ParseFromString(wire)
+    assert back.data_bytes == want1
+    assert b2 == srcs[1].tobytes() and b3 == srcs[2][:n - 5].tobytes()
+    held = hostmem.bytes_from(srcs[3].ctypes.data, n)
+    view = memoryview(held)
+    for _ in range(3):
+        hostmem.bytes_from(srcs[0].ctypes.data, n)
+    assert bytes(view) == srcs[3].tobytes() and held == srcs[3].tobytes()
+    hostmem.release_pool()
+    assert not hostmem._pool
+    assert k1 is not None
+
+
+def test_release_pool_drops_tracked_payloads(monkeypatch):
+    monkeypatch.setattr(hostmem, "_RECYCLE", False)
+    hostmem.release_pool()
+    n = 8 << 20
+    src = _src(3, n)
+    b = hostmem.bytes_from(src.ctypes.data, n)
+    assert sys.getrefcount(b) == 3 and len(hostmem._pool) == 1
+    hostmem.release_pool()
+    assert sys.getrefcount(b) == 2 and b == src.tobytes()

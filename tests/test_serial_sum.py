@@ -92,3 +92,31 @@ def test_concurrent_callers():
         got = list(ex.map(lambda a: L.ofl_serial_sum_f32_mt(a.ctypes.data, a.size, None, 4), arrs))
     for a, g in zip(arrs, got):
         assert _same(g, _serial(a))
+
+
+def test_forked_child_does_not_deadlock():
+    """A fork()ed child inherits the pool's state but none of its threads:
+    its threaded sums run serially instead of waiting for workers that do
+    not exist (csrc/serial_sum.cpp Pool, pid recorded at creation)."""
+    import os
+    x = (np.random.default_rng(6).standard_normal(1 << 21) * 0.01).astype(np.float32)
+    L = _lib.lib()
+    want = _serial(x)
+    assert _same(L.ofl_serial_sum_f32_mt(x.ctypes.data, x.size, None, 8), want)  # the pool exists now
+    pid = os.fork()
+    if pid == 0:  # child: exit status says whether the sum was right
+        try:
+            ok = _same(L.ofl_serial_sum_f32_mt(x.ctypes.data, x.size, None, 8), want)
+        finally:
+            os._exit(0 if ok else 3)
+    import time
+    t0 = time.monotonic()
+    while time.monotonic() - t0 < 60:
+        done, status = os.waitpid(pid, os.WNOHANG)
+        if done:
+            assert os.WEXITSTATUS(status) == 0
+            return
+        time.sleep(0.05)
+    os.kill(pid, 9)
+    os.waitpid(pid, 0)
+    raise AssertionError("threaded sum in a forked child hung")
