@@ -378,48 +378,75 @@ int ofl_wavg_delta32_ranges(int ncollab, const float* const* xs, const double* w
                             float* delta32_out, void* stream);
 
 /* ---- gzip of rank arrays (csrc/deflate_kernels.hip) -------------------------
- * GZIPTransformer.forward (kc_pipeline.py:128-156, skc_pipeline.py:201-230,
- * stc_pipeline.py:185-215) compresses the float32 ranks with gzip.compress;
- * gzip.decompress reads any valid stream, so this produces one on the GPU: a
- * multi-member gzip stream (4096 float32 values per member, one
- * dynamic-Huffman deflate block each: copies of each value's previous
- * occurrence, literals at first occurrences), CRC-32 and ISIZE per member.
- * Every member header carries an RFC 1952 extra field 'BC' (SLEN 2) holding
- * the member's byte size - 1 (as BGZF does), which gzip.decompress skips.
- * x: DEVICE float32 [n], every value an integer 0..31 (the ranks the lossy
- * pipelines write; anything else -> OFL_EINVAL, nothing written).  out: HOST
- * buffer of out_cap >= ofl_gzip_ranks_bound(n) bytes; *out_len = stream
- * length.  When out is mapped pinned memory (hipHostMalloc, torch
- * pin_memory) the kernels write the stream into it directly and the batches
- * of members run without host round trips; pageable memory gets one D2H per
- * batch.  ws: device, ofl_gzip_ranks_workspace_bytes(n).  Synchronous.
- * Errors: ofl_gzip_last_error(). */
+ * GZIPTransformer.forward (kc_pipeline.py:128-141, skc_pipeline.py:201-215,
+ * stc_pipeline.py:185-199) compresses the float32 ranks with gzip.compress;
+ * GZIPTransformer.backward (kc_pipeline.py:152-156) is gzip.decompress, which
+ * reads any valid stream.  ofl_gzip_ranks produces one on the GPU (TLZ): a
+ * multi-member gzip stream, one member per 131072 float32 values (512 KiB),
+ * each ONE dynamic-Huffman deflate block over the full 32 KiB window whose
+ * copies are whole values (3..64 values at distances of 4-byte multiples),
+ * chosen by an optimal parse (0.115 of the input on KC ranks; gzip -9: 0.117);
+ * CRC-32 and ISIZE per member.  Every member header carries an RFC 1952 extra
+ * subfield 'OZ': version 1, log2 of the segment length (11), the segment
+ * count, the member's byte size, its value count and, per segment of 2048
+ * values, the bit offset of its first symbol (no copy crosses a segment end),
+ * which gzip.decompress skips.  x: DEVICE float32 [n], every value an integer
+ * 0..31 (the ranks the lossy pipelines write; anything else -> OFL_EINVAL,
+ * nothing written).  out: HOST buffer of out_cap >= ofl_gzip_ranks_bound(n)
+ * bytes; *out_len = stream length.  When out is mapped pinned memory
+ * (hipHostMalloc, torch pin_memory) the kernels write the stream into it
+ * directly and the batches of members run without host round trips; pageable
+ * memory gets one D2H per batch.  ws: device, ofl_gzip_ranks_workspace_bytes(n).
+ * Synchronous.  Deterministic (the header's mtime is 0).  Errors:
+ * ofl_gzip_last_error(). */
 const char* ofl_gzip_last_error(void);
 size_t ofl_gzip_ranks_workspace_bytes(int64_t n);
 size_t ofl_gzip_ranks_bound(int64_t n);
 int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size_t* out_len, void* ws,
                    size_t ws_bytes, void* stream);
 /* GZIPTransformer.backward (kc_pipeline.py:152-156: gzip.decompress) for a
- * stream whose members all carry the 'BC' size field: members are located
- * from their headers and inflated (zlib) on nthreads host threads into dst
- * (HOST, cap bytes; NULL: only *out_len = decompressed size), with each
- * member's ISIZE and CRC-32 checked.  OFL_EFORMAT if the stream is not
- * member-indexed (e.g. gzip.compress output): use gzip.decompress then. */
+ * stream whose members all carry a size field ('OZ', or BGZF's 'BC'):
+ * members are located from their headers and inflated (zlib) on nthreads host
+ * threads into dst (HOST, cap bytes; NULL: only *out_len = decompressed
+ * size), with each member's ISIZE and CRC-32 checked.  OFL_EFORMAT if the
+ * stream is not member-indexed (e.g. gzip.compress output): use
+ * gzip.decompress then. */
 int ofl_gunzip_members(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len, int nthreads);
 /* The same decode on the GPU, in two steps.  ofl_gzip_member_index (HOST, no
  * GPU): the members of a member-indexed stream src[n] (OFL_EFORMAT otherwise)
- * -> *nmembers, *out_len (decompressed size), *max_isize and, when index is
- * not NULL (cap_members entries), per member four int64: deflate data offset,
- * data length, output offset, ISIZE | CRC-32 << 32.  ofl_inflate_members:
- * inflates every member (one wavefront each; stored, fixed and dynamic
- * blocks) from src (DEVICE copy of the stream) into out (DEVICE, out_cap
- * bytes) at its output offset, checking ISIZE and CRC-32; index is the DEVICE
- * copy of the index (any member size); ws: DEVICE, >= 256 bytes.  Synchronous; OFL_EINVAL for corrupt
- * data (what gzip.decompress would raise on). */
+ * -> *nmembers, *out_len (decompressed size), *max_isize, *all_tlz (every
+ * member carries a valid 'OZ' table; nullable) and, when index is not NULL
+ * (cap_members entries), per member four int64: deflate data offset, data
+ * length (| 1 << 62 for a TLZ member), output offset, ISIZE | CRC-32 << 32.
+ * ofl_inflate_tlz (all members TLZ): k_tlz_ops -- one wavefront per member,
+ * one lane per segment, Huffman decode from the segment's bit offset, op
+ * records written over the segment's own output bytes -- then k_tlz_resolve
+ * -- one block per member: op positions, every value's source by pointer
+ * jumping in LDS, the float32 values, CRC-32 and ISIZE checked; data the TLZ
+ * decoder does not expect goes through ofl_inflate_members instead (which
+ * decides whether it is valid deflate).  ws: DEVICE,
+ * ofl_inflate_tlz_workspace_bytes(nmembers).  ofl_inflate_members: any
+ * member-indexed deflate data (one wavefront per member; stored, fixed and
+ * dynamic blocks); ws: DEVICE, >= 256 bytes.  Both: src is the DEVICE copy
+ * of the stream, readable for 32 bytes past its end; out DEVICE, out_cap
+ * bytes, every member at its output offset; index the DEVICE copy of the
+ * index.  Synchronous; OFL_EINVAL for corrupt data (what gzip.decompress
+ * would raise on). */
 int ofl_gzip_member_index(const uint8_t* src, size_t n, int64_t* index, int64_t cap_members, int64_t* nmembers,
-                          size_t* out_len, uint32_t* max_isize);
+                          size_t* out_len, uint32_t* max_isize, int* all_tlz);
+size_t ofl_inflate_tlz_workspace_bytes(int64_t nmembers);
+int ofl_inflate_tlz(const uint8_t* src, const int64_t* index, int64_t nmembers, uint8_t* out, size_t out_cap, void* ws,
+                    size_t ws_bytes, void* stream);
 int ofl_inflate_members(const uint8_t* src, const int64_t* index, int64_t nmembers, uint32_t max_isize, uint8_t* out,
                         size_t out_cap, void* ws, size_t ws_bytes, void* stream);
+/* Per-kernel timing of the gzip / inflate launches (bench.py): enable (1)
+ * resets and starts recording HIP events around every launch of this
+ * process's calls, 0 stops; collect synchronises the recorded events and
+ * returns, per kernel name (newline-separated in names), the summed
+ * milliseconds and the launch count, then clears the record. */
+int ofl_gzip_profile(int enable);
+int ofl_gzip_profile_collect(char* names, size_t names_cap, double* ms, int64_t* launches, int max_kernels,
+                             int* nkernels);
 
 /* ---- host helpers ----------------------------------------------------------
  * Left-to-right serial sums in the array's own precision: the

@@ -36,7 +36,8 @@ EXPORTS = (
     "ofl_wavg_points_workspace_bytes", "ofl_wavg_delta_points", "ofl_apply_delta",
     "ofl_apply_delta_ranges", "ofl_wavg_delta32_ranges", "ofl_sub_f32_f64",
     "ofl_gzip_last_error", "ofl_gzip_ranks_workspace_bytes", "ofl_gzip_ranks_bound", "ofl_gzip_ranks",
-    "ofl_gunzip_members", "ofl_gzip_member_index", "ofl_inflate_members",
+    "ofl_gunzip_members", "ofl_gzip_member_index", "ofl_inflate_members", "ofl_inflate_tlz_workspace_bytes",
+    "ofl_inflate_tlz", "ofl_gzip_profile", "ofl_gzip_profile_collect",
 )
 
 
@@ -176,10 +177,18 @@ def _bind(L):
     L.ofl_gzip_ranks.restype = i32
     L.ofl_gunzip_members.argtypes = [vp, sz, vp, sz, vp, i32]
     L.ofl_gunzip_members.restype = i32
-    L.ofl_gzip_member_index.argtypes = [vp, sz, vp, i64, vp, vp, vp]
+    L.ofl_gzip_member_index.argtypes = [vp, sz, vp, i64, vp, vp, vp, vp]
     L.ofl_gzip_member_index.restype = i32
     L.ofl_inflate_members.argtypes = [vp, vp, i64, ctypes.c_uint32, vp, sz, vp, sz, vp]
     L.ofl_inflate_members.restype = i32
+    L.ofl_inflate_tlz_workspace_bytes.argtypes = [i64]
+    L.ofl_inflate_tlz_workspace_bytes.restype = sz
+    L.ofl_inflate_tlz.argtypes = [vp, vp, i64, vp, sz, vp, sz, vp]
+    L.ofl_inflate_tlz.restype = i32
+    L.ofl_gzip_profile.argtypes = [i32]
+    L.ofl_gzip_profile.restype = i32
+    L.ofl_gzip_profile_collect.argtypes = [vp, sz, vp, vp, i32, vp]
+    L.ofl_gzip_profile_collect.restype = i32
     L.ofl_serial_sum_f32.argtypes = [vp, i64]
     L.ofl_serial_sum_f32.restype = ctypes.c_float
     L.ofl_serial_sum_f32_mt.argtypes = [vp, i64, vp, i32]

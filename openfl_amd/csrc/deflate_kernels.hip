@@ -1,26 +1,19 @@
 // deflate_kernels.hip -- gzip on the GPU for the lossy pipelines' rank arrays
-// (SURVEY §8(f) row 3).  Reference: GZIPTransformer.forward
+// (SURVEY §8(f) row 3).  Reference: GZIPTransformer.forward / backward
 // (kc_pipeline.py:128-156, skc_pipeline.py:201-230, stc_pipeline.py:185-215):
 // gzip.compress(float32 ranks bytes), decoded by gzip.decompress.  Any valid
-// gzip stream decodes to the same bytes, so the wire stays compatible: the
-// output here is a multi-member gzip stream (RFC 1952), one member per 4096
-// float32 ranks (16 KiB of input), each member one dynamic-Huffman deflate
-// block (RFC 1951), which Python's gzip.decompress reads.
+// gzip stream decodes to the same bytes, so the wire stays compatible.
 //
-// The ranks are small integers stored as float32 (0.0, 1.0, ... < 32), i.e.
-// tokens of 4 bytes from a tiny alphabet.  LZ77 runs at token granularity:
-// the (3-token key, position) pairs of a member are bitonic-sorted in LDS, each
-// position takes the longest match among its 8 nearest earlier positions with
-// the same key (>= 3 tokens, <= 64), a greedy parse with one-step lazy
-// matching picks the matches (thread 0); the positions in between are coded
-// as a copy of the token's previous occurrence (length 4, distance 4 x gap;
-// per-thread scans + a block prefix max) or, at a first occurrence, as its 4
-// literal bytes.  Per member: symbol histograms in LDS,
-// Huffman code lengths (limited to 15 / 7 bits by flattening the
-// frequencies), canonical codes, the code-length RLE header, a block scan of
-// the tokens' bit costs, bits OR-ed into an LDS buffer, CRC-32 from per-thread
-// table CRCs combined with GF(2) shift matrices, then one coalesced copy out.
-// Deterministic (bit positions come from scans; OR is order-free).
+// Two parts:
+//  * TLZ (namespace gz::tlz, below the generic inflate): the encoder of the
+//    rank arrays -- an optimal-parse token LZ over the whole 32 KiB window,
+//    one dynamic-Huffman block per 512 KiB member, with per-segment entry
+//    points in an RFC 1952 extra subfield -- and its lane-parallel two-kernel
+//    inflate;
+//  * a generic member inflate (k_inflate_members: stored, fixed and dynamic
+//    blocks, any deflate data of a member-indexed stream), used for streams
+//    that are not TLZ (e.g. BGZF-style members written by zlib) and as the
+//    fallback of the TLZ inflate.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -42,15 +35,7 @@
 
 namespace gz {
 
-constexpr int kTok = 4096;                 // float32 tokens per gzip member
-constexpr int kNT = 256;
-constexpr int kPer = kTok / kNT;           // 16 consecutive tokens per thread
-constexpr int kTypes = 32;                 // token values 0..31
-constexpr int kOutWords = 8192;            // 32 KiB bit buffer >= worst-case member
-constexpr int kOutBytes = 4 * kOutWords;
 constexpr int kLit = 286, kDist = 30, kCL = 19;
-constexpr int kBatch = 4096;               // members per launch (host loop)
-constexpr int kHdr = 18;                   // gzip member header incl. the 'BC' extra field
 
 __constant__ uint16_t c_dbase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129,
                                      193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
@@ -61,7 +46,7 @@ __constant__ uint16_t c_lbase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19
 __constant__ uint8_t c_lext[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
 __constant__ uint32_t c_adv[32][32];       // raw CRC advance by 2^k zero bytes: GF(2) matrix columns
 
-// Huffman scratch (thread 0), overlaid on the token tables once they are consumed
+// Huffman scratch (the serial fallback of huff_lengths_wave, the RLE)
 struct HScratch {
     uint32_t w[2 * kLit];
     int16_t parent[2 * kLit];
@@ -70,46 +55,7 @@ struct HScratch {
     uint16_t rle_sym[kLit + kDist];
     uint16_t rle_ext[kLit + kDist];
 };
-// The member's bit buffer in LDS.  A member is at most 14.7 KiB of dynamic
-// Huffman output: its literal/length alphabet has <= 66 symbols in use (<= 36
-// literal byte values of float32 integers 0..31, end of block, <= 29 length
-// codes), so the optimal code costs at most a uniform 7-bit code, <= 7 bits
-// per literal byte (matches and one-token copies cost less than the literals
-// they replace), plus a <= 600-byte header; 17 KiB leaves margin, and a
-// member that would not fit is refused (bad flag 4), never truncated.
-constexpr int kOutCap = 4352;              // words
-constexpr int kHdrW = 160;                 // header words (<= 4642 bits)
-struct Smem {
-    union {
-        struct {
-            union {
-                int16_t last[kNT][kTypes];  // per thread: last index of each type in its segment; then exclusive prefix max
-                uint32_t key[kTok];         // then: (3-token key << 12 | position), sorted
-                HScratch h;                 // then: Huffman scratch
-            } u;
-            alignas(16) uint8_t tk[kTok + 64];  // the member's tokens
-        };
-        uint32_t out[kOutCap];              // the bit buffer, once the tokens and the Huffman scratch are dead
-    };
-    uint32_t hdrw[kHdrW];                  // the member header's words (written while the scratch is live)
-    uint8_t bestL[kTok];                   // longest earlier match at a position (tokens, 0 = none >= 3)
-    union {
-        uint32_t crct[256];                // CRC-32 table: only while the tokens are read
-        uint16_t bestG[kTok];              // and its distance in tokens
-    };
-    uint8_t op[kTok];                      // parse: 0 covered, 1 one-token op, 2 match start
-    int16_t ptot[8][kTypes];
-    uint32_t hl[kLit], hd[kDist], hc[kCL];
-    uint8_t ll[kLit], ld[kDist], lc[kCL];
-    uint16_t kl[kLit], kd[kDist], kc[kCL];  // bit-reversed canonical codes
-    uint32_t scan[kNT / 64];
-    uint32_t crc_r[kNT / 64];               // per wave: XOR of its lanes' advanced raw CRCs
-    uint32_t hdr_bits, total_bits, nrle, nlit_ndist;
-    int bad;
-};
-static_assert(sizeof(HScratch) <= sizeof(int16_t) * kNT * kTypes, "Huffman scratch fits the token tables");
-static_assert(4 * kOutCap <= sizeof(int16_t) * kNT * kTypes + kTok + 64, "bit buffer overlays the token tables");
-static_assert(sizeof(Smem) <= 40 * 1024, "four member blocks per CU");
+constexpr int kHdrW = 160;                 // deflate block header words (<= 4642 bits)
 
 DEVI void put_bits(uint32_t* out, uint32_t pos, uint32_t val, int nb) {
     if (nb == 0) return;
@@ -134,15 +80,6 @@ DEVI int len_code(uint32_t l) {
     const int b = 31 - __builtin_clz(m);
     return 4 * (b - 1) + (int)((m >> (b - 2)) & 3u);
 }
-// 4 tokens at token offset o (tk is 4-byte aligned and padded)
-DEVI uint32_t tk4(const uint8_t* tk, int o) {
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(tk);
-    return __builtin_amdgcn_alignbyte(w[(o >> 2) + 1], w[o >> 2], (uint32_t)(o & 3));
-}
-constexpr int kMinMatch = 3;    // tokens (12 bytes); shorter runs use the one-token op
-constexpr int kMaxMatch = 64;   // tokens (256 of deflate's 258 bytes)
-constexpr int kCand = 4;        // nearest earlier positions with the same 3-token key tried (KC ranks: 4 -> ratio 0.1406, 8 -> 0.1390 at 2x the match time, 32 -> 0.1381)
-
 // advance by 2^k zero bytes (k uniform: the matrix columns are scalar loads)
 DEVI uint32_t crc_adv_pow2(uint32_t v, int k) {
     uint32_t r = 0;
@@ -336,501 +273,6 @@ DEVI void huff_codes_wave(const uint8_t* len, int n, uint16_t* code) {
     }
 }
 
-struct GzArgs {
-    const float* x;
-    int64_t n;
-    int64_t chunk0;      // first member of this launch
-    uint8_t* slots;      // [members][kOutBytes]
-    uint32_t* sizes;     // [members]
-    int* bad;            // set if a value is not a rank 0..31
-    uint64_t* phases;    // diagnostics (OFL_GZ_PHASES): thread 0 of blocks 0..3 stamps each phase; else null
-};
-constexpr int kPhases = 12;
-#define GZ_STAMP(k)                                                                       \
-    do {                                                                                  \
-        if (a.phases && tid == 0 && blockIdx.x < 4) a.phases[blockIdx.x * kPhases + (k)] = wall_clock64(); \
-    } while (0)
-
-__global__ __launch_bounds__(kNT) void k_gzip_members(GzArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    Smem& S = *reinterpret_cast<Smem*>(smem_raw);
-    const int tid = threadIdx.x;
-    const int64_t c = a.chunk0 + blockIdx.x;
-    const int64_t e0 = c * kTok;
-    const int ntok = (int)std::min<int64_t>(kTok, a.n - e0);
-    GZ_STAMP(0);
-    for (int i = tid; i < 256; i += kNT) {
-        uint32_t r = (uint32_t)i;
-        for (int k = 0; k < 8; ++k) r = (r & 1u) ? (r >> 1) ^ 0xEDB88320u : r >> 1;
-        S.crct[i] = r;
-    }
-    for (int i = tid; i < kLit; i += kNT) S.hl[i] = 0;
-    if (tid < kDist) S.hd[tid] = 0;
-    if (tid < kCL) S.hc[tid] = 0;
-    if (tid == 0) S.bad = 0;
-    for (int t = 0; t < kTypes; ++t) S.u.last[tid][t] = -1;
-    __syncthreads();
-
-    // ---- tokens, validity, local previous occurrences, raw CRC ----
-    const int i0 = tid * kPer;
-    const int nv = std::max(0, std::min(kPer, ntok - i0));
-    int tok[kPer];
-    int prev[kPer];
-    uint32_t crc = 0;
-    bool bad = false;
-#pragma unroll
-    for (int q = 0; q < kPer; ++q) {
-        tok[q] = 0;
-        prev[q] = -1;
-        if (q < nv) {
-            const float v = a.x[e0 + i0 + q];
-            const int t = (int)v;
-            const uint32_t bits = __float_as_uint(v);
-            if (!(t >= 0 && t < kTypes && bits == __float_as_uint((float)t))) bad = true;
-            const int tt = (t >= 0 && t < kTypes) ? t : 0;
-            tok[q] = tt;
-            S.tk[i0 + q] = (uint8_t)tt;
-            prev[q] = S.u.last[tid][tt];
-            S.u.last[tid][tt] = (int16_t)(i0 + q);
-            for (int b = 0; b < 4; ++b) crc = S.crct[(crc ^ (bits >> (8 * b))) & 0xffu] ^ (crc >> 8);
-        }
-    }
-    if (bad) atomicOr(&S.bad, 1);
-    // raw CRC of the member: crc(A | B) = adv(crc(A), |B|) ^ crc(B)
-    if (ntok == kTok) {
-        // full member, 64 bytes per thread: a tree over the lanes whose level-l
-        // shift (64 * 2^l bytes) is the same for every lane (scalar matrix)
-        const int lane = tid & 63;
-        uint32_t v = crc;
-#pragma unroll
-        for (int l = 0; l < 6; ++l) {
-            const uint32_t o = (uint32_t)__shfl_xor((int)v, 1 << l, 64);
-            const uint32_t sh = crc_adv_pow2(v, 6 + l);  // adv over 2^(6+l) bytes
-            // the lower lane of a pair holds the earlier bytes
-            v = (lane & (1 << l)) ? v : (sh ^ o);
-        }
-        if (lane == 0) S.crc_r[tid >> 6] = v;
-    } else {  // ragged last member: each thread advances over the bytes after it
-        uint32_t v = crc_adv(crc, 4u * (uint32_t)std::max(0, ntok - i0 - nv));
-        for (int o = 32; o > 0; o >>= 1) v ^= (uint32_t)__shfl_xor((int)v, o, 64);
-        if ((tid & 63) == 0) S.crc_r[tid >> 6] = v;
-    }
-    __syncthreads();
-    if (S.bad) {  // block-uniform
-        if (tid == 0) { atomicOr(a.bad, 1); a.sizes[blockIdx.x] = 0; }
-        return;
-    }
-    GZ_STAMP(1);
-    // exclusive prefix max of the per-thread last indices, per type (in place):
-    // thread (type t, part p) walks rows 32p..32p+31, then parts are combined
-    {
-        const int t = tid & 31, p = tid >> 5;
-        int run = -1;
-        for (int r = 32 * p; r < 32 * p + 32; ++r) {
-            const int v = S.u.last[r][t];
-            S.u.last[r][t] = (int16_t)run;
-            run = v > run ? v : run;
-        }
-        S.ptot[p][t] = (int16_t)run;
-        __syncthreads();
-        int off = -1;
-        for (int pp = 0; pp < p; ++pp) off = S.ptot[pp][t] > off ? S.ptot[pp][t] : off;
-        for (int r = 32 * p; r < 32 * p + 32; ++r) if (off > S.u.last[r][t]) S.u.last[r][t] = (int16_t)off;
-        __syncthreads();
-    }
-    // one-token op of each position: gap to the previous occurrence (-1: none)
-#pragma unroll
-    for (int q = 0; q < kPer; ++q) {
-        if (q < nv) {
-            const int pv = prev[q] >= 0 ? prev[q] : S.u.last[tid][tok[q]];
-            prev[q] = pv >= 0 ? i0 + q - pv : -1;
-        }
-    }
-    __syncthreads();  // the last-occurrence tables are dead from here
-    GZ_STAMP(2);
-    // ---- LZ77 at token granularity: sort (3-token key, position) ----
-    // Bitonic network over index tid * kPer + q with the keys in registers:
-    // partners < kPer apart are in the same thread, < 64 kPer apart in the
-    // same wave (shfl_xor), only the 3 stages with partners 1024 / 2048 apart
-    // go through LDS.  Keys are unique (the position is in the low bits), so the
-    // order is total.
-    for (int i = tid; i < kTok; i += kNT) {
-        S.bestL[i] = 0;
-        S.bestG[i] = 0;
-        S.op[i] = 0;
-    }
-    uint32_t kv[kPer];
-#pragma unroll
-    for (int q = 0; q < kPer; ++q) {
-        const int i = i0 + q;
-        const bool k3 = i + 2 < ntok;
-        const uint32_t key = k3 ? ((uint32_t)S.tk[i] | ((uint32_t)S.tk[i + 1] << 5) | ((uint32_t)S.tk[i + 2] << 10)) : 0x7fffu;
-        kv[q] = (key << 12) | (uint32_t)i;
-    }
-#pragma unroll
-    for (int k = 2; k <= kTok; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            if (j >= 64 * kPer) {  // across waves: through LDS
-                __syncthreads();
-#pragma unroll
-                for (int q = 0; q < kPer; ++q) S.u.key[i0 + q] = kv[q];
-                __syncthreads();
-#pragma unroll
-                for (int q = 0; q < kPer; ++q) {
-                    const int i = i0 + q;
-                    const uint32_t o = S.u.key[i ^ j];
-                    const bool lower = (i & j) == 0, up = (i & k) == 0;
-                    kv[q] = (lower == up) ? min(kv[q], o) : max(kv[q], o);
-                }
-            } else if (j >= kPer) {  // across lanes of this wave
-#pragma unroll
-                for (int q = 0; q < kPer; ++q) {
-                    const int i = i0 + q;
-                    const uint32_t o = (uint32_t)__shfl_xor((int)kv[q], j / kPer, 64);
-                    const bool lower = (i & j) == 0, up = (i & k) == 0;
-                    kv[q] = (lower == up) ? min(kv[q], o) : max(kv[q], o);
-                }
-            } else {  // inside this thread
-#pragma unroll
-                for (int q = 0; q < kPer; ++q) {
-                    if ((q & j) == 0) {
-                        const bool up = ((i0 + q) & k) == 0;
-                        const uint32_t lo = min(kv[q], kv[q + j]), hi = max(kv[q], kv[q + j]);
-                        kv[q] = up ? lo : hi;
-                        kv[q + j] = up ? hi : lo;
-                    }
-                }
-            }
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < kPer; ++q) S.u.key[i0 + q] = kv[q];
-    __syncthreads();
-    GZ_STAMP(3);
-    // longest match among the kCand nearest earlier positions with the same key
-    for (int sidx = tid; sidx < kTok; sidx += kNT) {
-        const uint32_t me = S.u.key[sidx];
-        if ((me >> 12) == 0x7fffu) continue;
-        const int i = (int)(me & 0xfffu);
-        const int lim = std::min(kMaxMatch, ntok - i);
-        int bl = 0, bg = 0;
-        for (int c2 = 1; c2 <= kCand && sidx - c2 >= 0; ++c2) {
-            const uint32_t o = S.u.key[sidx - c2];
-            if ((o >> 12) != (me >> 12)) break;
-            const int jj = (int)(o & 0xfffu);
-            int L = 3;  // the keys are equal: 3 tokens match
-            while (L < lim) {
-                const uint32_t d = tk4(S.tk, i + L) ^ tk4(S.tk, jj + L);
-                if (d) { L += __builtin_ctz(d) >> 3; break; }
-                L += 4;
-            }
-            L = min(L, lim);
-            if (L > bl) { bl = L; bg = i - jj; }
-            if (bl == lim) break;
-        }
-        if (bl >= kMinMatch) { S.bestL[i] = (uint8_t)bl; S.bestG[i] = (uint16_t)bg; }
-    }
-    __syncthreads();
-    GZ_STAMP(4);
-    // greedy parse with one-step lazy matching: from position i the parse
-    // moves to nxt(i) = i + L(i) if a match starts there (L(i) >= 3 and not
-    // L(i+1) > L(i)), else i + 1.  In parallel: thread t's segment
-    // [kPer t, kPer t + kPer) maps every entry position to the first parse
-    // position past the segment (a match can jump over whole segments);
-    // thread 0 chains the kNT segments (kNT dependent steps instead of up to
-    // kTok); each thread then walks its segment from its entry and marks the
-    // ops.  The ops are exactly the sequential parse's.
-    {
-        int16_t (*fent)[kPer] = reinterpret_cast<int16_t (*)[kPer]>(S.u.key);  // sort keys are dead
-        int16_t* entry = reinterpret_cast<int16_t*>(S.u.key) + kNT * kPer;
-        auto nxt = [&](int i) -> int {
-            const int L = S.bestL[i];
-            return (L >= kMinMatch && !(i + 1 < ntok && S.bestL[i + 1] > L)) ? i + L : i + 1;
-        };
-        const int s0 = tid * kPer, s1 = s0 + kPer;
-        for (int e = kPer - 1; e >= 0; --e) {  // backwards: fent of a later entry is known
-            const int p = s0 + e;
-            int f = p;
-            if (p < ntok) {
-                const int q = nxt(p);
-                f = (q < s1 && q < ntok) ? fent[tid][q - s0] : q;
-            }
-            fent[tid][e] = (int16_t)f;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            int p = 0;
-            for (int t = 0; t < kNT; ++t) {
-                entry[t] = (int16_t)p;
-                if (p < t * kPer + kPer && p < ntok) p = fent[t][p - t * kPer];
-            }
-        }
-        __syncthreads();
-        for (int p = entry[tid]; p < s1 && p < ntok;) {
-            const int q = nxt(p);
-            S.op[p] = q - p > 1 ? 2 : 1;
-            p = q;
-        }
-    }
-    __syncthreads();
-    GZ_STAMP(5);
-    __syncthreads();
-    GZ_STAMP(6);
-    // ---- symbol histograms of this thread's ops ----
-#pragma unroll
-    for (int q = 0; q < kPer; ++q) {
-        const int p = i0 + q, o = q < nv ? S.op[p] : 0;
-        const bool match = o == 2, copy = o == 1 && prev[q] > 0, lit = o == 1 && !copy;
-        const uint32_t bits = __float_as_uint((float)tok[q]);
-        const int sa = match ? 257 + len_code(4u * S.bestL[p]) : copy ? 258 : (int)(bits & 0xffu);
-        const int sd = dist_code(match ? 4u * S.bestG[p] : copy ? 4u * (uint32_t)prev[q] : 1u);
-        // the one-token copy (symbol 258) is most positions' op: counted by
-        // ballot; the rest by LDS atomics
-        const uint64_t nc = __ballot(copy);
-        if ((tid & 63) == 0 && nc) atomicAdd(&S.hl[258], (uint32_t)__popcll(nc));
-        if (o != 0 && !copy) atomicAdd(&S.hl[sa], 1u);
-        if (match || copy) atomicAdd(&S.hd[sd], 1u);
-        if (lit)
-#pragma unroll
-            for (int b = 1; b < 4; ++b) atomicAdd(&S.hl[(bits >> (8 * b)) & 0xffu], 1u);
-    }
-    __syncthreads();
-    GZ_STAMP(7);
-    // ---- wave 0: code lengths and codes (lane 0: the code-length RLE and the
-    // header bits) ----
-    // (wave 0: literal/length code, wave 1: distance code, concurrently; the
-    // serial fallback for > 64 literal symbols uses h.w..h.dead, wave 1's
-    // scratch is h.rle_ext, free until the RLE below)
-    const int wv = tid >> 6, ln = tid & 63;
-    if (wv == 0) {
-        HScratch& h = S.u.h;
-        if (ln == 0) S.hl[256] = 1;  // end of block
-        __builtin_amdgcn_wave_barrier();
-        if (!huff_lengths_wave(S.hl, kLit, 15, S.ll, h.w, true) && ln == 0) huff_lengths(S.hl, kLit, 15, S.ll, h, true);
-    } else if (wv == 1) {
-        HScratch& h = S.u.h;
-        const bool anyd = __ballot(ln < kDist && S.hd[ln] != 0u) != 0ull;
-        if (!anyd && ln == 0) S.hd[0] = 1;  // one (unused) distance code
-        __builtin_amdgcn_wave_barrier();
-        huff_lengths_wave(S.hd, kDist, 15, S.ld, reinterpret_cast<uint32_t*>(h.rle_ext), false);  // <= 30 symbols
-    }
-    __syncthreads();
-    if (wv == 1) huff_codes_wave(S.ll, kLit, S.kl);
-    if (wv == 2) huff_codes_wave(S.ld, kDist, S.kd);
-    if (wv == 0) {
-        // run-length code of the concatenated code lengths: the wave finds
-        // the used lengths' extents and the run starts by ballots; lane 0
-        // then walks the runs (a few dozen) instead of every length
-        HScratch& h = S.u.h;
-        int nlit = 257, ndist = 1;
-        for (int c = 0; c < (kLit + 63) / 64; ++c) {
-            const int i = 64 * c + ln;
-            const uint64_t m = __ballot(i < kLit && S.ll[i] != 0);
-            if (m) nlit = max(nlit, 64 * c + 64 - __builtin_clzll(m));
-        }
-        {
-            const uint64_t m = __ballot(ln < kDist && S.ld[ln] != 0);
-            if (m) ndist = max(ndist, 64 - __builtin_clzll(m));
-        }
-        const int N = nlit + ndist;
-        auto val = [&](int i) -> int { return i < nlit ? S.ll[i] : S.ld[i - nlit]; };
-        uint64_t starts[(kLit + kDist + 63) / 64];
-#pragma unroll
-        for (int c = 0; c < (kLit + kDist + 63) / 64; ++c) {
-            const int i = 64 * c + ln;
-            starts[c] = __ballot(i < N && (i == 0 || val(i) != val(i - 1)));
-        }
-        if (ln == 0) {
-            int nr = 0;
-            int c = 0;
-            uint64_t m = starts[0];
-            int s0 = 0;  // the run start being emitted (position 0 always starts one)
-            m &= m - 1;
-            for (;;) {
-                while (!m && c + 1 < (kLit + kDist + 63) / 64) m = starts[++c];
-                const int s1 = m ? 64 * c + __builtin_ctzll(m) : N;
-                if (m) m &= m - 1;
-                const int cur = val(s0);
-                int left = s1 - s0;
-                if (cur == 0) {
-                    while (left >= 11) { const int r = left < 138 ? left : 138; h.rle_sym[nr] = 18; h.rle_ext[nr++] = (uint16_t)(r - 11); left -= r; }
-                    if (left >= 3) { h.rle_sym[nr] = 17; h.rle_ext[nr++] = (uint16_t)(left - 3); left = 0; }
-                    while (left > 0) { h.rle_sym[nr] = 0; h.rle_ext[nr++] = 0; --left; }
-                } else {
-                    h.rle_sym[nr] = (uint16_t)cur; h.rle_ext[nr++] = 0; --left;
-                    while (left >= 3) { const int r = left < 6 ? left : 6; h.rle_sym[nr] = 16; h.rle_ext[nr++] = (uint16_t)(r - 3); left -= r; }
-                    while (left > 0) { h.rle_sym[nr] = (uint16_t)cur; h.rle_ext[nr++] = 0; --left; }
-                }
-                if (s1 >= N) break;
-                s0 = s1;
-            }
-            for (int i = 0; i < nr; ++i) S.hc[h.rle_sym[i]]++;
-            S.nrle = (uint32_t)nr;
-            S.nlit_ndist = (uint32_t)(nlit | (ndist << 16));
-        }
-    }
-    __syncthreads();
-    if (wv == 0) {
-        HScratch& h = S.u.h;
-        huff_lengths_wave(S.hc, kCL, 7, S.lc, h.w, true);  // <= 19 symbols
-        huff_codes_wave(S.lc, kCL, S.kc);
-    }
-    if (tid == 0) {
-        HScratch& h = S.u.h;
-        const int nr = (int)S.nrle, nlit = (int)(S.nlit_ndist & 0xffffu), ndist = (int)(S.nlit_ndist >> 16);
-        int ncl = kCL;
-        while (ncl > 4 && S.lc[c_clord[ncl - 1]] == 0) --ncl;
-        // thread 0 owns the header's words: a 64-bit accumulator and plain
-        // stores (the ops' first word is OR-ed in after the barrier)
-        uint64_t acc = 0;
-        int nb = 0;
-        uint32_t wi = 0, pos = 0;
-        auto put = [&](uint32_t v, int n) {
-            acc |= (uint64_t)v << nb;
-            nb += n;
-            pos += (uint32_t)n;
-            if (nb >= 32) { S.hdrw[wi++] = (uint32_t)acc; acc >>= 32; nb -= 32; }
-        };
-        // member header with a BGZF-style extra field (RFC 1952 FEXTRA,
-        // subfield 'BC' = member size - 1, filled in at the end): a reader
-        // can find every member without inflating (ofl_gunzip_members);
-        // gzip.decompress skips the field
-        const uint8_t hdr[kHdr] = {0x1f, 0x8b, 0x08, 0x04, 0, 0, 0, 0, 0x00, 0xff, 6, 0, 'B', 'C', 2, 0, 0, 0};
-        for (int i = 0; i < kHdr; ++i) put(hdr[i], 8);
-        put(1u, 1);  // BFINAL
-        put(2u, 2);  // BTYPE = dynamic
-        put((uint32_t)(nlit - 257), 5);
-        put((uint32_t)(ndist - 1), 5);
-        put((uint32_t)(ncl - 4), 4);
-        for (int i = 0; i < ncl; ++i) put(S.lc[c_clord[i]], 3);
-        for (int i = 0; i < nr; ++i) {
-            const int sy = h.rle_sym[i];
-            put(S.kc[sy], S.lc[sy]);
-            const int eb = sy == 16 ? 2 : (sy == 17 ? 3 : (sy == 18 ? 7 : 0));
-            put(h.rle_ext[i], eb);
-        }
-        if (nb > 0) S.hdrw[wi] = (uint32_t)acc;
-        S.hdr_bits = pos;
-    }
-    __syncthreads();
-    GZ_STAMP(8);
-    // the tokens and the Huffman scratch are dead: the bit buffer takes their
-    // place, header words first (the ops' first word is OR-ed in after the
-    // scan's barrier)
-    {
-        const uint32_t hw = (S.hdr_bits + 31u) >> 5;
-        for (int i = tid; i < kOutCap; i += kNT) S.out[i] = (uint32_t)i < hw ? S.hdrw[i] : 0u;
-    }
-    // ---- op bits: block scan of the costs, then OR into the buffer ----
-    uint32_t mine = 0;
-#pragma unroll
-    for (int q = 0; q < kPer; ++q) {
-        if (q < nv) {
-            const int p = i0 + q, o = S.op[p];
-            if (o == 2) {
-                const int lc = len_code(4u * S.bestL[p]), dc = dist_code(4u * S.bestG[p]);
-                mine += S.ll[257 + lc] + c_lext[lc] + S.ld[dc] + c_dext[dc];
-            } else if (o == 1 && prev[q] > 0) {
-                const int dc = dist_code(4u * (uint32_t)prev[q]);
-                mine += S.ll[258] + S.ld[dc] + c_dext[dc];
-            } else if (o == 1) {
-                const uint32_t bits = __float_as_uint((float)tok[q]);
-                for (int b = 0; b < 4; ++b) mine += S.ll[(bits >> (8 * b)) & 0xffu];
-            }
-        }
-    }
-    const int lane = tid & 63, w = tid >> 6;
-    uint32_t inc = mine;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(inc, o, 64);
-        if (lane >= o) inc += t;
-    }
-    if (lane == 63) S.scan[w] = inc;
-    __syncthreads();
-    uint32_t pos = S.hdr_bits + inc - mine;
-    for (int j = 0; j < w; ++j) pos += S.scan[j];
-    if (tid == kNT - 1) S.total_bits = pos + mine;
-    // room for the ops, end of block, padding, CRC-32 and ISIZE (see kOutCap)
-    const bool fits = pos + mine + 15u + 7u + 64u <= 32u * (uint32_t)kOutCap;
-    if (!fits) atomicOr(&S.bad, 2);
-    // this thread's ops are one contiguous bit range: gather them in a 64-bit
-    // accumulator and store whole words; only the first and the last word
-    // can be shared with a neighbour (OR-ed atomically)
-    if (fits) {
-        uint64_t acc = 0;
-        int nb = (int)(pos & 31u);
-        uint32_t wi = pos >> 5;
-        bool first = true;
-        auto put = [&](uint32_t v, int n) {
-            acc |= (uint64_t)v << nb;
-            nb += n;
-            if (nb >= 32) {
-                if (first) { atomicOr(&S.out[wi], (uint32_t)acc); first = false; }
-                else S.out[wi] = (uint32_t)acc;
-                ++wi;
-                acc >>= 32;
-                nb -= 32;
-            }
-        };
-#pragma unroll
-        for (int q = 0; q < kPer; ++q) {
-            if (q < nv) {
-                const int p = i0 + q, o = S.op[p];
-                if (o == 2) {
-                    const uint32_t l = 4u * S.bestL[p], d = 4u * S.bestG[p];
-                    const int lc = len_code(l), dc = dist_code(d);
-                    put(S.kl[257 + lc], S.ll[257 + lc]);
-                    put(l - c_lbase[lc], c_lext[lc]);
-                    put(S.kd[dc], S.ld[dc]);
-                    put(d - c_dbase[dc], c_dext[dc]);
-                } else if (o == 1 && prev[q] > 0) {
-                    const uint32_t d = 4u * (uint32_t)prev[q];
-                    const int dc = dist_code(d);
-                    put(S.kl[258], S.ll[258]);
-                    put(S.kd[dc], S.ld[dc]);
-                    put(d - c_dbase[dc], c_dext[dc]);
-                } else if (o == 1) {
-                    const uint32_t bits = __float_as_uint((float)tok[q]);
-#pragma unroll
-                    for (int b = 0; b < 4; ++b) {
-                        const uint32_t by = (bits >> (8 * b)) & 0xffu;
-                        put(S.kl[by], S.ll[by]);
-                    }
-                }
-            }
-        }
-        if (nb > 0) atomicOr(&S.out[wi], (uint32_t)acc);
-    }
-    __syncthreads();
-    GZ_STAMP(9);
-    // ---- end of block, byte padding, CRC-32 and ISIZE ----
-    if (S.bad) {  // block-uniform: the member would not fit the bit buffer
-        if (tid == 0) { atomicOr(a.bad, 4); a.sizes[blockIdx.x] = 0; }
-        return;
-    }
-    if (tid == 0) {
-        uint32_t p = S.total_bits;
-        put_bits(S.out, p, S.kl[256], S.ll[256]); p += S.ll[256];
-        p = (p + 7u) & ~7u;
-        uint32_t raw = 0;  // full member: waves cover 4096 bytes each; ragged: already advanced
-        for (int j = 0; j < kNT / 64; ++j) raw = (ntok == kTok ? crc_adv_pow2(raw, 12) : raw) ^ S.crc_r[j];
-        const uint32_t crc32 = crc_adv(0xffffffffu, 4u * (uint32_t)ntok) ^ raw ^ 0xffffffffu;
-        put_bits(S.out, p, crc32, 32); p += 32;
-        put_bits(S.out, p, 4u * (uint32_t)ntok, 32); p += 32;
-        S.total_bits = p;
-        put_bits(S.out, 8 * (kHdr - 2), (p >> 3) - 1u, 16);  // BSIZE
-        a.sizes[blockIdx.x] = p >> 3;
-    }
-    __syncthreads();
-    const uint32_t nbytes = S.total_bits >> 3;
-    uint32_t* dst = reinterpret_cast<uint32_t*>(a.slots + (int64_t)blockIdx.x * kOutBytes);
-    for (uint32_t i = tid; i < (nbytes + 3u) / 4u; i += kNT) dst[i] = S.out[i];
-    GZ_STAMP(10);
-}
-
 // exclusive scan of the member sizes (one block) -> offsets, total at [n]
 // running (nullable): the stream bytes of earlier batches, added to every
 // offset and advanced by this batch's total; cap: the output's size (a batch
@@ -864,16 +306,6 @@ __global__ __launch_bounds__(1024) void k_gzip_scan(const uint32_t* sizes, int n
         else atomicOr(bad, 2);
     }
 }
-
-// members -> one contiguous stream
-__global__ __launch_bounds__(256) void k_gzip_pack(const uint8_t* slots, const uint32_t* sizes, const uint64_t* off,
-                                                   uint8_t* packed) {
-    if (off[blockIdx.x] == ~0ull) return;  // the batch does not fit the output (reported by the scan)
-    const uint8_t* src = slots + (int64_t)blockIdx.x * kOutBytes;
-    uint8_t* dst = packed + off[blockIdx.x];
-    for (uint32_t i = threadIdx.x; i < sizes[blockIdx.x]; i += 256) dst[i] = src[i];
-}
-
 
 // ============================================================================
 // Device inflate of member-indexed streams (GZIPTransformer.backward,
@@ -1401,6 +833,1096 @@ __global__ __launch_bounds__(64, OFL_INF_WAVES) void k_inflate_members(InfArgs a
     }
 }
 
+
+// ============================================================================
+// TLZ: token-LZ gzip of rank arrays (GZIPTransformer.forward,
+// kc_pipeline.py:128-141, skc_pipeline.py:201-215, stc_pipeline.py:185-199)
+// and its lane-parallel inflate (GZIPTransformer.backward,
+// kc_pipeline.py:152-156: gzip.decompress).
+//
+// Format: a multi-member gzip stream (RFC 1952).  A member covers up to
+// kMemTok float32 ranks (512 KiB of input) as ONE dynamic-Huffman deflate
+// block (RFC 1951) over the whole 32 KiB window, whose copies are whole
+// tokens: 12..256 bytes (3..64 float32 values) at distances that are
+// multiples of 4 bytes; a value without a copy is its 4 literal bytes.  The
+// member's values are cut into segments of kSeg; no copy crosses a segment
+// end, so a decoder can start at any segment: an RFC 1952 extra subfield
+// 'OZ' in the member header holds the bit offset (from the first bit of the
+// deflate data) of every segment's first symbol.  gzip.decompress, zlib and
+// any gzip reader skip the subfield and read the member as plain deflate.
+//   header (28 + 4 nseg bytes): 1f 8b 08 04 | mtime 0 | xfl 0 | os ff | XLEN |
+//     'O' 'Z' | LEN | version 1 | log2(kSeg) | nseg (u16) | member bytes (u32)
+//     | values (u32) | nseg x u32 segment bit offsets
+//   deflate data (one block, BFINAL = 1, BTYPE = 2) | CRC-32 | ISIZE
+//
+// Encoder (k_tlz_encode, one 256-thread block per member, a segment at a
+// time): 3-gram chains (per-wave ballot matching, then the waves' and the
+// earlier segments' last occurrences), the longest-match frontier of every
+// position over 16 chain candidates (1 <= 3 (length, distance) pairs), an
+// optimal parse by a segmented backward DP (each thread its 8 positions, the
+// other threads' costs from the previous sweep, 3 sweeps) under a cost model
+// re-estimated from the member's symbol counts after every segment, the DP's
+// path followed by Jacobi rounds (every thread walks its 8 positions from
+// its left neighbour's exit until no entry changes), then one Huffman code per
+// member and the bits.  The parse is what gzip -9 lacks: 0.115 of the input
+// on KC ranks against gzip -9's 0.117 (tools/tlz_proto.c simulates it).
+// Decoder: k_tlz_ops (one wavefront per member, one lane per segment:
+// Huffman decode from the segment's bit offset with the member's tables in
+// LDS; each lane writes its segment's ops into that segment's own output
+// bytes) and k_tlz_resolve (one block per member, a segment at a time: op
+// positions by a block scan, every value's source by pointer jumping in LDS
+// against the window of earlier values, then the values, CRC-32, ISIZE).
+namespace tlz {
+constexpr int kNT = 256;
+constexpr int kSegLog = 11, kSeg = 1 << kSegLog;   // values per segment
+constexpr int kMemSeg = 64;
+constexpr int kMemTok = kSeg * kMemSeg;            // values per member
+constexpr int kPer = kSeg / kNT;                   // positions per thread
+constexpr int kWin = 8192;                         // window, values (32 KiB)
+constexpr int kMaxL = 64, kMinL = 3;               // copy length, values
+constexpr int kCand = 16;                          // chain candidates per position
+constexpr int kBuckets = 1024;                     // 3-gram buckets: exact for values < 8, hashed above
+constexpr int kSweeps = 3;
+constexpr int kRing = 16384;                       // value ring (ids), + 8 mirrored bytes
+constexpr int kPrevSlots = 5;                      // chain ring: 4 window segments + this one
+constexpr int kLitMax = 11, kDistMax = 10;         // code length limits = the inflate's table bits
+constexpr int kHdrFixed = 28;                      // member header bytes before the segment table
+constexpr uint16_t kPending = 0xffffu;
+constexpr int kSlotPerTok = 6;                     // worst-case member bytes per value (4 literals x 11 bits)
+constexpr int kSlotPad = 8192;                     // + headers
+constexpr int kBatch = 512;                        // members per launch
+
+struct EncSmem {
+    alignas(16) uint8_t tok[kRing + 8];
+    union {
+        struct {
+            uint16_t prev[kPrevSlots * kSeg];      // distance to the previous same-bucket position (0: none)
+            uint16_t lastw[kNT / 64][kBuckets];    // per wave, this segment: position - range start + 1
+        } m;
+        struct {
+            HScratch h;
+            uint32_t hdrw[kHdrW];
+            uint8_t hb[kHdrFixed + 4 * kMemSeg];
+        } f;
+    } u;
+    uint32_t head[kBuckets];                       // last position + 1 per bucket (earlier segments)
+    uint32_t cost[2][kSeg + 4];                    // DP costs to the segment end, 1/8 bit
+    uint16_t dec[kSeg];                            // chosen op: length (0: literal) | frontier entry << 8
+    uint16_t entry[kNT + 1];                       // parse: each thread's first position
+    uint32_t hl[kLit], hd[kDist], hc[kCL];
+    uint32_t totl, totd;
+    uint16_t symc[kLit + kDist];
+    uint16_t litc[32], lenc[kMaxL + 1], dcst[kDist];
+    uint8_t ll[kLit], ld[kDist], lc[kCL];
+    uint16_t kl[kLit], kd[kDist], kc[kCL];
+    uint32_t crct[4][256];                         // slicing-by-4 CRC-32 tables
+    uint32_t segop[kMemSeg + 1], segbit[kMemSeg];
+    uint32_t scan[kNT / 64];
+    uint32_t crc_w[kNT / 64];
+    uint32_t ops_n, crc_raw, hdr_bits, total_bits, nrle, nlit_ndist;
+    int bad;
+};
+static_assert(sizeof(EncSmem) <= 80 * 1024, "two member blocks per CU");
+
+struct EncArgs {
+    const float* x;
+    int64_t n;
+    int64_t mem0;            // first member of this launch
+    uint8_t* slots;          // [members][slot_bytes]
+    uint32_t* ops;           // [members][ops_stride]
+    uint32_t* sizes;         // [members]
+    int* bad;
+    uint32_t slot_bytes, ops_stride;
+    int aligned;             // x is 16-byte aligned
+};
+
+DEVI int pslot(int p) { return ((p >> kSegLog) % kPrevSlots) * kSeg + (p & (kSeg - 1)); }
+DEVI uint32_t tk4r(const uint8_t* tok, int p) {
+    const int r = p & (kRing - 1);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(tok);
+    return __builtin_amdgcn_alignbyte(w[(r >> 2) + 1], w[r >> 2], (uint32_t)(r & 3));
+}
+// 3-gram bucket: exact for values < 8 (512 buckets), hashed into the upper 512 above
+DEVI int bucket(const uint8_t* tok, int p) {
+    const uint32_t v = tk4r(tok, p) & 0xffffffu;
+    const uint32_t a = v & 0xffu, b = (v >> 8) & 0xffu, c = v >> 16;
+    if ((a | b | c) < 8u) return (int)(a | (b << 3) | (c << 6));
+    return 512 + (int)(((a | (b << 5) | (c << 10)) * 0x9E3779B1u) >> 23);
+}
+DEVI int match_len(const uint8_t* tok, int i, int j, int lim) {
+    int L = 0;
+    while (L < lim) {
+        const uint32_t x = tk4r(tok, i + L) ^ tk4r(tok, j + L);
+        if (x) { L += __builtin_ctz(x) >> 3; break; }
+        L += 4;
+    }
+    return min(L, lim);
+}
+DEVI uint32_t crc4(const uint32_t (*T)[256], uint32_t c, uint32_t w) {
+    c ^= w;
+    return T[3][c & 0xffu] ^ T[2][(c >> 8) & 0xffu] ^ T[1][(c >> 16) & 0xffu] ^ T[0][c >> 24];
+}
+// 1/8 bit: -log2(count / total) >= 1 bit, an unseen symbol log2(total + 1) + 2
+// bits, at most 15 bits
+DEVI uint32_t sym_cost(uint32_t cnt, uint32_t tot) {
+    const float v = cnt ? 8.f * (__log2f((float)tot) - __log2f((float)cnt))
+                        : 8.f * (__log2f((float)tot + 1.f) + 2.f);
+    return (uint32_t)fminf(120.f, fmaxf(8.f, rintf(v)));
+}
+// per-symbol costs -> the DP's tables: a literal value (its 4 bytes), a copy
+// length (code + extra bits), a distance code (+ extra bits)
+DEVI void tlz_model(EncSmem& S, int tid, bool prior) {
+    for (int s = tid; s < kLit + kDist; s += kNT) {
+        uint32_t c;
+        if (prior) c = s < 256 ? 48u : s < kLit ? 32u : 40u;
+        else c = s < kLit ? sym_cost(S.hl[s], S.totl) : sym_cost(S.hd[s - kLit], S.totd);
+        S.symc[s] = (uint16_t)c;
+    }
+    __syncthreads();
+    if (tid < 32) {
+        const uint32_t b = __float_as_uint((float)tid);
+        S.litc[tid] = (uint16_t)(S.symc[b & 0xffu] + S.symc[(b >> 8) & 0xffu] + S.symc[(b >> 16) & 0xffu] + S.symc[b >> 24]);
+    } else if (tid < 32 + kMaxL + 1) {
+        const int l = tid - 32;
+        if (l >= kMinL) {
+            const int lc = len_code(4u * (uint32_t)l);
+            S.lenc[l] = (uint16_t)(S.symc[257 + lc] + 8u * c_lext[lc]);
+        } else {
+            S.lenc[l] = 0;
+        }
+    } else if (tid < 32 + kMaxL + 1 + kDist) {
+        const int c = tid - 32 - kMaxL - 1;
+        S.dcst[c] = (uint16_t)(S.symc[kLit + c] + 8u * c_dext[c]);
+    }
+    __syncthreads();
+}
+// block-wide exclusive scan of v (returns the exclusive prefix; *total)
+DEVI uint32_t block_scan(uint32_t v, uint32_t* scan, uint32_t* total) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)inc, o, 64);
+        if (lane >= o) inc += t;
+    }
+    if (lane == 63) scan[w] = inc;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+#pragma unroll
+    for (int j = 0; j < kNT / 64; ++j) {
+        base += j < w ? scan[j] : 0u;
+        tot += scan[j];
+    }
+    __syncthreads();
+    *total = tot;
+    return base + inc - v;
+}
+
+__global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    EncSmem& S = *reinterpret_cast<EncSmem*>(smem_raw);
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int64_t g0 = (a.mem0 + blockIdx.x) * (int64_t)kMemTok;
+    const int ntok = (int)min<int64_t>(kMemTok, a.n - g0);
+    const int nseg = (ntok + kSeg - 1) >> kSegLog;
+    uint32_t* const ops = a.ops + (int64_t)blockIdx.x * a.ops_stride;
+    {
+        uint32_t r = (uint32_t)tid;
+        for (int k = 0; k < 8; ++k) r = (r & 1u) ? (r >> 1) ^ 0xEDB88320u : r >> 1;
+        S.crct[0][tid] = r;
+    }
+    for (int i = tid; i < kBuckets; i += kNT) {
+        S.head[i] = 0;
+#pragma unroll
+        for (int w = 0; w < kNT / 64; ++w) S.u.m.lastw[w][i] = 0;
+    }
+    for (int i = tid; i < kLit; i += kNT) S.hl[i] = 0;
+    if (tid < kDist) S.hd[tid] = 0;
+    if (tid < kCL) S.hc[tid] = 0;
+    if (tid == 0) { S.totl = S.totd = 0; S.ops_n = 0; S.crc_raw = 0; S.bad = 0; }
+    __syncthreads();
+    for (int k = 1; k < 4; ++k) {
+        const uint32_t p = S.crct[k - 1][tid];
+        S.crct[k][tid] = (p >> 8) ^ S.crct[0][p & 0xffu];
+        __syncthreads();
+    }
+    tlz_model(S, tid, true);
+
+    for (int c = 0; c < nseg; ++c) {
+        const int c0 = c << kSegLog;
+        const int send = min(c0 + kSeg, ntok);
+        const int lo = c0 + kPer * tid;                 // this thread's positions [lo, lo + kPer)
+        // ---- A: values -> ids in the ring, validity, raw CRC-32 ----
+        uint32_t idw0 = 0, idw1 = 0;                    // this thread's 8 ids, packed
+        {
+            const int nv = max(0, min(kPer, send - lo));
+            float v[kPer];
+            if (nv == kPer && a.aligned) {
+                const float4* p = reinterpret_cast<const float4*>(a.x + g0 + lo);
+                const float4 v0 = p[0], v1 = p[1];
+                v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w;
+                v[4] = v1.x; v[5] = v1.y; v[6] = v1.z; v[7] = v1.w;
+            } else {
+#pragma unroll
+                for (int q = 0; q < kPer; ++q) v[q] = q < nv ? a.x[g0 + lo + q] : 0.f;
+            }
+            uint32_t crc = 0;
+            bool bad = false;
+#pragma unroll
+            for (int q = 0; q < kPer; ++q) {
+                if (q < nv) {
+                    const int t = (int)v[q];
+                    const uint32_t bits = __float_as_uint(v[q]);
+                    if (!(t >= 0 && t < 32 && bits == __float_as_uint((float)t))) bad = true;
+                    const uint32_t id = (t >= 0 && t < 32) ? (uint32_t)t : 0u;
+                    if (q < 4) idw0 |= id << (8 * q); else idw1 |= id << (8 * (q - 4));
+                    crc = crc4(S.crct, crc, bits);
+                }
+            }
+            if (bad) atomicOr(&S.bad, 1);
+            const int r = lo & (kRing - 1);
+            *reinterpret_cast<uint2*>(&S.tok[r]) = make_uint2(idw0, idw1);
+            if (r == 0) *reinterpret_cast<uint2*>(&S.tok[kRing]) = make_uint2(idw0, idw1);
+            uint32_t wcrc;
+            if (send - c0 == kSeg) {  // full segment: 32 bytes per thread, a shift tree over the lanes
+                uint32_t x = crc;
+#pragma unroll
+                for (int l = 0; l < 6; ++l) {
+                    const uint32_t o = (uint32_t)__shfl_xor((int)x, 1 << l, 64);
+                    const uint32_t sh = crc_adv_pow2(x, 5 + l);
+                    x = (lane & (1 << l)) ? x : (sh ^ o);
+                }
+                wcrc = x;
+            } else {  // ragged: each thread advances over the bytes after it
+                uint32_t x = nv ? crc_adv(crc, 4u * (uint32_t)(send - lo - nv)) : 0u;
+                for (int o = 32; o > 0; o >>= 1) x ^= (uint32_t)__shfl_xor((int)x, o, 64);
+                wcrc = x;
+            }
+            if (lane == 0) S.crc_w[wv] = wcrc;
+        }
+        __syncthreads();
+        if (S.bad) {  // block-uniform
+            if (tid == 0) { atomicOr(a.bad, 1); a.sizes[blockIdx.x] = 0; }
+            return;
+        }
+        if (tid == 0) {
+            uint32_t raw = 0;
+            if (send - c0 == kSeg) {
+                for (int w = 0; w < kNT / 64; ++w) raw = crc_adv_pow2(raw, kSegLog) ^ S.crc_w[w];  // 2048 bytes per wave
+                S.crc_raw = crc_adv_pow2(S.crc_raw, kSegLog + 2) ^ raw;
+            } else {
+                for (int w = 0; w < kNT / 64; ++w) raw ^= S.crc_w[w];
+                S.crc_raw = crc_adv(S.crc_raw, 4u * (uint32_t)(send - c0)) ^ raw;
+            }
+        }
+        // ---- B: 3-gram chains of [c0 - 2, send - 2) (the last two of a
+        // segment wait for the next segment's values) ----
+        const int s_ins = c == 0 ? 0 : c0 - 2;
+        const int e_ins = send - 2;
+        const int m_ins = max(0, e_ins - s_ins);
+        const int part = (m_ins + kNT - 1) / kNT * 64;
+        const int w_lo = s_ins + wv * part, w_hi = min(e_ins, w_lo + part);
+        for (int p0 = w_lo; p0 < w_hi; p0 += 64) {
+            const int p = p0 + lane;
+            const bool act = p < w_hi;
+            const int bk = act ? bucket(S.tok, p) : 0;
+            uint64_t m = __ballot(act);
+#pragma unroll
+            for (int b = 0; b < 10; ++b) {
+                const bool on = ((bk >> b) & 1) != 0;
+                const uint64_t bb = __ballot(act && on);
+                m &= on ? bb : ~bb;
+            }
+            const uint64_t below = m & ((1ull << lane) - 1ull);
+            uint32_t d;
+            if (below) {
+                d = (uint32_t)(lane - (63 - __builtin_clzll(below)));
+            } else {
+                const uint32_t lw = act ? S.u.m.lastw[wv][bk] : 0u;
+                d = lw ? (uint32_t)(p - (s_ins + (int)lw - 1)) : kPending;
+            }
+            if (act) {
+                S.u.m.prev[pslot(p)] = (uint16_t)d;
+                if ((m >> lane) == 1ull) S.u.m.lastw[wv][bk] = (uint16_t)(p - s_ins + 1);
+            }
+        }
+        __syncthreads();
+        for (int p0 = w_lo; p0 < w_hi; p0 += 64) {
+            const int p = p0 + lane;
+            if (p < w_hi && S.u.m.prev[pslot(p)] == kPending) {
+                const int bk = bucket(S.tok, p);
+                uint32_t d = 0;
+                bool found = false;
+                for (int w2 = wv - 1; w2 >= 0 && !found; --w2) {
+                    const uint32_t lw = S.u.m.lastw[w2][bk];
+                    if (lw) { d = (uint32_t)(p - (s_ins + (int)lw - 1)); found = true; }
+                }
+                if (!found) {
+                    const uint32_t h = S.head[bk];
+                    if (h && p - (int)(h - 1u) <= kWin) d = (uint32_t)(p - (int)(h - 1u));
+                }
+                S.u.m.prev[pslot(p)] = (uint16_t)d;
+            }
+        }
+        __syncthreads();
+        for (int b = tid; b < kBuckets; b += kNT) {  // heads; the wave tables cleared for the next segment
+            for (int w2 = kNT / 64 - 1; w2 >= 0; --w2) {
+                const uint32_t lw = S.u.m.lastw[w2][b];
+                if (lw) { S.head[b] = (uint32_t)s_ins + lw; break; }
+            }
+#pragma unroll
+            for (int w2 = 0; w2 < kNT / 64; ++w2) S.u.m.lastw[w2][b] = 0;
+        }
+        // ---- C: each position's frontier of (length, distance) pairs ----
+        uint32_t fa[kPer], fb[kPer], fc[kPer];  // entries: length | distance << 7 (lengths increasing)
+        int nf[kPer];
+        {
+            int j[kPer], bl[kPer], lim[kPer];
+            bool act[kPer];
+#pragma unroll
+            for (int q = 0; q < kPer; ++q) {
+                const int i = lo + q;
+                fa[q] = fb[q] = fc[q] = 0;
+                nf[q] = 0;
+                bl[q] = 0;
+                lim[q] = min(kMaxL, send - i);
+                act[q] = lim[q] >= kMinL;
+                j[q] = i;
+                if (act[q]) {
+                    const uint32_t pd = S.u.m.prev[pslot(i)];
+                    if (pd == 0) act[q] = false;
+                    else j[q] = i - (int)pd;
+                }
+            }
+#pragma unroll 1
+            for (int step = 0; step < kCand; ++step) {
+                bool any = false;
+#pragma unroll
+                for (int q = 0; q < kPer; ++q) {
+                    if (!act[q]) continue;
+                    const int i = lo + q;
+                    if (i - j[q] > kWin) { act[q] = false; continue; }
+                    const int L = match_len(S.tok, i, j[q], lim[q]);
+                    if (L >= kMinL && L > bl[q]) {
+                        const uint32_t e = (uint32_t)L | ((uint32_t)(i - j[q]) << 7);
+                        if (nf[q] == 0) fa[q] = e; else if (nf[q] == 1) fb[q] = e; else fc[q] = e;
+                        nf[q] = min(nf[q] + 1, 3);
+                        bl[q] = L;
+                        if (L == lim[q]) { act[q] = false; continue; }
+                    }
+                    const uint32_t pd = S.u.m.prev[pslot(j[q])];
+                    if (pd == 0) act[q] = false;
+                    else j[q] -= (int)pd;
+                    any |= act[q];
+                }
+                if (!any) break;
+            }
+        }
+        // ---- D: segmented backward DP (3 sweeps) ----
+        uint32_t dca[kPer], dcb[kPer], dcc[kPer];
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+            dca[q] = nf[q] > 0 ? S.dcst[dist_code(4u * (fa[q] >> 7))] : 0u;
+            dcb[q] = nf[q] > 1 ? S.dcst[dist_code(4u * (fb[q] >> 7))] : 0u;
+            dcc[q] = nf[q] > 2 ? S.dcst[dist_code(4u * (fc[q] >> 7))] : 0u;
+        }
+        for (int k = tid; k <= kSeg; k += kNT) {
+            const int rem = max(0, send - c0 - k);
+            S.cost[1][k] = 32u * (uint32_t)rem;  // sweep 0's estimate beyond a thread's positions: 4 bits per value
+            if (k >= send - c0) S.cost[0][k] = 0;
+        }
+        __syncthreads();
+        const int klo = kPer * tid;  // segment-relative
+#pragma unroll 1
+        for (int sw = 0; sw < kSweeps; ++sw) {
+            uint32_t* cur = S.cost[sw & 1];
+            const uint32_t* prv = S.cost[(sw + 1) & 1];
+#pragma unroll
+            for (int q = kPer - 1; q >= 0; --q) {
+                const int k = klo + q;
+                if (c0 + k >= send) continue;
+                auto C = [&](int kk) -> uint32_t { return kk < klo + kPer ? cur[kk] : prv[kk]; };
+                const uint32_t id = ((q < 4 ? idw0 : idw1) >> (8 * (q & 3))) & 0xffu;
+                uint32_t best = S.litc[id] + C(k + 1);
+                uint32_t ch = 0;
+                int l0 = kMinL;
+#pragma unroll
+                for (int e = 0; e < 3; ++e) {
+                    if (e >= nf[q]) break;
+                    const uint32_t ent = e == 0 ? fa[q] : e == 1 ? fb[q] : fc[q];
+                    const uint32_t dc = e == 0 ? dca[q] : e == 1 ? dcb[q] : dcc[q];
+                    const int L = (int)(ent & 127u);
+                    for (int l = l0; l <= L; ++l) {
+                        const uint32_t cc = S.lenc[l] + dc + C(k + l);
+                        if (cc < best) { best = cc; ch = (uint32_t)l | ((uint32_t)e << 8); }
+                    }
+                    l0 = L + 1;
+                }
+                cur[k] = best;
+                if (sw == kSweeps - 1) S.dec[k] = (uint16_t)ch;
+            }
+            __syncthreads();
+        }
+        // ---- E: the DP's path from the segment start: Jacobi rounds ----
+        auto nxt = [&](int p) -> int { const int l = S.dec[p - c0] & 0xff; return p + (l ? l : 1); };
+        {
+            int p = tid == 0 ? c0 : max(c0, lo - kMaxL);
+            while (p < lo && p < send) p = nxt(p);
+            S.entry[tid] = (uint16_t)(p - c0);
+        }
+        __syncthreads();
+#pragma unroll 1
+        for (;;) {
+            int p = c0 + S.entry[tid];
+            while (p < lo + kPer && p < send) p = nxt(p);
+            __syncthreads();
+            int changed = 0;
+            if (tid + 1 < kNT && (int)S.entry[tid + 1] != p - c0) { S.entry[tid + 1] = (uint16_t)(p - c0); changed = 1; }
+            if (!__syncthreads_or(changed)) break;
+        }
+        // ---- F: this segment's ops, in order; symbol counts ----
+        {
+            uint32_t opm = 0;
+            for (int p = c0 + S.entry[tid]; p < lo + kPer && p < send; p = nxt(p)) opm |= 1u << (p - lo);
+            uint32_t tot;
+            const uint32_t off = block_scan((uint32_t)__popc(opm), S.scan, &tot);
+            const uint32_t base = S.ops_n;
+            uint32_t k = base + off;
+            uint32_t nl = 0, nd = 0;
+#pragma unroll
+            for (int q = 0; q < kPer; ++q) {
+                if (!((opm >> q) & 1u)) continue;
+                const uint32_t dq = S.dec[klo + q];
+                const uint32_t l = dq & 0xffu;
+                uint32_t rec;
+                if (l == 0) {
+                    const uint32_t id = ((q < 4 ? idw0 : idw1) >> (8 * (q & 3))) & 0xffu;
+                    rec = 0x80000000u | id;
+                    const uint32_t b = __float_as_uint((float)id);
+#pragma unroll
+                    for (int y = 0; y < 4; ++y) atomicAdd(&S.hl[(b >> (8 * y)) & 0xffu], 1u);
+                    nl += 4;
+                } else {
+                    const uint32_t e = dq >> 8;
+                    const uint32_t ent = e == 0 ? fa[q] : e == 1 ? fb[q] : fc[q];
+                    const uint32_t d = ent >> 7;
+                    rec = l | (d << 7);
+                    atomicAdd(&S.hl[257 + len_code(4u * l)], 1u);
+                    atomicAdd(&S.hd[dist_code(4u * d)], 1u);
+                    nl += 1;
+                    nd += 1;
+                }
+                ops[k++] = rec;
+            }
+            if (nl) atomicAdd(&S.totl, nl);
+            if (nd) atomicAdd(&S.totd, nd);
+            if (tid == 0) S.segop[c] = base;
+            __syncthreads();
+            if (tid == 0) S.ops_n = base + tot;
+        }
+        if (c + 1 < nseg) tlz_model(S, tid, false);  // its barriers also order ops_n and the histograms
+        else __syncthreads();
+    }
+
+    // ---- G: the member's Huffman code (lengths limited to the inflate's table bits) ----
+    const int ln = lane;
+    if (wv == 0) {
+        HScratch& h = S.u.f.h;
+        if (ln == 0) S.hl[256] = 1;  // end of block
+        __builtin_amdgcn_wave_barrier();
+        if (!huff_lengths_wave(S.hl, kLit, kLitMax, S.ll, h.w, true) && ln == 0) huff_lengths(S.hl, kLit, kLitMax, S.ll, h, true);
+    } else if (wv == 1) {
+        HScratch& h = S.u.f.h;
+        const bool anyd = __ballot(ln < kDist && S.hd[ln] != 0u) != 0ull;
+        if (!anyd && ln == 0) S.hd[0] = 1;  // one (unused) distance code
+        __builtin_amdgcn_wave_barrier();
+        huff_lengths_wave(S.hd, kDist, kDistMax, S.ld, reinterpret_cast<uint32_t*>(h.rle_ext), false);
+    }
+    __syncthreads();
+    if (wv == 1) huff_codes_wave(S.ll, kLit, S.kl);
+    if (wv == 2) huff_codes_wave(S.ld, kDist, S.kd);
+    if (wv == 0) {  // run-length code of the code lengths (as RFC 1951 3.2.7)
+        HScratch& h = S.u.f.h;
+        int nlit = 257, ndist = 1;
+        for (int cc = 0; cc < (kLit + 63) / 64; ++cc) {
+            const int i = 64 * cc + ln;
+            const uint64_t m = __ballot(i < kLit && S.ll[i] != 0);
+            if (m) nlit = max(nlit, 64 * cc + 64 - __builtin_clzll(m));
+        }
+        {
+            const uint64_t m = __ballot(ln < kDist && S.ld[ln] != 0);
+            if (m) ndist = max(ndist, 64 - __builtin_clzll(m));
+        }
+        const int N = nlit + ndist;
+        auto val = [&](int i) -> int { return i < nlit ? S.ll[i] : S.ld[i - nlit]; };
+        uint64_t starts[(kLit + kDist + 63) / 64];
+#pragma unroll
+        for (int cc = 0; cc < (kLit + kDist + 63) / 64; ++cc) {
+            const int i = 64 * cc + ln;
+            starts[cc] = __ballot(i < N && (i == 0 || val(i) != val(i - 1)));
+        }
+        if (ln == 0) {
+            int nr = 0, cc = 0, s0 = 0;
+            uint64_t m = starts[0];
+            m &= m - 1;
+            for (;;) {
+                while (!m && cc + 1 < (kLit + kDist + 63) / 64) m = starts[++cc];
+                const int s1 = m ? 64 * cc + __builtin_ctzll(m) : N;
+                if (m) m &= m - 1;
+                const int cur = val(s0);
+                int left = s1 - s0;
+                if (cur == 0) {
+                    while (left >= 11) { const int r = left < 138 ? left : 138; h.rle_sym[nr] = 18; h.rle_ext[nr++] = (uint16_t)(r - 11); left -= r; }
+                    if (left >= 3) { h.rle_sym[nr] = 17; h.rle_ext[nr++] = (uint16_t)(left - 3); left = 0; }
+                    while (left > 0) { h.rle_sym[nr] = 0; h.rle_ext[nr++] = 0; --left; }
+                } else {
+                    h.rle_sym[nr] = (uint16_t)cur; h.rle_ext[nr++] = 0; --left;
+                    while (left >= 3) { const int r = left < 6 ? left : 6; h.rle_sym[nr] = 16; h.rle_ext[nr++] = (uint16_t)(r - 3); left -= r; }
+                    while (left > 0) { h.rle_sym[nr] = (uint16_t)cur; h.rle_ext[nr++] = 0; --left; }
+                }
+                if (s1 >= N) break;
+                s0 = s1;
+            }
+            for (int i = 0; i < nr; ++i) S.hc[h.rle_sym[i]]++;
+            S.nrle = (uint32_t)nr;
+            S.nlit_ndist = (uint32_t)(nlit | (ndist << 16));
+        }
+    }
+    __syncthreads();
+    if (wv == 0) {
+        HScratch& h = S.u.f.h;
+        huff_lengths_wave(S.hc, kCL, 7, S.lc, h.w, true);
+        huff_codes_wave(S.lc, kCL, S.kc);
+    }
+    if (tid == 0) {  // the deflate block header's bits (words of the member's data start)
+        HScratch& h = S.u.f.h;
+        const int nr = (int)S.nrle, nlit = (int)(S.nlit_ndist & 0xffffu), ndist = (int)(S.nlit_ndist >> 16);
+        int ncl = kCL;
+        while (ncl > 4 && S.lc[c_clord[ncl - 1]] == 0) --ncl;
+        uint64_t acc = 0;
+        int nb = 0;
+        uint32_t wi = 0, pos = 0;
+        auto put = [&](uint32_t v, int n) {
+            acc |= (uint64_t)v << nb;
+            nb += n;
+            pos += (uint32_t)n;
+            if (nb >= 32) { S.u.f.hdrw[wi++] = (uint32_t)acc; acc >>= 32; nb -= 32; }
+        };
+        put(1u, 1);  // BFINAL
+        put(2u, 2);  // BTYPE = dynamic
+        put((uint32_t)(nlit - 257), 5);
+        put((uint32_t)(ndist - 1), 5);
+        put((uint32_t)(ncl - 4), 4);
+        for (int i = 0; i < ncl; ++i) put(S.lc[c_clord[i]], 3);
+        for (int i = 0; i < nr; ++i) {
+            const int sy = h.rle_sym[i];
+            put(S.kc[sy], S.lc[sy]);
+            const int eb = sy == 16 ? 2 : (sy == 17 ? 3 : (sy == 18 ? 7 : 0));
+            put(h.rle_ext[i], eb);
+        }
+        if (nb > 0) S.u.f.hdrw[wi] = (uint32_t)acc;
+        S.hdr_bits = pos;
+    }
+    __syncthreads();
+
+    // ---- H: bits of the ops (a block scan of their costs), segment offsets ----
+    const uint32_t nops = S.ops_n, H = S.hdr_bits;
+    const uint32_t o_lo = (uint32_t)((uint64_t)nops * tid / kNT), o_hi = (uint32_t)((uint64_t)nops * (tid + 1) / kNT);
+    auto op_bits = [&](uint32_t rec) -> uint32_t {
+        if (rec >> 31) {
+            const uint32_t b = __float_as_uint((float)(rec & 31u));
+            return (uint32_t)S.ll[b & 0xffu] + S.ll[(b >> 8) & 0xffu] + S.ll[(b >> 16) & 0xffu] + S.ll[b >> 24];
+        }
+        const uint32_t l = rec & 127u, d = rec >> 7;
+        const int lc = len_code(4u * l), dc = dist_code(4u * d);
+        return (uint32_t)S.ll[257 + lc] + c_lext[lc] + S.ld[dc] + c_dext[dc];
+    };
+    uint32_t mine = 0;
+    for (uint32_t o = o_lo; o < o_hi; ++o) mine += op_bits(ops[o]);
+    uint32_t tot;
+    const uint32_t pos0 = H + block_scan(mine, S.scan, &tot);
+    {
+        int sidx = 0;
+        while (sidx < nseg && S.segop[sidx] < o_lo) ++sidx;
+        uint32_t pos = pos0;
+        for (uint32_t o = o_lo; o < o_hi && sidx < nseg; ++o) {
+            if (S.segop[sidx] == o) S.segbit[sidx++] = pos;
+            pos += op_bits(ops[o]);
+        }
+    }
+    if (tid == 0) S.total_bits = H + tot;
+    const uint32_t D = (uint32_t)(kHdrFixed + 4 * nseg);  // header bytes (a multiple of 4)
+    uint32_t* const slot = reinterpret_cast<uint32_t*>(a.slots + (int64_t)blockIdx.x * a.slot_bytes);
+    uint32_t* const dw = slot + D / 4;                    // the deflate data's words
+    {
+        const uint32_t nw = (H + tot + 15u + 7u + 64u + 31u) / 32u + 1u;
+        for (uint32_t i = tid; i < nw; i += kNT) dw[i] = 0;
+    }
+    __syncthreads();
+    if (tid == 0)
+        for (uint32_t i = 0; i < (H + 31u) / 32u; ++i) atomicOr(&dw[i], S.u.f.hdrw[i]);
+    {
+        uint64_t acc = 0;
+        int nb = (int)(pos0 & 31u);
+        uint32_t wi = pos0 >> 5;
+        bool first = true;
+        auto put = [&](uint32_t v, int n) {
+            acc |= (uint64_t)v << nb;
+            nb += n;
+            if (nb >= 32) {
+                if (first) { atomicOr(&dw[wi], (uint32_t)acc); first = false; }
+                else dw[wi] = (uint32_t)acc;
+                ++wi;
+                acc >>= 32;
+                nb -= 32;
+            }
+        };
+        for (uint32_t o = o_lo; o < o_hi; ++o) {
+            const uint32_t rec = ops[o];
+            if (rec >> 31) {
+                const uint32_t b = __float_as_uint((float)(rec & 31u));
+#pragma unroll
+                for (int y = 0; y < 4; ++y) {
+                    const uint32_t by = (b >> (8 * y)) & 0xffu;
+                    put(S.kl[by], S.ll[by]);
+                }
+            } else {
+                const uint32_t l = 4u * (rec & 127u), d = 4u * (rec >> 7);
+                const int lc = len_code(l), dc = dist_code(d);
+                put(S.kl[257 + lc], S.ll[257 + lc]);
+                put(l - c_lbase[lc], c_lext[lc]);
+                put(S.kd[dc], S.ld[dc]);
+                put(d - c_dbase[dc], c_dext[dc]);
+            }
+        }
+        if (nb > 0) atomicOr(&dw[wi], (uint32_t)acc);
+    }
+    __syncthreads();
+    // ---- I: end of block, CRC-32, ISIZE, the member header ----
+    if (tid == 0) {
+        uint32_t p = S.total_bits;
+        put_bits(dw, p, S.kl[256], S.ll[256]);
+        p += S.ll[256];
+        p = (p + 7u) & ~7u;
+        const uint32_t crc32 = crc_adv(0xffffffffu, 4u * (uint32_t)ntok) ^ S.crc_raw ^ 0xffffffffu;
+        put_bits(dw, p, crc32, 32);
+        p += 32;
+        put_bits(dw, p, 4u * (uint32_t)ntok, 32);
+        p += 32;
+        const uint32_t bytes = D + p / 8u;
+        uint8_t* hb = S.u.f.hb;
+        const uint32_t len = 12u + 4u * (uint32_t)nseg, xlen = 4u + len;
+        const uint8_t fixed[16] = {0x1f, 0x8b, 0x08, 0x04, 0, 0, 0, 0, 0x00, 0xff, (uint8_t)xlen, (uint8_t)(xlen >> 8),
+                                   'O', 'Z', (uint8_t)len, (uint8_t)(len >> 8)};
+        for (int i = 0; i < 16; ++i) hb[i] = fixed[i];
+        hb[16] = 1;
+        hb[17] = (uint8_t)kSegLog;
+        hb[18] = (uint8_t)nseg;
+        hb[19] = (uint8_t)(nseg >> 8);
+        for (int i = 0; i < 4; ++i) {
+            hb[20 + i] = (uint8_t)(bytes >> (8 * i));
+            hb[24 + i] = (uint8_t)((uint32_t)ntok >> (8 * i));
+        }
+        for (int s = 0; s < nseg; ++s)
+            for (int i = 0; i < 4; ++i) hb[kHdrFixed + 4 * s + i] = (uint8_t)(S.segbit[s] >> (8 * i));
+        for (uint32_t i = 0; i < D / 4; ++i) slot[i] = reinterpret_cast<const uint32_t*>(hb)[i];
+        a.sizes[blockIdx.x] = bytes;
+    }
+}
+
+// ---- inflate --------------------------------------------------------------
+constexpr int kDecLitBits = kLitMax, kDecDistBits = kDistMax;
+using DecLit = InfCodeT<kDecLitBits, 288>;
+using DecDist = InfCodeT<kDecDistBits, 32>;
+struct DecSmem {
+    DecLit lit;
+    DecDist dist;
+    uint8_t lens[320];
+};
+struct DecArgs {
+    const uint8_t* src;      // device stream (readable 32 bytes past every member)
+    const int64_t* idx;      // per member: data offset, data length | kind << 62, output offset, isize | crc << 32
+    int64_t nmem;
+    uint8_t* out;
+    uint64_t out_cap;
+    uint32_t* cnt;           // [nmem][kMemSeg] ops per segment
+    int* status;
+};
+
+// bytes of the stream (any alignment) through a 128-bit block register pair
+struct BitIn {
+    const uint4* base;       // 16-byte aligned
+    uint4 cur, nxt;
+    int64_t blk;             // block index of cur
+    int wi;                  // next word of cur
+    uint64_t bb;
+    int bc;
+    DEVI uint32_t word(int k) const { return k == 0 ? cur.x : k == 1 ? cur.y : k == 2 ? cur.z : cur.w; }
+    DEVI void start(const uint8_t* src, uint64_t bit) {  // src 16-byte aligned
+        base = reinterpret_cast<const uint4*>(src);
+        blk = (int64_t)(bit >> 7);
+        cur = base[blk];
+        nxt = base[blk + 1];
+        wi = (int)((bit >> 5) & 3u);
+        const int sk = (int)(bit & 31u);
+        bb = (uint64_t)(word(wi) >> sk);
+        bc = 32 - sk;
+        adv();
+        fill();
+    }
+    DEVI void adv() {
+        if (++wi == 4) { cur = nxt; ++blk; nxt = base[blk + 1]; wi = 0; }
+    }
+    DEVI void fill() {  // >= 33 bits in bb
+        while (bc <= 32) {
+            bb |= (uint64_t)word(wi) << bc;
+            bc += 32;
+            adv();
+        }
+    }
+    DEVI uint32_t peek() const { return (uint32_t)bb; }
+    DEVI void drop(int n) { bb >>= n; bc -= n; }
+    DEVI uint32_t get(int n) { const uint32_t v = (uint32_t)(bb & ((1ull << n) - 1ull)); drop(n); return v; }
+    DEVI uint64_t pos() const { return (uint64_t)(blk * 128 + wi * 32) - (uint64_t)bc; }
+};
+
+// K1: one wavefront per member; the block header on all lanes (wave-uniform),
+// then lane s decodes segment s's symbols into op records written over that
+// segment's own output bytes (kSeg values = 8 KiB >= 4 bytes per op).
+__global__ __launch_bounds__(64) void k_tlz_ops(DecArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    DecSmem& S = *reinterpret_cast<DecSmem*>(smem_raw);
+    const int lane = threadIdx.x;
+    const int64_t m = blockIdx.x;
+    if (m >= a.nmem) return;
+    const int64_t* ix = a.idx + 4 * m;
+    const int64_t doff = ix[0];
+    const uint32_t in_len = (uint32_t)ix[1];
+    const int64_t out_off = ix[2];
+    const uint32_t isize = (uint32_t)((uint64_t)ix[3] & 0xffffffffu);
+    const uint8_t* data = a.src + doff;
+    const uint32_t ntok = isize / 4u;
+    const int nseg = (int)((ntok + kSeg - 1) >> kSegLog);
+    int err = 0;
+    if ((isize & 3u) || ntok == 0 || nseg > kMemSeg || (out_off & 3) || (uint64_t)out_off + isize > a.out_cap) err = kInfRange;
+    // the 'OZ' subfield ends where the deflate data starts
+    const uint8_t* oz = data - 4 * nseg - 16;
+    if (!err) {
+        auto u32at = [&](const uint8_t* p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24); };
+        if (oz[0] != 'O' || oz[1] != 'Z' || oz[4] != 1 || oz[5] != kSegLog || ((uint32_t)oz[6] | ((uint32_t)oz[7] << 8)) != (uint32_t)nseg ||
+            u32at(oz + 12) != ntok)
+            err = kInfCorrupt;
+    }
+    if (err) {
+        if (lane == 0) atomicOr(a.status, err);
+        return;
+    }
+    auto seg_bit = [&](int s) -> uint32_t {
+        const uint8_t* p = data - 4 * nseg + 4 * s;
+        return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+    };
+    const uint64_t dbit = 8ull * (uint64_t)doff;  // the data's first bit in the stream
+    // ---- the block header, on every lane (wave-uniform) ----
+    BitIn in;
+    in.start(a.src, dbit);
+    if (in.get(1) != 1u || in.get(2) != 2u) err = kInfCorrupt;  // BFINAL, dynamic
+    int nlit = 0, ndist = 0;
+    if (!err) {
+        nlit = (int)in.get(5) + 257;
+        ndist = (int)in.get(5) + 1;
+        const int ncl = (int)in.get(4) + 4;
+        if (nlit > 286 || ndist > 30) err = kInfCorrupt;
+        for (int i = lane; i < 19; i += 64) S.lens[i] = 0;
+        __builtin_amdgcn_wave_barrier();
+        for (int i = 0; i < ncl && !err; ++i) {
+            in.fill();
+            const uint32_t v = in.get(3);
+            if (lane == 0) S.lens[c_clord[i]] = (uint8_t)v;
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (!err && !inf_build(S.lit, S.lens, 19, kAlphaPlain)) err = kInfCorrupt;
+        const int total = nlit + ndist;
+        int i = 0;
+        while (!err && i < total) {
+            in.fill();
+            const uint32_t e = S.lit.fast[in.peek() & (uint32_t)(DecLit::kSize - 1)];
+            const int l = (int)(e & 15u);
+            if (!l || (e & 0x300u)) { err = kInfCorrupt; break; }
+            in.drop(l);
+            const int sy = (int)(e >> 16);
+            if (sy < 16) {
+                if (lane == 0) S.lens[i] = (uint8_t)sy;
+                ++i;
+                continue;
+            }
+            int rep, val = 0;
+            if (sy == 16) {
+                if (i == 0) { err = kInfCorrupt; break; }
+                __builtin_amdgcn_wave_barrier();
+                val = S.lens[i - 1];
+                rep = 3 + (int)in.get(2);
+            } else if (sy == 17) {
+                rep = 3 + (int)in.get(3);
+            } else {
+                rep = 11 + (int)in.get(7);
+            }
+            if (i + rep > total) { err = kInfCorrupt; break; }
+            __builtin_amdgcn_wave_barrier();
+            for (int k = lane; k < rep; k += 64) S.lens[i + k] = (uint8_t)val;
+            __builtin_amdgcn_wave_barrier();
+            i += rep;
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (!err) {
+            // every code must fit the first-level tables (the encoder limits them)
+            bool longc = false;
+            for (int k = lane; k < total; k += 64) longc |= S.lens[k] > (k < nlit ? kDecLitBits : kDecDistBits);
+            if (__ballot(longc) || S.lens[256] == 0) err = kInfCorrupt;
+        }
+        if (!err) {
+            const uint8_t dl = lane < ndist ? S.lens[nlit + lane] : 0;
+            __builtin_amdgcn_wave_barrier();
+            for (int k = nlit + lane; k < 288; k += 64) S.lens[k] = 0;
+            __builtin_amdgcn_wave_barrier();
+            if (lane < 32) S.lens[288 + lane] = lane < ndist ? dl : 0;
+            __builtin_amdgcn_wave_barrier();
+            if (!inf_build(S.lit, S.lens, nlit, kAlphaLit) || !inf_build(S.dist, S.lens + 288, ndist, kAlphaDist)) err = kInfCorrupt;
+        }
+        if (!err && in.pos() != dbit + seg_bit(0)) err = kInfCorrupt;  // the ops start where the table says
+    }
+    if (err) {
+        if (lane == 0) atomicOr(a.status, err);
+        return;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // ---- lane s: segment s ----
+    const int s = lane;
+    if (s < nseg) {
+        const uint32_t T = min((uint32_t)kSeg, ntok - ((uint32_t)s << kSegLog));
+        uint32_t* const opo = reinterpret_cast<uint32_t*>(a.out + out_off + ((int64_t)s << (kSegLog + 2)));
+        in.start(a.src, dbit + seg_bit(s));
+        uint32_t produced = 0, nops = 0;
+        const uint32_t before = (uint32_t)s << kSegLog;  // values of the member before this segment
+        while (produced < T) {
+            in.fill();
+            uint32_t e = S.lit.fast[in.peek() & (uint32_t)(DecLit::kSize - 1)];
+            int l = (int)(e & 15u);
+            if (!l) { err = kInfCorrupt; break; }
+            in.drop(l);
+            uint32_t kind = (e >> 8) & 3u;
+            if (kind == (uint32_t)kKindLit) {  // a value's 4 literal bytes
+                uint32_t bytes = e >> 16;
+                in.fill();
+#pragma unroll
+                for (int y = 1; y < 4; ++y) {
+                    e = S.lit.fast[in.peek() & (uint32_t)(DecLit::kSize - 1)];
+                    l = (int)(e & 15u);
+                    if (!l || ((e >> 8) & 3u) != (uint32_t)kKindLit) { err = kInfCorrupt; break; }
+                    in.drop(l);
+                    bytes |= (e >> 16) << (8 * y);
+                }
+                if (err) break;
+                const float f = __uint_as_float(bytes);
+                const int id = (int)f;
+                if (!(id >= 0 && id < 32 && __float_as_uint((float)id) == bytes)) { err = kInfCorrupt; break; }
+                opo[nops++] = 0x80000000u | (uint32_t)id;
+                produced += 1;
+            } else if (kind == (uint32_t)kKindCopy) {
+                const uint32_t len = (e >> 16) + in.get((int)((e >> 4) & 15u));
+                in.fill();
+                const uint32_t f = S.dist.fast[in.peek() & (uint32_t)(DecDist::kSize - 1)];
+                const int l2 = (int)(f & 15u);
+                if (!l2 || ((f >> 8) & 3u) != (uint32_t)kKindCopy) { err = kInfCorrupt; break; }
+                in.drop(l2);
+                const uint32_t d = (f >> 16) + in.get((int)((f >> 4) & 15u));
+                const uint32_t lt = len >> 2, dt = d >> 2;
+                if ((len & 3u) || (d & 3u) || lt < (uint32_t)kMinL || lt > (uint32_t)kMaxL || produced + lt > T ||
+                    dt > before + produced || dt > (uint32_t)kWin) { err = kInfCorrupt; break; }
+                opo[nops++] = lt | (dt << 7);
+                produced += lt;
+            } else {
+                err = kInfCorrupt;
+                break;
+            }
+        }
+        if (!err) {
+            if (s + 1 < nseg) {
+                if (in.pos() != dbit + seg_bit(s + 1)) err = kInfCorrupt;
+            } else {  // end of block, then the data ends at the next byte boundary
+                in.fill();
+                const uint32_t e = S.lit.fast[in.peek() & (uint32_t)(DecLit::kSize - 1)];
+                const int l = (int)(e & 15u);
+                if (!l || ((e >> 8) & 3u) != (uint32_t)kKindEnd) err = kInfCorrupt;
+                else {
+                    in.drop(l);
+                    if ((in.pos() - dbit + 7u) / 8u != in_len) err = kInfCorrupt;
+                }
+            }
+        }
+        a.cnt[m * kMemSeg + s] = nops;
+        if (err) atomicOr(a.status, err);
+    }
+}
+
+// K2: one block per member; per segment: op positions (block scan), each
+// value's source (pointer jumping in LDS; sources before the segment are in
+// the value ring), the values as float32, CRC-32 of the member, ISIZE.
+struct ResSmem {
+    uint8_t v[kRing];              // ids by member position (ring)
+    uint32_t opr[kSeg];            // the segment's op records
+    uint16_t e[kSeg];              // 0x8000 | id (resolved) or the distance to the source
+    uint32_t crct[4][256];
+    uint32_t scan[kNT / 64];
+    uint32_t crc_w[kNT / 64];
+    uint32_t crc_raw;
+};
+__global__ __launch_bounds__(kNT) void k_tlz_resolve(DecArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    ResSmem& S = *reinterpret_cast<ResSmem*>(smem_raw);
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int64_t m = blockIdx.x;
+    if (m >= a.nmem) return;
+    if (*reinterpret_cast<volatile int*>(a.status)) return;  // K1 found corrupt data (block-uniform)
+    const int64_t* ix = a.idx + 4 * m;
+    const int64_t out_off = ix[2];
+    const uint32_t isize = (uint32_t)((uint64_t)ix[3] & 0xffffffffu), want_crc = (uint32_t)((uint64_t)ix[3] >> 32);
+    const uint32_t ntok = isize / 4u;
+    const int nseg = (int)((ntok + kSeg - 1) >> kSegLog);
+    {
+        uint32_t r = (uint32_t)tid;
+        for (int k = 0; k < 8; ++k) r = (r & 1u) ? (r >> 1) ^ 0xEDB88320u : r >> 1;
+        S.crct[0][tid] = r;
+    }
+    if (tid == 0) S.crc_raw = 0;
+    __syncthreads();
+    for (int k = 1; k < 4; ++k) {
+        const uint32_t p = S.crct[k - 1][tid];
+        S.crct[k][tid] = (p >> 8) ^ S.crct[0][p & 0xffu];
+        __syncthreads();
+    }
+    int bad = 0;
+    for (int s = 0; s < nseg; ++s) {
+        const int c0 = s << kSegLog;
+        const int T = (int)min((uint32_t)kSeg, ntok - (uint32_t)c0);
+        const uint32_t nops = a.cnt[m * kMemSeg + s];
+        float* const yo = reinterpret_cast<float*>(a.out + out_off) + c0;
+        const uint32_t* opi = reinterpret_cast<const uint32_t*>(yo);
+        for (uint32_t k = tid; k < nops; k += kNT) S.opr[k] = opi[k];
+        __syncthreads();
+        // positions: each thread a contiguous run of ops
+        const uint32_t o_lo = nops * tid / kNT, o_hi = nops * (tid + 1) / kNT;
+        uint32_t run = 0;
+        for (uint32_t o = o_lo; o < o_hi; ++o) { const uint32_t r = S.opr[o]; run += (r >> 31) ? 1u : (r & 127u); }
+        uint32_t tot;
+        uint32_t p = block_scan(run, S.scan, &tot);
+        if (tot != (uint32_t)T) { bad = kInfCorrupt; break; }  // block-uniform
+        for (uint32_t o = o_lo; o < o_hi; ++o) {
+            const uint32_t r = S.opr[o];
+            if (r >> 31) {
+                S.e[p++] = (uint16_t)(0x8000u | (r & 31u));
+            } else {
+                const uint32_t l = r & 127u, d = r >> 7;
+                for (uint32_t k = 0; k < l; ++k) S.e[p + k] = (uint16_t)d;
+                p += l;
+            }
+        }
+        __syncthreads();
+        // pointer jumping: an unresolved entry points at its source; a source
+        // before the segment is a value of the ring
+#pragma unroll 1
+        for (;;) {
+            int pend = 0;
+            for (int k = tid; k < T; k += kNT) {
+                const uint32_t e = S.e[k];
+                if (e & 0x8000u) continue;
+                const int src = k - (int)e;
+                uint32_t ne;
+                if (src < 0) ne = 0x8000u | S.v[(c0 + src) & (kRing - 1)];
+                else {
+                    const uint32_t es = S.e[src];
+                    ne = (es & 0x8000u) ? es : e + es;
+                }
+                S.e[k] = (uint16_t)ne;
+                pend |= !(ne & 0x8000u);
+            }
+            if (!__syncthreads_or(pend)) break;
+        }
+        // values: ring, output (float32), raw CRC-32
+        {
+            const int k0 = kPer * tid;
+            const int nv = max(0, min(kPer, T - k0));
+            uint32_t crc = 0;
+            float f[kPer];
+#pragma unroll
+            for (int q = 0; q < kPer; ++q) {
+                const uint32_t id = q < nv ? (uint32_t)(S.e[k0 + q] & 31u) : 0u;
+                f[q] = (float)id;
+                if (q < nv) {
+                    S.v[(c0 + k0 + q) & (kRing - 1)] = (uint8_t)id;
+                    crc = crc4(S.crct, crc, __float_as_uint(f[q]));
+                }
+            }
+            if (nv == kPer) {
+                float4* y4 = reinterpret_cast<float4*>(yo + k0);
+                y4[0] = make_float4(f[0], f[1], f[2], f[3]);
+                y4[1] = make_float4(f[4], f[5], f[6], f[7]);
+            } else {
+                for (int q = 0; q < nv; ++q) yo[k0 + q] = f[q];
+            }
+            uint32_t wcrc;
+            if (T == kSeg) {
+                uint32_t x = crc;
+#pragma unroll
+                for (int l = 0; l < 6; ++l) {
+                    const uint32_t o = (uint32_t)__shfl_xor((int)x, 1 << l, 64);
+                    const uint32_t sh = crc_adv_pow2(x, 5 + l);
+                    x = (lane & (1 << l)) ? x : (sh ^ o);
+                }
+                wcrc = x;
+            } else {
+                uint32_t x = nv ? crc_adv(crc, 4u * (uint32_t)(T - k0 - nv)) : 0u;
+                for (int o = 32; o > 0; o >>= 1) x ^= (uint32_t)__shfl_xor((int)x, o, 64);
+                wcrc = x;
+            }
+            if (lane == 0) S.crc_w[wv] = wcrc;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t raw = 0;
+            if (T == kSeg) {
+                for (int w = 0; w < kNT / 64; ++w) raw = crc_adv_pow2(raw, kSegLog) ^ S.crc_w[w];
+                S.crc_raw = crc_adv_pow2(S.crc_raw, kSegLog + 2) ^ raw;
+            } else {
+                for (int w = 0; w < kNT / 64; ++w) raw ^= S.crc_w[w];
+                S.crc_raw = crc_adv(S.crc_raw, 4u * (uint32_t)T) ^ raw;
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        if (bad) atomicOr(a.status, bad);
+        else if ((crc_adv(0xffffffffu, isize) ^ S.crc_raw ^ 0xffffffffu) != want_crc) atomicOr(a.status, kInfCrc);
+    }
+}
+}  // namespace tlz
+
+// members -> one contiguous stream (slots of any stride)
+__global__ __launch_bounds__(256) void k_gzip_pack(const uint8_t* slots, uint64_t stride, const uint32_t* sizes,
+                                                   const uint64_t* off, uint8_t* packed) {
+    if (off[blockIdx.x] == ~0ull) return;  // the batch does not fit the output (reported by the scan)
+    const uint8_t* src = slots + (int64_t)blockIdx.x * stride;
+    uint8_t* dst = packed + off[blockIdx.x];
+    const uint32_t n = sizes[blockIdx.x];
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 3u);
+    if (mis == 0) {  // slots are 4-byte aligned: whole words where the destination is too
+        for (uint32_t i = threadIdx.x; i < n / 4u; i += 256)
+            reinterpret_cast<uint32_t*>(dst)[i] = reinterpret_cast<const uint32_t*>(src)[i];
+        for (uint32_t i = (n & ~3u) + threadIdx.x; i < n; i += 256) dst[i] = src[i];
+    } else {
+        for (uint32_t i = threadIdx.x; i < n; i += 256) dst[i] = src[i];
+    }
+}
+
 }  // namespace gz
 
 namespace {
@@ -1411,6 +1933,28 @@ int gzfail(int code, const std::string& m) { g_gzerr = m; return code; }
         hipError_t e_ = (x);                                                                            \
         if (e_ != hipSuccess) return gzfail(OFL_EHIP, std::string(#x " failed: ") + hipGetErrorString(e_)); \
     } while (0)
+
+// Optional per-kernel timing (bench.py's KC line): while enabled, every
+// gzip / inflate launch is bracketed by HIP events on its stream; collect
+// synchronises them and sums the time per kernel name.
+std::mutex g_prof_m;
+bool g_prof_on = false;
+struct ProfRec { const char* name; hipEvent_t a, b; };
+std::vector<ProfRec> g_prof_pending;
+thread_local hipEvent_t g_prof_a = nullptr;
+void gzprof_begin(hipStream_t st) {
+    if (!g_prof_on) return;
+    if (hipEventCreate(&g_prof_a) != hipSuccess || hipEventRecord(g_prof_a, st) != hipSuccess) g_prof_a = nullptr;
+}
+void gzprof_end(hipStream_t st, const char* name) {
+    if (!g_prof_on || !g_prof_a) return;
+    hipEvent_t b;
+    if (hipEventCreate(&b) != hipSuccess) return;
+    if (hipEventRecord(b, st) != hipSuccess) { (void)hipEventDestroy(b); return; }
+    std::lock_guard<std::mutex> g(g_prof_m);
+    g_prof_pending.push_back({name, g_prof_a, b});
+    g_prof_a = nullptr;
+}
 
 // raw CRC-32 advance matrices for 2^k zero bytes
 void crc_matrices(uint32_t (&m)[32][32]) {
@@ -1429,19 +1973,32 @@ void crc_matrices(uint32_t (&m)[32][32]) {
     for (int k = 1; k < 32; ++k)
         for (int i = 0; i < 32; ++i) m[k][i] = apply(m[k - 1], apply(m[k - 1], 1u << i));
 }
-// the members of a member-indexed stream (every header carries the 'BC'
-// size field): deflate data range, output offset, ISIZE and CRC-32 of each
-struct GzMember { size_t in, in_len, out; uint32_t isize, crc; };
+// the members of a member-indexed stream (every header carries its size in
+// an RFC 1952 extra subfield: 'BC' (BGZF: size - 1, 16 bits) or 'OZ' (TLZ:
+// size, 32 bits, plus the segment table)): deflate data range, output
+// offset, ISIZE, CRC-32 and whether it is a TLZ member
+struct GzMember { size_t in, in_len, out; uint32_t isize, crc; bool tlz; };
 // one member at pos: its size (0 if the bytes there are not a member header
-// with the 'BC' field) and its record
+// with a size field) and its record
 size_t member_at(const uint8_t* src, size_t n, size_t pos, GzMember& m) {
     const uint8_t* h = src + pos;
     if (n - pos < 26 || h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || h[3] != 0x04) return 0;
     const size_t xlen = (size_t)h[10] | ((size_t)h[11] << 8);
+    if (12 + xlen > n - pos) return 0;
     size_t bsize = 0;
-    for (size_t q = 12; q + 4 <= 12 + xlen && 12 + xlen <= n - pos;) {
+    bool tlz = false;
+    for (size_t q = 12; q + 4 <= 12 + xlen;) {
         const size_t sl = (size_t)h[q + 2] | ((size_t)h[q + 3] << 8);
+        if (q + 4 + sl > 12 + xlen) return 0;
         if (h[q] == 'B' && h[q + 1] == 'C' && sl == 2) bsize = ((size_t)h[q + 4] | ((size_t)h[q + 5] << 8)) + 1;
+        if (h[q] == 'O' && h[q + 1] == 'Z' && sl >= 12) {
+            const uint8_t* z = h + q + 4;
+            const size_t nseg = (size_t)z[2] | ((size_t)z[3] << 8);
+            bsize = (size_t)z[4] | ((size_t)z[5] << 8) | ((size_t)z[6] << 16) | ((size_t)z[7] << 24);
+            // the segment table must end where the deflate data starts
+            tlz = z[0] == 1 && z[1] == gz::tlz::kSegLog && sl == 12 + 4 * nseg && q + 4 + sl == 12 + xlen &&
+                  nseg >= 1 && nseg <= (size_t)gz::tlz::kMemSeg;
+        }
         q += 4 + sl;
     }
     if (bsize < 12 + xlen + 8 || bsize > n - pos) return 0;
@@ -1450,6 +2007,14 @@ size_t member_at(const uint8_t* src, size_t n, size_t pos, GzMember& m) {
     m.in_len = bsize - 12 - xlen - 8;
     m.crc = (uint32_t)t[0] | ((uint32_t)t[1] << 8) | ((uint32_t)t[2] << 16) | ((uint32_t)t[3] << 24);
     m.isize = (uint32_t)t[4] | ((uint32_t)t[5] << 8) | ((uint32_t)t[6] << 16) | ((uint32_t)t[7] << 24);
+    // a TLZ member's value count (the OZ field) must match its ISIZE
+    if (tlz) {
+        const uint8_t* z = h + 16;
+        const size_t ntok = (size_t)z[8] | ((size_t)z[9] << 8) | ((size_t)z[10] << 16) | ((size_t)z[11] << 24);
+        const size_t nseg = (size_t)z[2] | ((size_t)z[3] << 8);
+        tlz = (m.isize & 3u) == 0 && ntok == m.isize / 4 && nseg == (ntok + gz::tlz::kSeg - 1) / gz::tlz::kSeg;
+    }
+    m.tlz = tlz;
     return bsize;
 }
 
@@ -1494,8 +2059,8 @@ int parse_members(const uint8_t* src, size_t n, std::vector<GzMember>& mem, size
                 GzMember m;
                 while (p < lim) {
                     const uint8_t* h = src + p;
-                    if (h[0] == 0x1f && p + 16 <= n && h[1] == 0x8b && h[2] == 8 && h[3] == 4 && h[12] == 'B' &&
-                        h[13] == 'C' && member_at(src, n, p, m))
+                    if (h[0] == 0x1f && p + 16 <= n && h[1] == 0x8b && h[2] == 8 && h[3] == 4 &&
+                        ((h[12] == 'B' && h[13] == 'C') || (h[12] == 'O' && h[13] == 'Z')) && member_at(src, n, p, m))
                         break;
                     ++p;
                 }
@@ -1507,7 +2072,7 @@ int parse_members(const uint8_t* src, size_t n, std::vector<GzMember>& mem, size
         for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
         work(0);
         for (auto& x : th) x.join();
-        // members are <= 64 KiB and pieces >= 4 MiB: every piece holds a
+        // members are < 1 MiB and pieces >= 4 MiB: every piece holds a
         // header; piece t's walk (from a true header, by induction from 0)
         // ends on a true header, which must be where piece t + 1 starts
         par_ok = start[0] == 0;
@@ -1538,14 +2103,33 @@ extern "C" {
 
 const char* ofl_gzip_last_error(void) { return g_gzerr.c_str(); }
 
+namespace {
+struct TlzLayout {
+    int64_t members, batch;
+    size_t slot, ops_stride;
+};
+TlzLayout tlz_layout(int64_t n) {
+    using namespace gz::tlz;
+    TlzLayout L;
+    L.members = std::max<int64_t>(1, (n + kMemTok - 1) / kMemTok);
+    L.batch = std::min<int64_t>(L.members, kBatch);
+    const int64_t per = std::min<int64_t>(std::max<int64_t>(n, 1), kMemTok);
+    L.slot = ((size_t)per * kSlotPerTok + kSlotPad + 255) & ~(size_t)255;
+    L.ops_stride = ((size_t)per + 63) & ~(size_t)63;
+    return L;
+}
+}  // namespace
+
 size_t ofl_gzip_ranks_workspace_bytes(int64_t n) {
-    const int64_t members = std::max<int64_t>(1, std::min<int64_t>((n + gz::kTok - 1) / gz::kTok, gz::kBatch));
-    return 2 * (size_t)members * gz::kOutBytes + 4 * (size_t)members + 8 * (size_t)(members + 1) + 1024;
+    const TlzLayout L = tlz_layout(n);
+    // slots | packed (pageable output) | ops | sizes | offsets | running | bad
+    return 2 * (size_t)L.batch * L.slot + 4 * (size_t)L.batch * L.ops_stride + 4 * (size_t)L.batch +
+           8 * (size_t)(L.batch + 1) + 1024;
 }
 
 size_t ofl_gzip_ranks_bound(int64_t n) {
-    const int64_t members = std::max<int64_t>(1, (n + gz::kTok - 1) / gz::kTok);
-    return (size_t)members * gz::kOutBytes;
+    const TlzLayout L = tlz_layout(n);
+    return (size_t)L.members * L.slot;
 }
 
 int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size_t* out_len, void* ws,
@@ -1557,19 +2141,19 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
         crc_matrices(m);
         hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(gz::c_adv), m, sizeof(m));
         if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)gz::k_gzip_members, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)sizeof(gz::Smem));
+            e = hipFuncSetAttribute((const void*)gz::tlz::k_tlz_encode, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)sizeof(gz::tlz::EncSmem));
         return e;
     }));
     hipStream_t st = static_cast<hipStream_t>(stream);
-    const int64_t members = (n + gz::kTok - 1) / gz::kTok;
-    const int64_t batch = std::min<int64_t>(members, gz::kBatch);
+    const TlzLayout L = tlz_layout(n);
     char* w = static_cast<char*>(ws);
     uint8_t* slots = reinterpret_cast<uint8_t*>(w);
-    uint8_t* packed = slots + (size_t)batch * gz::kOutBytes;
-    uint32_t* sizes = reinterpret_cast<uint32_t*>(packed + (size_t)batch * gz::kOutBytes);
-    uint64_t* off = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(sizes) + ((4 * (size_t)batch + 7) & ~(size_t)7));
-    uint64_t* running = off + batch + 1;
+    uint8_t* packed = slots + (size_t)L.batch * L.slot;
+    uint32_t* ops = reinterpret_cast<uint32_t*>(packed + (size_t)L.batch * L.slot);
+    uint32_t* sizes = ops + (size_t)L.batch * L.ops_stride;
+    uint64_t* off = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(sizes) + ((4 * (size_t)L.batch + 7) & ~(size_t)7));
+    uint64_t* running = off + L.batch + 1;
     int* bad = reinterpret_cast<int*>(running + 1);
     GZHIP(hipMemsetAsync(bad, 0, sizeof(int), st));
     // out is mapped pinned host memory (e.g. torch pin_memory): the pack
@@ -1582,22 +2166,24 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
             dout = static_cast<uint8_t*>(pa.devicePointer);
         (void)hipGetLastError();  // a pageable pointer is not an error here
     }
-    // diagnostics: OFL_GZ_PHASES=1 prints the phase stamps (10 ns ticks) of
-    // blocks 0..3 of the first launch to stderr
-    static const bool phases = getenv("OFL_GZ_PHASES") != nullptr;
-    uint64_t* d_ph = nullptr;
-    if (phases) GZHIP(hipMalloc(&d_ph, 8 * 4 * gz::kPhases));
-    if (phases) GZHIP(hipMemsetAsync(d_ph, 0, 8 * 4 * gz::kPhases, st));
+    const int aligned = (reinterpret_cast<uintptr_t>(x) & 15u) == 0;
+    auto enc = [&](int64_t c0, int nb) {
+        gz::tlz::EncArgs a{x, n, c0, slots, ops, sizes, bad, (uint32_t)L.slot, (uint32_t)L.ops_stride, aligned};
+        gzprof_begin(st);
+        hipLaunchKernelGGL(gz::tlz::k_tlz_encode, dim3(nb), dim3(gz::tlz::kNT), sizeof(gz::tlz::EncSmem), st, a);
+        gzprof_end(st, "tlz::k_tlz_encode");
+    };
     size_t total = 0;
     if (dout) {
         GZHIP(hipMemsetAsync(running, 0, sizeof(uint64_t), st));
-        for (int64_t c0 = 0; c0 < members; c0 += batch) {
-            const int nb = (int)std::min<int64_t>(batch, members - c0);
-            gz::GzArgs a{x, n, c0, slots, sizes, bad, c0 == 0 ? d_ph : nullptr};
-            hipLaunchKernelGGL(gz::k_gzip_members, dim3(nb), dim3(gz::kNT), sizeof(gz::Smem), st, a);
+        for (int64_t c0 = 0; c0 < L.members; c0 += L.batch) {
+            const int nb = (int)std::min<int64_t>(L.batch, L.members - c0);
+            enc(c0, nb);
             hipLaunchKernelGGL(gz::k_gzip_scan, dim3(1), dim3(1024), 0, st, sizes, nb, off, running,
                                (uint64_t)out_cap, bad);
-            hipLaunchKernelGGL(gz::k_gzip_pack, dim3(nb), dim3(256), 0, st, slots, sizes, off, dout);
+            gzprof_begin(st);
+            hipLaunchKernelGGL(gz::k_gzip_pack, dim3(nb), dim3(256), 0, st, slots, (uint64_t)L.slot, sizes, off, dout);
+            gzprof_end(st, "k_gzip_pack");
             GZHIP(hipGetLastError());
         }
         uint64_t tot = 0;
@@ -1606,39 +2192,26 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
         GZHIP(hipMemcpyAsync(&badh, bad, sizeof(int), hipMemcpyDeviceToHost, st));
         GZHIP(hipStreamSynchronize(st));
         if (badh & 1) return gzfail(OFL_EINVAL, "gzip ranks: values must be float32 integers 0..31");
-        if (badh & 4) return gzfail(OFL_EHIP, "gzip ranks: a member exceeded the device bit buffer");
         if (badh & 2) return gzfail(OFL_ESPACE, "gzip ranks: output buffer too small");
         total = tot;
     }
-    for (int64_t c0 = 0; !dout && c0 < members; c0 += batch) {
-        const int nb = (int)std::min<int64_t>(batch, members - c0);
-        gz::GzArgs a{x, n, c0, slots, sizes, bad, c0 == 0 ? d_ph : nullptr};
-        hipLaunchKernelGGL(gz::k_gzip_members, dim3(nb), dim3(gz::kNT), sizeof(gz::Smem), st, a);
+    for (int64_t c0 = 0; !dout && c0 < L.members; c0 += L.batch) {
+        const int nb = (int)std::min<int64_t>(L.batch, L.members - c0);
+        enc(c0, nb);
         hipLaunchKernelGGL(gz::k_gzip_scan, dim3(1), dim3(1024), 0, st, sizes, nb, off, (uint64_t*)nullptr,
                            ~0ull, bad);
-        hipLaunchKernelGGL(gz::k_gzip_pack, dim3(nb), dim3(256), 0, st, slots, sizes, off, packed);
+        hipLaunchKernelGGL(gz::k_gzip_pack, dim3(nb), dim3(256), 0, st, slots, (uint64_t)L.slot, sizes, off, packed);
         GZHIP(hipGetLastError());
         uint64_t tot = 0;
         int badh = 0;
         GZHIP(hipMemcpyAsync(&tot, off + nb, 8, hipMemcpyDeviceToHost, st));
         GZHIP(hipMemcpyAsync(&badh, bad, sizeof(int), hipMemcpyDeviceToHost, st));
         GZHIP(hipStreamSynchronize(st));
-        if (badh & 4) return gzfail(OFL_EHIP, "gzip ranks: a member exceeded the device bit buffer");
         if (badh) return gzfail(OFL_EINVAL, "gzip ranks: values must be float32 integers 0..31");
         if (total + tot > out_cap) return gzfail(OFL_ESPACE, "gzip ranks: output buffer too small");
         GZHIP(hipMemcpyAsync(out + total, packed, tot, hipMemcpyDeviceToHost, st));
         GZHIP(hipStreamSynchronize(st));
         total += tot;
-    }
-    if (d_ph) {
-        uint64_t h[4 * gz::kPhases];
-        GZHIP(hipMemcpy(h, d_ph, sizeof(h), hipMemcpyDeviceToHost));
-        GZHIP(hipFree(d_ph));
-        for (int b = 0; b < 4; ++b) {
-            fprintf(stderr, "gz phases block %d:", b);
-            for (int k = 1; k <= 10; ++k) fprintf(stderr, " %llu", (unsigned long long)(h[b * gz::kPhases + k] - h[b * gz::kPhases + k - 1]));
-            fprintf(stderr, "\n");
-        }
     }
     *out_len = total;
     return OFL_OK;
@@ -1689,7 +2262,7 @@ int ofl_gunzip_members(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, s
 }
 
 int ofl_gzip_member_index(const uint8_t* src, size_t n, int64_t* index, int64_t cap_members, int64_t* nmembers,
-                          size_t* out_len, uint32_t* max_isize) {
+                          size_t* out_len, uint32_t* max_isize, int* all_tlz) {
     if (!src || !nmembers || !out_len) return gzfail(OFL_EINVAL, "member index: null argument");
     std::vector<GzMember> mem;
     size_t total = 0;
@@ -1697,16 +2270,101 @@ int ofl_gzip_member_index(const uint8_t* src, size_t n, int64_t* index, int64_t 
     *nmembers = (int64_t)mem.size();
     *out_len = total;
     uint32_t mx = 0;
-    for (const GzMember& m : mem) mx = std::max(mx, m.isize);
+    bool tl = !mem.empty();
+    for (const GzMember& m : mem) { mx = std::max(mx, m.isize); tl = tl && m.tlz; }
     if (max_isize) *max_isize = mx;
+    if (all_tlz) *all_tlz = tl ? 1 : 0;
     if (!index) return OFL_OK;
     if (cap_members < (int64_t)mem.size()) return gzfail(OFL_ESPACE, "member index: index array too small");
     for (size_t i = 0; i < mem.size(); ++i) {
         index[4 * i + 0] = (int64_t)mem[i].in;
-        index[4 * i + 1] = (int64_t)mem[i].in_len;
+        index[4 * i + 1] = (int64_t)mem[i].in_len | (mem[i].tlz ? (int64_t)1 << 62 : 0);
         index[4 * i + 2] = (int64_t)mem[i].out;
         index[4 * i + 3] = (int64_t)((uint64_t)mem[i].isize | ((uint64_t)mem[i].crc << 32));
     }
+    return OFL_OK;
+}
+
+size_t ofl_inflate_tlz_workspace_bytes(int64_t nmembers) {
+    return 256 + 4 * (size_t)std::max<int64_t>(nmembers, 1) * gz::tlz::kMemSeg;
+}
+
+int ofl_inflate_tlz(const uint8_t* src, const int64_t* index, int64_t nmembers, uint8_t* out, size_t out_cap, void* ws,
+                    size_t ws_bytes, void* stream) {
+    if (nmembers < 0 || (nmembers && (!src || !index || !out))) return gzfail(OFL_EINVAL, "inflate: null argument");
+    if (!ws || ws_bytes < ofl_inflate_tlz_workspace_bytes(nmembers)) return gzfail(OFL_ESPACE, "inflate: workspace too small");
+    if (nmembers == 0) return OFL_OK;
+    GZHIP(ofl_util::per_device_once([] {
+        uint32_t m[32][32];
+        crc_matrices(m);
+        return hipMemcpyToSymbol(HIP_SYMBOL(gz::c_adv), m, sizeof(m));
+    }));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    int* status = static_cast<int*>(ws);
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + 256);
+    GZHIP(hipMemsetAsync(status, 0, sizeof(int), st));
+    gz::tlz::DecArgs a{src, index, nmembers, out, (uint64_t)out_cap, cnt, status};
+    gzprof_begin(st);
+    hipLaunchKernelGGL(gz::tlz::k_tlz_ops, dim3((unsigned)nmembers), dim3(64), sizeof(gz::tlz::DecSmem), st, a);
+    gzprof_end(st, "tlz::k_tlz_ops");
+    gzprof_begin(st);
+    hipLaunchKernelGGL(gz::tlz::k_tlz_resolve, dim3((unsigned)nmembers), dim3(gz::tlz::kNT), sizeof(gz::tlz::ResSmem), st, a);
+    gzprof_end(st, "tlz::k_tlz_resolve");
+    GZHIP(hipGetLastError());
+    int h = 0;
+    GZHIP(hipMemcpyAsync(&h, status, sizeof(int), hipMemcpyDeviceToHost, st));
+    GZHIP(hipStreamSynchronize(st));
+    if (h & gz::kInfRange) return gzfail(OFL_ESPACE, "inflate: a member's output falls outside out");
+    if (h) {
+        // not what the TLZ decoder expects: the generic inflate decides (any
+        // valid deflate data decodes there; corrupt data fails there too)
+        uint32_t mx = 0;
+        std::vector<int64_t> hidx(4 * (size_t)nmembers);
+        GZHIP(hipMemcpy(hidx.data(), index, 8 * hidx.size(), hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < nmembers; ++i) mx = std::max(mx, (uint32_t)((uint64_t)hidx[4 * i + 3] & 0xffffffffu));
+        return ofl_inflate_members(src, index, nmembers, mx, out, out_cap, ws, ws_bytes, stream);
+    }
+    return OFL_OK;
+}
+
+int ofl_gzip_profile(int enable) {
+    std::lock_guard<std::mutex> g(g_prof_m);
+    for (ProfRec& r : g_prof_pending) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+    g_prof_pending.clear();
+    g_prof_on = enable != 0;
+    return OFL_OK;
+}
+
+int ofl_gzip_profile_collect(char* names, size_t names_cap, double* ms, int64_t* launches, int max_kernels, int* nkernels) {
+    if (!names || !ms || !launches || !nkernels) return gzfail(OFL_EINVAL, "profile: null argument");
+    std::lock_guard<std::mutex> g(g_prof_m);
+    std::vector<std::string> nm;
+    std::vector<double> t;
+    std::vector<int64_t> k;
+    for (ProfRec& r : g_prof_pending) {
+        float e = 0.f;
+        GZHIP(hipEventSynchronize(r.b));
+        GZHIP(hipEventElapsedTime(&e, r.a, r.b));
+        size_t i = 0;
+        while (i < nm.size() && nm[i] != r.name) ++i;
+        if (i == nm.size()) { nm.push_back(r.name); t.push_back(0.0); k.push_back(0); }
+        t[i] += e;
+        k[i] += 1;
+        (void)hipEventDestroy(r.a);
+        (void)hipEventDestroy(r.b);
+    }
+    g_prof_pending.clear();
+    std::string all;
+    const int nk = (int)std::min<size_t>(nm.size(), (size_t)max_kernels);
+    for (int i = 0; i < nk; ++i) {
+        all += nm[i];
+        all += '\n';
+        ms[i] = t[i];
+        launches[i] = k[i];
+    }
+    if (all.size() + 1 > names_cap) return gzfail(OFL_ESPACE, "profile: names buffer too small");
+    std::memcpy(names, all.c_str(), all.size() + 1);
+    *nkernels = nk;
     return OFL_OK;
 }
 
@@ -1742,6 +2400,7 @@ int ofl_inflate_members(const uint8_t* src, const int64_t* index, int64_t nmembe
     // members resident per CU from 26 to 15, and the decode is bound by the
     // scalar issue of many members, not by one member's steps
     static const bool pair = [] { const char* v = getenv("OFL_GZ_PAIR"); return v && v[0] == '1'; }();
+    gzprof_begin(st);
     if (!window && pair)
         hipLaunchKernelGGL((gz::k_inflate_members<1024, true, true>), dim3((unsigned)nmembers), dim3(64),
                            sizeof(gz::InfSmem<1024, true>), st, a);
@@ -1754,6 +2413,7 @@ int ofl_inflate_members(const uint8_t* src, const int64_t* index, int64_t nmembe
     else
         hipLaunchKernelGGL((gz::k_inflate_members<65536, false, false>), dim3((unsigned)nmembers), dim3(64),
                            sizeof(gz::InfSmem<65536, false>), st, a);
+    gzprof_end(st, "k_inflate_members");
     GZHIP(hipGetLastError());
     int h = 0;
     GZHIP(hipMemcpyAsync(&h, status, sizeof(int), hipMemcpyDeviceToHost, st));

@@ -254,8 +254,9 @@ def lut_decode_batch(ranks_arena, offsets, numels, maps, out_arena):
 @_on_device
 def gzip_ranks(x):
     """gzip.compress of a float32 device array of ranks (integers 0..31), on
-    the GPU (ofl_gzip_ranks): a multi-member gzip stream that gzip.decompress
-    reads back to x's bytes.  Raises CodecError for other values."""
+    the GPU (ofl_gzip_ranks, TLZ: optimal-parse token LZ, one deflate block
+    per 512 KiB member): a multi-member gzip stream that gzip.decompress reads
+    back to x's bytes.  Raises CodecError for other values."""
     _check_dev(x)
     L = _lib.lib()
     n = x.numel()
@@ -264,8 +265,8 @@ def gzip_ranks(x):
     ws = _ws_bytes(x.device, int(L.ofl_gzip_ranks_workspace_bytes(n)))
     bound = int(L.ofl_gzip_ranks_bound(n))
     # pinned output sized for a rank stream (a quarter of the input: rank
-    # streams compress to 0.05-0.2); the worst-case bound (8x the input) only
-    # after an OFL_ESPACE
+    # streams compress to 0.05-0.2); the worst-case bound (1.5x the input)
+    # only after an OFL_ESPACE
     for cap in (min(bound, n + (1 << 20)), bound):
         out = _buf("host", "gz_out", cap, pinned=True)
         ln = ctypes.c_size_t()
@@ -281,8 +282,8 @@ def gzip_ranks(x):
 
 def gunzip(data, threads=8, out=None):
     """gzip.decompress (kc_pipeline.py:152-156) of `data` -> uint8 numpy array.
-    Member-indexed streams (the device gzip's, every member carrying the 'BC'
-    size field) inflate in parallel on native threads (ofl_gunzip_members),
+    Member-indexed streams (the device gzip's, every member carrying its size
+    in an extra subfield) inflate in parallel on native threads (ofl_gunzip_members),
     into `out` (a uint8 numpy array, e.g. a pinned staging view) when given;
     any other stream goes through gzip.decompress."""
     L = _lib.lib()
@@ -354,22 +355,23 @@ def _buf(device, name, nbytes, pinned=False):
 def gunzip_device(data, out):
     """gzip.decompress (kc_pipeline.py:152-156) of `data` into `out`, a uint8
     DEVICE tensor (returns the view of the decompressed bytes).  Member-indexed
-    streams (the device gzip's) inflate on the GPU (ofl_gzip_member_index on
-    the host, ofl_inflate_members: one wavefront per member, ISIZE and CRC-32
-    checked): the compressed bytes cross PCIe instead of the decompressed ones.
-    Any other gzip stream (e.g. gzip.compress output) is a different format:
-    gzip.decompress on the host, then one H2D."""
+    streams inflate on the GPU from the compressed bytes (the index is built
+    on the host from the member headers, ofl_gzip_member_index): the device
+    gzip's TLZ members through ofl_inflate_tlz (one lane per 2048-value
+    segment, then the copies resolved in LDS; CRC-32 and ISIZE checked), other
+    member-indexed streams through ofl_inflate_members (one wavefront per
+    member).  Any other gzip stream (e.g. gzip.compress output) is a
+    different format: gzip.decompress on the host, then one H2D."""
     if not (out.is_cuda and out.dtype == torch.uint8 and out.is_contiguous()):
         raise _lib.CodecError("gunzip_device: out must be a contiguous uint8 device tensor")
     L = _lib.lib()
     src = np.frombuffer(data, np.uint8)
     dev = out.device
-    nm, tot, mx = ctypes.c_int64(), ctypes.c_size_t(), ctypes.c_uint32()
-    # the stream goes H2D straight from the payload (pageable: the runtime
-    # streams it at the pinned rate, 2.7 ms for 144 MiB on this box,
-    # profiles/r02_hostcopy_probe.json), on a pool thread while this one
-    # indexes the members (both release the GIL)
-    d_in = _buf(dev, "gz_in", max(src.size, 1))
+    nm, tot, mx, tl = ctypes.c_int64(), ctypes.c_size_t(), ctypes.c_uint32(), ctypes.c_int()
+    # the stream goes H2D straight from the payload, on a pool thread while
+    # this one indexes the members (both release the GIL); the inflate
+    # kernels read up to 32 bytes past the stream, hence the padding
+    d_in = _buf(dev, "gz_in", src.size + 64)
     # d_in belongs to the caller's current stream, and the inflate runs there:
     # the pool thread enqueues the copy on that same stream
     caller_stream = torch.cuda.current_stream(dev)
@@ -388,8 +390,8 @@ def gunzip_device(data, out):
     idx = np.empty((cap, 4), np.int64)
     try:
         rc = L.ofl_gzip_member_index(src.ctypes.data if src.size else None, src.size, idx.ctypes.data, cap,
-                                     ctypes.byref(nm), ctypes.byref(tot), ctypes.byref(mx)) if src.size \
-            else _lib.OFL_EFORMAT
+                                     ctypes.byref(nm), ctypes.byref(tot), ctypes.byref(mx), ctypes.byref(tl)) \
+            if src.size else _lib.OFL_EFORMAT
     finally:
         copy.result()
     if rc == _lib.OFL_EFORMAT:
@@ -405,9 +407,14 @@ def gunzip_device(data, out):
     idx = idx[:nm.value]
     d_idx = _buf(dev, "gz_idx", max(idx.nbytes, 8))
     d_idx[:idx.nbytes].copy_(torch.from_numpy(idx.view(np.uint8).reshape(-1)))
-    ws = _buf(dev, "gz_status", 256)
-    _lib.check_gzip(L.ofl_inflate_members(d_in.data_ptr(), d_idx.data_ptr(), nm.value, mx.value, out.data_ptr(),
-                                          out.numel(), ws.data_ptr(), ws.numel(), _stream(dev)))
+    if tl.value:
+        ws = _buf(dev, "gz_status", int(L.ofl_inflate_tlz_workspace_bytes(nm.value)))
+        _lib.check_gzip(L.ofl_inflate_tlz(d_in.data_ptr(), d_idx.data_ptr(), nm.value, out.data_ptr(), out.numel(),
+                                          ws.data_ptr(), ws.numel(), _stream(dev)))
+    else:
+        ws = _buf(dev, "gz_status", 256)
+        _lib.check_gzip(L.ofl_inflate_members(d_in.data_ptr(), d_idx.data_ptr(), nm.value, mx.value, out.data_ptr(),
+                                              out.numel(), ws.data_ptr(), ws.numel(), _stream(dev)))
     _trim_bufs()
     return out[:tot.value]
 
