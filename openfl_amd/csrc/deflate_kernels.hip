@@ -893,7 +893,7 @@ constexpr int kSlotPad = 8192;                     // + headers
 constexpr int kBatch = 512;                        // members per launch
 
 struct EncSmem {
-    alignas(16) uint8_t tok[kRing + 8];
+    alignas(16) uint8_t tok[kRing + 32];      // + the first 32 bytes again (a candidate's 20-byte read)
     union {
         struct {
             uint16_t prev[kPrevSlots * kSeg];      // distance to the previous same-bucket position (0: none)
@@ -934,7 +934,9 @@ struct EncArgs {
     int* bad;
     uint32_t slot_bytes, ops_stride;
     int aligned;             // x is 16-byte aligned
+    uint64_t* phases;        // diagnostics (OFL_GZ_PHASES): block 0's time per phase (10 ns ticks), else null
 };
+constexpr int kEncPhases = 16;
 
 DEVI int pslot(int p) { return ((p >> kSegLog) % kPrevSlots) * kSeg + (p & (kSeg - 1)); }
 DEVI uint32_t tk4r(const uint8_t* tok, int p) {
@@ -1022,6 +1024,12 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     EncSmem& S = *reinterpret_cast<EncSmem*>(smem_raw);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    uint64_t ph_t = 0, ph_acc[kEncPhases] = {};
+    const bool ph_on = a.phases && blockIdx.x == 0 && tid == 0;
+    auto PH = [&](int k) {
+        if (ph_on) { const uint64_t t = wall_clock64(); if (k > 0) ph_acc[k] += t - ph_t; ph_t = t; }
+    };
+    PH(0);
     const int64_t g0 = (a.mem0 + blockIdx.x) * (int64_t)kMemTok;
     const int ntok = (int)min<int64_t>(kMemTok, a.n - g0);
     const int nseg = (ntok + kSeg - 1) >> kSegLog;
@@ -1082,7 +1090,7 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
             if (bad) atomicOr(&S.bad, 1);
             const int r = lo & (kRing - 1);
             *reinterpret_cast<uint2*>(&S.tok[r]) = make_uint2(idw0, idw1);
-            if (r == 0) *reinterpret_cast<uint2*>(&S.tok[kRing]) = make_uint2(idw0, idw1);
+            if (r < 32) *reinterpret_cast<uint2*>(&S.tok[kRing + r]) = make_uint2(idw0, idw1);
             uint32_t wcrc;
             if (send - c0 == kSeg) {  // full segment: 32 bytes per thread, a shift tree over the lanes
                 uint32_t x = crc;
@@ -1115,6 +1123,7 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
                 S.crc_raw = crc_adv(S.crc_raw, 4u * (uint32_t)(send - c0)) ^ raw;
             }
         }
+        PH(1);
         // ---- B: 3-gram chains of [c0 - 2, send - 2) (the last two of a
         // segment wait for the next segment's values) ----
         const int s_ins = c == 0 ? 0 : c0 - 2;
@@ -1146,6 +1155,7 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
                 if ((m >> lane) == 1ull) S.u.m.lastw[wv][bk] = (uint16_t)(p - s_ins + 1);
             }
         }
+        PH(12);
         __syncthreads();
         for (int p0 = w_lo; p0 < w_hi; p0 += 64) {
             const int p = p0 + lane;
@@ -1173,10 +1183,28 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
 #pragma unroll
             for (int w2 = 0; w2 < kNT / 64; ++w2) S.u.m.lastw[w2][b] = 0;
         }
+        PH(2);
         // ---- C: each position's frontier of (length, distance) pairs ----
         uint32_t fa[kPer], fb[kPer], fc[kPer];  // entries: length | distance << 7 (lengths increasing)
         int nf[kPer];
         {
+            // chain candidates in increasing distance, branch-free: a
+            // candidate's first 16 values are compared at once (5 aligned LDS
+            // dwords, the 8 positions' loads issued together); only a match of
+            // 16 or more values walks further (rare)
+            const uint32_t* tw = reinterpret_cast<const uint32_t*>(S.tok);
+            constexpr int kCW = 3;  // values compared at once: 4 kCW
+            uint32_t ti[kPer][kCW];  // values i .. i + 4 kCW - 1 of each position
+            {
+                const int rb = (lo & (kRing - 1)) >> 2;  // lo is a multiple of 8
+                uint32_t w[kCW + 3];
+#pragma unroll
+                for (int k = 0; k < kCW + 3; ++k) w[k] = tw[rb + k];
+#pragma unroll
+                for (int q = 0; q < kPer; ++q)
+#pragma unroll
+                    for (int k = 0; k < kCW; ++k) ti[q][k] = __builtin_amdgcn_alignbyte(w[(q >> 2) + k + 1], w[(q >> 2) + k], (uint32_t)(q & 3));
+            }
             int j[kPer], bl[kPer], lim[kPer];
             bool act[kPer];
 #pragma unroll
@@ -1186,38 +1214,57 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
                 nf[q] = 0;
                 bl[q] = 0;
                 lim[q] = min(kMaxL, send - i);
-                act[q] = lim[q] >= kMinL;
-                j[q] = i;
-                if (act[q]) {
-                    const uint32_t pd = S.u.m.prev[pslot(i)];
-                    if (pd == 0) act[q] = false;
-                    else j[q] = i - (int)pd;
-                }
+                const uint32_t pd = lim[q] >= kMinL ? S.u.m.prev[pslot(i)] : 0u;
+                act[q] = pd != 0;
+                j[q] = i - (int)pd;
             }
 #pragma unroll 1
             for (int step = 0; step < kCand; ++step) {
                 bool any = false;
 #pragma unroll
-                for (int q = 0; q < kPer; ++q) {
-                    if (!act[q]) continue;
-                    const int i = lo + q;
-                    if (i - j[q] > kWin) { act[q] = false; continue; }
-                    const int L = match_len(S.tok, i, j[q], lim[q]);
-                    if (L >= kMinL && L > bl[q]) {
-                        const uint32_t e = (uint32_t)L | ((uint32_t)(i - j[q]) << 7);
-                        if (nf[q] == 0) fa[q] = e; else if (nf[q] == 1) fb[q] = e; else fc[q] = e;
-                        nf[q] = min(nf[q] + 1, 3);
-                        bl[q] = L;
-                        if (L == lim[q]) { act[q] = false; continue; }
+                for (int h = 0; h < kPer; h += 4) {  // two halves: fewer loads in flight, fewer registers
+                    uint32_t cw[4][kCW + 1], pd[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int q = h + u;
+                        const int jj = act[q] ? j[q] : lo;
+                        const int jb = (jj & (kRing - 1)) >> 2;
+#pragma unroll
+                        for (int k = 0; k <= kCW; ++k) cw[u][k] = tw[jb + k];
+                        pd[u] = S.u.m.prev[pslot(jj)];
                     }
-                    const uint32_t pd = S.u.m.prev[pslot(j[q])];
-                    if (pd == 0) act[q] = false;
-                    else j[q] -= (int)pd;
-                    any |= act[q];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int q = h + u;
+                        const int i = lo + q;
+                        const uint32_t sh = (uint32_t)(j[q] & 3);
+                        int L = 4 * kCW;
+#pragma unroll
+                        for (int k = kCW - 1; k >= 0; --k) {
+                            const uint32_t x = __builtin_amdgcn_alignbyte(cw[u][k + 1], cw[u][k], sh) ^ ti[q][k];
+                            L = x ? 4 * k + (__builtin_ctz(x) >> 3) : L;
+                        }
+                        const bool ok = act[q] && i - j[q] <= kWin;
+                        if (ok && L == 4 * kCW && lim[q] > 4 * kCW)  // rare: a long match walks on
+                            L = 4 * kCW + match_len(S.tok, i + 4 * kCW, j[q] + 4 * kCW, lim[q] - 4 * kCW);
+                        L = min(L, lim[q]);
+                        if (ok && L >= kMinL && L > bl[q]) {
+                            const uint32_t e = (uint32_t)L | ((uint32_t)(i - j[q]) << 7);
+                            fa[q] = nf[q] == 0 ? e : fa[q];
+                            fb[q] = nf[q] == 1 ? e : fb[q];
+                            fc[q] = nf[q] >= 2 ? e : fc[q];
+                            nf[q] = min(nf[q] + 1, 3);
+                            bl[q] = L;
+                        }
+                        act[q] = ok && bl[q] < lim[q] && pd[u] != 0;
+                        j[q] -= (int)pd[u];
+                        any |= act[q];
+                    }
                 }
                 if (!any) break;
             }
         }
+        PH(3);
         // ---- D: segmented backward DP (3 sweeps) ----
         uint32_t dca[kPer], dcb[kPer], dcc[kPer];
 #pragma unroll
@@ -1233,36 +1280,70 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
         }
         __syncthreads();
         const int klo = kPer * tid;  // segment-relative
+        {
+            // own positions' costs in registers (indices are compile-time
+            // after unrolling); lengths 3..10 branch-free, longer ones (rare)
+            // read the other threads' costs from LDS
+            constexpr int kU = 10;             // lengths unrolled: kMinL .. kU
+            constexpr int kW = kPer + kU - kPer;  // costs beyond this thread's positions within reach
+            uint32_t lenr[kU + 1];
+#pragma unroll
+            for (int l = kMinL; l <= kU; ++l) lenr[l] = S.lenc[l];
+            uint32_t litr[kPer];
+            int La[kPer], Lb[kPer], Lm[kPer];
+#pragma unroll
+            for (int q = 0; q < kPer; ++q) {
+                litr[q] = S.litc[((q < 4 ? idw0 : idw1) >> (8 * (q & 3))) & 0xffu];
+                La[q] = (int)(fa[q] & 127u);
+                Lb[q] = (int)(fb[q] & 127u);
+                Lm[q] = nf[q] == 0 ? 0 : (int)((nf[q] == 1 ? fa[q] : nf[q] == 2 ? fb[q] : fc[q]) & 127u);
+                if (c0 + klo + q >= send) Lm[q] = -1;  // no such position
+            }
 #pragma unroll 1
-        for (int sw = 0; sw < kSweeps; ++sw) {
-            uint32_t* cur = S.cost[sw & 1];
-            const uint32_t* prv = S.cost[(sw + 1) & 1];
+            for (int sw = 0; sw < kSweeps; ++sw) {
+                uint32_t* cur = S.cost[sw & 1];
+                const uint32_t* prv = S.cost[(sw + 1) & 1];
+                uint32_t pw[kW + 1];
 #pragma unroll
-            for (int q = kPer - 1; q >= 0; --q) {
-                const int k = klo + q;
-                if (c0 + k >= send) continue;
-                auto C = [&](int kk) -> uint32_t { return kk < klo + kPer ? cur[kk] : prv[kk]; };
-                const uint32_t id = ((q < 4 ? idw0 : idw1) >> (8 * (q & 3))) & 0xffu;
-                uint32_t best = S.litc[id] + C(k + 1);
-                uint32_t ch = 0;
-                int l0 = kMinL;
+                for (int u = 0; u <= kW; ++u) pw[u] = prv[min(klo + kPer + u, kSeg)];
+                uint32_t cr[kPer];
+                uint32_t chs[kPer];
 #pragma unroll
-                for (int e = 0; e < 3; ++e) {
-                    if (e >= nf[q]) break;
-                    const uint32_t ent = e == 0 ? fa[q] : e == 1 ? fb[q] : fc[q];
-                    const uint32_t dc = e == 0 ? dca[q] : e == 1 ? dcb[q] : dcc[q];
-                    const int L = (int)(ent & 127u);
-                    for (int l = l0; l <= L; ++l) {
-                        const uint32_t cc = S.lenc[l] + dc + C(k + l);
+                for (int q = kPer - 1; q >= 0; --q) {
+                    auto CV = [&](int kk) -> uint32_t { return kk < kPer ? cr[kk] : pw[kk - kPer]; };  // kk = q + l
+                    uint32_t best = litr[q] + CV(q + 1);
+                    uint32_t ch = 0;
+#pragma unroll
+                    for (int l = kMinL; l <= kU; ++l) {
+                        const uint32_t e = l <= La[q] ? 0u : l <= Lb[q] ? 1u : 2u;
+                        const uint32_t dc = e == 0 ? dca[q] : e == 1 ? dcb[q] : dcc[q];
+                        const uint32_t cc = lenr[l] + dc + CV(q + l);
+                        const bool take = l <= Lm[q] && cc < best;
+                        best = take ? cc : best;
+                        ch = take ? ((uint32_t)l | (e << 8)) : ch;
+                    }
+                    // longer lengths: only each frontier entry's own (full) length
+#pragma unroll
+                    for (int e = 0; e < 3; ++e) {
+                        const int l = e == 0 ? La[q] : e == 1 ? Lb[q] : Lm[q];
+                        if (l <= kU || l > Lm[q] || (e == 2 && nf[q] < 3) || (e == 1 && nf[q] < 2)) continue;
+                        const uint32_t dc = e == 0 ? dca[q] : e == 1 ? dcb[q] : dcc[q];
+                        const uint32_t cc = S.lenc[l] + dc + prv[klo + q + l];
                         if (cc < best) { best = cc; ch = (uint32_t)l | ((uint32_t)e << 8); }
                     }
-                    l0 = L + 1;
+                    cr[q] = Lm[q] < 0 ? 0u : best;
+                    chs[q] = ch;
                 }
-                cur[k] = best;
-                if (sw == kSweeps - 1) S.dec[k] = (uint16_t)ch;
+#pragma unroll
+                for (int q = 0; q < kPer; ++q) {
+                    if (Lm[q] < 0) continue;
+                    cur[klo + q] = cr[q];
+                    if (sw == kSweeps - 1) S.dec[klo + q] = (uint16_t)chs[q];
+                }
+                __syncthreads();
             }
-            __syncthreads();
         }
+        PH(4);
         // ---- E: the DP's path from the segment start: Jacobi rounds ----
         auto nxt = [&](int p) -> int { const int l = S.dec[p - c0] & 0xff; return p + (l ? l : 1); };
         {
@@ -1278,14 +1359,18 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
             __syncthreads();
             int changed = 0;
             if (tid + 1 < kNT && (int)S.entry[tid + 1] != p - c0) { S.entry[tid + 1] = (uint16_t)(p - c0); changed = 1; }
+            if (ph_on) ++ph_acc[11];
             if (!__syncthreads_or(changed)) break;
         }
+        PH(5);
         // ---- F: this segment's ops, in order; symbol counts ----
         {
             uint32_t opm = 0;
             for (int p = c0 + S.entry[tid]; p < lo + kPer && p < send; p = nxt(p)) opm |= 1u << (p - lo);
+            PH(13);
             uint32_t tot;
             const uint32_t off = block_scan((uint32_t)__popc(opm), S.scan, &tot);
+            PH(14);
             const uint32_t base = S.ops_n;
             uint32_t k = base + off;
             uint32_t nl = 0, nd = 0;
@@ -1320,8 +1405,10 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
             __syncthreads();
             if (tid == 0) S.ops_n = base + tot;
         }
+        PH(6);
         if (c + 1 < nseg) tlz_model(S, tid, false);  // its barriers also order ops_n and the histograms
         else __syncthreads();
+        PH(7);
     }
 
     // ---- G: the member's Huffman code (lengths limited to the inflate's table bits) ----
@@ -1425,6 +1512,7 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
     }
     __syncthreads();
 
+    PH(8);
     // ---- H: bits of the ops (a block scan of their costs), segment offsets ----
     const uint32_t nops = S.ops_n, H = S.hdr_bits;
     const uint32_t o_lo = (uint32_t)((uint64_t)nops * tid / kNT), o_hi = (uint32_t)((uint64_t)nops * (tid + 1) / kNT);
@@ -1528,6 +1616,9 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
         for (uint32_t i = 0; i < D / 4; ++i) slot[i] = reinterpret_cast<const uint32_t*>(hb)[i];
         a.sizes[blockIdx.x] = bytes;
     }
+    PH(9);
+    if (ph_on)
+        for (int k = 0; k < kEncPhases; ++k) a.phases[k] = ph_acc[k];
 }
 
 // ---- inflate --------------------------------------------------------------
@@ -2167,8 +2258,17 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
         (void)hipGetLastError();  // a pageable pointer is not an error here
     }
     const int aligned = (reinterpret_cast<uintptr_t>(x) & 15u) == 0;
+    // diagnostics: OFL_GZ_PHASES=1 prints block 0's phase times (10 ns ticks,
+    // summed over its segments; [11] = Jacobi rounds) of the first launch
+    static const bool phases = getenv("OFL_GZ_PHASES") != nullptr;
+    uint64_t* d_ph = nullptr;
+    if (phases) {
+        GZHIP(hipMalloc(&d_ph, 8 * gz::tlz::kEncPhases));
+        GZHIP(hipMemsetAsync(d_ph, 0, 8 * gz::tlz::kEncPhases, st));
+    }
     auto enc = [&](int64_t c0, int nb) {
-        gz::tlz::EncArgs a{x, n, c0, slots, ops, sizes, bad, (uint32_t)L.slot, (uint32_t)L.ops_stride, aligned};
+        gz::tlz::EncArgs a{x, n, c0, slots, ops, sizes, bad, (uint32_t)L.slot, (uint32_t)L.ops_stride, aligned,
+                           c0 == 0 ? d_ph : nullptr};
         gzprof_begin(st);
         hipLaunchKernelGGL(gz::tlz::k_tlz_encode, dim3(nb), dim3(gz::tlz::kNT), sizeof(gz::tlz::EncSmem), st, a);
         gzprof_end(st, "tlz::k_tlz_encode");
@@ -2212,6 +2312,17 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
         GZHIP(hipMemcpyAsync(out + total, packed, tot, hipMemcpyDeviceToHost, st));
         GZHIP(hipStreamSynchronize(st));
         total += tot;
+    }
+    if (d_ph) {
+        uint64_t h[gz::tlz::kEncPhases];
+        GZHIP(hipMemcpy(h, d_ph, sizeof(h), hipMemcpyDeviceToHost));
+        GZHIP(hipFree(d_ph));
+        fprintf(stderr, "tlz phases (block 0, 10 ns ticks): load %llu chains[B1 %llu rest %llu] frontier %llu dp %llu parse %llu "
+                "ops[walk %llu scan %llu rec %llu] model %llu code %llu bits %llu | jacobi rounds %llu\n",
+                (unsigned long long)h[1], (unsigned long long)h[12], (unsigned long long)h[2], (unsigned long long)h[3],
+                (unsigned long long)h[4], (unsigned long long)h[5], (unsigned long long)h[13], (unsigned long long)h[14],
+                (unsigned long long)h[6], (unsigned long long)h[7], (unsigned long long)h[8], (unsigned long long)h[9],
+                (unsigned long long)h[11]);
     }
     *out_len = total;
     return OFL_OK;

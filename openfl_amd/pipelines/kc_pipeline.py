@@ -47,7 +47,7 @@ class KCPipeline(TransformationPipeline):
     """plan.yaml: template openfl_amd.pipelines.KCPipeline, settings n_clusters
     (p_sparsity accepted and ignored, like the reference :160-181)."""
 
-    def __init__(self, p_sparsity=0.01, n_clusters=6, device="cpu", gzip_level=9, gzip_backend="host", **kwargs):
+    def __init__(self, p_sparsity=0.01, n_clusters=6, device="cpu", gzip_level=9, gzip_backend="device", **kwargs):
         self.p = p_sparsity
         self.n_cluster = n_clusters
         super().__init__(transformers=[KmeansTransformer(n_clusters, device), GZIPTransformer(gzip_level, backend=gzip_backend)],

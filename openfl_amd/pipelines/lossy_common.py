@@ -25,13 +25,13 @@ def float_to_int(np_array):
 
 
 class GZIPTransformer(Transformer):
-    """float32 bytes -> gzip (lossless).  backend="host": gzip.compress at
-    `level` (large payloads as a multi-member stream compressed on host
-    threads); backend="device": the GPU gzip of rank arrays
-    (lossy.gzip_ranks, csrc/deflate_kernels.hip).  Either way
-    gzip.decompress reads the stream back to the same bytes."""
+    """float32 bytes -> gzip (lossless).  backend="device" (the pipelines'
+    default): the GPU gzip of rank arrays (lossy.gzip_ranks, TLZ in
+    csrc/deflate_kernels.hip); backend="host": gzip.compress at `level`
+    (large payloads as a multi-member stream compressed on host threads).
+    Either way gzip.decompress reads the stream back to the same bytes."""
 
-    def __init__(self, level=9, threads=8, backend="host"):
+    def __init__(self, level=9, threads=8, backend="device"):
         if backend not in ("host", "device"):
             raise ValueError("gzip backend must be 'host' or 'device'")
         self.lossy = False

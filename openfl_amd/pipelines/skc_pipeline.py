@@ -37,7 +37,7 @@ class SKCPipeline(TransformationPipeline):
     """plan.yaml: template openfl_amd.pipelines.SKCPipeline, settings
     p_sparsity, n_clusters (:233-262)."""
 
-    def __init__(self, p_sparsity=0.1, n_clusters=6, device="cpu", gzip_level=9, gzip_backend="host", **kwargs):
+    def __init__(self, p_sparsity=0.1, n_clusters=6, device="cpu", gzip_level=9, gzip_backend="device", **kwargs):
         self.p = p_sparsity
         self.n_cluster = n_clusters
         sp = SparsityTransformer(self.p, device)

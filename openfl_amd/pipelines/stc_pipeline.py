@@ -74,7 +74,7 @@ class STCPipeline(TransformationPipeline):
     """plan.yaml: template openfl_amd.pipelines.STCPipeline, settings p_sparsity
     (n_clusters accepted and ignored, like the reference :218-245)."""
 
-    def __init__(self, p_sparsity=0.1, n_clusters=6, device="cpu", gzip_level=9, gzip_backend="host", **kwargs):
+    def __init__(self, p_sparsity=0.1, n_clusters=6, device="cpu", gzip_level=9, gzip_backend="device", **kwargs):
         self.p = p_sparsity
         sp = SparsityTransformer(self.p, device)
         super().__init__(transformers=[sp, TernaryTransformer(device, share=sp),

@@ -334,7 +334,8 @@ def test_gzip_ranks_roundtrip(case):
     z = lossy.gzip_ranks(torch.from_numpy(x).to(DEV))
     assert gzip.decompress(z) == x.tobytes()
     assert z == lossy.gzip_ranks(torch.from_numpy(x).to(DEV))      # deterministic
-    # every member carries its 'BC' size field: the native parallel inflate reads it
+    # every member carries its 'OZ' subfield (size, segment table): the native
+    # parallel inflate reads it
     import ctypes
     from openfl_amd import _lib
     src = np.frombuffer(z, np.uint8)
@@ -354,14 +355,77 @@ def test_gzip_ranks_roundtrip(case):
     LB.check_gzip(L.ofl_gzip_ranks(xd.data_ptr(), x.size, pageable.ctypes.data, cap, ctypes.byref(ln), wsb.data_ptr(),
                                    wsb.numel(), torch.cuda.current_stream().cuda_stream))
     assert pageable[:ln.value].tobytes() == z
-    # and the device inflate (ofl_inflate_members) straight into HBM
+    # and the device inflate (TLZ: one lane per segment, copies resolved in
+    # LDS) straight into HBM
     out = torch.full((x.nbytes + 64,), 7, dtype=torch.uint8, device=DEV)
     got = lossy.gunzip_device(z, out)
     assert got.numel() == x.nbytes and got.cpu().numpy().tobytes() == x.tobytes()
     assert int(out[x.nbytes:].eq(7).all())                            # nothing written past the data
-    if case == "kc6":
+    # the generic member inflate reads the same stream (plain deflate)
+    assert _inflate_generic(z, x.nbytes) == x.tobytes()
+    if case == "kc6":  # the optimal parse beats gzip -9 on k-means ranks
         ref = len(gzip.compress(x.tobytes(), compresslevel=9))
-        assert len(z) < 1.35 * ref, (len(z), ref)   # ratio 0.139 vs gzip -9 0.118
+        assert len(z) < ref, (len(z), ref)
+
+
+def _nseg(z):
+    return int.from_bytes(z[18:20], "little")
+
+
+def _inflate_generic(z, nbytes):
+    """ofl_inflate_members (one wavefront per member, any deflate data) on a
+    stream: the TLZ members are plain deflate to it."""
+    import ctypes
+    from openfl_amd import _lib
+    L = _lib.lib()
+    src = np.frombuffer(z, np.uint8)
+    cap = src.size // 26 + 1
+    idx = np.empty((cap, 4), np.int64)
+    nm, tot, mx, tl = ctypes.c_int64(), ctypes.c_size_t(), ctypes.c_uint32(), ctypes.c_int()
+    _lib.check_gzip(L.ofl_gzip_member_index(src.ctypes.data, src.size, idx.ctypes.data, cap, ctypes.byref(nm),
+                                            ctypes.byref(tot), ctypes.byref(mx), ctypes.byref(tl)))
+    assert tl.value == 1 and tot.value == nbytes
+    d_in = torch.zeros(src.size + 64, dtype=torch.uint8, device=DEV)
+    d_in[:src.size] = torch.from_numpy(src.copy())
+    d_idx = torch.from_numpy(idx[:nm.value].copy()).to(DEV)
+    out = torch.zeros(nbytes + 64, dtype=torch.uint8, device=DEV)
+    ws = torch.empty(256, dtype=torch.uint8, device=DEV)
+    _lib.check_gzip(L.ofl_inflate_members(d_in.data_ptr(), d_idx.data_ptr(), nm.value, mx.value, out.data_ptr(),
+                                          out.numel(), ws.data_ptr(), ws.numel(), torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    return out[:nbytes].cpu().numpy().tobytes()
+
+
+def test_tlz_rejects_corrupt_streams():
+    """A corrupted TLZ stream fails loudly on the device path where
+    gzip.decompress fails (the TLZ decoder hands what it does not expect to
+    the generic inflate, which decides); a flipped CRC-32 is reported as such;
+    the untouched stream decodes."""
+    from openfl_amd import _lib, lossy
+    x = np.random.default_rng(5).choice(6, 300_000, p=[0.07, 0.2, 0.23, 0.23, 0.2, 0.07]).astype(np.float32)
+    z = lossy.gzip_ranks(torch.from_numpy(x).to(DEV))
+    out = torch.zeros(x.nbytes + 64, dtype=torch.uint8, device=DEV)
+    assert lossy.gunzip_device(z, out).cpu().numpy().tobytes() == x.tobytes()
+    first = int.from_bytes(z[20:24], "little")                # the first member's size ('OZ' field)
+    bad_crc = bytearray(z)
+    bad_crc[first - 8] ^= 0x5A
+    with pytest.raises(_lib.CodecError, match="CRC"):
+        lossy.gunzip_device(bytes(bad_crc), out)
+    hdr = 28 + 4 * _nseg(z)
+    for off in (hdr + 40, hdr + first // 3, first // 2, first - 12):
+        bad = bytearray(z)
+        bad[off] ^= 0xFF
+        with pytest.raises((_lib.CodecError, EOFError, OSError, zlib.error)):
+            gzip.decompress(bytes(bad))
+        with pytest.raises(_lib.CodecError):
+            lossy.gunzip_device(bytes(bad), out)
+    # a segment entry point moved: gzip.decompress ignores the table, and so
+    # does the device path's fallback (the TLZ decoder refuses the member, the
+    # generic inflate reads it as the plain deflate it is)
+    bad = bytearray(z)
+    bad[28 + 4] ^= 0x01
+    assert gzip.decompress(bytes(bad)) == x.tobytes()
+    assert lossy.gunzip_device(bytes(bad), out).cpu().numpy().tobytes() == x.tobytes()
 
 
 def test_gzip_ranks_rejects_non_ranks():
@@ -526,3 +590,27 @@ def test_inflate_members_rejects_corrupt_streams():
 def zlib_error():
     import zlib
     return zlib.error
+
+
+@pytest.mark.parametrize("name", ["KCPipeline", "STCPipeline", "SKCPipeline"])
+def test_default_gzip_backend_is_device_and_reference_readable(name):
+    """The pipelines' default gzip backend is the GPU one (TLZ), and its payload
+    is what the reference's GZIPTransformer.backward reads: plain
+    gzip.decompress (kc_pipeline.py:152-156) gives the float32 ranks, which
+    the reference's LUT backward (sequential key -> value replacement,
+    kc_pipeline.py:79-83) turns into the array our backward returns."""
+    import openfl_amd.pipelines as P
+    x = np.random.default_rng(9).standard_normal((700, 300)).astype(np.float32)
+    pipe = getattr(P, name)(n_clusters=6, device=DEV)
+    assert pipe.transformers[-1].backend == "device"
+    np.random.seed(3)
+    payload, mds = pipe.forward(x)
+    assert int.from_bytes(payload[12:14], "little") == int.from_bytes(b"OZ", "little")  # a TLZ member
+    ranks = np.frombuffer(gzip.decompress(payload), np.float32)
+    assert ranks.size == x.size
+    m = next(d["int_to_float"] for d in mds if "int_to_float" in d)
+    ref = ranks.copy()
+    for k in m:                                   # the reference's in-place LUT, in the mapping's order
+        ref[ref == k] = m[k]
+    y = pipe.backward(payload, [dict(d) for d in mds])
+    np.testing.assert_array_equal(y.reshape(-1), ref)

@@ -58,13 +58,15 @@ def test_member_index_for_the_device_inflate():
     src = np.frombuffer(z, np.uint8)
     nm, tot, mx = ctypes.c_int64(), ctypes.c_size_t(), ctypes.c_uint32()
     assert L.ofl_gzip_member_index(src.ctypes.data, src.size, None, 0, ctypes.byref(nm), ctypes.byref(tot),
-                                   ctypes.byref(mx)) == 0
+                                   ctypes.byref(mx), None) == 0
     assert (nm.value, tot.value, mx.value) == (13, len(raw), 16384)
     idx = np.zeros((nm.value, 4), np.int64)
     assert L.ofl_gzip_member_index(src.ctypes.data, src.size, idx.ctypes.data, nm.value - 1, ctypes.byref(nm),
-                                   ctypes.byref(tot), ctypes.byref(mx)) == _lib.OFL_ESPACE
+                                   ctypes.byref(tot), ctypes.byref(mx), None) == _lib.OFL_ESPACE
+    tl = ctypes.c_int(7)
     assert L.ofl_gzip_member_index(src.ctypes.data, src.size, idx.ctypes.data, nm.value, ctypes.byref(nm),
-                                   ctypes.byref(tot), ctypes.byref(mx)) == 0
+                                   ctypes.byref(tot), ctypes.byref(mx), ctypes.byref(tl)) == 0
+    assert tl.value == 0  # 'BC' members are not TLZ
     for k, (off, ln, out, meta) in enumerate(idx.tolist()):
         meta &= (1 << 64) - 1
         part = raw[16384 * k:16384 * (k + 1)]
@@ -72,7 +74,39 @@ def test_member_index_for_the_device_inflate():
         assert zlib.decompress(z[off:off + ln], -15) == part
     plain = np.frombuffer(gzip.compress(raw), np.uint8)
     assert L.ofl_gzip_member_index(plain.ctypes.data, plain.size, None, 0, ctypes.byref(nm), ctypes.byref(tot),
-                                   ctypes.byref(mx)) == _lib.OFL_EFORMAT
+                                   ctypes.byref(mx), None) == _lib.OFL_EFORMAT
+
+
+def test_oz_members_index_and_host_inflate():
+    """Members carrying the TLZ 'OZ' subfield (size, value count, segment
+    table): the index flags them (bit 62 of the data length, all_tlz), the
+    host parallel inflate and gzip.decompress read them, and a value count
+    that contradicts ISIZE clears the flag."""
+    import ctypes
+    import zlib
+    from tests.bgzf import oz_members
+    raw = np.random.default_rng(4).integers(0, 6, 131072 * 2 + 5000).astype(np.float32).tobytes()
+    z = oz_members(raw)
+    assert gzip.decompress(z) == raw
+    L = _lib.lib()
+    src = np.frombuffer(z, np.uint8)
+    nm, tot, mx, tl = ctypes.c_int64(), ctypes.c_size_t(), ctypes.c_uint32(), ctypes.c_int()
+    idx = np.zeros((8, 4), np.int64)
+    assert L.ofl_gzip_member_index(src.ctypes.data, src.size, idx.ctypes.data, 8, ctypes.byref(nm), ctypes.byref(tot),
+                                   ctypes.byref(mx), ctypes.byref(tl)) == 0
+    assert (nm.value, tot.value, tl.value) == (3, len(raw), 1)
+    for k in range(3):
+        off, ln = int(idx[k, 0]), int(idx[k, 1])
+        assert ln >> 62 == 1
+        ln &= (1 << 62) - 1
+        assert zlib.decompress(z[off:off + ln], -15) == raw[4 * 131072 * k:4 * 131072 * (k + 1)]
+    assert lossy.gunzip(z, 4).tobytes() == raw
+    bad = bytearray(z)
+    bad[24] ^= 1                                  # the first member's value count
+    src = np.frombuffer(bytes(bad), np.uint8)
+    assert L.ofl_gzip_member_index(src.ctypes.data, src.size, idx.ctypes.data, 8, ctypes.byref(nm), ctypes.byref(tot),
+                                   ctypes.byref(mx), ctypes.byref(tl)) == 0
+    assert tl.value == 0 and idx[0, 1] >> 62 == 0 and idx[1, 1] >> 62 == 1
 
 
 @pytest.mark.parametrize("fake", [False, True])
@@ -95,5 +129,5 @@ def test_large_stream_parallel_index(fake):
     src = np.frombuffer(z, np.uint8)
     nm, tot, mx = ctypes.c_int64(), ctypes.c_size_t(), ctypes.c_uint32()
     assert L.ofl_gzip_member_index(src.ctypes.data, src.size, None, 0, ctypes.byref(nm), ctypes.byref(tot),
-                                   ctypes.byref(mx)) == 0
+                                   ctypes.byref(mx), None) == 0
     assert nm.value == -(-len(raw) // 60_000) and tot.value == len(raw)

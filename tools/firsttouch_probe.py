@@ -40,7 +40,7 @@ def access(z):
     idx = np.empty((cap, 4), np.int64)
     t0 = time.perf_counter()
     L.ofl_gzip_member_index(src.ctypes.data, src.size, idx.ctypes.data, cap, ctypes.byref(nm), ctypes.byref(tt),
-                            ctypes.byref(mx))
+                            ctypes.byref(mx), None)
     t1 = time.perf_counter()
     lossy._parallel_copy(stage.data_ptr(), src.ctypes.data, src.size)
     t2 = time.perf_counter()

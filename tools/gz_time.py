@@ -51,10 +51,10 @@ L = _lib.lib()
 src = np.frombuffer(z, np.uint8)
 nm, tot, mx = ctypes.c_int64(), ctypes.c_size_t(), ctypes.c_uint32()
 t0 = time.perf_counter()
-L.ofl_gzip_member_index(src.ctypes.data, src.size, None, 0, ctypes.byref(nm), ctypes.byref(tot), ctypes.byref(mx))
+L.ofl_gzip_member_index(src.ctypes.data, src.size, None, 0, ctypes.byref(nm), ctypes.byref(tot), ctypes.byref(mx), None)
 idx = np.empty((nm.value, 4), np.int64)
 L.ofl_gzip_member_index(src.ctypes.data, src.size, idx.ctypes.data, nm.value, ctypes.byref(nm), ctypes.byref(tot),
-                        ctypes.byref(mx))
+                        ctypes.byref(mx), None)
 t1 = time.perf_counter()
 pin = torch.empty(src.size + idx.nbytes + 8, dtype=torch.uint8).pin_memory()
 pn = pin.numpy()

@@ -46,7 +46,7 @@ for it in range(steps + 1):
     idx = np.empty((cap, 4), np.int64)
     t = tick("inflate.alloc", t)
     L.ofl_gzip_member_index(src.ctypes.data, src.size, idx.ctypes.data, cap, ctypes.byref(nm), ctypes.byref(tt),
-                            ctypes.byref(mx))
+                            ctypes.byref(mx), None)
     t = tick("inflate.index", t)
     idx = idx[:nm.value]
     ioff = (src.size + 7) // 8 * 8
