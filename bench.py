@@ -208,7 +208,47 @@ def secondary(name, n_bits, steps, warmup, dev, wave_mib, streams, cpu=False, gr
     return out
 
 
-KC_TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r03_final_kc_pipeline_hbm_traffic.json")
+KC_TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r04_kc_pipeline_hbm_traffic.json")
+
+
+def _kc_kernel_profile(encode, decode, dev, steps=2):
+    """Per-kernel time of the KC step, measured: HIP events around every
+    gzip / inflate launch inside the library (ofl_gzip_profile) and torch
+    events around the k-means and LUT calls (several small kernels each), in
+    a serialized pass right after the timed region.  -> {name: {...}}."""
+    import ctypes
+    import torch
+    from openfl_amd import _lib
+    L = _lib.lib()
+    calls = {}
+
+    def timed(name, fn, *a, **kw):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        r = fn(*a, **kw)
+        e1.record()
+        calls.setdefault(name, []).append((e0, e1))
+        return r
+    _lib.check_gzip(L.ofl_gzip_profile(1))
+    try:
+        for _ in range(steps):
+            decode(*encode(timed), timed)
+        torch.cuda.synchronize()
+        names = ctypes.create_string_buffer(8192)
+        ms = np.zeros(64, np.float64)
+        ln = np.zeros(64, np.int64)
+        nk = ctypes.c_int()
+        _lib.check_gzip(L.ofl_gzip_profile_collect(names, 8192, ms.ctypes.data, ln.ctypes.data, 64, ctypes.byref(nk)))
+    finally:
+        L.ofl_gzip_profile(0)
+    out = {}
+    for name, t, k in zip(names.value.decode().split("\n")[:nk.value], ms, ln):
+        out[name] = {"ms_per_step": float(t) / steps, "launches_per_step": int(k) / steps, "avg_us": 1e3 * float(t) / max(int(k), 1)}
+    for name, evs in calls.items():
+        t = sum(a.elapsed_time(b) for a, b in evs)
+        out[name] = {"ms_per_step": t / steps, "launches_per_step": len(evs) / steps, "avg_us": 1e3 * t / len(evs),
+                     "note": "one library call of several kernels (torch events around the call)"}
+    return {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in v.items()} for k, v in out.items()}
 
 
 def kc_pipeline(steps, warmup, dev, extras=True):
@@ -244,10 +284,13 @@ def kc_pipeline(steps, warmup, dev, extras=True):
     ph = {"kmeans": 0.0, "gzip": 0.0, "inflate": 0.0, "lut": 0.0}
     ranks_bytes = ranks.view(torch.uint8)
 
-    def encode():
+    def plain(name, fn, *a, **kw):
+        return fn(*a, **kw)
+
+    def encode(call=plain):
         t0 = time.perf_counter()
-        _, _, _, uniq = lossy.kmeans_batch(x, offs, numels, 6, n_init=6, seed=int(rng.randint(0, 2 ** 31 - 1)),
-                                           ranks_out=ranks)
+        _, _, _, uniq = call("lossy::kmeans_batch", lossy.kmeans_batch, x, offs, numels, 6, n_init=6,
+                             seed=int(rng.randint(0, 2 ** 31 - 1)), ranks_out=ranks)
         t1 = time.perf_counter()
         z = lossy.gzip_ranks(ranks)
         t2 = time.perf_counter()
@@ -255,11 +298,11 @@ def kc_pipeline(steps, warmup, dev, extras=True):
         ph["gzip"] += t2 - t1
         return z, [{i: u for i, u in enumerate(uq)} for uq in uniq]
 
-    def decode(z, maps):
+    def decode(z, maps, call=plain):
         t0 = time.perf_counter()
         lossy.gunzip_device(z, ranks_bytes)
         t1 = time.perf_counter()
-        lossy.lut_decode_batch(ranks, offs, numels, maps, y)
+        call("lossy::lut_decode_batch", lossy.lut_decode_batch, ranks, offs, numels, maps, y)
         torch.cuda.synchronize()
         ph["lut"] += time.perf_counter() - t1
         ph["inflate"] += t1 - t0
@@ -285,6 +328,13 @@ def kc_pipeline(steps, warmup, dev, extras=True):
             "frac": round(alg / wall / 1e9 / PEAK_HBM_GBPS, 5), "alg_bytes_per_step": alg, "traffic": None,
             "scope": "KC step = forward + backward of the set (wall time, gzip and inflate included); "
                      "algorithmic bytes = 4n x read + stream write + stream read + 4n y write"}
+    name = None
+    if extras:  # (the PMC passes of tools/kc_bench.py count the timed steps' dispatches only)
+        kern = _kc_kernel_profile(encode, decode, dev)
+        name = max(kern, key=lambda k: kern[k]["ms_per_step"])
+        roof["dominant_kernel"] = dict(kern[name], name=name,
+                                       source="HIP events in a serialized profile pass after the timed region")
+        roof["kernels"] = kern
     if os.path.exists(KC_TRAFFIC_JSON):
         with open(KC_TRAFFIC_JSON) as f:
             tj = json.load(f)
@@ -292,10 +342,10 @@ def kc_pipeline(steps, warmup, dev, extras=True):
         roof["traffic_unit"] = "HBM bytes per step (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction)"
         roof["traffic_source"] = (os.path.relpath(KC_TRAFFIC_JSON, ROOT)
                                   + " (rocprofv3 --pmc passes of tools/kc_bench.py, KC kernels only, not this run)")
-        if tj.get("kernels"):
-            name, k = max(tj["kernels"].items(),
-                          key=lambda kv: kv[1].get("avg_us", 0.0) * kv[1]["dispatches_per_step"])
-            roof["dominant_kernel"] = dict(k, name=name)
+        pk = (tj.get("kernels") or {}).get(name) if name else None
+        if pk and pk.get("dispatches_per_step"):
+            roof["dominant_kernel"]["traffic_per_launch"] = pk["hbm_bytes_per_step"] / pk["dispatches_per_step"] \
+                if "hbm_bytes_per_step" in pk else None
     if not extras:
         return {"value": round(nbytes / wall / 2 ** 30, 3), "unit": "GiB/s", "ms_per_step": round(1e3 * wall, 3),
                 "phases_ms": phases, "wire_ratio": round(len(z) / nbytes, 4), "roofline": roof,

@@ -884,7 +884,6 @@ constexpr int kCand = 16;                          // chain candidates per posit
 constexpr int kBuckets = 1024;                     // 3-gram buckets: exact for values < 8, hashed above
 constexpr int kSweeps = 3;
 constexpr int kRing = 16384;                       // value ring (ids), + 8 mirrored bytes
-constexpr int kPrevSlots = 5;                      // chain ring: 4 window segments + this one
 constexpr int kLitMax = 11, kDistMax = 10;         // code length limits = the inflate's table bits
 constexpr int kHdrFixed = 28;                      // member header bytes before the segment table
 constexpr uint16_t kPending = 0xffffu;
@@ -896,8 +895,11 @@ struct EncSmem {
     alignas(16) uint8_t tok[kRing + 32];      // + the first 32 bytes again (a candidate's 20-byte read)
     union {
         struct {
-            uint16_t prev[kPrevSlots * kSeg];      // distance to the previous same-bucket position (0: none)
-            uint16_t lastw[kNT / 64][kBuckets];    // per wave, this segment: position - range start + 1
+            uint16_t prev[kRing];                  // distance to the previous same-bucket position (0: none), by position mod kRing
+            union {
+                uint16_t lastw[kNT / 64][kBuckets];  // chains: per wave, this segment: position - range start + 1
+                uint16_t cost[2][kSeg + 8];        // then the DP's costs to the segment end, 1/8 bit, mod 2^16
+            };
         } m;
         struct {
             HScratch h;
@@ -906,7 +908,6 @@ struct EncSmem {
         } f;
     } u;
     uint32_t head[kBuckets];                       // last position + 1 per bucket (earlier segments)
-    uint32_t cost[2][kSeg + 4];                    // DP costs to the segment end, 1/8 bit
     uint16_t dec[kSeg];                            // chosen op: length (0: literal) | frontier entry << 8
     uint16_t entry[kNT + 1];                       // parse: each thread's first position
     uint32_t hl[kLit], hd[kDist], hc[kCL];
@@ -938,7 +939,10 @@ struct EncArgs {
 };
 constexpr int kEncPhases = 16;
 
-DEVI int pslot(int p) { return ((p >> kSegLog) % kPrevSlots) * kSeg + (p & (kSeg - 1)); }
+DEVI int pslot(int p) { return p & (kRing - 1); }
+// the DP's costs live modulo 2^16: all candidates of one position lie within
+// 64 values of each other, < 64 x 4 literals x 15 bits x 8 < 2^15 apart
+DEVI bool lt16(uint32_t a, uint32_t b) { return (int16_t)(uint16_t)(a - b) < 0; }
 DEVI uint32_t tk4r(const uint8_t* tok, int p) {
     const int r = p & (kRing - 1);
     const uint32_t* w = reinterpret_cast<const uint32_t*>(tok);
@@ -1056,6 +1060,8 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
     }
     tlz_model(S, tid, true);
 
+    uint32_t crc_acc = 0, crc_last = 0;
+    int nv_last = 0;
     for (int c = 0; c < nseg; ++c) {
         const int c0 = c << kSegLog;
         const int send = min(c0 + kSeg, ntok);
@@ -1088,40 +1094,23 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
                 }
             }
             if (bad) atomicOr(&S.bad, 1);
+            for (int b = tid; b < kBuckets; b += kNT)  // the chains' wave tables (they share memory with the DP's costs)
+#pragma unroll
+                for (int w2 = 0; w2 < kNT / 64; ++w2) S.u.m.lastw[w2][b] = 0;
             const int r = lo & (kRing - 1);
             *reinterpret_cast<uint2*>(&S.tok[r]) = make_uint2(idw0, idw1);
             if (r < 32) *reinterpret_cast<uint2*>(&S.tok[kRing + r]) = make_uint2(idw0, idw1);
-            uint32_t wcrc;
-            if (send - c0 == kSeg) {  // full segment: 32 bytes per thread, a shift tree over the lanes
-                uint32_t x = crc;
-#pragma unroll
-                for (int l = 0; l < 6; ++l) {
-                    const uint32_t o = (uint32_t)__shfl_xor((int)x, 1 << l, 64);
-                    const uint32_t sh = crc_adv_pow2(x, 5 + l);
-                    x = (lane & (1 << l)) ? x : (sh ^ o);
-                }
-                wcrc = x;
-            } else {  // ragged: each thread advances over the bytes after it
-                uint32_t x = nv ? crc_adv(crc, 4u * (uint32_t)(send - lo - nv)) : 0u;
-                for (int o = 32; o > 0; o >>= 1) x ^= (uint32_t)__shfl_xor((int)x, o, 64);
-                wcrc = x;
-            }
-            if (lane == 0) S.crc_w[wv] = wcrc;
+            // raw CRC-32 by Horner per thread: acc covers this thread's pieces
+            // of the full segments so far (each advanced by the 8 KiB of every
+            // later segment); the last segment's piece and the combination
+            // over the threads follow the loop
+            if (c + 1 < nseg) crc_acc = crc_adv_pow2(crc_acc, kSegLog + 2) ^ crc;
+            else crc_last = crc, nv_last = nv;
         }
         __syncthreads();
         if (S.bad) {  // block-uniform
             if (tid == 0) { atomicOr(a.bad, 1); a.sizes[blockIdx.x] = 0; }
             return;
-        }
-        if (tid == 0) {
-            uint32_t raw = 0;
-            if (send - c0 == kSeg) {
-                for (int w = 0; w < kNT / 64; ++w) raw = crc_adv_pow2(raw, kSegLog) ^ S.crc_w[w];  // 2048 bytes per wave
-                S.crc_raw = crc_adv_pow2(S.crc_raw, kSegLog + 2) ^ raw;
-            } else {
-                for (int w = 0; w < kNT / 64; ++w) raw ^= S.crc_w[w];
-                S.crc_raw = crc_adv(S.crc_raw, 4u * (uint32_t)(send - c0)) ^ raw;
-            }
         }
         PH(1);
         // ---- B: 3-gram chains of [c0 - 2, send - 2) (the last two of a
@@ -1175,13 +1164,11 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
             }
         }
         __syncthreads();
-        for (int b = tid; b < kBuckets; b += kNT) {  // heads; the wave tables cleared for the next segment
+        for (int b = tid; b < kBuckets; b += kNT) {  // heads
             for (int w2 = kNT / 64 - 1; w2 >= 0; --w2) {
                 const uint32_t lw = S.u.m.lastw[w2][b];
                 if (lw) { S.head[b] = (uint32_t)s_ins + lw; break; }
             }
-#pragma unroll
-            for (int w2 = 0; w2 < kNT / 64; ++w2) S.u.m.lastw[w2][b] = 0;
         }
         PH(2);
         // ---- C: each position's frontier of (length, distance) pairs ----
@@ -1273,10 +1260,11 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
             dcb[q] = nf[q] > 1 ? S.dcst[dist_code(4u * (fb[q] >> 7))] : 0u;
             dcc[q] = nf[q] > 2 ? S.dcst[dist_code(4u * (fc[q] >> 7))] : 0u;
         }
+        __syncthreads();  // the wave tables are dead: the DP's costs take their memory
         for (int k = tid; k <= kSeg; k += kNT) {
             const int rem = max(0, send - c0 - k);
-            S.cost[1][k] = 32u * (uint32_t)rem;  // sweep 0's estimate beyond a thread's positions: 4 bits per value
-            if (k >= send - c0) S.cost[0][k] = 0;
+            S.u.m.cost[1][k] = (uint16_t)(32u * (uint32_t)rem);  // sweep 0's estimate beyond a thread's positions: 4 bits per value
+            if (k >= send - c0) S.u.m.cost[0][k] = 0;
         }
         __syncthreads();
         const int klo = kPer * tid;  // segment-relative
@@ -1284,7 +1272,7 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
             // own positions' costs in registers (indices are compile-time
             // after unrolling); lengths 3..10 branch-free, longer ones (rare)
             // read the other threads' costs from LDS
-            constexpr int kU = 10;             // lengths unrolled: kMinL .. kU
+            constexpr int kU = 6;              // lengths unrolled: kMinL .. kU (longer: only the entries' own lengths; the same ratio, tools/tlz_proto.c)
             constexpr int kW = kPer + kU - kPer;  // costs beyond this thread's positions within reach
             uint32_t lenr[kU + 1];
 #pragma unroll
@@ -1301,8 +1289,8 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
             }
 #pragma unroll 1
             for (int sw = 0; sw < kSweeps; ++sw) {
-                uint32_t* cur = S.cost[sw & 1];
-                const uint32_t* prv = S.cost[(sw + 1) & 1];
+                uint16_t* cur = S.u.m.cost[sw & 1];
+                const uint16_t* prv = S.u.m.cost[(sw + 1) & 1];
                 uint32_t pw[kW + 1];
 #pragma unroll
                 for (int u = 0; u <= kW; ++u) pw[u] = prv[min(klo + kPer + u, kSeg)];
@@ -1318,7 +1306,7 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
                         const uint32_t e = l <= La[q] ? 0u : l <= Lb[q] ? 1u : 2u;
                         const uint32_t dc = e == 0 ? dca[q] : e == 1 ? dcb[q] : dcc[q];
                         const uint32_t cc = lenr[l] + dc + CV(q + l);
-                        const bool take = l <= Lm[q] && cc < best;
+                        const bool take = l <= Lm[q] && lt16(cc, best);
                         best = take ? cc : best;
                         ch = take ? ((uint32_t)l | (e << 8)) : ch;
                     }
@@ -1329,7 +1317,7 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
                         if (l <= kU || l > Lm[q] || (e == 2 && nf[q] < 3) || (e == 1 && nf[q] < 2)) continue;
                         const uint32_t dc = e == 0 ? dca[q] : e == 1 ? dcb[q] : dcc[q];
                         const uint32_t cc = S.lenc[l] + dc + prv[klo + q + l];
-                        if (cc < best) { best = cc; ch = (uint32_t)l | ((uint32_t)e << 8); }
+                        if (lt16(cc, best)) { best = cc; ch = (uint32_t)l | ((uint32_t)e << 8); }
                     }
                     cr[q] = Lm[q] < 0 ? 0u : best;
                     chs[q] = ch;
@@ -1337,7 +1325,7 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
 #pragma unroll
                 for (int q = 0; q < kPer; ++q) {
                     if (Lm[q] < 0) continue;
-                    cur[klo + q] = cr[q];
+                    cur[klo + q] = (uint16_t)cr[q];
                     if (sw == kSweeps - 1) S.dec[klo + q] = (uint16_t)chs[q];
                 }
                 __syncthreads();
@@ -1411,6 +1399,19 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
         PH(7);
     }
 
+    {  // the member's raw CRC-32: every thread's pieces advanced to the member's end, XOR-ed
+        const uint32_t bl = 4u * (uint32_t)(ntok - ((nseg - 1) << kSegLog));  // bytes of the last segment
+        uint32_t r = nv_last ? crc_adv(crc_last, bl - 32u * (uint32_t)tid - 4u * (uint32_t)nv_last) : 0u;
+        if (nseg > 1) r ^= crc_adv(crc_acc, (uint32_t)(kSeg * 4) + bl - 32u * (uint32_t)(tid + 1));
+        for (int o = 32; o > 0; o >>= 1) r ^= (uint32_t)__shfl_xor((int)r, o, 64);
+        if (lane == 0) S.crc_w[wv] = r;
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t x = 0;
+            for (int w = 0; w < kNT / 64; ++w) x ^= S.crc_w[w];
+            S.crc_raw = x;
+        }
+    }
     // ---- G: the member's Huffman code (lengths limited to the inflate's table bits) ----
     const int ln = lane;
     if (wv == 0) {
