@@ -437,6 +437,15 @@ int ofl_gzip_member_index(const uint8_t* src, size_t n, int64_t* index, int64_t 
 size_t ofl_inflate_tlz_workspace_bytes(int64_t nmembers);
 int ofl_inflate_tlz(const uint8_t* src, const int64_t* index, int64_t nmembers, uint8_t* out, size_t out_cap, void* ws,
                     size_t ws_bytes, void* stream);
+/* ofl_inflate_tlz in pieces, so the pieces' H2D can overlap the inflate of
+ * earlier ones: _async launches members [first, first + count) of the index
+ * (no synchronisation; first == 0 also resets the status word), _wait
+ * synchronises the stream, checks every launched member and, if the TLZ
+ * decoder refused any, runs ofl_inflate_members over all nmembers. */
+int ofl_inflate_tlz_async(const uint8_t* src, const int64_t* index, int64_t first, int64_t count, uint8_t* out,
+                          size_t out_cap, void* ws, size_t ws_bytes, void* stream);
+int ofl_inflate_tlz_wait(const uint8_t* src, const int64_t* index, int64_t nmembers, uint8_t* out, size_t out_cap,
+                         void* ws, size_t ws_bytes, void* stream);
 int ofl_inflate_members(const uint8_t* src, const int64_t* index, int64_t nmembers, uint32_t max_isize, uint8_t* out,
                         size_t out_cap, void* ws, size_t ws_bytes, void* stream);
 /* Per-kernel timing of the gzip / inflate launches (bench.py): enable (1)

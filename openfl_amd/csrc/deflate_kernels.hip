@@ -873,7 +873,7 @@ __global__ __launch_bounds__(64, OFL_INF_WAVES) void k_inflate_members(InfArgs a
 // positions by a block scan, every value's source by pointer jumping in LDS
 // against the window of earlier values, then the values, CRC-32, ISIZE).
 namespace tlz {
-constexpr int kNT = 256;
+constexpr int kNT = 512;                           // encoder threads per member block
 constexpr int kSegLog = 11, kSeg = 1 << kSegLog;   // values per segment
 constexpr int kMemSeg = 64;
 constexpr int kMemTok = kSeg * kMemSeg;            // values per member
@@ -881,8 +881,9 @@ constexpr int kPer = kSeg / kNT;                   // positions per thread
 constexpr int kWin = 8192;                         // window, values (32 KiB)
 constexpr int kMaxL = 64, kMinL = 3;               // copy length, values
 constexpr int kCand = 16;                          // chain candidates per position
-constexpr int kBuckets = 1024;                     // 3-gram buckets: exact for values < 8, hashed above
-constexpr int kSweeps = 3;
+constexpr int kBuckets = 512;                      // 3-gram buckets: exact for values < 8, hashed (into the same) above
+constexpr int kBucketBits = 9;
+constexpr int kSweeps = 4;                         // DP sweeps (segments of kPer = 4 positions; tools/tlz_proto.c)
 constexpr int kRing = 16384;                       // value ring (ids), + 8 mirrored bytes
 constexpr int kLitMax = 11, kDistMax = 10;         // code length limits = the inflate's table bits
 constexpr int kHdrFixed = 28;                      // member header bytes before the segment table
@@ -899,6 +900,7 @@ struct EncSmem {
             union {
                 uint16_t lastw[kNT / 64][kBuckets];  // chains: per wave, this segment: position - range start + 1
                 uint16_t cost[2][kSeg + 8];        // then the DP's costs to the segment end, 1/8 bit, mod 2^16
+                uint32_t hw[kNT / 64][(kLit + kDist + 1) / 2];  // then per-wave symbol counts of the segment, two u16 per word
             };
         } m;
         struct {
@@ -907,7 +909,7 @@ struct EncSmem {
             uint8_t hb[kHdrFixed + 4 * kMemSeg];
         } f;
     } u;
-    uint32_t head[kBuckets];                       // last position + 1 per bucket (earlier segments)
+    uint32_t head[2][kBuckets];                    // last position + 1 per bucket (earlier segments); segment c reads [c & 1], writes [~c & 1]
     uint16_t dec[kSeg];                            // chosen op: length (0: literal) | frontier entry << 8
     uint16_t entry[kNT + 1];                       // parse: each thread's first position
     uint32_t hl[kLit], hd[kDist], hc[kCL];
@@ -948,12 +950,13 @@ DEVI uint32_t tk4r(const uint8_t* tok, int p) {
     const uint32_t* w = reinterpret_cast<const uint32_t*>(tok);
     return __builtin_amdgcn_alignbyte(w[(r >> 2) + 1], w[r >> 2], (uint32_t)(r & 3));
 }
-// 3-gram bucket: exact for values < 8 (512 buckets), hashed into the upper 512 above
+// 3-gram bucket: exact for values < 8 (512 buckets), hashed into the same
+// 512 above (a collision only adds chain entries the comparison rejects)
 DEVI int bucket(const uint8_t* tok, int p) {
     const uint32_t v = tk4r(tok, p) & 0xffffffu;
     const uint32_t a = v & 0xffu, b = (v >> 8) & 0xffu, c = v >> 16;
     if ((a | b | c) < 8u) return (int)(a | (b << 3) | (c << 6));
-    return 512 + (int)(((a | (b << 5) | (c << 10)) * 0x9E3779B1u) >> 23);
+    return (int)(((a | (b << 5) | (c << 10)) * 0x9E3779B1u) >> (32 - kBucketBits));
 }
 DEVI int match_len(const uint8_t* tok, int i, int j, int lim) {
     int L = 0;
@@ -1002,7 +1005,8 @@ DEVI void tlz_model(EncSmem& S, int tid, bool prior) {
     }
     __syncthreads();
 }
-// block-wide exclusive scan of v (returns the exclusive prefix; *total)
+// block-wide exclusive scan of v over NT threads (returns the exclusive prefix; *total)
+template <int NT>
 DEVI uint32_t block_scan(uint32_t v, uint32_t* scan, uint32_t* total) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     uint32_t inc = v;
@@ -1015,7 +1019,7 @@ DEVI uint32_t block_scan(uint32_t v, uint32_t* scan, uint32_t* total) {
     __syncthreads();
     uint32_t base = 0, tot = 0;
 #pragma unroll
-    for (int j = 0; j < kNT / 64; ++j) {
+    for (int j = 0; j < NT / 64; ++j) {
         base += j < w ? scan[j] : 0u;
         tot += scan[j];
     }
@@ -1024,7 +1028,7 @@ DEVI uint32_t block_scan(uint32_t v, uint32_t* scan, uint32_t* total) {
     return base + inc - v;
 }
 
-__global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_tlz_encode(EncArgs a) {  // 2 blocks per CU: 4 waves per SIMD
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     EncSmem& S = *reinterpret_cast<EncSmem*>(smem_raw);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1038,13 +1042,13 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
     const int ntok = (int)min<int64_t>(kMemTok, a.n - g0);
     const int nseg = (ntok + kSeg - 1) >> kSegLog;
     uint32_t* const ops = a.ops + (int64_t)blockIdx.x * a.ops_stride;
-    {
+    if (tid < 256) {
         uint32_t r = (uint32_t)tid;
         for (int k = 0; k < 8; ++k) r = (r & 1u) ? (r >> 1) ^ 0xEDB88320u : r >> 1;
         S.crct[0][tid] = r;
     }
     for (int i = tid; i < kBuckets; i += kNT) {
-        S.head[i] = 0;
+        S.head[0][i] = S.head[1][i] = 0;
 #pragma unroll
         for (int w = 0; w < kNT / 64; ++w) S.u.m.lastw[w][i] = 0;
     }
@@ -1054,8 +1058,10 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
     if (tid == 0) { S.totl = S.totd = 0; S.ops_n = 0; S.crc_raw = 0; S.bad = 0; }
     __syncthreads();
     for (int k = 1; k < 4; ++k) {
-        const uint32_t p = S.crct[k - 1][tid];
-        S.crct[k][tid] = (p >> 8) ^ S.crct[0][p & 0xffu];
+        if (tid < 256) {
+            const uint32_t p = S.crct[k - 1][tid];
+            S.crct[k][tid] = (p >> 8) ^ S.crct[0][p & 0xffu];
+        }
         __syncthreads();
     }
     tlz_model(S, tid, true);
@@ -1067,15 +1073,17 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
         const int send = min(c0 + kSeg, ntok);
         const int lo = c0 + kPer * tid;                 // this thread's positions [lo, lo + kPer)
         // ---- A: values -> ids in the ring, validity, raw CRC-32 ----
-        uint32_t idw0 = 0, idw1 = 0;                    // this thread's 8 ids, packed
+        uint32_t idw[kPer / 4] = {};                    // this thread's ids, packed 4 per word
         {
             const int nv = max(0, min(kPer, send - lo));
             float v[kPer];
             if (nv == kPer && a.aligned) {
                 const float4* p = reinterpret_cast<const float4*>(a.x + g0 + lo);
-                const float4 v0 = p[0], v1 = p[1];
-                v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w;
-                v[4] = v1.x; v[5] = v1.y; v[6] = v1.z; v[7] = v1.w;
+#pragma unroll
+                for (int u = 0; u < kPer / 4; ++u) {
+                    const float4 v0 = p[u];
+                    v[4 * u] = v0.x; v[4 * u + 1] = v0.y; v[4 * u + 2] = v0.z; v[4 * u + 3] = v0.w;
+                }
             } else {
 #pragma unroll
                 for (int q = 0; q < kPer; ++q) v[q] = q < nv ? a.x[g0 + lo + q] : 0.f;
@@ -1089,7 +1097,7 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
                     const uint32_t bits = __float_as_uint(v[q]);
                     if (!(t >= 0 && t < 32 && bits == __float_as_uint((float)t))) bad = true;
                     const uint32_t id = (t >= 0 && t < 32) ? (uint32_t)t : 0u;
-                    if (q < 4) idw0 |= id << (8 * q); else idw1 |= id << (8 * (q - 4));
+                    idw[q >> 2] |= id << (8 * (q & 3));
                     crc = crc4(S.crct, crc, bits);
                 }
             }
@@ -1098,8 +1106,11 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
 #pragma unroll
                 for (int w2 = 0; w2 < kNT / 64; ++w2) S.u.m.lastw[w2][b] = 0;
             const int r = lo & (kRing - 1);
-            *reinterpret_cast<uint2*>(&S.tok[r]) = make_uint2(idw0, idw1);
-            if (r < 32) *reinterpret_cast<uint2*>(&S.tok[kRing + r]) = make_uint2(idw0, idw1);
+#pragma unroll
+            for (int u = 0; u < kPer / 4; ++u) {
+                reinterpret_cast<uint32_t*>(S.tok)[(r >> 2) + u] = idw[u];
+                if (r + 4 * u < 32) reinterpret_cast<uint32_t*>(S.tok)[((kRing + r) >> 2) + u] = idw[u];
+            }
             // raw CRC-32 by Horner per thread: acc covers this thread's pieces
             // of the full segments so far (each advanced by the 8 KiB of every
             // later segment); the last segment's piece and the combination
@@ -1146,6 +1157,9 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
         }
         PH(12);
         __syncthreads();
+        // pending positions: the last occurrence in an earlier wave's part,
+        // else before the segment; meanwhile the heads of the next segment
+        const uint32_t* head = S.head[c & 1];
         for (int p0 = w_lo; p0 < w_hi; p0 += 64) {
             const int p = p0 + lane;
             if (p < w_hi && S.u.m.prev[pslot(p)] == kPending) {
@@ -1157,18 +1171,19 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
                     if (lw) { d = (uint32_t)(p - (s_ins + (int)lw - 1)); found = true; }
                 }
                 if (!found) {
-                    const uint32_t h = S.head[bk];
+                    const uint32_t h = head[bk];
                     if (h && p - (int)(h - 1u) <= kWin) d = (uint32_t)(p - (int)(h - 1u));
                 }
                 S.u.m.prev[pslot(p)] = (uint16_t)d;
             }
         }
-        __syncthreads();
-        for (int b = tid; b < kBuckets; b += kNT) {  // heads
+        for (int b = tid; b < kBuckets; b += kNT) {
+            uint32_t h = head[b];
             for (int w2 = kNT / 64 - 1; w2 >= 0; --w2) {
                 const uint32_t lw = S.u.m.lastw[w2][b];
-                if (lw) { S.head[b] = (uint32_t)s_ins + lw; break; }
+                if (lw) { h = (uint32_t)s_ins + lw; break; }
             }
+            S.head[(c + 1) & 1][b] = h;
         }
         PH(2);
         // ---- C: each position's frontier of (length, distance) pairs ----
@@ -1279,13 +1294,24 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
             for (int l = kMinL; l <= kU; ++l) lenr[l] = S.lenc[l];
             uint32_t litr[kPer];
             int La[kPer], Lb[kPer], Lm[kPer];
+            // lengths above kU: only each frontier entry's own length; its
+            // length + distance cost is the same in every sweep
+            int el[kPer][3];
+            uint32_t ec[kPer][3];
 #pragma unroll
             for (int q = 0; q < kPer; ++q) {
-                litr[q] = S.litc[((q < 4 ? idw0 : idw1) >> (8 * (q & 3))) & 0xffu];
+                litr[q] = S.litc[(idw[q >> 2] >> (8 * (q & 3))) & 0xffu];
                 La[q] = (int)(fa[q] & 127u);
                 Lb[q] = (int)(fb[q] & 127u);
                 Lm[q] = nf[q] == 0 ? 0 : (int)((nf[q] == 1 ? fa[q] : nf[q] == 2 ? fb[q] : fc[q]) & 127u);
                 if (c0 + klo + q >= send) Lm[q] = -1;  // no such position
+#pragma unroll
+                for (int e = 0; e < 3; ++e) {
+                    const int l = e == 0 ? La[q] : e == 1 ? Lb[q] : Lm[q];
+                    const bool use = l > kU && l <= Lm[q] && nf[q] > e;
+                    el[q][e] = use ? l : 0;
+                    ec[q][e] = use ? S.lenc[l] + (e == 0 ? dca[q] : e == 1 ? dcb[q] : dcc[q]) : 0u;
+                }
             }
 #pragma unroll 1
             for (int sw = 0; sw < kSweeps; ++sw) {
@@ -1294,6 +1320,11 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
                 uint32_t pw[kW + 1];
 #pragma unroll
                 for (int u = 0; u <= kW; ++u) pw[u] = prv[min(klo + kPer + u, kSeg)];
+                uint32_t ev[kPer][3];  // the costs after each long entry (beyond this thread's positions: previous sweep)
+#pragma unroll
+                for (int q = 0; q < kPer; ++q)
+#pragma unroll
+                    for (int e = 0; e < 3; ++e) ev[q][e] = prv[min(klo + q + el[q][e], kSeg)];
                 uint32_t cr[kPer];
                 uint32_t chs[kPer];
 #pragma unroll
@@ -1310,14 +1341,12 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
                         best = take ? cc : best;
                         ch = take ? ((uint32_t)l | (e << 8)) : ch;
                     }
-                    // longer lengths: only each frontier entry's own (full) length
 #pragma unroll
                     for (int e = 0; e < 3; ++e) {
-                        const int l = e == 0 ? La[q] : e == 1 ? Lb[q] : Lm[q];
-                        if (l <= kU || l > Lm[q] || (e == 2 && nf[q] < 3) || (e == 1 && nf[q] < 2)) continue;
-                        const uint32_t dc = e == 0 ? dca[q] : e == 1 ? dcb[q] : dcc[q];
-                        const uint32_t cc = S.lenc[l] + dc + prv[klo + q + l];
-                        if (lt16(cc, best)) { best = cc; ch = (uint32_t)l | ((uint32_t)e << 8); }
+                        const uint32_t cc = ec[q][e] + ev[q][e];
+                        const bool take = el[q][e] != 0 && lt16(cc, best);
+                        best = take ? cc : best;
+                        ch = take ? ((uint32_t)el[q][e] | ((uint32_t)e << 8)) : ch;
                     }
                     cr[q] = Lm[q] < 0 ? 0u : best;
                     chs[q] = ch;
@@ -1334,6 +1363,7 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
         PH(4);
         // ---- E: the DP's path from the segment start: Jacobi rounds ----
         auto nxt = [&](int p) -> int { const int l = S.dec[p - c0] & 0xff; return p + (l ? l : 1); };
+        for (int i = tid; i < (kNT / 64) * ((kLit + kDist + 1) / 2); i += kNT) (&S.u.m.hw[0][0])[i] = 0;  // F's tables (the DP's costs are dead)
         {
             int p = tid == 0 ? c0 : max(c0, lo - kMaxL);
             while (p < lo && p < send) p = nxt(p);
@@ -1357,11 +1387,14 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
             for (int p = c0 + S.entry[tid]; p < lo + kPer && p < send; p = nxt(p)) opm |= 1u << (p - lo);
             PH(13);
             uint32_t tot;
-            const uint32_t off = block_scan((uint32_t)__popc(opm), S.scan, &tot);
+            const uint32_t off = block_scan<kNT>((uint32_t)__popc(opm), S.scan, &tot);
             PH(14);
             const uint32_t base = S.ops_n;
             uint32_t k = base + off;
             uint32_t nl = 0, nd = 0;
+            // symbol counts into this wave's own table (same-wave atomics only)
+            uint32_t* const hw = S.u.m.hw[wv];
+            auto cnt = [&](int sym) { atomicAdd(&hw[sym >> 1], (sym & 1) ? 0x10000u : 1u); };
 #pragma unroll
             for (int q = 0; q < kPer; ++q) {
                 if (!((opm >> q) & 1u)) continue;
@@ -1369,40 +1402,49 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
                 const uint32_t l = dq & 0xffu;
                 uint32_t rec;
                 if (l == 0) {
-                    const uint32_t id = ((q < 4 ? idw0 : idw1) >> (8 * (q & 3))) & 0xffu;
+                    const uint32_t id = (idw[q >> 2] >> (8 * (q & 3))) & 0xffu;
                     rec = 0x80000000u | id;
                     const uint32_t b = __float_as_uint((float)id);
 #pragma unroll
-                    for (int y = 0; y < 4; ++y) atomicAdd(&S.hl[(b >> (8 * y)) & 0xffu], 1u);
+                    for (int y = 0; y < 4; ++y) cnt((int)((b >> (8 * y)) & 0xffu));
                     nl += 4;
                 } else {
                     const uint32_t e = dq >> 8;
                     const uint32_t ent = e == 0 ? fa[q] : e == 1 ? fb[q] : fc[q];
                     const uint32_t d = ent >> 7;
                     rec = l | (d << 7);
-                    atomicAdd(&S.hl[257 + len_code(4u * l)], 1u);
-                    atomicAdd(&S.hd[dist_code(4u * d)], 1u);
+                    cnt(257 + len_code(4u * l));
+                    cnt(kLit + dist_code(4u * d));
                     nl += 1;
                     nd += 1;
                 }
                 ops[k++] = rec;
             }
-            if (nl) atomicAdd(&S.totl, nl);
-            if (nd) atomicAdd(&S.totd, nd);
+            for (int o = 32; o > 0; o >>= 1) {
+                nl += (uint32_t)__shfl_xor((int)nl, o, 64);
+                nd += (uint32_t)__shfl_xor((int)nd, o, 64);
+            }
+            if (lane == 0) { atomicAdd(&S.totl, nl); atomicAdd(&S.totd, nd); }
             if (tid == 0) S.segop[c] = base;
             __syncthreads();
             if (tid == 0) S.ops_n = base + tot;
+            for (int sym = tid; sym < kLit + kDist; sym += kNT) {  // merge the waves' counts
+                uint32_t v = 0;
+#pragma unroll
+                for (int w = 0; w < kNT / 64; ++w) v += (S.u.m.hw[w][sym >> 1] >> (16 * (sym & 1))) & 0xffffu;
+                if (sym < kLit) S.hl[sym] += v; else S.hd[sym - kLit] += v;
+            }
         }
         PH(6);
-        if (c + 1 < nseg) tlz_model(S, tid, false);  // its barriers also order ops_n and the histograms
-        else __syncthreads();
+        __syncthreads();  // the merged counts
+        if (c + 1 < nseg) tlz_model(S, tid, false);
         PH(7);
     }
 
     {  // the member's raw CRC-32: every thread's pieces advanced to the member's end, XOR-ed
         const uint32_t bl = 4u * (uint32_t)(ntok - ((nseg - 1) << kSegLog));  // bytes of the last segment
-        uint32_t r = nv_last ? crc_adv(crc_last, bl - 32u * (uint32_t)tid - 4u * (uint32_t)nv_last) : 0u;
-        if (nseg > 1) r ^= crc_adv(crc_acc, (uint32_t)(kSeg * 4) + bl - 32u * (uint32_t)(tid + 1));
+        uint32_t r = nv_last ? crc_adv(crc_last, bl - 4u * kPer * (uint32_t)tid - 4u * (uint32_t)nv_last) : 0u;
+        if (nseg > 1) r ^= crc_adv(crc_acc, (uint32_t)(kSeg * 4) + bl - 4u * kPer * (uint32_t)(tid + 1));
         for (int o = 32; o > 0; o >>= 1) r ^= (uint32_t)__shfl_xor((int)r, o, 64);
         if (lane == 0) S.crc_w[wv] = r;
         __syncthreads();
@@ -1529,7 +1571,7 @@ __global__ __launch_bounds__(kNT, 2) void k_tlz_encode(EncArgs a) {
     uint32_t mine = 0;
     for (uint32_t o = o_lo; o < o_hi; ++o) mine += op_bits(ops[o]);
     uint32_t tot;
-    const uint32_t pos0 = H + block_scan(mine, S.scan, &tot);
+    const uint32_t pos0 = H + block_scan<kNT>(mine, S.scan, &tot);
     {
         int sidx = 0;
         while (sidx < nseg && S.segop[sidx] < o_lo) ++sidx;
@@ -1859,16 +1901,17 @@ __global__ __launch_bounds__(64) void k_tlz_ops(DecArgs a) {
 // K2: one block per member; per segment: op positions (block scan), each
 // value's source (pointer jumping in LDS; sources before the segment are in
 // the value ring), the values as float32, CRC-32 of the member, ISIZE.
+constexpr int kRNT = 256, kRPer = kSeg / kRNT;     // resolve: threads per member block, values per thread
 struct ResSmem {
     uint8_t v[kRing];              // ids by member position (ring)
     uint32_t opr[kSeg];            // the segment's op records
     uint16_t e[kSeg];              // 0x8000 | id (resolved) or the distance to the source
     uint32_t crct[4][256];
-    uint32_t scan[kNT / 64];
-    uint32_t crc_w[kNT / 64];
+    uint32_t scan[kRNT / 64];
+    uint32_t crc_w[kRNT / 64];
     uint32_t crc_raw;
 };
-__global__ __launch_bounds__(kNT) void k_tlz_resolve(DecArgs a) {
+__global__ __launch_bounds__(kRNT) void k_tlz_resolve(DecArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     ResSmem& S = *reinterpret_cast<ResSmem*>(smem_raw);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1899,14 +1942,14 @@ __global__ __launch_bounds__(kNT) void k_tlz_resolve(DecArgs a) {
         const uint32_t nops = a.cnt[m * kMemSeg + s];
         float* const yo = reinterpret_cast<float*>(a.out + out_off) + c0;
         const uint32_t* opi = reinterpret_cast<const uint32_t*>(yo);
-        for (uint32_t k = tid; k < nops; k += kNT) S.opr[k] = opi[k];
+        for (uint32_t k = tid; k < nops; k += kRNT) S.opr[k] = opi[k];
         __syncthreads();
         // positions: each thread a contiguous run of ops
-        const uint32_t o_lo = nops * tid / kNT, o_hi = nops * (tid + 1) / kNT;
+        const uint32_t o_lo = nops * tid / kRNT, o_hi = nops * (tid + 1) / kRNT;
         uint32_t run = 0;
         for (uint32_t o = o_lo; o < o_hi; ++o) { const uint32_t r = S.opr[o]; run += (r >> 31) ? 1u : (r & 127u); }
         uint32_t tot;
-        uint32_t p = block_scan(run, S.scan, &tot);
+        uint32_t p = block_scan<kRNT>(run, S.scan, &tot);
         if (tot != (uint32_t)T) { bad = kInfCorrupt; break; }  // block-uniform
         for (uint32_t o = o_lo; o < o_hi; ++o) {
             const uint32_t r = S.opr[o];
@@ -1924,7 +1967,7 @@ __global__ __launch_bounds__(kNT) void k_tlz_resolve(DecArgs a) {
 #pragma unroll 1
         for (;;) {
             int pend = 0;
-            for (int k = tid; k < T; k += kNT) {
+            for (int k = tid; k < T; k += kRNT) {
                 const uint32_t e = S.e[k];
                 if (e & 0x8000u) continue;
                 const int src = k - (int)e;
@@ -1941,12 +1984,12 @@ __global__ __launch_bounds__(kNT) void k_tlz_resolve(DecArgs a) {
         }
         // values: ring, output (float32), raw CRC-32
         {
-            const int k0 = kPer * tid;
-            const int nv = max(0, min(kPer, T - k0));
+            const int k0 = kRPer * tid;
+            const int nv = max(0, min(kRPer, T - k0));
             uint32_t crc = 0;
-            float f[kPer];
+            float f[kRPer];
 #pragma unroll
-            for (int q = 0; q < kPer; ++q) {
+            for (int q = 0; q < kRPer; ++q) {
                 const uint32_t id = q < nv ? (uint32_t)(S.e[k0 + q] & 31u) : 0u;
                 f[q] = (float)id;
                 if (q < nv) {
@@ -1954,10 +1997,10 @@ __global__ __launch_bounds__(kNT) void k_tlz_resolve(DecArgs a) {
                     crc = crc4(S.crct, crc, __float_as_uint(f[q]));
                 }
             }
-            if (nv == kPer) {
+            if (nv == kRPer && (reinterpret_cast<uintptr_t>(yo + k0) & 15u) == 0) {
                 float4* y4 = reinterpret_cast<float4*>(yo + k0);
-                y4[0] = make_float4(f[0], f[1], f[2], f[3]);
-                y4[1] = make_float4(f[4], f[5], f[6], f[7]);
+#pragma unroll
+                for (int u = 0; u < kRPer / 4; ++u) y4[u] = make_float4(f[4 * u], f[4 * u + 1], f[4 * u + 2], f[4 * u + 3]);
             } else {
                 for (int q = 0; q < nv; ++q) yo[k0 + q] = f[q];
             }
@@ -1982,10 +2025,10 @@ __global__ __launch_bounds__(kNT) void k_tlz_resolve(DecArgs a) {
         if (tid == 0) {
             uint32_t raw = 0;
             if (T == kSeg) {
-                for (int w = 0; w < kNT / 64; ++w) raw = crc_adv_pow2(raw, kSegLog) ^ S.crc_w[w];
+                for (int w = 0; w < kRNT / 64; ++w) raw = crc_adv_pow2(raw, kSegLog) ^ S.crc_w[w];
                 S.crc_raw = crc_adv_pow2(S.crc_raw, kSegLog + 2) ^ raw;
             } else {
-                for (int w = 0; w < kNT / 64; ++w) raw ^= S.crc_w[w];
+                for (int w = 0; w < kRNT / 64; ++w) raw ^= S.crc_w[w];
                 S.crc_raw = crc_adv(S.crc_raw, 4u * (uint32_t)T) ^ raw;
             }
         }
@@ -2046,6 +2089,21 @@ void gzprof_end(hipStream_t st, const char* name) {
     std::lock_guard<std::mutex> g(g_prof_m);
     g_prof_pending.push_back({name, g_prof_a, b});
     g_prof_a = nullptr;
+}
+
+// the device's side stream for the gzip's pack launches (created once per
+// device; the pack of batch k overlaps the encode of batch k + 1)
+hipError_t gz_side_stream(hipStream_t* out) {
+    static std::mutex m;
+    static hipStream_t side[64] = {};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    std::lock_guard<std::mutex> g(m);
+    if (!side[dev]) e = hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking);
+    *out = side[dev];
+    return e;
 }
 
 // raw CRC-32 advance matrices for 2^k zero bytes
@@ -2214,9 +2272,10 @@ TlzLayout tlz_layout(int64_t n) {
 
 size_t ofl_gzip_ranks_workspace_bytes(int64_t n) {
     const TlzLayout L = tlz_layout(n);
-    // slots | packed (pageable output) | ops | sizes | offsets | running | bad
-    return 2 * (size_t)L.batch * L.slot + 4 * (size_t)L.batch * L.ops_stride + 4 * (size_t)L.batch +
-           8 * (size_t)(L.batch + 1) + 1024;
+    // slots x 2 (the second is the pageable path's staging) | ops | sizes x 2 |
+    // offsets x 2 | running | bad
+    return 2 * (size_t)L.batch * L.slot + 4 * (size_t)L.batch * L.ops_stride + 8 * (size_t)L.batch +
+           16 * (size_t)(L.batch + 1) + 1024;
 }
 
 size_t ofl_gzip_ranks_bound(int64_t n) {
@@ -2240,12 +2299,20 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
     hipStream_t st = static_cast<hipStream_t>(stream);
     const TlzLayout L = tlz_layout(n);
     char* w = static_cast<char*>(ws);
-    uint8_t* slots = reinterpret_cast<uint8_t*>(w);
-    uint8_t* packed = slots + (size_t)L.batch * L.slot;
-    uint32_t* ops = reinterpret_cast<uint32_t*>(packed + (size_t)L.batch * L.slot);
-    uint32_t* sizes = ops + (size_t)L.batch * L.ops_stride;
-    uint64_t* off = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(sizes) + ((4 * (size_t)L.batch + 7) & ~(size_t)7));
-    uint64_t* running = off + L.batch + 1;
+    uint8_t* slots2[2];                              // double-buffered member slots (pinned output path)
+    slots2[0] = reinterpret_cast<uint8_t*>(w);
+    slots2[1] = slots2[0] + (size_t)L.batch * L.slot;
+    uint8_t* slots = slots2[0];
+    uint8_t* packed = slots2[1];                     // the pageable path's staging
+    uint32_t* ops = reinterpret_cast<uint32_t*>(slots2[1] + (size_t)L.batch * L.slot);
+    uint32_t* sizes2[2];
+    sizes2[0] = ops + (size_t)L.batch * L.ops_stride;
+    sizes2[1] = sizes2[0] + L.batch;
+    uint32_t* sizes = sizes2[0];
+    uint64_t* off = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(sizes2[1] + L.batch) + 8 -
+                                                (reinterpret_cast<uintptr_t>(sizes2[1] + L.batch) & 7u));
+    uint64_t* off2[2] = {off, off + L.batch + 1};
+    uint64_t* running = off2[1] + L.batch + 1;
     int* bad = reinterpret_cast<int*>(running + 1);
     GZHIP(hipMemsetAsync(bad, 0, sizeof(int), st));
     // out is mapped pinned host memory (e.g. torch pin_memory): the pack
@@ -2267,8 +2334,8 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
         GZHIP(hipMalloc(&d_ph, 8 * gz::tlz::kEncPhases));
         GZHIP(hipMemsetAsync(d_ph, 0, 8 * gz::tlz::kEncPhases, st));
     }
-    auto enc = [&](int64_t c0, int nb) {
-        gz::tlz::EncArgs a{x, n, c0, slots, ops, sizes, bad, (uint32_t)L.slot, (uint32_t)L.ops_stride, aligned,
+    auto enc = [&](int64_t c0, int nb, uint8_t* sl, uint32_t* sz) {
+        gz::tlz::EncArgs a{x, n, c0, sl, ops, sz, bad, (uint32_t)L.slot, (uint32_t)L.ops_stride, aligned,
                            c0 == 0 ? d_ph : nullptr};
         gzprof_begin(st);
         hipLaunchKernelGGL(gz::tlz::k_tlz_encode, dim3(nb), dim3(gz::tlz::kNT), sizeof(gz::tlz::EncSmem), st, a);
@@ -2276,29 +2343,56 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
     };
     size_t total = 0;
     if (dout) {
-        GZHIP(hipMemsetAsync(running, 0, sizeof(uint64_t), st));
-        for (int64_t c0 = 0; c0 < L.members; c0 += L.batch) {
-            const int nb = (int)std::min<int64_t>(L.batch, L.members - c0);
-            enc(c0, nb);
-            hipLaunchKernelGGL(gz::k_gzip_scan, dim3(1), dim3(1024), 0, st, sizes, nb, off, running,
-                               (uint64_t)out_cap, bad);
-            gzprof_begin(st);
-            hipLaunchKernelGGL(gz::k_gzip_pack, dim3(nb), dim3(256), 0, st, slots, (uint64_t)L.slot, sizes, off, dout);
-            gzprof_end(st, "k_gzip_pack");
-            GZHIP(hipGetLastError());
+        // batch k encodes on the caller's stream into slots[k & 1]; its scan +
+        // pack run on the side stream, overlapping the encode of batch k + 1
+        hipStream_t sd = nullptr;
+        GZHIP(gz_side_stream(&sd));
+        const int64_t nbatch = (L.members + L.batch - 1) / L.batch;
+        hipEvent_t ev_enc[2] = {}, ev_pack[2] = {};
+        for (int i = 0; i < 2; ++i) {
+            GZHIP(hipEventCreateWithFlags(&ev_enc[i], hipEventDisableTiming));
+            GZHIP(hipEventCreateWithFlags(&ev_pack[i], hipEventDisableTiming));
         }
+        GZHIP(hipMemsetAsync(running, 0, sizeof(uint64_t), st));
+        GZHIP(hipEventRecord(ev_pack[1], st));  // orders the side stream after the memsets
+        GZHIP(hipStreamWaitEvent(sd, ev_pack[1], 0));
+        int err = 0;
+        for (int64_t k = 0; k < nbatch && !err; ++k) {
+            const int64_t c0 = k * L.batch;
+            const int b = (int)(k & 1);
+            const int nb = (int)std::min<int64_t>(L.batch, L.members - c0);
+            if (k >= 2) GZHIP(hipStreamWaitEvent(st, ev_pack[b], 0));  // slots[b] packed
+            enc(c0, nb, slots2[b], sizes2[b]);
+            GZHIP(hipEventRecord(ev_enc[b], st));
+            GZHIP(hipStreamWaitEvent(sd, ev_enc[b], 0));
+            hipLaunchKernelGGL(gz::k_gzip_scan, dim3(1), dim3(1024), 0, sd, sizes2[b], nb, off2[b], running,
+                               (uint64_t)out_cap, bad);
+            gzprof_begin(sd);
+            hipLaunchKernelGGL(gz::k_gzip_pack, dim3(nb), dim3(256), 0, sd, slots2[b], (uint64_t)L.slot, sizes2[b],
+                               off2[b], dout);
+            gzprof_end(sd, "k_gzip_pack");
+            GZHIP(hipEventRecord(ev_pack[b], sd));
+            if (hipGetLastError() != hipSuccess) err = 1;
+        }
+        GZHIP(hipEventRecord(ev_pack[0], sd));
+        GZHIP(hipStreamWaitEvent(st, ev_pack[0], 0));  // the caller's stream sees every pack
         uint64_t tot = 0;
         int badh = 0;
         GZHIP(hipMemcpyAsync(&tot, running, 8, hipMemcpyDeviceToHost, st));
         GZHIP(hipMemcpyAsync(&badh, bad, sizeof(int), hipMemcpyDeviceToHost, st));
         GZHIP(hipStreamSynchronize(st));
+        for (int i = 0; i < 2; ++i) {
+            (void)hipEventDestroy(ev_enc[i]);
+            (void)hipEventDestroy(ev_pack[i]);
+        }
+        if (err) return gzfail(OFL_EHIP, "gzip ranks: kernel launch failed");
         if (badh & 1) return gzfail(OFL_EINVAL, "gzip ranks: values must be float32 integers 0..31");
         if (badh & 2) return gzfail(OFL_ESPACE, "gzip ranks: output buffer too small");
         total = tot;
     }
     for (int64_t c0 = 0; !dout && c0 < L.members; c0 += L.batch) {
         const int nb = (int)std::min<int64_t>(L.batch, L.members - c0);
-        enc(c0, nb);
+        enc(c0, nb, slots, sizes);
         hipLaunchKernelGGL(gz::k_gzip_scan, dim3(1), dim3(1024), 0, st, sizes, nb, off, (uint64_t*)nullptr,
                            ~0ull, bad);
         hipLaunchKernelGGL(gz::k_gzip_pack, dim3(nb), dim3(256), 0, st, slots, (uint64_t)L.slot, sizes, off, packed);
@@ -2401,11 +2495,10 @@ size_t ofl_inflate_tlz_workspace_bytes(int64_t nmembers) {
     return 256 + 4 * (size_t)std::max<int64_t>(nmembers, 1) * gz::tlz::kMemSeg;
 }
 
-int ofl_inflate_tlz(const uint8_t* src, const int64_t* index, int64_t nmembers, uint8_t* out, size_t out_cap, void* ws,
-                    size_t ws_bytes, void* stream) {
-    if (nmembers < 0 || (nmembers && (!src || !index || !out))) return gzfail(OFL_EINVAL, "inflate: null argument");
-    if (!ws || ws_bytes < ofl_inflate_tlz_workspace_bytes(nmembers)) return gzfail(OFL_ESPACE, "inflate: workspace too small");
-    if (nmembers == 0) return OFL_OK;
+int ofl_inflate_tlz_async(const uint8_t* src, const int64_t* index, int64_t first, int64_t count, uint8_t* out,
+                          size_t out_cap, void* ws, size_t ws_bytes, void* stream) {
+    if (first < 0 || count < 0 || (count && (!src || !index || !out))) return gzfail(OFL_EINVAL, "inflate: null argument");
+    if (!ws || ws_bytes < ofl_inflate_tlz_workspace_bytes(first + count)) return gzfail(OFL_ESPACE, "inflate: workspace too small");
     GZHIP(ofl_util::per_device_once([] {
         uint32_t m[32][32];
         crc_matrices(m);
@@ -2413,16 +2506,26 @@ int ofl_inflate_tlz(const uint8_t* src, const int64_t* index, int64_t nmembers, 
     }));
     hipStream_t st = static_cast<hipStream_t>(stream);
     int* status = static_cast<int*>(ws);
-    uint32_t* cnt = reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + 256);
-    GZHIP(hipMemsetAsync(status, 0, sizeof(int), st));
-    gz::tlz::DecArgs a{src, index, nmembers, out, (uint64_t)out_cap, cnt, status};
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + 256) + first * gz::tlz::kMemSeg;
+    if (first == 0) GZHIP(hipMemsetAsync(status, 0, sizeof(int), st));
+    if (count == 0) return OFL_OK;
+    gz::tlz::DecArgs a{src, index + 4 * first, count, out, (uint64_t)out_cap, cnt, status};
     gzprof_begin(st);
-    hipLaunchKernelGGL(gz::tlz::k_tlz_ops, dim3((unsigned)nmembers), dim3(64), sizeof(gz::tlz::DecSmem), st, a);
+    hipLaunchKernelGGL(gz::tlz::k_tlz_ops, dim3((unsigned)count), dim3(64), sizeof(gz::tlz::DecSmem), st, a);
     gzprof_end(st, "tlz::k_tlz_ops");
     gzprof_begin(st);
-    hipLaunchKernelGGL(gz::tlz::k_tlz_resolve, dim3((unsigned)nmembers), dim3(gz::tlz::kNT), sizeof(gz::tlz::ResSmem), st, a);
+    hipLaunchKernelGGL(gz::tlz::k_tlz_resolve, dim3((unsigned)count), dim3(gz::tlz::kRNT), sizeof(gz::tlz::ResSmem), st, a);
     gzprof_end(st, "tlz::k_tlz_resolve");
     GZHIP(hipGetLastError());
+    return OFL_OK;
+}
+
+int ofl_inflate_tlz_wait(const uint8_t* src, const int64_t* index, int64_t nmembers, uint8_t* out, size_t out_cap,
+                         void* ws, size_t ws_bytes, void* stream) {
+    if (nmembers == 0) return OFL_OK;
+    if (!ws || ws_bytes < ofl_inflate_tlz_workspace_bytes(nmembers)) return gzfail(OFL_ESPACE, "inflate: workspace too small");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    int* status = static_cast<int*>(ws);
     int h = 0;
     GZHIP(hipMemcpyAsync(&h, status, sizeof(int), hipMemcpyDeviceToHost, st));
     GZHIP(hipStreamSynchronize(st));
@@ -2437,6 +2540,13 @@ int ofl_inflate_tlz(const uint8_t* src, const int64_t* index, int64_t nmembers, 
         return ofl_inflate_members(src, index, nmembers, mx, out, out_cap, ws, ws_bytes, stream);
     }
     return OFL_OK;
+}
+
+int ofl_inflate_tlz(const uint8_t* src, const int64_t* index, int64_t nmembers, uint8_t* out, size_t out_cap, void* ws,
+                    size_t ws_bytes, void* stream) {
+    if (nmembers < 0 || (nmembers && (!src || !index || !out))) return gzfail(OFL_EINVAL, "inflate: null argument");
+    if (int rc = ofl_inflate_tlz_async(src, index, 0, nmembers, out, out_cap, ws, ws_bytes, stream)) return rc;
+    return ofl_inflate_tlz_wait(src, index, nmembers, out, out_cap, ws, ws_bytes, stream);
 }
 
 int ofl_gzip_profile(int enable) {

@@ -383,17 +383,31 @@ def gunzip_device(data, out):
             with torch.cuda.device(dev):
                 _lib.check(L.ofl_copy_h2d_async(d_in.data_ptr(), src.ctypes.data, src.size,
                                                 caller_stream.cuda_stream))
-    copy = _h2d_pool().submit(h2d)
     # one pass over the headers: a member takes >= 26 bytes, so n // 26 + 1
     # entries always suffice (untouched pages of the array cost nothing)
     cap = src.size // 26 + 1
     idx = np.empty((cap, 4), np.int64)
-    try:
-        rc = L.ofl_gzip_member_index(src.ctypes.data if src.size else None, src.size, idx.ctypes.data, cap,
-                                     ctypes.byref(nm), ctypes.byref(tot), ctypes.byref(mx), ctypes.byref(tl)) \
-            if src.size else _lib.OFL_EFORMAT
-    finally:
-        copy.result()
+    if src.size >= _PIPE_MIN:
+        # large streams: index first (a few ms at most), so a TLZ stream's H2D
+        # can go in member-aligned pieces that overlap the inflate
+        rc = L.ofl_gzip_member_index(src.ctypes.data, src.size, idx.ctypes.data, cap, ctypes.byref(nm),
+                                     ctypes.byref(tot), ctypes.byref(mx), ctypes.byref(tl))
+        if rc == _lib.OFL_OK and tl.value and nm.value >= 2:
+            if tot.value > out.numel():
+                raise _lib.CodecError("gunzip_device: output buffer too small")
+            _pipelined_inflate(L, src, idx[:nm.value], d_in, out, dev, caller_stream)
+            _trim_bufs()
+            return out[:tot.value]
+        if rc != _lib.OFL_EFORMAT:
+            _h2d_pool().submit(h2d).result()
+    else:
+        copy = _h2d_pool().submit(h2d)
+        try:
+            rc = L.ofl_gzip_member_index(src.ctypes.data if src.size else None, src.size, idx.ctypes.data, cap,
+                                         ctypes.byref(nm), ctypes.byref(tot), ctypes.byref(mx), ctypes.byref(tl)) \
+                if src.size else _lib.OFL_EFORMAT
+        finally:
+            copy.result()
     if rc == _lib.OFL_EFORMAT:
         raw = np.frombuffer(gzip.decompress(bytes(data)), np.uint8)
         if raw.size > out.numel():
@@ -417,6 +431,56 @@ def gunzip_device(data, out):
                                               out.numel(), ws.data_ptr(), ws.numel(), _stream(dev)))
     _trim_bufs()
     return out[:tot.value]
+
+
+_PIPE_MIN = 16 << 20     # streams from this size inflate in pieces behind their H2D
+_PIPE_PIECES = 6
+_copy_streams = {}
+
+
+def _pipelined_inflate(L, src, idx, d_in, out, dev, caller_stream):
+    """TLZ inflate of a large stream in member-aligned pieces: a pool thread
+    copies piece k to the device on a copy stream while the caller's stream
+    inflates the pieces before it (ofl_inflate_tlz_async), then one
+    synchronisation and status check (ofl_inflate_tlz_wait)."""
+    nmem = idx.shape[0]
+    d_idx = _buf(dev, "gz_idx", max(idx.nbytes, 8))
+    d_idx[:idx.nbytes].copy_(torch.from_numpy(idx.view(np.uint8).reshape(-1)))
+    ws = _buf(dev, "gz_status", int(L.ofl_inflate_tlz_workspace_bytes(nmem)))
+    cut = np.linspace(0, nmem, min(_PIPE_PIECES, nmem) + 1).astype(np.int64)
+    ends = (idx[:, 0] + (idx[:, 1] & ((1 << 62) - 1)) + 8).astype(np.int64)  # member end: data + trailer
+    with _pool_lock:
+        cs = _copy_streams.get(dev.index)
+        if cs is None:
+            cs = _copy_streams[dev.index] = torch.cuda.Stream(device=dev)
+    events = [torch.cuda.Event() for _ in range(len(cut) - 1)]
+
+    def copier():
+        with torch.cuda.device(dev):
+            start = 0
+            for k in range(len(cut) - 1):
+                stop = int(ends[cut[k + 1] - 1]) if k + 2 < len(cut) else src.size
+                _lib.check(L.ofl_copy_h2d_async(d_in.data_ptr() + start, src.ctypes.data + start, stop - start,
+                                                cs.cuda_stream))
+                events[k].record(cs)
+                start = stop
+                ready[k].set()
+    import threading as _th
+    ready = [_th.Event() for _ in events]
+    job = _h2d_pool().submit(copier)
+    try:
+        for k in range(len(cut) - 1):
+            while not ready[k].wait(0.001):
+                if job.done():
+                    job.result()  # raises the copier's error
+            caller_stream.wait_event(events[k])
+            _lib.check_gzip(L.ofl_inflate_tlz_async(d_in.data_ptr(), d_idx.data_ptr(), int(cut[k]),
+                                                    int(cut[k + 1] - cut[k]), out.data_ptr(), out.numel(),
+                                                    ws.data_ptr(), ws.numel(), caller_stream.cuda_stream))
+    finally:
+        job.result()
+    _lib.check_gzip(L.ofl_inflate_tlz_wait(d_in.data_ptr(), d_idx.data_ptr(), nmem, out.data_ptr(), out.numel(),
+                                           ws.data_ptr(), ws.numel(), caller_stream.cuda_stream))
 
 
 _h2d_executor = None
