@@ -78,24 +78,27 @@ def _serial_sums(flats):
     return out
 
 
-def eden_seed(data, mode="reference", total=None):
-    """Seed of EdenTransformer.forward (:771-772); draws ONE np.random value.
-    total: the precomputed serial sum (forward_batch computes them in parallel)."""
+def eden_seed(data, mode="reference", total=None, draw=None):
+    """Seed of EdenTransformer.forward (:771-772); draws ONE np.random value
+    (unless `draw` is that value, taken earlier).  total: the precomputed
+    serial sum (forward_batch computes them in parallel)."""
     if total is None:
         flat = data.reshape(-1)
         if mode == "fast":
             flat = flat[:_FAST_SEED_PREFIX]
         total = _serial_sum(flat)
-    seed = (hash(total * 13 + 7) + np.random.randint(1, 2 ** 16)) % (2 ** 16)
+    seed = (hash(total * 13 + 7) + (np.random.randint(1, 2 ** 16) if draw is None else int(draw))) % (2 ** 16)
     return int(float(seed))
 
 
-def eden_seeds(totals):
+def eden_seeds(totals, draws=None):
     """eden_seed for many tensors in order from their serial sums: one
     np.random.randint(1, 2**16, size=T) call -- the legacy generator yields the
     same values and end state as T single calls (MT19937 32-bit bounded draws
-    are unbuffered), without T Python-level calls."""
-    draws = np.random.randint(1, 2 ** 16, size=len(totals)) if len(totals) else []
+    are unbuffered), without T Python-level calls.  draws: the values, if the
+    callers drew them already."""
+    if draws is None:
+        draws = np.random.randint(1, 2 ** 16, size=len(totals)) if len(totals) else []
     return [int(float((hash(t * 13 + 7) + int(r)) % (2 ** 16))) for t, r in zip(totals, draws)]
 
 
@@ -601,7 +604,7 @@ def _batch_decode(eden, items):
 class EdenTransformer(Transformer):
     """Eden quantising transformer (:723-818)."""
 
-    def __init__(self, n_bits=8, dim_threshold=100, device="cpu", seed_mode="reference"):
+    def __init__(self, n_bits=8, dim_threshold=100, device="cpu", seed_mode="reference", combine=True):
         self.lossy = True
         self.eden = Eden(nbits=n_bits, device=device)
         self.dim_threshold = dim_threshold
@@ -609,29 +612,70 @@ class EdenTransformer(Transformer):
         if seed_mode not in ("reference", "fast"):
             raise ValueError("seed_mode must be 'reference' or 'fast'")
         self.seed_mode = seed_mode
+        # concurrent per-tensor calls (the gRPC pool's threads) are merged into
+        # batches, one per device slot (openfl_amd/combining.py)
+        self.combine = bool(combine)
+        self._comb_lock = threading.Lock()
+        self._fwd_comb, self._bwd_comb = {}, {}
+
+    def _combiner(self, table, run):
+        slot = self.eden._thread_devices.slot() if getattr(self.eden, "_thread_devices", None) is not None else 0
+        with self._comb_lock:
+            c = table.get(slot)
+            if c is None:
+                from openfl_amd.combining import Combiner
+                c = table[slot] = Combiner(run)
+            return c
+
+    def _metadata(self, shape, seed, total_dim, scales, dims):
+        md = {"int_list": list(shape), "int_to_float": {0: float(seed), 1: float(total_dim)}}
+        k = 2
+        for scale, dim in zip(scales, dims):
+            md["int_to_float"][k] = scale
+            md["int_to_float"][k + 1] = float(dim)
+            k += 2
+        return md
+
+    def _forward_one(self, data, draw=None):
+        """forward of one tensor above the threshold (draw: its np.random
+        value, if the caller took it already)."""
+        if self.seed_mode == "reference":  # the seed's sum taken while the input is staged
+            (int_array, scale_list, dim_list, total_dim), seed = self.eden.compress(
+                data, None, seed_of_sum=lambda total: eden_seed(None, total=total, draw=draw))
+        else:
+            seed = eden_seed(data, self.seed_mode, draw=draw)
+            int_array, scale_list, dim_list, total_dim = self.eden.compress(data, seed)
+        b = int_array.base
+        payload = b if isinstance(b, bytes) and len(b) == int_array.nbytes else int_array.tobytes()
+        return payload, self._metadata(data.shape, seed, total_dim, scale_list, dim_list)
+
+    def _forward_items(self, items):
+        """The combiner's batch: [(array, draw)] -> [(bytes, metadata)]."""
+        if len(items) == 1:
+            return [self._forward_one(*items[0])]
+        return self._forward_many([a for a, _ in items], [r for _, r in items])
+
+    def _backward_items(self, items):
+        """The combiner's batch: [(bytes, metadata)] -> [array]."""
+        if len(items) == 1:
+            data, md = items[0]
+            out = self.eden.decompress(np.frombuffer(data, dtype=np.uint8), md["int_to_float"])
+            return [out.reshape(list(md["int_list"]))]
+        return self.backward_batch(items)
 
     def forward(self, data, **kwargs):
-        metadata = {"int_list": list(data.shape)}
         if data.size > self.dim_threshold:
-            if self.seed_mode == "reference":  # the seed's sum taken while the input is staged
-                (int_array, scale_list, dim_list, total_dim), seed = self.eden.compress(
-                    data, None, seed_of_sum=lambda total: eden_seed(None, total=total))
-            else:
-                seed = eden_seed(data, self.seed_mode)
-                int_array, scale_list, dim_list, total_dim = self.eden.compress(data, seed)
-            metadata["int_to_float"] = {0: float(seed), 1: float(total_dim)}
-            k = 2
-            for scale, dim in zip(scale_list, dim_list):
-                metadata["int_to_float"][k] = scale
-                metadata["int_to_float"][k + 1] = float(dim)
-                k += 2
-            b = int_array.base
-            return (b if isinstance(b, bytes) and len(b) == int_array.nbytes else int_array.tobytes()), metadata
+            if not self.combine:
+                return self._forward_one(data)
+            draw = np.random.randint(1, 2 ** 16)  # this call's draw, in call order
+            return self._combiner(self._fwd_comb, self._forward_items).call((data, draw))
         eden_seed(data, self.seed_mode)  # the reference draws its RNG value for every tensor (:771)
         return self.no_comp.forward(data)
 
     def backward(self, data, metadata, **kwargs):
         if np.prod(metadata["int_list"]) > self.dim_threshold:  # reference: >= (:808), see module doc
+            if self.combine:
+                return self._combiner(self._bwd_comb, self._backward_items).call((data, metadata))
             out = self.eden.decompress(np.frombuffer(data, dtype=np.uint8), metadata["int_to_float"])
             # already a fresh float32 array: astype would only copy it again
             return out.reshape(list(metadata["int_list"]))
@@ -643,24 +687,20 @@ class EdenTransformer(Transformer):
         """[forward(a) for a in arrays], with the Eden tensors coded in one
         batch: the seeds' serial sums run in parallel host threads, then the
         np.random draws happen in tensor order exactly as per-tensor calls do."""
-        arrays = [np.asarray(a) for a in arrays]
+        return self._forward_many([np.asarray(a) for a in arrays])
+
+    def _forward_many(self, arrays, draws=None):
         big = [i for i, a in enumerate(arrays) if a.size > self.dim_threshold]
         # the seeds' serial sums (native threads, no GIL) run while this
         # thread stages the Eden tensors and starts their H2D
         sums = _threads().submit(_serial_sums, [a.reshape(-1)[:_FAST_SEED_PREFIX] if self.seed_mode == "fast"
                                                 else a.reshape(-1) for a in arrays])
         staged = _batch_stage(self.eden, [arrays[i] for i in big]) if big else None
-        seeds = eden_seeds(sums.result())
+        seeds = eden_seeds(sums.result(), draws)
         enc = _batch_encode(self.eden, staged, [seeds[i] for i in big]) if big else []
         out = [None] * len(arrays)
         for i, (planes, scales, dims) in zip(big, enc):
-            md = {"int_list": list(arrays[i].shape), "int_to_float": {0: float(seeds[i]), 1: float(arrays[i].size)}}
-            k = 2
-            for sc, d in zip(scales, dims):
-                md["int_to_float"][k] = sc
-                md["int_to_float"][k + 1] = float(d)
-                k += 2
-            out[i] = (planes, md)
+            out[i] = (planes, self._metadata(arrays[i].shape, seeds[i], arrays[i].size, scales, dims))
         for i, a in enumerate(arrays):
             if out[i] is None:
                 out[i] = self.no_comp.forward(a)
@@ -683,8 +723,8 @@ class EdenPipeline(TransformationPipeline):
     """plan.yaml: template openfl_amd.pipelines.EdenPipeline, settings n_bits /
     dim_threshold / device (:821-851); extra keyword seed_mode."""
 
-    def __init__(self, n_bits=8, dim_threshold=100, device="cpu", seed_mode="reference", **kwargs):
-        transformers = [EdenTransformer(n_bits, dim_threshold, device, seed_mode)]
+    def __init__(self, n_bits=8, dim_threshold=100, device="cpu", seed_mode="reference", combine=True, **kwargs):
+        transformers = [EdenTransformer(n_bits, dim_threshold, device, seed_mode, combine)]
         super().__init__(transformers=transformers, **kwargs)
 
     def forward(self, data, **kwargs):

@@ -693,3 +693,53 @@ def test_small_set_bit_identical(nbits):
         outs.append((p.cpu(), s.cpu(), y.cpu(), y2.cpu()))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def test_concurrent_plugin_calls_combine():
+    """Concurrent per-tensor forward / backward calls (the gRPC pool's threads,
+    aggregator_server.py:305) go through the combining queue
+    (openfl_amd/combining.py): each caller gets exactly the bytes, metadata and
+    values the serial per-tensor path gives for its seed, and the seeds use
+    the np.random draws of the calls (one per call, as the reference)."""
+    from openfl_amd.pipelines import EdenPipeline
+    from openfl_amd.pipelines.eden_pipeline import _serial_sum
+    pipe = EdenPipeline(n_bits=8, device=DEV)
+    tr = pipe.transformers[0]
+    assert tr.combine
+    rng = np.random.default_rng(29)
+    xs = [(rng.standard_normal(int(n)) * 0.01).astype(np.float32) for n in rng.integers(200, 300_000, 48)]
+    np.random.seed(5)
+    fwd = [None] * len(xs)
+
+    def enc(i):
+        fwd[i] = pipe.forward(xs[i])
+    th = [threading.Thread(target=lambda k=k: [enc(i) for i in range(k, len(xs), 8)]) for k in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    draws = sorted(np.random.RandomState(5).randint(1, 2 ** 16, size=len(xs)).tolist())
+    got = []
+    for x, (payload, mds) in zip(xs, fwd):
+        md = mds[0]["int_to_float"]
+        seed = int(md[0])
+        got.append((seed - hash(_serial_sum(x) * 13 + 7)) % (2 ** 16))
+        planes, scales, dims, total = tr.eden.compress(x, seed)
+        assert payload == planes.tobytes()
+        assert [md[2 + 2 * k] for k in range(len(dims))] == list(scales)
+    assert sorted(got) == [d % (2 ** 16) for d in draws]
+    dec = [None] * len(xs)
+
+    def de(i):
+        dec[i] = pipe.backward(fwd[i][0], [dict(m) for m in fwd[i][1]])
+    th = [threading.Thread(target=lambda k=k: [de(i) for i in range(k, len(xs), 8)]) for k in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for i, x in enumerate(xs):
+        md = fwd[i][1][0]["int_to_float"]
+        ref = tr.eden.decompress(np.frombuffer(fwd[i][0], np.uint8), md)
+        np.testing.assert_array_equal(dec[i], ref.reshape(x.shape))
+    c = next(iter(tr._fwd_comb.values()))
+    assert c.items == len(xs)
