@@ -211,6 +211,15 @@ int ofl_eden_decode_host_x(ofl_eden_plan_t plan, const void* planes_host, size_t
                            void* out_dev, void* y_host, size_t y_bytes, void* ws, size_t ws_bytes, void* stream);
 /* hipMemcpyAsync host -> device on `stream` (no synchronisation). */
 int ofl_copy_h2d_async(void* dst_dev, const void* src_host, size_t bytes, void* stream);
+/* The same copy from PAGEABLE host memory (a received payload), staged: the
+ * bytes go in 4 MiB chunks through a library-owned pinned ring on up to
+ * nthreads (<= 8) host threads, each chunk's async H2D on `stream` issued as
+ * soon as it is staged, so the host copies and the DMAs run together.
+ * Returns when every chunk is staged and enqueued: the source may be
+ * released then, and work enqueued on `stream` afterwards sees the data.
+ * Calls are serialized on the ring; copies under 8 MiB go straight to
+ * hipMemcpyAsync. */
+int ofl_copy_h2d_staged(void* dst_dev, const void* src_host, size_t bytes, int nthreads, void* stream);
 
 /* ---- profiling (bench.py) --------------------------------------------------
  * While enabled, every encode/decode of the plan records a HIP event before

@@ -22,7 +22,7 @@ EXPORTS = (
     "ofl_eden_plan_destroy", "ofl_eden_plan_set_schedule", "ofl_eden_plan_num_waves",
     "ofl_eden_plan_get_schedule", "ofl_eden_plan_set_row2", "ofl_eden_plan_set_sset", "ofl_eden_plan_set_fuse", "ofl_eden_plan_num_slices", "ofl_eden_plan_planes_bytes",
     "ofl_eden_plan_workspace_bytes", "ofl_eden_plan_tensor_info", "ofl_eden_plan_tensor_dims",
-    "ofl_eden_encode", "ofl_eden_encode_wavg", "ofl_eden_decode", "ofl_eden_decode_add", "ofl_eden_encode_host", "ofl_eden_decode_host", "ofl_eden_encode_mapped", "ofl_eden_decode_mapped", "ofl_eden_encode_seeded", "ofl_copy_h2d_chunked", "ofl_eden_encode_host_x", "ofl_eden_decode_host_x", "ofl_copy_h2d_async", "ofl_eden_plan_profile", "ofl_eden_plan_num_launches",
+    "ofl_eden_encode", "ofl_eden_encode_wavg", "ofl_eden_decode", "ofl_eden_decode_add", "ofl_eden_encode_host", "ofl_eden_decode_host", "ofl_eden_encode_mapped", "ofl_eden_decode_mapped", "ofl_eden_encode_seeded", "ofl_copy_h2d_chunked", "ofl_eden_encode_host_x", "ofl_eden_decode_host_x", "ofl_copy_h2d_async", "ofl_copy_h2d_staged", "ofl_eden_plan_profile", "ofl_eden_plan_num_launches",
     "ofl_eden_plan_launch_info", "ofl_eden_plan_profile_collect", "ofl_serial_sum_f32", "ofl_serial_sum_f32_mt", "ofl_serial_sum_copy_f32",
     "ofl_serial_sum_f64", "ofl_host_copy_many", "ofl_serial_sums_many", "ofl_lossy_last_error", "ofl_lossy_workspace_bytes", "ofl_kmeans1d_fit",
     "ofl_kmeans1d_batch_workspace_bytes", "ofl_kmeans1d_batch",
@@ -101,6 +101,8 @@ def _bind(L):
     L.ofl_eden_decode_host_x.restype = i32
     L.ofl_copy_h2d_async.argtypes = [vp, vp, sz, vp]
     L.ofl_copy_h2d_async.restype = i32
+    L.ofl_copy_h2d_staged.argtypes = [vp, vp, sz, i32, vp]
+    L.ofl_copy_h2d_staged.restype = i32
     L.ofl_eden_plan_profile.argtypes = [vp, i32]
     L.ofl_eden_plan_profile.restype = i32
     L.ofl_eden_plan_num_launches.argtypes = [vp, i32]

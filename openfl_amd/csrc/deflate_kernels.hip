@@ -2041,20 +2041,42 @@ __global__ __launch_bounds__(kRNT) void k_tlz_resolve(DecArgs a) {
 }
 }  // namespace tlz
 
-// members -> one contiguous stream (slots of any stride)
+// members -> one contiguous stream (slots of any stride).  The destination is
+// usually mapped pinned host memory, written across PCIe: every store is an
+// aligned 16-byte one (the source realigned with alignbyte; slots are 4-byte
+// aligned), only the < 16 bytes at either end of a member are byte stores.
+// (Byte stores for the 3 in 4 members that start misaligned ran at 8.5 GB/s.)
 __global__ __launch_bounds__(256) void k_gzip_pack(const uint8_t* slots, uint64_t stride, const uint32_t* sizes,
                                                    const uint64_t* off, uint8_t* packed) {
     if (off[blockIdx.x] == ~0ull) return;  // the batch does not fit the output (reported by the scan)
     const uint8_t* src = slots + (int64_t)blockIdx.x * stride;
     uint8_t* dst = packed + off[blockIdx.x];
     const uint32_t n = sizes[blockIdx.x];
-    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 3u);
-    if (mis == 0) {  // slots are 4-byte aligned: whole words where the destination is too
-        for (uint32_t i = threadIdx.x; i < n / 4u; i += 256)
-            reinterpret_cast<uint32_t*>(dst)[i] = reinterpret_cast<const uint32_t*>(src)[i];
-        for (uint32_t i = (n & ~3u) + threadIdx.x; i < n; i += 256) dst[i] = src[i];
-    } else {
+    const uint32_t head = (uint32_t)((16u - (reinterpret_cast<uintptr_t>(dst) & 15u)) & 15u);
+    if (n <= head + 16u) {
         for (uint32_t i = threadIdx.x; i < n; i += 256) dst[i] = src[i];
+        return;
+    }
+    const uint32_t body = (n - head) >> 4;  // aligned 16-byte stores
+    const uint32_t tail0 = head + 16u * body;
+    if (threadIdx.x < head) dst[threadIdx.x] = src[threadIdx.x];
+    for (uint32_t i = tail0 + threadIdx.x; i < n; i += 256) dst[i] = src[i];
+    const uint32_t sh = head & 3u;             // source offset of the body, mod 4
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(src + (head & ~3u));
+    uint4* d = reinterpret_cast<uint4*>(dst + head);
+    for (uint32_t i = threadIdx.x; i < body; i += 256) {
+        const uint32_t* q = s + 4u * i;
+        uint4 v;
+        if (sh == 0) {
+            v = make_uint4(q[0], q[1], q[2], q[3]);
+        } else {  // the 5th word is within the slot: the body ends >= 1 byte before n
+            const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
+            v.x = __builtin_amdgcn_alignbyte(w1, w0, sh);
+            v.y = __builtin_amdgcn_alignbyte(w2, w1, sh);
+            v.z = __builtin_amdgcn_alignbyte(w3, w2, sh);
+            v.w = __builtin_amdgcn_alignbyte(w4, w3, sh);
+        }
+        d[i] = v;
     }
 }
 
@@ -2104,6 +2126,18 @@ hipError_t gz_side_stream(hipStream_t* out) {
     if (!side[dev]) e = hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking);
     *out = side[dev];
     return e;
+}
+
+// a small pinned host block per thread (the gzip's per-batch offsets, read by
+// the host while the next batch encodes); allocated once, kept
+hipError_t gz_pinned_info(uint64_t** out) {
+    thread_local uint64_t* p = nullptr;
+    if (!p) {
+        const hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), 64, hipHostMallocDefault);
+        if (e != hipSuccess) { p = nullptr; return e; }
+    }
+    *out = p;
+    return hipSuccess;
 }
 
 // raw CRC-32 advance matrices for 2^k zero bytes
@@ -2257,6 +2291,7 @@ namespace {
 struct TlzLayout {
     int64_t members, batch;
     size_t slot, ops_stride;
+    size_t stage;  // a batch's device staging for the D2H: 1 byte per value
 };
 TlzLayout tlz_layout(int64_t n) {
     using namespace gz::tlz;
@@ -2266,6 +2301,7 @@ TlzLayout tlz_layout(int64_t n) {
     const int64_t per = std::min<int64_t>(std::max<int64_t>(n, 1), kMemTok);
     L.slot = ((size_t)per * kSlotPerTok + kSlotPad + 255) & ~(size_t)255;
     L.ops_stride = ((size_t)per + 63) & ~(size_t)63;
+    L.stage = ((size_t)L.batch * (size_t)per + 255) & ~(size_t)255;
     return L;
 }
 }  // namespace
@@ -2273,9 +2309,9 @@ TlzLayout tlz_layout(int64_t n) {
 size_t ofl_gzip_ranks_workspace_bytes(int64_t n) {
     const TlzLayout L = tlz_layout(n);
     // slots x 2 (the second is the pageable path's staging) | ops | sizes x 2 |
-    // offsets x 2 | running | bad
+    // offsets x 2 | running | bad | D2H staging x 2
     return 2 * (size_t)L.batch * L.slot + 4 * (size_t)L.batch * L.ops_stride + 8 * (size_t)L.batch +
-           16 * (size_t)(L.batch + 1) + 1024;
+           16 * (size_t)(L.batch + 1) + 1024 + 2 * L.stage;
 }
 
 size_t ofl_gzip_ranks_bound(int64_t n) {
@@ -2314,6 +2350,9 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
     uint64_t* off2[2] = {off, off + L.batch + 1};
     uint64_t* running = off2[1] + L.batch + 1;
     int* bad = reinterpret_cast<int*>(running + 1);
+    uint8_t* stage2[2];
+    stage2[0] = reinterpret_cast<uint8_t*>((reinterpret_cast<uintptr_t>(bad + 1) + 255) & ~(uintptr_t)255);
+    stage2[1] = stage2[0] + L.stage;
     GZHIP(hipMemsetAsync(bad, 0, sizeof(int), st));
     // out is mapped pinned host memory (e.g. torch pin_memory): the pack
     // kernel writes the stream straight into it and the batches run back to
@@ -2343,39 +2382,71 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
     };
     size_t total = 0;
     if (dout) {
-        // batch k encodes on the caller's stream into slots[k & 1]; its scan +
-        // pack run on the side stream, overlapping the encode of batch k + 1
+        // batch k encodes on the caller's stream into slots[k & 1]; its scan,
+        // pack and D2H run on the side stream, overlapping the encode of
+        // batch k + 1.  The pack goes to device staging and the stream
+        // crosses PCIe by DMA (a kernel's stores into mapped host memory are
+        // one small PCIe write each: 8.5 GB/s); the host learns a batch's
+        // offset and size from the scan while the next batch encodes.  A
+        // batch larger than its staging (> 1 byte per value: nearly
+        // incompressible ranks) is packed straight into the mapped output.
         hipStream_t sd = nullptr;
         GZHIP(gz_side_stream(&sd));
+        uint64_t* hinfo = nullptr;
+        GZHIP(gz_pinned_info(&hinfo));  // [2][2]: a batch's first offset and end
         const int64_t nbatch = (L.members + L.batch - 1) / L.batch;
-        hipEvent_t ev_enc[2] = {}, ev_pack[2] = {};
+        hipEvent_t ev_enc[2] = {}, ev_pack[2] = {}, ev_scan[2] = {};
         for (int i = 0; i < 2; ++i) {
             GZHIP(hipEventCreateWithFlags(&ev_enc[i], hipEventDisableTiming));
             GZHIP(hipEventCreateWithFlags(&ev_pack[i], hipEventDisableTiming));
+            GZHIP(hipEventCreateWithFlags(&ev_scan[i], hipEventDisableTiming));
         }
         GZHIP(hipMemsetAsync(running, 0, sizeof(uint64_t), st));
         GZHIP(hipEventRecord(ev_pack[1], st));  // orders the side stream after the memsets
         GZHIP(hipStreamWaitEvent(sd, ev_pack[1], 0));
         int err = 0;
+        auto finish = [&](int64_t k) -> int {  // batch k: scan known -> pack + D2H on the side stream
+            const int b = (int)(k & 1);
+            const int nb = (int)std::min<int64_t>(L.batch, L.members - k * L.batch);
+            GZHIP(hipEventSynchronize(ev_scan[b]));
+            const uint64_t first = hinfo[2 * b], end = hinfo[2 * b + 1];
+            gzprof_begin(sd);
+            if (first != ~0ull && end - first <= L.stage) {
+                hipLaunchKernelGGL(gz::k_gzip_pack, dim3(nb), dim3(256), 0, sd, slots2[b], (uint64_t)L.slot, sizes2[b],
+                                   off2[b], reinterpret_cast<uint8_t*>(reinterpret_cast<uintptr_t>(stage2[b]) - first));
+                gzprof_end(sd, "k_gzip_pack");
+                gzprof_begin(sd);
+                if (end > first) GZHIP(hipMemcpyAsync(out + first, stage2[b], end - first, hipMemcpyDeviceToHost, sd));
+                gzprof_end(sd, "gzip D2H (DMA)");
+            } else {  // (an overflowing batch is reported by the scan: the pack skips it)
+                hipLaunchKernelGGL(gz::k_gzip_pack, dim3(nb), dim3(256), 0, sd, slots2[b], (uint64_t)L.slot, sizes2[b],
+                                   off2[b], dout);
+                gzprof_end(sd, "k_gzip_pack");
+            }
+            GZHIP(hipEventRecord(ev_pack[b], sd));
+            return OFL_OK;
+        };
         for (int64_t k = 0; k < nbatch && !err; ++k) {
             const int64_t c0 = k * L.batch;
             const int b = (int)(k & 1);
             const int nb = (int)std::min<int64_t>(L.batch, L.members - c0);
-            if (k >= 2) GZHIP(hipStreamWaitEvent(st, ev_pack[b], 0));  // slots[b] packed
+            if (k >= 2) GZHIP(hipStreamWaitEvent(st, ev_pack[b], 0));  // slots[b] and stage[b] free
             enc(c0, nb, slots2[b], sizes2[b]);
             GZHIP(hipEventRecord(ev_enc[b], st));
+            if (k >= 1)
+                if (int rc = finish(k - 1)) return rc;
             GZHIP(hipStreamWaitEvent(sd, ev_enc[b], 0));
             hipLaunchKernelGGL(gz::k_gzip_scan, dim3(1), dim3(1024), 0, sd, sizes2[b], nb, off2[b], running,
                                (uint64_t)out_cap, bad);
-            gzprof_begin(sd);
-            hipLaunchKernelGGL(gz::k_gzip_pack, dim3(nb), dim3(256), 0, sd, slots2[b], (uint64_t)L.slot, sizes2[b],
-                               off2[b], dout);
-            gzprof_end(sd, "k_gzip_pack");
-            GZHIP(hipEventRecord(ev_pack[b], sd));
+            GZHIP(hipMemcpyAsync(hinfo + 2 * b, off2[b], 8, hipMemcpyDeviceToHost, sd));
+            GZHIP(hipMemcpyAsync(hinfo + 2 * b + 1, off2[b] + nb, 8, hipMemcpyDeviceToHost, sd));
+            GZHIP(hipEventRecord(ev_scan[b], sd));
             if (hipGetLastError() != hipSuccess) err = 1;
         }
+        if (!err)
+            if (int rc = finish(nbatch - 1)) return rc;
         GZHIP(hipEventRecord(ev_pack[0], sd));
-        GZHIP(hipStreamWaitEvent(st, ev_pack[0], 0));  // the caller's stream sees every pack
+        GZHIP(hipStreamWaitEvent(st, ev_pack[0], 0));  // the caller's stream sees every pack and copy
         uint64_t tot = 0;
         int badh = 0;
         GZHIP(hipMemcpyAsync(&tot, running, 8, hipMemcpyDeviceToHost, st));
@@ -2384,6 +2455,7 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
         for (int i = 0; i < 2; ++i) {
             (void)hipEventDestroy(ev_enc[i]);
             (void)hipEventDestroy(ev_pack[i]);
+            (void)hipEventDestroy(ev_scan[i]);
         }
         if (err) return gzfail(OFL_EHIP, "gzip ranks: kernel launch failed");
         if (badh & 1) return gzfail(OFL_EINVAL, "gzip ranks: values must be float32 integers 0..31");

@@ -3598,6 +3598,87 @@ int ofl_copy_h2d_async(void* dst_dev, const void* src_host, size_t bytes, void* 
     return OFL_OK;
 }
 
+namespace {
+// Pinned staging ring of ofl_copy_h2d_staged: kStageSlots slots per thread,
+// each with the event of the DMA that last read it.  Process-wide, allocated
+// on first use and kept (hipHostMalloc is slow; 64 MiB at most).
+constexpr size_t kStageChunk = 4u << 20;
+constexpr int kStageSlots = 2, kStageMaxThreads = 8;
+struct StageRing {
+    std::mutex mu;
+    int device = -1;
+    char* slot[kStageMaxThreads][kStageSlots] = {};
+    hipEvent_t ev[kStageMaxThreads][kStageSlots] = {};
+    bool used[kStageMaxThreads][kStageSlots] = {};
+};
+StageRing& stage_ring() {
+    static StageRing* r = new StageRing;  // never destroyed (pinned memory outlives static teardown order)
+    return *r;
+}
+}  // namespace
+
+int ofl_copy_h2d_staged(void* dst_dev, const void* src_host, size_t bytes, int nthreads, void* stream) {
+    if (!bytes) return OFL_OK;
+    if (!dst_dev || !src_host) return fail(OFL_EINVAL, "copy_h2d_staged: null argument");
+    if (bytes < 2 * kStageChunk) return ofl_copy_h2d_async(dst_dev, src_host, bytes, stream);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const size_t nchunk = (bytes + kStageChunk - 1) / kStageChunk;
+    const int nt = (int)std::min<size_t>(nchunk, (size_t)std::max(1, std::min(nthreads, kStageMaxThreads)));
+    StageRing& R = stage_ring();
+    std::lock_guard<std::mutex> g(R.mu);
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    if (R.device != dev) {  // events belong to a device: a call on another one rebuilds them
+        for (int t = 0; t < kStageMaxThreads; ++t)
+            for (int s = 0; s < kStageSlots; ++s) {
+                if (R.ev[t][s]) {
+                    HIP_TRY(hipEventSynchronize(R.ev[t][s]));
+                    HIP_TRY(hipEventDestroy(R.ev[t][s]));
+                    R.ev[t][s] = nullptr;
+                }
+                R.used[t][s] = false;
+            }
+        R.device = dev;
+    }
+    for (int t = 0; t < nt; ++t)
+        for (int s = 0; s < kStageSlots; ++s) {
+            if (!R.slot[t][s]) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&R.slot[t][s]), kStageChunk, hipHostMallocDefault));
+            if (!R.ev[t][s]) HIP_TRY(hipEventCreateWithFlags(&R.ev[t][s], hipEventDisableTiming));
+        }
+    // thread t stages chunks t, t + nt, ... through its own slots: the host
+    // copies of several threads and the DMAs of earlier chunks run together
+    std::atomic<int> err{0};
+    auto work = [&](int t) {
+        int k = 0;
+        for (size_t c = (size_t)t; c < nchunk && !err.load(std::memory_order_relaxed); c += (size_t)nt, ++k) {
+            const int s = k % kStageSlots;
+            const size_t o = c * kStageChunk, n = std::min(kStageChunk, bytes - o);
+            hipError_t e = hipSuccess;
+            if (R.used[t][s]) e = hipEventSynchronize(R.ev[t][s]);
+            if (e == hipSuccess) {
+                memcpy(R.slot[t][s], static_cast<const char*>(src_host) + o, n);
+                e = hipMemcpyAsync(static_cast<char*>(dst_dev) + o, R.slot[t][s], n, hipMemcpyHostToDevice, st);
+            }
+            if (e == hipSuccess) e = hipEventRecord(R.ev[t][s], st);
+            if (e != hipSuccess) {
+                err.store((int)e);
+                return;
+            }
+            R.used[t][s] = true;
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t)
+        th.emplace_back([&, t] {
+            (void)hipSetDevice(dev);
+            work(t);
+        });
+    work(0);
+    for (auto& x : th) x.join();
+    if (err.load()) HIP_TRY(static_cast<hipError_t>(err.load()));
+    return OFL_OK;
+}
+
 int ofl_eden_plan_profile(ofl_eden_plan_t pl, int enable) {
     if (!pl) return fail(OFL_EINVAL, "null plan");
     std::lock_guard<std::mutex> g(pl->mu);

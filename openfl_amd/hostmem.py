@@ -16,8 +16,11 @@ Large payloads (>= 8 MiB) that bytes_from made are tracked in a small pool
 for one purpose by default: when the caller has dropped one (the pool holds
 the only reference), the pool hands its last reference to a background
 thread, so the munmap of the dead payload (~37k pages for a 144 MiB stream,
-~8.7 ms on the GPU box) is not paid on the caller's thread.  Nothing is ever
-written into a `bytes` in this default mode; hostmem.release_pool() drops
+~8.7 ms on the GPU box) is not paid on the caller's thread.  That thread
+frees the pages in slices, pausing while a large H2D from pageable memory
+runs (hostmem.quiet(), around gunzip_device's copy): page freeing beside the
+runtime's staging slowed the copy ~7x.  No live `bytes` is ever written in
+this default mode; hostmem.release_pool() drops
 every tracked reference at once, and tracked payloads older than
 OFL_HOST_POOL_IDLE_S seconds (default 30) are dropped at the next call.
 
@@ -76,16 +79,62 @@ def _refcount_is_pool_only(ent):
     return ctypes.c_ssize_t.from_address(id(ent[0])).value == 1
 
 
+_MADV_DONTNEED = 4
+_SLICE = 8 << 20
+_quiet_n = 0
+_quiet_cv = threading.Condition()
+
+
+class quiet:
+    """Context manager around a large H2D from pageable memory: while one is
+    open, the release thread does not free pages.  Freeing a dead payload's
+    ~30k pages (munmap, or madvise) beside the runtime's staging of another
+    payload slowed that copy ~7x on the GPU box (tools/h2d_probe.py: a 128 MiB
+    H2D 2.8 ms alone, 20 ms median beside a release; KC inflate 7 -> 25 ms)."""
+
+    def __enter__(self):
+        global _quiet_n
+        with _quiet_cv:
+            _quiet_n += 1
+        return self
+
+    def __exit__(self, *exc):
+        global _quiet_n
+        with _quiet_cv:
+            _quiet_n -= 1
+            _quiet_cv.notify_all()
+        return False
+
+
+def _release(objs):
+    """Free dead payloads (the only references are in `objs`): their whole
+    pages are discarded in 8 MiB slices (madvise DONTNEED), each slice only
+    while no quiet() section is open (waiting at most 1 s per slice), then
+    the objects are freed (a munmap of a range with no pages left)."""
+    libc = _c()
+    for b in objs:
+        a = _bytes_addr(b)
+        lo = (a + 4095) & ~4095              # the headers sit before the data, in the first page
+        hi = (a + len(b)) & ~4095
+        for s in range(lo, hi, _SLICE):
+            with _quiet_cv:
+                _quiet_cv.wait_for(lambda: _quiet_n == 0, timeout=1.0)
+            libc.madvise(ctypes.c_void_p(s), min(_SLICE, hi - s), _MADV_DONTNEED)
+    with _quiet_cv:
+        _quiet_cv.wait_for(lambda: _quiet_n == 0, timeout=1.0)
+    objs.clear()
+
+
 def _drop_later(objs):
     """Release the last references to dead payloads on a background thread
-    (their munmap off the caller's thread).  Nothing is written into them."""
+    (their page release and munmap off the caller's thread)."""
     global _reaper
     if not objs:
         return
     if _reaper is None:
         from concurrent.futures import ThreadPoolExecutor
         _reaper = ThreadPoolExecutor(max_workers=1, thread_name_prefix="ofl-hostmem-release")
-    _reaper.submit(objs.clear)
+    _reaper.submit(_release, objs)
 
 
 def _release_dead():

@@ -6,6 +6,7 @@ semantics are cited per function (paths relative to /root/reference).
 """
 import ctypes
 import gzip
+import os
 import threading
 from concurrent.futures import ThreadPoolExecutor
 
@@ -379,35 +380,21 @@ def gunzip_device(data, out):
     def h2d():
         # straight from the immutable payload through the C ABI (no torch
         # wrapper of a read-only buffer); the caller's stream orders it
+        # (no page freeing meanwhile: hostmem.quiet)
         if src.size:
-            with torch.cuda.device(dev):
-                _lib.check(L.ofl_copy_h2d_async(d_in.data_ptr(), src.ctypes.data, src.size,
-                                                caller_stream.cuda_stream))
+            with torch.cuda.device(dev), hostmem.quiet():
+                _lib.check(_h2d(L, d_in.data_ptr(), src.ctypes.data, src.size, caller_stream.cuda_stream))
     # one pass over the headers: a member takes >= 26 bytes, so n // 26 + 1
     # entries always suffice (untouched pages of the array cost nothing)
     cap = src.size // 26 + 1
     idx = np.empty((cap, 4), np.int64)
-    if src.size >= _PIPE_MIN:
-        # large streams: index first (a few ms at most), so a TLZ stream's H2D
-        # can go in member-aligned pieces that overlap the inflate
-        rc = L.ofl_gzip_member_index(src.ctypes.data, src.size, idx.ctypes.data, cap, ctypes.byref(nm),
-                                     ctypes.byref(tot), ctypes.byref(mx), ctypes.byref(tl))
-        if rc == _lib.OFL_OK and tl.value and nm.value >= 2:
-            if tot.value > out.numel():
-                raise _lib.CodecError("gunzip_device: output buffer too small")
-            _pipelined_inflate(L, src, idx[:nm.value], d_in, out, dev, caller_stream)
-            _trim_bufs()
-            return out[:tot.value]
-        if rc != _lib.OFL_EFORMAT:
-            _h2d_pool().submit(h2d).result()
-    else:
-        copy = _h2d_pool().submit(h2d)
-        try:
-            rc = L.ofl_gzip_member_index(src.ctypes.data if src.size else None, src.size, idx.ctypes.data, cap,
-                                         ctypes.byref(nm), ctypes.byref(tot), ctypes.byref(mx), ctypes.byref(tl)) \
-                if src.size else _lib.OFL_EFORMAT
-        finally:
-            copy.result()
+    copy = _h2d_pool().submit(h2d)
+    try:
+        rc = L.ofl_gzip_member_index(src.ctypes.data if src.size else None, src.size, idx.ctypes.data, cap,
+                                     ctypes.byref(nm), ctypes.byref(tot), ctypes.byref(mx), ctypes.byref(tl)) \
+            if src.size else _lib.OFL_EFORMAT
+    finally:
+        copy.result()
     if rc == _lib.OFL_EFORMAT:
         raw = np.frombuffer(gzip.decompress(bytes(data)), np.uint8)
         if raw.size > out.numel():
@@ -433,54 +420,15 @@ def gunzip_device(data, out):
     return out[:tot.value]
 
 
-_PIPE_MIN = 16 << 20     # streams from this size inflate in pieces behind their H2D
-_PIPE_PIECES = 6
-_copy_streams = {}
+_H2D_THREADS = int(os.environ.get("OFL_H2D_THREADS", "2"))  # host threads staging a large pageable payload (0: one plain hipMemcpyAsync)
 
 
-def _pipelined_inflate(L, src, idx, d_in, out, dev, caller_stream):
-    """TLZ inflate of a large stream in member-aligned pieces: a pool thread
-    copies piece k to the device on a copy stream while the caller's stream
-    inflates the pieces before it (ofl_inflate_tlz_async), then one
-    synchronisation and status check (ofl_inflate_tlz_wait)."""
-    nmem = idx.shape[0]
-    d_idx = _buf(dev, "gz_idx", max(idx.nbytes, 8))
-    d_idx[:idx.nbytes].copy_(torch.from_numpy(idx.view(np.uint8).reshape(-1)))
-    ws = _buf(dev, "gz_status", int(L.ofl_inflate_tlz_workspace_bytes(nmem)))
-    cut = np.linspace(0, nmem, min(_PIPE_PIECES, nmem) + 1).astype(np.int64)
-    ends = (idx[:, 0] + (idx[:, 1] & ((1 << 62) - 1)) + 8).astype(np.int64)  # member end: data + trailer
-    with _pool_lock:
-        cs = _copy_streams.get(dev.index)
-        if cs is None:
-            cs = _copy_streams[dev.index] = torch.cuda.Stream(device=dev)
-    events = [torch.cuda.Event() for _ in range(len(cut) - 1)]
-
-    def copier():
-        with torch.cuda.device(dev):
-            start = 0
-            for k in range(len(cut) - 1):
-                stop = int(ends[cut[k + 1] - 1]) if k + 2 < len(cut) else src.size
-                _lib.check(L.ofl_copy_h2d_async(d_in.data_ptr() + start, src.ctypes.data + start, stop - start,
-                                                cs.cuda_stream))
-                events[k].record(cs)
-                start = stop
-                ready[k].set()
-    import threading as _th
-    ready = [_th.Event() for _ in events]
-    job = _h2d_pool().submit(copier)
-    try:
-        for k in range(len(cut) - 1):
-            while not ready[k].wait(0.001):
-                if job.done():
-                    job.result()  # raises the copier's error
-            caller_stream.wait_event(events[k])
-            _lib.check_gzip(L.ofl_inflate_tlz_async(d_in.data_ptr(), d_idx.data_ptr(), int(cut[k]),
-                                                    int(cut[k + 1] - cut[k]), out.data_ptr(), out.numel(),
-                                                    ws.data_ptr(), ws.numel(), caller_stream.cuda_stream))
-    finally:
-        job.result()
-    _lib.check_gzip(L.ofl_inflate_tlz_wait(d_in.data_ptr(), d_idx.data_ptr(), nmem, out.data_ptr(), out.numel(),
-                                           ws.data_ptr(), ws.numel(), caller_stream.cuda_stream))
+def _h2d(L, dst, src, nbytes, stream):
+    """H2D of a pageable payload: staged through the library's pinned ring on
+    _H2D_THREADS threads (ofl_copy_h2d_staged), or one hipMemcpyAsync."""
+    if _H2D_THREADS > 0:
+        return L.ofl_copy_h2d_staged(dst, src, nbytes, _H2D_THREADS, stream)
+    return L.ofl_copy_h2d_async(dst, src, nbytes, stream)
 
 
 _h2d_executor = None

@@ -10,6 +10,7 @@ Tolerances:
     centres carried in the input dtype.
 """
 import gzip
+import zlib
 
 import numpy as np
 import pytest
@@ -614,3 +615,27 @@ def test_default_gzip_backend_is_device_and_reference_readable(name):
         ref[ref == k] = m[k]
     y = pipe.backward(payload, [dict(d) for d in mds])
     np.testing.assert_array_equal(y.reshape(-1), ref)
+
+
+@pytest.mark.parametrize("n,threads", [(5, 2), ((8 << 20) - 1, 2), ((8 << 20) + 4097, 2), ((37 << 20) + 3, 4),
+                                       ((21 << 20) + 1, 8)])
+def test_copy_h2d_staged(n, threads):
+    """ofl_copy_h2d_staged (the pinned-ring H2D of a received payload): the
+    device bytes equal the source, the bytes past the copy are untouched, and
+    back-to-back calls reusing the ring (other sizes, other thread counts)
+    stay correct."""
+    from openfl_amd import _lib, hostmem
+    L = _lib.lib()
+    rng = np.random.default_rng(n)
+    d = torch.full((n + 64,), 7, dtype=torch.uint8, device=DEV)
+    st = torch.cuda.current_stream().cuda_stream
+    for rep in range(3):
+        arr = rng.integers(0, 256, n, dtype=np.uint8)
+        src = hostmem.bytes_from(arr.ctypes.data, n)
+        with hostmem.quiet():
+            _lib.check(L.ofl_copy_h2d_staged(d.data_ptr(), np.frombuffer(src, np.uint8).ctypes.data, n,
+                                             threads + rep, st))
+        del src  # the source may go as soon as the call returns
+        torch.cuda.synchronize()
+        assert d[:n].cpu().numpy().tobytes() == arr.tobytes()
+        assert bool(d[n:].eq(7).all())

@@ -156,3 +156,36 @@ def test_release_pool_drops_tracked_payloads(monkeypatch):
     assert sys.getrefcount(b) == 3 and len(hostmem._pool) == 1
     hostmem.release_pool()
     assert sys.getrefcount(b) == 2 and b == src.tobytes()
+
+
+def test_release_pauses_inside_quiet(monkeypatch):
+    """The release thread frees no pages while a quiet() section (a large H2D
+    from pageable memory) is open, and frees them once it closes."""
+    import threading
+    import time
+    monkeypatch.setattr(hostmem, "_RECYCLE", False)
+    hostmem.release_pool()
+    calls = []
+    real = hostmem._c()
+
+    class Spy:
+        def madvise(self, a, n, adv):
+            calls.append(time.monotonic())
+            return real.madvise(a, n, adv)
+    monkeypatch.setattr(hostmem, "_c", lambda: Spy())
+    n = 24 << 20
+    src = _src(4, n)
+    b = hostmem.bytes_from(src.ctypes.data, n)
+    if hostmem._reaper is not None:   # earlier tests' releases finish first
+        hostmem._reaper.submit(lambda: None).result(10)
+    calls.clear()
+    done = threading.Event()
+    with hostmem.quiet():
+        del b
+        hostmem._release_dead()          # hands the dead payload to the release thread
+        hostmem._reaper.submit(done.set)
+        time.sleep(0.2)
+        assert not calls and not done.is_set()
+        t_open = time.monotonic()
+    assert done.wait(5)
+    assert len(calls) >= 3 and min(calls) >= t_open   # 8 MiB slices, all after the section closed
