@@ -604,7 +604,7 @@ def _batch_decode(eden, items):
 class EdenTransformer(Transformer):
     """Eden quantising transformer (:723-818)."""
 
-    def __init__(self, n_bits=8, dim_threshold=100, device="cpu", seed_mode="reference", combine=True):
+    def __init__(self, n_bits=8, dim_threshold=100, device="cpu", seed_mode="reference", combine=False):
         self.lossy = True
         self.eden = Eden(nbits=n_bits, device=device)
         self.dim_threshold = dim_threshold
@@ -612,8 +612,12 @@ class EdenTransformer(Transformer):
         if seed_mode not in ("reference", "fast"):
             raise ValueError("seed_mode must be 'reference' or 'fast'")
         self.seed_mode = seed_mode
-        # concurrent per-tensor calls (the gRPC pool's threads) are merged into
-        # batches, one per device slot (openfl_amd/combining.py)
+        # combine=True: concurrent per-tensor calls (the gRPC pool's threads)
+        # are merged into batches, one per device slot (openfl_amd/combining.py).
+        # Off by default: measured on ResNet-50 with 2 collaborator threads the
+        # merged batches (1.5 calls on average) ran at 0.92 GiB/s against 3.08
+        # for the same threads calling independently, whose host work (staging,
+        # serial sums) runs in parallel (profiles/r04_e2e_resnet50_2collab.json)
         self.combine = bool(combine)
         self._comb_lock = threading.Lock()
         self._fwd_comb, self._bwd_comb = {}, {}
@@ -723,7 +727,7 @@ class EdenPipeline(TransformationPipeline):
     """plan.yaml: template openfl_amd.pipelines.EdenPipeline, settings n_bits /
     dim_threshold / device (:821-851); extra keyword seed_mode."""
 
-    def __init__(self, n_bits=8, dim_threshold=100, device="cpu", seed_mode="reference", combine=True, **kwargs):
+    def __init__(self, n_bits=8, dim_threshold=100, device="cpu", seed_mode="reference", combine=False, **kwargs):
         transformers = [EdenTransformer(n_bits, dim_threshold, device, seed_mode, combine)]
         super().__init__(transformers=transformers, **kwargs)
 

@@ -703,9 +703,9 @@ def test_concurrent_plugin_calls_combine():
     the np.random draws of the calls (one per call, as the reference)."""
     from openfl_amd.pipelines import EdenPipeline
     from openfl_amd.pipelines.eden_pipeline import _serial_sum
-    pipe = EdenPipeline(n_bits=8, device=DEV)
+    assert not EdenPipeline(n_bits=8, device=DEV).transformers[0].combine  # opt-in
+    pipe = EdenPipeline(n_bits=8, device=DEV, combine=True)
     tr = pipe.transformers[0]
-    assert tr.combine
     rng = np.random.default_rng(29)
     xs = [(rng.standard_normal(int(n)) * 0.01).astype(np.float32) for n in rng.integers(200, 300_000, 48)]
     np.random.seed(5)
