@@ -1034,7 +1034,10 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     uint64_t ph_t = 0, ph_acc[kEncPhases] = {};
     const bool ph_on = a.phases && blockIdx.x == 0 && tid == 0;
+    // (diagnostics: a barrier before every mark, so a phase's time is its
+    // slowest wave's, not wave 0's; launch-uniform condition)
     auto PH = [&](int k) {
+        if (a.phases) __syncthreads();
         if (ph_on) { const uint64_t t = wall_clock64(); if (k > 0) ph_acc[k] += t - ph_t; ph_t = t; }
     };
     PH(0);
