@@ -880,10 +880,16 @@ constexpr int kMemTok = kSeg * kMemSeg;            // values per member
 constexpr int kPer = kSeg / kNT;                   // positions per thread
 constexpr int kWin = 8192;                         // window, values (32 KiB)
 constexpr int kMaxL = 64, kMinL = 3;               // copy length, values
-constexpr int kCand = 16;                          // chain candidates per position
+#ifndef OFL_TLZ_CAND
+#define OFL_TLZ_CAND 16
+#endif
+#ifndef OFL_TLZ_SWEEPS
+#define OFL_TLZ_SWEEPS 4
+#endif
+constexpr int kCand = OFL_TLZ_CAND;                // chain candidates per position (A/B: -DOFL_TLZ_CAND)
 constexpr int kBuckets = 512;                      // 3-gram buckets: exact for values < 8, hashed (into the same) above
 constexpr int kBucketBits = 9;
-constexpr int kSweeps = 4;                         // DP sweeps (segments of kPer = 4 positions; tools/tlz_proto.c)
+constexpr int kSweeps = OFL_TLZ_SWEEPS;            // DP sweeps (segments of kPer = 4 positions; tools/tlz_proto.c)
 constexpr int kRing = 16384;                       // value ring (ids), + 8 mirrored bytes
 constexpr int kLitMax = 11, kDistMax = 10;         // code length limits = the inflate's table bits
 constexpr int kHdrFixed = 28;                      // member header bytes before the segment table
@@ -1188,6 +1194,11 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             }
             S.head[(c + 1) & 1][b] = h;
         }
+        // the frontier reads the chain links of every position, pending ones
+        // resolved just above by other waves (without this barrier a wave
+        // could read a link before its writer: valid output, but not
+        // deterministic -- tools/tlz_check.py "det")
+        __syncthreads();
         PH(2);
         // ---- C: each position's frontier of (length, distance) pairs ----
         uint32_t fa[kPer], fb[kPer], fc[kPer];  // entries: length | distance << 7 (lengths increasing)

@@ -639,3 +639,25 @@ def test_copy_h2d_staged(n, threads):
         torch.cuda.synchronize()
         assert d[:n].cpu().numpy().tobytes() == arr.tobytes()
         assert bool(d[n:].eq(7).all())
+
+
+@pytest.mark.parametrize("case", ["ternary", "kc6", "runs"])
+def test_gzip_ranks_deterministic_repeats(case):
+    """The device gzip's bytes do not depend on wave timing: several encodes
+    of one input (many members, blocks racing each other on the CUs) give
+    one stream.  (A missing barrier between the chain links' last writes and
+    the match search once made ternary ranks encode differently run to run.)"""
+    from openfl_amd import lossy
+    rng = np.random.default_rng(7)
+    n = (1 << 21) + 333
+    if case == "ternary":
+        x = rng.choice(3, n, p=[0.05, 0.9, 0.05]).astype(np.float32)
+    elif case == "kc6":
+        x = rng.choice(6, n, p=[0.07, 0.2, 0.23, 0.23, 0.2, 0.07]).astype(np.float32)
+    else:
+        x = np.repeat(rng.integers(0, 6, n // 37 + 1), 37)[:n].astype(np.float32)
+    xd = torch.from_numpy(x).to(DEV)
+    z = lossy.gzip_ranks(xd)
+    assert gzip.decompress(z) == x.tobytes()
+    for _ in range(5):
+        assert lossy.gzip_ranks(xd) == z
