@@ -560,7 +560,9 @@ def main(argv=None):
         # PMC counters cannot be read from inside this process: the committed
         # rocprofv3 --pmc passes of this same workload and default schedule
         # (tools/pmc_run.sh), only when this run uses that schedule
-        traffic_src = os.path.join(ROOT, "profiles", "r03_final_llama3_8b_hbm_traffic.json")
+        traffic_src = os.path.join(ROOT, "profiles", "r04_llama3_8b_hbm_traffic.json")
+        if not os.path.exists(traffic_src):
+            traffic_src = os.path.join(ROOT, "profiles", "r03_final_llama3_8b_hbm_traffic.json")
     if traffic_src and os.path.exists(traffic_src):
         with open(traffic_src) as f:
             traffic = json.load(f).get("hbm_bytes_per_step")
