@@ -1078,6 +1078,11 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     uint32_t crc_acc = 0, crc_last = 0;
     int nv_last = 0;
     for (int c = 0; c < nseg; ++c) {
+        // thread-derived values recomputed every segment from an opaque tid
+        // (hoisted out of the loop, they were spilled and reloaded instead)
+        uint32_t tid_o = threadIdx.x;
+        asm volatile("" : "+v"(tid_o));
+        const int tid = (int)tid_o, lane = tid & 63, wv = tid >> 6;
         const int c0 = c << kSegLog;
         const int send = min(c0 + kSeg, ntok);
         const int lo = c0 + kPer * tid;                 // this thread's positions [lo, lo + kPer)
@@ -1281,13 +1286,22 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             }
         }
         PH(3);
-        // ---- D: segmented backward DP (3 sweeps) ----
-        uint32_t dca[kPer], dcb[kPer], dcc[kPer];
+        // ---- D: segmented backward DP (kSweeps sweeps) ----
+        // The per-position state is kept packed, so that the whole segment
+        // loop fits the 128 VGPRs of two blocks per CU: unpacked (13
+        // registers per position) it spilled, and the spills' scratch
+        // traffic reached HBM (3.6 GB per 512-member launch, PMC).
+        //   pk[q]  = La | Lb << 7 | (Lm + 1) << 14 | literal cost << 21
+        //   dc3[q] = distance costs of entries a | b << 8 | c << 16 (each <= 224)
+        //   lx0/lx1[q] = the entries' own long lengths (> kU) and their
+        //            length + distance costs, (l | cost << 7) in 16 bits
+        uint32_t dc3[kPer];
 #pragma unroll
         for (int q = 0; q < kPer; ++q) {
-            dca[q] = nf[q] > 0 ? S.dcst[dist_code(4u * (fa[q] >> 7))] : 0u;
-            dcb[q] = nf[q] > 1 ? S.dcst[dist_code(4u * (fb[q] >> 7))] : 0u;
-            dcc[q] = nf[q] > 2 ? S.dcst[dist_code(4u * (fc[q] >> 7))] : 0u;
+            const uint32_t da = nf[q] > 0 ? min(255u, (uint32_t)S.dcst[dist_code(4u * (fa[q] >> 7))]) : 0u;
+            const uint32_t db = nf[q] > 1 ? min(255u, (uint32_t)S.dcst[dist_code(4u * (fb[q] >> 7))]) : 0u;
+            const uint32_t dc = nf[q] > 2 ? min(255u, (uint32_t)S.dcst[dist_code(4u * (fc[q] >> 7))]) : 0u;
+            dc3[q] = da | (db << 8) | (dc << 16);
         }
         __syncthreads();  // the wave tables are dead: the DP's costs take their memory
         for (int k = tid; k <= kSeg; k += kNT) {
@@ -1299,33 +1313,32 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         const int klo = kPer * tid;  // segment-relative
         {
             // own positions' costs in registers (indices are compile-time
-            // after unrolling); lengths 3..10 branch-free, longer ones (rare)
-            // read the other threads' costs from LDS
+            // after unrolling); lengths kMinL..kU branch-free, longer ones
+            // only as the frontier entries' own lengths, whose costs beyond
+            // this thread's positions come from the previous sweep
             constexpr int kU = 6;              // lengths unrolled: kMinL .. kU (longer: only the entries' own lengths; the same ratio, tools/tlz_proto.c)
-            constexpr int kW = kPer + kU - kPer;  // costs beyond this thread's positions within reach
+            constexpr int kW = kU;             // costs beyond this thread's positions within reach
             uint32_t lenr[kU + 1];
 #pragma unroll
             for (int l = kMinL; l <= kU; ++l) lenr[l] = S.lenc[l];
-            uint32_t litr[kPer];
-            int La[kPer], Lb[kPer], Lm[kPer];
-            // lengths above kU: only each frontier entry's own length; its
-            // length + distance cost is the same in every sweep
-            int el[kPer][3];
-            uint32_t ec[kPer][3];
+            uint32_t pk[kPer], lx0[kPer], lx1[kPer];
 #pragma unroll
             for (int q = 0; q < kPer; ++q) {
-                litr[q] = S.litc[(idw[q >> 2] >> (8 * (q & 3))) & 0xffu];
-                La[q] = (int)(fa[q] & 127u);
-                Lb[q] = (int)(fb[q] & 127u);
-                Lm[q] = nf[q] == 0 ? 0 : (int)((nf[q] == 1 ? fa[q] : nf[q] == 2 ? fb[q] : fc[q]) & 127u);
-                if (c0 + klo + q >= send) Lm[q] = -1;  // no such position
+                const uint32_t lit = min(511u, (uint32_t)S.litc[(idw[q >> 2] >> (8 * (q & 3))) & 0xffu]);
+                const int La = (int)(fa[q] & 127u), Lb = (int)(fb[q] & 127u);
+                int Lm = nf[q] == 0 ? 0 : (int)((nf[q] == 1 ? fa[q] : nf[q] == 2 ? fb[q] : fc[q]) & 127u);
+                if (c0 + klo + q >= send) Lm = -1;  // no such position
+                pk[q] = (uint32_t)La | ((uint32_t)Lb << 7) | ((uint32_t)(Lm + 1) << 14) | (lit << 21);
+                uint32_t E[3];
 #pragma unroll
                 for (int e = 0; e < 3; ++e) {
-                    const int l = e == 0 ? La[q] : e == 1 ? Lb[q] : Lm[q];
-                    const bool use = l > kU && l <= Lm[q] && nf[q] > e;
-                    el[q][e] = use ? l : 0;
-                    ec[q][e] = use ? S.lenc[l] + (e == 0 ? dca[q] : e == 1 ? dcb[q] : dcc[q]) : 0u;
+                    const int l = e == 0 ? La : e == 1 ? Lb : Lm;
+                    const bool use = l > kU && l <= Lm && nf[q] > e;
+                    const uint32_t dcost = (dc3[q] >> (8 * e)) & 255u;
+                    E[e] = use ? (uint32_t)l | (min(511u, (uint32_t)S.lenc[l] + dcost) << 7) : 0u;
                 }
+                lx0[q] = E[0] | (E[1] << 16);
+                lx1[q] = E[2];
             }
 #pragma unroll 1
             for (int sw = 0; sw < kSweeps; ++sw) {
@@ -1334,40 +1347,39 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                 uint32_t pw[kW + 1];
 #pragma unroll
                 for (int u = 0; u <= kW; ++u) pw[u] = prv[min(klo + kPer + u, kSeg)];
-                uint32_t ev[kPer][3];  // the costs after each long entry (beyond this thread's positions: previous sweep)
-#pragma unroll
-                for (int q = 0; q < kPer; ++q)
-#pragma unroll
-                    for (int e = 0; e < 3; ++e) ev[q][e] = prv[min(klo + q + el[q][e], kSeg)];
                 uint32_t cr[kPer];
                 uint32_t chs[kPer];
 #pragma unroll
                 for (int q = kPer - 1; q >= 0; --q) {
                     auto CV = [&](int kk) -> uint32_t { return kk < kPer ? cr[kk] : pw[kk - kPer]; };  // kk = q + l
-                    uint32_t best = litr[q] + CV(q + 1);
+                    const uint32_t P = pk[q];
+                    const int La = (int)(P & 127u), Lb = (int)((P >> 7) & 127u), Lm = (int)((P >> 14) & 127u) - 1;
+                    const uint32_t D = dc3[q];
+                    uint32_t best = (P >> 21) + CV(q + 1);
                     uint32_t ch = 0;
 #pragma unroll
                     for (int l = kMinL; l <= kU; ++l) {
-                        const uint32_t e = l <= La[q] ? 0u : l <= Lb[q] ? 1u : 2u;
-                        const uint32_t dc = e == 0 ? dca[q] : e == 1 ? dcb[q] : dcc[q];
-                        const uint32_t cc = lenr[l] + dc + CV(q + l);
-                        const bool take = l <= Lm[q] && lt16(cc, best);
+                        const uint32_t e = l <= La ? 0u : l <= Lb ? 1u : 2u;
+                        const uint32_t cc = lenr[l] + ((D >> (8 * e)) & 255u) + CV(q + l);
+                        const bool take = l <= Lm && lt16(cc, best);
                         best = take ? cc : best;
                         ch = take ? ((uint32_t)l | (e << 8)) : ch;
                     }
 #pragma unroll
                     for (int e = 0; e < 3; ++e) {
-                        const uint32_t cc = ec[q][e] + ev[q][e];
-                        const bool take = el[q][e] != 0 && lt16(cc, best);
+                        const uint32_t En = e == 0 ? (lx0[q] & 0xffffu) : e == 1 ? (lx0[q] >> 16) : lx1[q];
+                        const int el = (int)(En & 127u);
+                        const uint32_t cc = (En >> 7) + prv[min(klo + q + el, kSeg)];
+                        const bool take = el != 0 && lt16(cc, best);
                         best = take ? cc : best;
-                        ch = take ? ((uint32_t)el[q][e] | ((uint32_t)e << 8)) : ch;
+                        ch = take ? ((uint32_t)el | ((uint32_t)e << 8)) : ch;
                     }
-                    cr[q] = Lm[q] < 0 ? 0u : best;
+                    cr[q] = Lm < 0 ? 0u : best;
                     chs[q] = ch;
                 }
 #pragma unroll
                 for (int q = 0; q < kPer; ++q) {
-                    if (Lm[q] < 0) continue;
+                    if ((int)((pk[q] >> 14) & 127u) == 0) continue;  // Lm < 0: no such position
                     cur[klo + q] = (uint16_t)cr[q];
                     if (sw == kSweeps - 1) S.dec[klo + q] = (uint16_t)chs[q];
                 }
