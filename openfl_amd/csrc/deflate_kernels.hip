@@ -1254,6 +1254,9 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                         for (int k = 0; k <= kCW; ++k) cw[u][k] = tw[jb + k];
                         pd[u] = S.u.m.prev[pslot(jj)];
                     }
+                    int Lq[4];
+                    bool okq[4], longq[4];
+                    bool anylong = false;
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
                         const int q = h + u;
@@ -1265,18 +1268,36 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                             const uint32_t x = __builtin_amdgcn_alignbyte(cw[u][k + 1], cw[u][k], sh) ^ ti[q][k];
                             L = x ? 4 * k + (__builtin_ctz(x) >> 3) : L;
                         }
-                        const bool ok = act[q] && i - j[q] <= kWin;
-                        if (ok && L == 4 * kCW && lim[q] > 4 * kCW)  // rare: a long match walks on
-                            L = 4 * kCW + match_len(S.tok, i + 4 * kCW, j[q] + 4 * kCW, lim[q] - 4 * kCW);
-                        L = min(L, lim[q]);
-                        if (ok && L >= kMinL && L > bl[q]) {
-                            const uint32_t e = (uint32_t)L | ((uint32_t)(i - j[q]) << 7);
-                            fa[q] = nf[q] == 0 ? e : fa[q];
-                            fb[q] = nf[q] == 1 ? e : fb[q];
-                            fc[q] = nf[q] >= 2 ? e : fc[q];
-                            nf[q] = min(nf[q] + 1, 3);
-                            bl[q] = L;
+                        okq[u] = act[q] && i - j[q] <= kWin;
+                        longq[u] = okq[u] && L == 4 * kCW && lim[q] > 4 * kCW;
+                        anylong |= longq[u];
+                        Lq[u] = L;
+                    }
+                    // rare: a long match walks on.  One wave-uniform test for
+                    // the four positions (per-position divergent branches cost
+                    // ~50 scalar instructions per step even when no lane took them)
+                    if (__builtin_expect(__ballot(anylong) != 0ull, 0)) {
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int q = h + u;
+                            if (longq[u])
+                                Lq[u] = 4 * kCW + match_len(S.tok, lo + q + 4 * kCW, j[q] + 4 * kCW, lim[q] - 4 * kCW);
                         }
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int q = h + u;
+                        const int i = lo + q;
+                        const bool ok = okq[u];
+                        const int L = min(Lq[u], lim[q]);
+                        // branch-free (selects, no exec-mask juggling)
+                        const bool imp = ok && L >= kMinL && L > bl[q];
+                        const uint32_t e = (uint32_t)L | ((uint32_t)(i - j[q]) << 7);
+                        fa[q] = imp && nf[q] == 0 ? e : fa[q];
+                        fb[q] = imp && nf[q] == 1 ? e : fb[q];
+                        fc[q] = imp && nf[q] >= 2 ? e : fc[q];
+                        nf[q] = imp ? min(nf[q] + 1, 3) : nf[q];
+                        bl[q] = imp ? L : bl[q];
                         act[q] = ok && bl[q] < lim[q] && pd[u] != 0;
                         j[q] -= (int)pd[u];
                         any |= act[q];
