@@ -81,16 +81,31 @@ inline float pow2f(int k) {  // 2^k, -126 <= k <= 127
 constexpr int16_t kNoBinade = -32768;
 
 // A small persistent pool: try_run(n, w, f) calls f(0..n-1) on the caller and
-// (at least) w workers.  One job at a time; a caller that finds the pool busy
-// gets false and runs serially (concurrent plugin calls keep their own core).
-// Fork-safe: a fork()ed child inherits the pool's state but none of its
-// threads, so a pool created in another process (pid recorded at creation)
-// always reports busy and the caller runs serially.
+// (at least) w workers.  One job at a time per pool; Pool::run tries a few
+// pools in turn, so concurrent plugin calls (the gRPC server's threads) each
+// get workers of their own, and only a caller that finds every pool busy
+// runs serially.  Fork-safe: a fork()ed child inherits the pools' state but
+// none of their threads, so a pool created in another process (pid recorded
+// at creation) always reports busy and the caller runs serially.
 class Pool {
    public:
-    static Pool& get() {
-        static Pool* p = new Pool;  // never destroyed: its threads live as long as the process
-        return *p;
+    static bool run(int n, int workers, const std::function<void(int)>& f) {
+        static const int npools = [] {
+            const char* e = getenv("OFL_SUM_POOLS");
+            return std::max(1, std::min(16, e ? atoi(e) : 4));
+        }();
+        static std::mutex m;
+        static Pool* pools[16] = {};  // never destroyed: their threads live as long as the process
+        for (int i = 0; i < npools; ++i) {
+            Pool* p;
+            {
+                std::lock_guard<std::mutex> g(m);
+                if (!pools[i]) pools[i] = new Pool;
+                p = pools[i];
+            }
+            if (p->try_run(n, workers, f)) return true;
+        }
+        return false;
     }
     bool try_run(int n, int workers, const std::function<void(int)>& f) {
         if (getpid() != pid_) return false;
@@ -309,8 +324,8 @@ float serial_sum_f32_mt_cb(const float* x, int64_t n, float* dst, int nthreads, 
                 subs[k].dsum = (a0 + a1) + (a2 + a3);
             }
         };
-        if (!Pool::get().try_run(parts, nthreads - 1, fa)) {
-            // the pool is busy (another caller): the plain chain for the rest
+        if (!Pool::run(parts, nthreads - 1, fa)) {
+            // every pool is busy (other callers): the plain chain for the rest
             if (dst) std::memcpy(dst + c0, xc, sizeof(float) * (n - c0));
             if (after_copy) after_copy(ctx);
             return serial_loop(xc, n - c0, s);
@@ -328,7 +343,7 @@ float serial_sum_f32_mt_cb(const float* x, int64_t n, float* dst, int nthreads, 
             range(i, k0, k1);
             for (int64_t k = k0; k < k1; ++k) phase_b(xc + k * kG, (int)std::min<int64_t>(kG, nc - k * kG), subs[k]);
         };
-        if (!Pool::get().try_run(parts, nthreads - 1, fb))
+        if (!Pool::run(parts, nthreads - 1, fb))
             for (int i = 0; i < parts; ++i) fb(i);
         // phase C: in order, exact
         const double t2 = debug_on() ? now_s() : 0.0;

@@ -181,18 +181,20 @@ def main():
             continue
         from concurrent.futures import ThreadPoolExecutor
         pipe = EdenPipeline(n_bits=8, dim_threshold=100, device="cuda:0", combine=combine)
+        rounds = []
         with ThreadPoolExecutor(max_workers=len(sds)) as ex:
-            for r in range(3):
+            for r in range(int(os.environ.get("E2E_ROUNDS", "3"))):
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 outs = list(ex.map(lambda sd: run_plugin(sd, pipe, P), sds))
                 dt = time.perf_counter() - t0
+                rounds.append(round(dt, 4))
         c = pipe.transformers[0]
         nb = sum(x.batches for x in list(c._fwd_comb.values()) + list(c._bwd_comb.values()))
         ni = sum(x.items for x in list(c._fwd_comb.values()) + list(c._bwd_comb.values()))
         res[key] = {"s": round(dt, 4), "GiB_s": round(in_bytes / dt / 2 ** 30, 3), "threads": len(sds),
                     "wire_bytes": sum(o[1] for o in outs), "rel_err": round(rel_err(sds[0], outs[0][0]), 6),
-                    "combined_calls_per_batch": round(ni / nb, 3) if nb else None}
+                    "combined_calls_per_batch": round(ni / nb, 3) if nb else None, "round_s": rounds}
     if "batched" in modes:
         for mode in ("reference", "fast"):
             pipe = EdenPipeline(n_bits=8, dim_threshold=100, device="cuda:0", seed_mode=mode)
