@@ -1171,33 +1171,33 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         }
         PH(12);
         __syncthreads();
-        // pending positions: the last occurrence in an earlier wave's part,
-        // else before the segment; meanwhile the heads of the next segment
+        // per bucket, in place: an exclusive prefix max of the waves' last
+        // occurrences (the nearest one in an earlier wave's part: parts are
+        // in wave order), and the next segment's heads; then every pending
+        // position takes its link with one read
         const uint32_t* head = S.head[c & 1];
+        for (int b = tid; b < kBuckets; b += kNT) {
+            uint32_t run = 0;
+#pragma unroll
+            for (int w2 = 0; w2 < kNT / 64; ++w2) {
+                const uint32_t t = S.u.m.lastw[w2][b];
+                S.u.m.lastw[w2][b] = (uint16_t)run;
+                run = max(run, t);
+            }
+            S.head[(c + 1) & 1][b] = run ? (uint32_t)s_ins + run : head[b];
+        }
+        __syncthreads();
         for (int p0 = w_lo; p0 < w_hi; p0 += 64) {
             const int p = p0 + lane;
             if (p < w_hi && S.u.m.prev[pslot(p)] == kPending) {
                 const int bk = bucket(S.tok, p);
+                const uint32_t lw = S.u.m.lastw[wv][bk];
+                const uint32_t h = head[bk];
                 uint32_t d = 0;
-                bool found = false;
-                for (int w2 = wv - 1; w2 >= 0 && !found; --w2) {
-                    const uint32_t lw = S.u.m.lastw[w2][bk];
-                    if (lw) { d = (uint32_t)(p - (s_ins + (int)lw - 1)); found = true; }
-                }
-                if (!found) {
-                    const uint32_t h = head[bk];
-                    if (h && p - (int)(h - 1u) <= kWin) d = (uint32_t)(p - (int)(h - 1u));
-                }
+                if (lw) d = (uint32_t)(p - (s_ins + (int)lw - 1));
+                else if (h && p - (int)(h - 1u) <= kWin) d = (uint32_t)(p - (int)(h - 1u));
                 S.u.m.prev[pslot(p)] = (uint16_t)d;
             }
-        }
-        for (int b = tid; b < kBuckets; b += kNT) {
-            uint32_t h = head[b];
-            for (int w2 = kNT / 64 - 1; w2 >= 0; --w2) {
-                const uint32_t lw = S.u.m.lastw[w2][b];
-                if (lw) { h = (uint32_t)s_ins + lw; break; }
-            }
-            S.head[(c + 1) & 1][b] = h;
         }
         // the frontier reads the chain links of every position, pending ones
         // resolved just above by other waves (without this barrier a wave
