@@ -208,7 +208,7 @@ def secondary(name, n_bits, steps, warmup, dev, wave_mib, streams, cpu=False, gr
     return out
 
 
-KC_TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r04_kc_pipeline_hbm_traffic.json")
+KC_TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r04_final_kc_pipeline_hbm_traffic.json")
 
 
 def _kc_kernel_profile(encode, decode, dev, steps=2):
