@@ -661,3 +661,26 @@ def test_gzip_ranks_deterministic_repeats(case):
     assert gzip.decompress(z) == x.tobytes()
     for _ in range(5):
         assert lossy.gzip_ranks(xd) == z
+
+
+def test_gzip_ranks_full_size_kc_set():
+    """BASELINE config 3 at its full size (2^28 ranks = the 1 GiB set): the
+    device gzip's stream is a valid gzip stream whose gzip.decompress is the
+    ranks' bytes (the reference's GZIPTransformer.backward), the device
+    inflate returns the same bytes, the stream is smaller than gzip -9's
+    ratio bound for this distribution, and it is deterministic."""
+    from openfl_amd import lossy
+    n = 1 << 28
+    g = torch.Generator(device=DEV).manual_seed(11)
+    p = torch.tensor([0.074, 0.1816, 0.2444, 0.2444, 0.1816, 0.074], device=DEV)
+    x = torch.empty(n, dtype=torch.float32, device=DEV)
+    for o in range(0, n, 1 << 24):
+        x[o:o + (1 << 24)] = torch.multinomial(p, 1 << 24, replacement=True, generator=g).to(torch.float32)
+    z = lossy.gzip_ranks(x)
+    assert len(z) / (4 * n) < 0.1174          # gzip -9 on this distribution: 0.1173-0.1174
+    host = x.cpu().numpy().tobytes()
+    assert gzip.decompress(z) == host
+    out = torch.empty(4 * n + 64, dtype=torch.uint8, device=DEV)
+    got = lossy.gunzip_device(z, out)
+    assert got.numel() == 4 * n and torch.equal(got.view(torch.float32), x)
+    assert lossy.gzip_ranks(x) == z
