@@ -1732,27 +1732,18 @@ struct DecArgs {
 
 // bytes of the stream (any alignment) through a 128-bit block register pair
 struct BitIn {
-    // Each lane streams its own segment's bits: the 16-byte blocks are
-    // requested 3 blocks (~100 symbols) ahead of their use, so the load
-    // latency of these uncoalesced per-lane streams is hidden (one block
-    // ahead left k_tlz_ops waiting on nearly every refill).  Blocks past `lim`
-    // (the member's last readable block) are not requested.
     const uint4* base;       // 16-byte aligned
-    uint4 cur, q1, q2, q3;
-    int64_t blk, lim;        // block index of cur, last block that may be read
+    uint4 cur, nxt;
+    int64_t blk;             // block index of cur
     int wi;                  // next word of cur
     uint64_t bb;
     int bc;
     DEVI uint32_t word(int k) const { return k == 0 ? cur.x : k == 1 ? cur.y : k == 2 ? cur.z : cur.w; }
-    DEVI uint4 ld(int64_t b) const { return base[b < lim ? b : lim]; }
-    DEVI void start(const uint8_t* src, uint64_t bit, int64_t lim_blk) {  // src 16-byte aligned
+    DEVI void start(const uint8_t* src, uint64_t bit) {  // src 16-byte aligned
         base = reinterpret_cast<const uint4*>(src);
-        lim = lim_blk;
         blk = (int64_t)(bit >> 7);
-        cur = ld(blk);
-        q1 = ld(blk + 1);
-        q2 = ld(blk + 2);
-        q3 = ld(blk + 3);
+        cur = base[blk];
+        nxt = base[blk + 1];
         wi = (int)((bit >> 5) & 3u);
         const int sk = (int)(bit & 31u);
         bb = (uint64_t)(word(wi) >> sk);
@@ -1761,7 +1752,7 @@ struct BitIn {
         fill();
     }
     DEVI void adv() {
-        if (++wi == 4) { cur = q1; q1 = q2; q2 = q3; ++blk; q3 = ld(blk + 3); wi = 0; }
+        if (++wi == 4) { cur = nxt; ++blk; nxt = base[blk + 1]; wi = 0; }
     }
     DEVI void fill() {  // >= 33 bits in bb
         while (bc <= 32) {
@@ -1812,12 +1803,9 @@ __global__ __launch_bounds__(64) void k_tlz_ops(DecArgs a) {
         return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
     };
     const uint64_t dbit = 8ull * (uint64_t)doff;  // the data's first bit in the stream
-    // blocks that may be read: up to 32 bytes past the member's trailer (the
-    // stream is readable 32 bytes past its end)
-    const int64_t lim_blk = (doff + (int64_t)in_len + 8 + 32) / 16 - 1;
     // ---- the block header, on every lane (wave-uniform) ----
     BitIn in;
-    in.start(a.src, dbit, lim_blk);
+    in.start(a.src, dbit);
     if (in.get(1) != 1u || in.get(2) != 2u) err = kInfCorrupt;  // BFINAL, dynamic
     int nlit = 0, ndist = 0;
     if (!err) {
@@ -1893,7 +1881,7 @@ __global__ __launch_bounds__(64) void k_tlz_ops(DecArgs a) {
     if (s < nseg) {
         const uint32_t T = min((uint32_t)kSeg, ntok - ((uint32_t)s << kSegLog));
         uint32_t* const opo = reinterpret_cast<uint32_t*>(a.out + out_off + ((int64_t)s << (kSegLog + 2)));
-        in.start(a.src, dbit + seg_bit(s), lim_blk);
+        in.start(a.src, dbit + seg_bit(s));
         uint32_t produced = 0, nops = 0;
         const uint32_t before = (uint32_t)s << kSegLog;  // values of the member before this segment
         while (produced < T) {
