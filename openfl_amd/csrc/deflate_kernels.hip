@@ -1884,6 +1884,27 @@ __global__ __launch_bounds__(64) void k_tlz_ops(DecArgs a) {
         in.start(a.src, dbit + seg_bit(s));
         uint32_t produced = 0, nops = 0;
         const uint32_t before = (uint32_t)s << kSegLog;  // values of the member before this segment
+        // op records are collected four at a time and stored as one 16-byte
+        // write: every lane writes its own segment's region, so a store
+        // instruction is 64 scattered transactions, and one per record made
+        // the stores the kernel's limit
+        uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;
+        const bool al16 = (reinterpret_cast<uintptr_t>(opo) & 15u) == 0;
+        auto emit = [&](uint32_t rec) {
+            const uint32_t k = nops & 3u;
+            b0 = k == 0 ? rec : b0;
+            b1 = k == 1 ? rec : b1;
+            b2 = k == 2 ? rec : b2;
+            b3 = k == 3 ? rec : b3;
+            if (k == 3) {
+                if (al16) {
+                    reinterpret_cast<uint4*>(opo)[nops >> 2] = make_uint4(b0, b1, b2, b3);
+                } else {  // a member whose output does not start 16-byte aligned
+                    opo[nops - 3] = b0; opo[nops - 2] = b1; opo[nops - 1] = b2; opo[nops] = b3;
+                }
+            }
+            ++nops;
+        };
         while (produced < T) {
             in.fill();
             uint32_t e = S.lit.fast[in.peek() & (uint32_t)(DecLit::kSize - 1)];
@@ -1906,7 +1927,7 @@ __global__ __launch_bounds__(64) void k_tlz_ops(DecArgs a) {
                 const float f = __uint_as_float(bytes);
                 const int id = (int)f;
                 if (!(id >= 0 && id < 32 && __float_as_uint((float)id) == bytes)) { err = kInfCorrupt; break; }
-                opo[nops++] = 0x80000000u | (uint32_t)id;
+                emit(0x80000000u | (uint32_t)id);
                 produced += 1;
             } else if (kind == (uint32_t)kKindCopy) {
                 const uint32_t len = (e >> 16) + in.get((int)((e >> 4) & 15u));
@@ -1919,7 +1940,7 @@ __global__ __launch_bounds__(64) void k_tlz_ops(DecArgs a) {
                 const uint32_t lt = len >> 2, dt = d >> 2;
                 if ((len & 3u) || (d & 3u) || lt < (uint32_t)kMinL || lt > (uint32_t)kMaxL || produced + lt > T ||
                     dt > before + produced || dt > (uint32_t)kWin) { err = kInfCorrupt; break; }
-                opo[nops++] = lt | (dt << 7);
+                emit(lt | (dt << 7));
                 produced += lt;
             } else {
                 err = kInfCorrupt;
@@ -1939,6 +1960,12 @@ __global__ __launch_bounds__(64) void k_tlz_ops(DecArgs a) {
                     if ((in.pos() - dbit + 7u) / 8u != in_len) err = kInfCorrupt;
                 }
             }
+        }
+        {  // the last < 4 records
+            const uint32_t k = nops & 3u, q = nops & ~3u;
+            if (k > 0) opo[q] = b0;
+            if (k > 1) opo[q + 1] = b1;
+            if (k > 2) opo[q + 2] = b2;
         }
         a.cnt[m * kMemSeg + s] = nops;
         if (err) atomicOr(a.status, err);
