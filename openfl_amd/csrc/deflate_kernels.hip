@@ -1976,7 +1976,12 @@ __global__ __launch_bounds__(64) void k_tlz_ops(DecArgs a) {
 // value's source (pointer jumping in LDS; sources before the segment are in
 // the value ring), the values as float32, CRC-32 of the member, ISIZE.
 constexpr int kRNT = 256, kRPer = kSeg / kRNT;     // resolve: threads per member block, values per thread
+// resolve's CRC advances: table i advances by 2^(5 + i) bytes for i < 7 (a
+// thread's 32 bytes .. a wave's 2 KiB), table 7 by a segment's 8 KiB
+static_assert(kSegLog == 11, "resolve's CRC tables assume 2048-value segments");
+DEVI int adv_k(int i) { return i < 7 ? 5 + i : 13; }
 struct ResSmem {
+    uint32_t adv[8][8][16];        // CRC advance by 2^adv_k(i) bytes, per input nibble (table form of c_adv)
     uint8_t v[kRing];              // ids by member position (ring)
     uint32_t opr[kSeg];            // the segment's op records
     uint16_t e[kSeg];              // 0x8000 | id (resolved) or the distance to the source
@@ -2003,12 +2008,27 @@ __global__ __launch_bounds__(kRNT) void k_tlz_resolve(DecArgs a) {
         S.crct[0][tid] = r;
     }
     if (tid == 0) S.crc_raw = 0;
+    // the advances as nibble tables: adv(x) = XOR_j T[j][nibble j of x], 8
+    // independent LDS reads instead of a 32-step loop over the matrix columns
+    for (int e = tid; e < 8 * 8 * 16; e += kRNT) {
+        const int i = e >> 7, j = (e >> 4) & 7, v = e & 15;
+        uint32_t r = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) r ^= ((v >> b) & 1) ? c_adv[adv_k(i)][4 * j + b] : 0u;
+        S.adv[i][j][v] = r;
+    }
     __syncthreads();
     for (int k = 1; k < 4; ++k) {
         const uint32_t p = S.crct[k - 1][tid];
         S.crct[k][tid] = (p >> 8) ^ S.crct[0][p & 0xffu];
         __syncthreads();
     }
+    auto advt = [&](uint32_t x, int i) -> uint32_t {
+        uint32_t r = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r ^= S.adv[i][j][(x >> (4 * j)) & 15u];
+        return r;
+    };
     int bad = 0;
     for (int s = 0; s < nseg; ++s) {
         const int c0 = s << kSegLog;
@@ -2084,7 +2104,7 @@ __global__ __launch_bounds__(kRNT) void k_tlz_resolve(DecArgs a) {
 #pragma unroll
                 for (int l = 0; l < 6; ++l) {
                     const uint32_t o = (uint32_t)__shfl_xor((int)x, 1 << l, 64);
-                    const uint32_t sh = crc_adv_pow2(x, 5 + l);
+                    const uint32_t sh = advt(x, l);  // 2^(5 + l) bytes
                     x = (lane & (1 << l)) ? x : (sh ^ o);
                 }
                 wcrc = x;
@@ -2099,8 +2119,8 @@ __global__ __launch_bounds__(kRNT) void k_tlz_resolve(DecArgs a) {
         if (tid == 0) {
             uint32_t raw = 0;
             if (T == kSeg) {
-                for (int w = 0; w < kRNT / 64; ++w) raw = crc_adv_pow2(raw, kSegLog) ^ S.crc_w[w];
-                S.crc_raw = crc_adv_pow2(S.crc_raw, kSegLog + 2) ^ raw;
+                for (int w = 0; w < kRNT / 64; ++w) raw = advt(raw, 6) ^ S.crc_w[w];  // 2^kSegLog bytes
+                S.crc_raw = advt(S.crc_raw, 7) ^ raw;                                   // 2^(kSegLog + 2)
             } else {
                 for (int w = 0; w < kRNT / 64; ++w) raw ^= S.crc_w[w];
                 S.crc_raw = crc_adv(S.crc_raw, 4u * (uint32_t)T) ^ raw;
