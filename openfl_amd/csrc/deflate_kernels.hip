@@ -925,6 +925,7 @@ struct EncSmem {
     uint8_t ll[kLit], ld[kDist], lc[kCL];
     uint16_t kl[kLit], kd[kDist], kc[kCL];
     uint32_t crct[4][256];                         // slicing-by-4 CRC-32 tables
+    uint32_t adv13[8][16];                         // CRC advance by a segment's 8 KiB, per input nibble
     uint32_t segop[kMemSeg + 1], segbit[kMemSeg];
     uint32_t scan[kNT / 64];
     uint32_t crc_w[kNT / 64];
@@ -1055,6 +1056,12 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         uint32_t r = (uint32_t)tid;
         for (int k = 0; k < 8; ++k) r = (r & 1u) ? (r >> 1) ^ 0xEDB88320u : r >> 1;
         S.crct[0][tid] = r;
+    } else if (tid < 256 + 128) {  // the per-segment CRC advance as nibble tables
+        const int e = tid - 256, j = e >> 4, v = e & 15;
+        uint32_t r = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) r ^= ((v >> b) & 1) ? c_adv[kSegLog + 2][4 * j + b] : 0u;
+        S.adv13[j][v] = r;
     }
     for (int i = tid; i < kBuckets; i += kNT) {
         S.head[0][i] = S.head[1][i] = 0;
@@ -1129,7 +1136,12 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             // of the full segments so far (each advanced by the 8 KiB of every
             // later segment); the last segment's piece and the combination
             // over the threads follow the loop
-            if (c + 1 < nseg) crc_acc = crc_adv_pow2(crc_acc, kSegLog + 2) ^ crc;
+            if (c + 1 < nseg) {
+                uint32_t adv = 0;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) adv ^= S.adv13[j][(crc_acc >> (4 * j)) & 15u];
+                crc_acc = adv ^ crc;
+            }
             else crc_last = crc, nv_last = nv;
         }
         __syncthreads();
