@@ -926,6 +926,7 @@ struct EncSmem {
     uint16_t kl[kLit], kd[kDist], kc[kCL];
     uint32_t crct[4][256];                         // slicing-by-4 CRC-32 tables
     uint32_t adv13[8][16];                         // CRC advance by a segment's 8 KiB, per input nibble
+    uint32_t cid4[kPer][32];                       // raw CRC of a thread's 16 bytes with only value q = id (from 0)
     uint32_t segop[kMemSeg + 1], segbit[kMemSeg];
     uint32_t scan[kNT / 64];
     uint32_t crc_w[kNT / 64];
@@ -1080,6 +1081,18 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         }
         __syncthreads();
     }
+    // the raw CRC is linear: a thread's 16 bytes (4 values, ids < 32) hash to
+    // the XOR of one table entry per value, 4 independent reads instead of
+    // 16 dependent ones
+    if (tid < kPer * 32) {
+        const int q = tid >> 5;
+        const uint32_t bits = __float_as_uint((float)(tid & 31));
+        uint32_t cr = 0;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) cr = crc4(S.crct, cr, k == q ? bits : 0u);
+        S.cid4[q][tid & 31] = cr;
+    }
+    __syncthreads();
     tlz_model(S, tid, true);
 
     uint32_t crc_acc = 0, crc_last = 0;
@@ -1119,8 +1132,14 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                     if (!(t >= 0 && t < 32 && bits == __float_as_uint((float)t))) bad = true;
                     const uint32_t id = (t >= 0 && t < 32) ? (uint32_t)t : 0u;
                     idw[q >> 2] |= id << (8 * (q & 3));
-                    crc = crc4(S.crct, crc, bits);
+                    crc ^= S.cid4[q][id];  // (a bad value fails the member: its CRC is never used)
                 }
+            }
+            if (nv < kPer) {  // a partial last piece: the values' own chain
+                crc = 0;
+#pragma unroll
+                for (int q = 0; q < kPer; ++q)
+                    if (q < nv) crc = crc4(S.crct, crc, __float_as_uint(v[q]));
             }
             if (bad) atomicOr(&S.bad, 1);
             for (int b = tid; b < kBuckets; b += kNT)  // the chains' wave tables (they share memory with the DP's costs)
@@ -1991,9 +2010,11 @@ constexpr int kRNT = 256, kRPer = kSeg / kRNT;     // resolve: threads per membe
 // resolve's CRC advances: table i advances by 2^(5 + i) bytes for i < 7 (a
 // thread's 32 bytes .. a wave's 2 KiB), table 7 by a segment's 8 KiB
 static_assert(kSegLog == 11, "resolve's CRC tables assume 2048-value segments");
+static_assert(kRPer * 32 == kRNT, "one thread per (value slot, id) entry of the resolve's CRC table");
 DEVI int adv_k(int i) { return i < 7 ? 5 + i : 13; }
 struct ResSmem {
     uint32_t adv[8][8][16];        // CRC advance by 2^adv_k(i) bytes, per input nibble (table form of c_adv)
+    uint32_t cid[kRPer][32];       // raw CRC of a thread's 32 bytes with only value q = id (from 0)
     uint8_t v[kRing];              // ids by member position (ring)
     uint32_t opr[kSeg];            // the segment's op records
     uint16_t e[kSeg];              // 0x8000 | id (resolved) or the distance to the source
@@ -2035,6 +2056,15 @@ __global__ __launch_bounds__(kRNT) void k_tlz_resolve(DecArgs a) {
         S.crct[k][tid] = (p >> 8) ^ S.crct[0][p & 0xffu];
         __syncthreads();
     }
+    {  // the raw CRC is linear: a thread's 32 bytes hash to the XOR of one entry per value
+        const int q = tid >> 5;
+        const uint32_t bits = __float_as_uint((float)(tid & 31));
+        uint32_t cr = 0;
+#pragma unroll
+        for (int k = 0; k < kRPer; ++k) cr = crc4(S.crct, cr, k == q ? bits : 0u);
+        S.cid[q][tid & 31] = cr;
+    }
+    __syncthreads();
     auto advt = [&](uint32_t x, int i) -> uint32_t {
         uint32_t r = 0;
 #pragma unroll
@@ -2100,8 +2130,14 @@ __global__ __launch_bounds__(kRNT) void k_tlz_resolve(DecArgs a) {
                 f[q] = (float)id;
                 if (q < nv) {
                     S.v[(c0 + k0 + q) & (kRing - 1)] = (uint8_t)id;
-                    crc = crc4(S.crct, crc, __float_as_uint(f[q]));
+                    crc ^= S.cid[q][id];
                 }
+            }
+            if (nv < kRPer) {  // a partial last piece: the values' own chain
+                crc = 0;
+#pragma unroll
+                for (int q = 0; q < kRPer; ++q)
+                    if (q < nv) crc = crc4(S.crct, crc, __float_as_uint(f[q]));
             }
             if (nv == kRPer && (reinterpret_cast<uintptr_t>(yo + k0) & 15u) == 0) {
                 float4* y4 = reinterpret_cast<float4*>(yo + k0);
