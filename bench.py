@@ -342,10 +342,12 @@ def kc_pipeline(steps, warmup, dev, extras=True):
         roof["traffic_unit"] = "HBM bytes per step (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction)"
         roof["traffic_source"] = (os.path.relpath(KC_TRAFFIC_JSON, ROOT)
                                   + " (rocprofv3 --pmc passes of tools/kc_bench.py, KC kernels only, not this run)")
-        pk = (tj.get("kernels") or {}).get(name) if name else None
-        if pk and pk.get("dispatches_per_step"):
-            roof["dominant_kernel"]["traffic_per_launch"] = pk["hbm_bytes_per_step"] / pk["dispatches_per_step"] \
-                if "hbm_bytes_per_step" in pk else None
+        # PMC bytes per dispatch of the dominant kernel (the traffic file's names
+        # carry the namespace, e.g. gz::tlz::k_tlz_encode for tlz::k_tlz_encode)
+        kern_pmc = tj.get("kernels") or {}
+        pk = next((v for k, v in kern_pmc.items() if name and (k == name or k.endswith("::" + name))), None)
+        if pk:
+            roof["dominant_kernel"]["traffic_per_launch"] = pk["read_bytes_per_dispatch"] + pk["write_bytes_per_dispatch"]
     if not extras:
         return {"value": round(nbytes / wall / 2 ** 30, 3), "unit": "GiB/s", "ms_per_step": round(1e3 * wall, 3),
                 "phases_ms": phases, "wire_ratio": round(len(z) / nbytes, 4), "roofline": roof,
