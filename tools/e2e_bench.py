@@ -183,12 +183,14 @@ def main():
         pipe = EdenPipeline(n_bits=8, dim_threshold=100, device="cuda:0", combine=combine)
         rounds = []
         with ThreadPoolExecutor(max_workers=len(sds)) as ex:
-            for r in range(int(os.environ.get("E2E_ROUNDS", "3"))):
+            for r in range(int(os.environ.get("E2E_ROUNDS", "5"))):
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 outs = list(ex.map(lambda sd: run_plugin(sd, pipe, P), sds))
-                dt = time.perf_counter() - t0
-                rounds.append(round(dt, 4))
+                rounds.append(round(time.perf_counter() - t0, 4))
+        # the median of the rounds after the first (single rounds vary by
+        # up to 2x with the host's scheduling of the two caller threads)
+        dt = float(np.median(rounds[1:])) if len(rounds) > 1 else rounds[0]
         c = pipe.transformers[0]
         nb = sum(x.batches for x in list(c._fwd_comb.values()) + list(c._bwd_comb.values()))
         ni = sum(x.items for x in list(c._fwd_comb.values()) + list(c._bwd_comb.values()))
