@@ -1241,11 +1241,12 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         int nf[kPer];
         {
             // chain candidates in increasing distance, branch-free: a
-            // candidate's first 16 values are compared at once (5 aligned LDS
-            // dwords, the 8 positions' loads issued together); only a match of
-            // 16 or more values walks further (rare)
+            // candidate's first 8 values are compared at once (3 aligned LDS
+            // dwords, the 4 positions' loads issued together); a match of 8
+            // or more values walks further behind one wave-uniform test (12
+            // values at once cost 4 % more encode time for the same stream)
             const uint32_t* tw = reinterpret_cast<const uint32_t*>(S.tok);
-            constexpr int kCW = 3;  // values compared at once: 4 kCW
+            constexpr int kCW = 2;  // values compared at once: 4 kCW
             uint32_t ti[kPer][kCW];  // values i .. i + 4 kCW - 1 of each position
             {
                 const int rb = (lo & (kRing - 1)) >> 2;  // lo is a multiple of 8
