@@ -403,9 +403,10 @@ int ofl_wavg_delta32_ranges(int ncollab, const float* const* xs, const double* w
  * 0..31 (the ranks the lossy pipelines write; anything else -> OFL_EINVAL,
  * nothing written).  out: HOST buffer of out_cap >= ofl_gzip_ranks_bound(n)
  * bytes; *out_len = stream length.  When out is mapped pinned memory
- * (hipHostMalloc, torch pin_memory) the kernels write the stream into it
- * directly and the batches of members run without host round trips; pageable
- * memory gets one D2H per batch.  ws: device, ofl_gzip_ranks_workspace_bytes(n).
+ * (hipHostMalloc, torch pin_memory) each batch of members is packed into
+ * device staging and crosses PCIe by one DMA while the next batch encodes;
+ * pageable memory gets one synchronous D2H per batch.  ws: device,
+ * ofl_gzip_ranks_workspace_bytes(n).
  * Synchronous.  Deterministic (the header's mtime is 0).  Errors:
  * ofl_gzip_last_error(). */
 const char* ofl_gzip_last_error(void);
@@ -413,6 +414,14 @@ size_t ofl_gzip_ranks_workspace_bytes(int64_t n);
 size_t ofl_gzip_ranks_bound(int64_t n);
 int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size_t* out_len, void* ws,
                    size_t ws_bytes, void* stream);
+/* ofl_gzip_ranks that also leaves the stream in host_dst (HOST, pageable,
+ * host_cap >= out_cap bytes, e.g. the payload object's own buffer): each
+ * batch's bytes are copied out of `out` on nthreads host threads as soon as
+ * its DMA completes, while the next batch encodes, so only the last batch's
+ * copy follows the GPU work (GZIPTransformer.forward returns a fresh bytes,
+ * kc_pipeline.py:128-141). */
+int ofl_gzip_ranks_to(const float* x, int64_t n, uint8_t* out, size_t out_cap, uint8_t* host_dst, size_t host_cap,
+                      int nthreads, size_t* out_len, void* ws, size_t ws_bytes, void* stream);
 /* GZIPTransformer.backward (kc_pipeline.py:152-156: gzip.decompress) for a
  * stream whose members all carry a size field ('OZ', or BGZF's 'BC'):
  * members are located from their headers and inflated (zlib) on nthreads host

@@ -2462,9 +2462,13 @@ size_t ofl_gzip_ranks_bound(int64_t n) {
     return (size_t)L.members * L.slot;
 }
 
-int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size_t* out_len, void* ws,
-                   size_t ws_bytes, void* stream) {
+// host_dst (optional): a pageable buffer of host_cap bytes that receives the
+// stream too, each batch copied on nthreads host threads while the next batch
+// encodes (ofl_gzip_ranks_to)
+static int gzip_ranks_impl(const float* x, int64_t n, uint8_t* out, size_t out_cap, uint8_t* host_dst,
+                           size_t host_cap, int nthreads, size_t* out_len, void* ws, size_t ws_bytes, void* stream) {
     if (n < 1 || !x || !out || !out_len) return gzfail(OFL_EINVAL, "gzip ranks: empty input");
+    if (host_dst && host_cap < out_cap) return gzfail(OFL_EINVAL, "gzip ranks: host_cap < out_cap");
     if (!ws || ws_bytes < ofl_gzip_ranks_workspace_bytes(n)) return gzfail(OFL_ESPACE, "gzip ranks: workspace too small");
     GZHIP(ofl_util::per_device_once([] {  // __constant__ tables and attributes are per device
         uint32_t m[32][32];
@@ -2545,6 +2549,16 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
             GZHIP(hipEventCreateWithFlags(&ev_scan[i], hipEventDisableTiming));
         }
         GZHIP(hipMemsetAsync(running, 0, sizeof(uint64_t), st));
+        uint64_t copied = 0, bend[2] = {0, 0};  // host_dst holds out[0, copied); batch ends
+        auto host_copy = [&](uint64_t upto) {  // out[copied, upto) -> host_dst (its DMA complete)
+            if (host_dst && upto > copied) {
+                void* d = host_dst + copied;
+                const void* src = out + copied;
+                const int64_t nb = (int64_t)(upto - copied);
+                ofl_host_copy_many(1, &d, &src, &nb, nthreads);
+                copied = upto;
+            }
+        };
         GZHIP(hipEventRecord(ev_pack[1], st));  // orders the side stream after the memsets
         GZHIP(hipStreamWaitEvent(sd, ev_pack[1], 0));
         int err = 0;
@@ -2553,6 +2567,7 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
             const int nb = (int)std::min<int64_t>(L.batch, L.members - k * L.batch);
             GZHIP(hipEventSynchronize(ev_scan[b]));
             const uint64_t first = hinfo[2 * b], end = hinfo[2 * b + 1];
+            bend[b] = first == ~0ull ? 0 : end;
             gzprof_begin(sd);
             if (first != ~0ull && end - first <= L.stage) {
                 hipLaunchKernelGGL(gz::k_gzip_pack, dim3(nb), dim3(256), 0, sd, slots2[b], (uint64_t)L.slot, sizes2[b],
@@ -2585,6 +2600,10 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
             GZHIP(hipMemcpyAsync(hinfo + 2 * b + 1, off2[b] + nb, 8, hipMemcpyDeviceToHost, sd));
             GZHIP(hipEventRecord(ev_scan[b], sd));
             if (hipGetLastError() != hipSuccess) err = 1;
+            if (host_dst && k >= 1 && !err) {  // batch k - 1's bytes, while batch k encodes
+                GZHIP(hipEventSynchronize(ev_pack[(k - 1) & 1]));
+                host_copy(bend[(k - 1) & 1]);
+            }
         }
         if (!err)
             if (int rc = finish(nbatch - 1)) return rc;
@@ -2604,6 +2623,7 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
         if (badh & 1) return gzfail(OFL_EINVAL, "gzip ranks: values must be float32 integers 0..31");
         if (badh & 2) return gzfail(OFL_ESPACE, "gzip ranks: output buffer too small");
         total = tot;
+        host_copy(total);
     }
     for (int64_t c0 = 0; !dout && c0 < L.members; c0 += L.batch) {
         const int nb = (int)std::min<int64_t>(L.batch, L.members - c0);
@@ -2621,6 +2641,7 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
         if (total + tot > out_cap) return gzfail(OFL_ESPACE, "gzip ranks: output buffer too small");
         GZHIP(hipMemcpyAsync(out + total, packed, tot, hipMemcpyDeviceToHost, st));
         GZHIP(hipStreamSynchronize(st));
+        if (host_dst) memcpy(host_dst + total, out + total, tot);
         total += tot;
     }
     if (d_ph) {
@@ -2636,6 +2657,17 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
     }
     *out_len = total;
     return OFL_OK;
+}
+
+int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size_t* out_len, void* ws,
+                   size_t ws_bytes, void* stream) {
+    return gzip_ranks_impl(x, n, out, out_cap, nullptr, 0, 1, out_len, ws, ws_bytes, stream);
+}
+
+int ofl_gzip_ranks_to(const float* x, int64_t n, uint8_t* out, size_t out_cap, uint8_t* host_dst, size_t host_cap,
+                      int nthreads, size_t* out_len, void* ws, size_t ws_bytes, void* stream) {
+    if (!host_dst) return gzfail(OFL_EINVAL, "gzip ranks to: null host_dst");
+    return gzip_ranks_impl(x, n, out, out_cap, host_dst, host_cap, std::max(1, nthreads), out_len, ws, ws_bytes, stream);
 }
 
 // Host inflate of a member-indexed gzip stream (every member carries the

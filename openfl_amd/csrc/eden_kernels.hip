@@ -3610,11 +3610,11 @@ struct StageRing {
     char* slot[kStageMaxThreads][kStageSlots] = {};
     hipEvent_t ev[kStageMaxThreads][kStageSlots] = {};
     bool used[kStageMaxThreads][kStageSlots] = {};
+    static StageRing& get() {  // a member: the enclosing extern "C" block gives free functions C linkage
+        static StageRing* r = new StageRing;  // never destroyed (pinned memory outlives static teardown order)
+        return *r;
+    }
 };
-StageRing& stage_ring() {
-    static StageRing* r = new StageRing;  // never destroyed (pinned memory outlives static teardown order)
-    return *r;
-}
 }  // namespace
 
 int ofl_copy_h2d_staged(void* dst_dev, const void* src_host, size_t bytes, int nthreads, void* stream) {
@@ -3624,7 +3624,7 @@ int ofl_copy_h2d_staged(void* dst_dev, const void* src_host, size_t bytes, int n
     hipStream_t st = static_cast<hipStream_t>(stream);
     const size_t nchunk = (bytes + kStageChunk - 1) / kStageChunk;
     const int nt = (int)std::min<size_t>(nchunk, (size_t)std::max(1, std::min(nthreads, kStageMaxThreads)));
-    StageRing& R = stage_ring();
+    StageRing& R = StageRing::get();
     std::lock_guard<std::mutex> g(R.mu);
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));

@@ -256,6 +256,42 @@ def bytes_from(src_addr, n, threads=8, huge_min=8 << 20, par_min=1 << 20):
     return b
 
 
+def new_payload(cap):
+    """(b, addr) for a producer that writes a payload of at most cap bytes
+    straight into a new `bytes` (e.g. ofl_gzip_ranks_to, batch by batch while
+    the GPU works): an uninitialised object of capacity cap nobody else holds,
+    its 2 MiB-aligned interior marked MADV_HUGEPAGE as in bytes_from.  Pages
+    the producer never writes are never touched.  Finish it with
+    seal_payload(b, n) before anyone else sees it.  None below 8 MiB, with
+    OFL_HOST_RECYCLE=1 (that mode refills pooled payloads via bytes_from) or
+    when the CPython layout check fails."""
+    cap = int(cap)
+    if cap < _RECYCLE_MIN or _RECYCLE or not _bytes_layout_ok():
+        return None
+    b = _new_bytes(None, cap)
+    a = _bytes_addr(b)
+    lo = (a + _HUGE - 1) // _HUGE * _HUGE
+    hi = (a + cap) // _HUGE * _HUGE
+    if hi > lo:
+        _c().madvise(lo, hi - lo, _MADV_HUGEPAGE)  # advisory: a refusal only costs speed
+    return b, a
+
+
+def seal_payload(b, n):
+    """Set a new_payload object's length to the n bytes written (n <= its
+    capacity; the allocation keeps its capacity, untouched pages cost
+    nothing) and track it like a bytes_from payload.  Returns b."""
+    n = int(n)
+    a = id(b)
+    if not 0 <= n <= ctypes.c_ssize_t.from_address(a + 16).value:
+        raise ValueError("seal_payload: length exceeds the capacity")
+    ctypes.c_ssize_t.from_address(a + 16).value = n   # ob_size; ob_shash is still -1 (never hashed)
+    ctypes.c_char.from_address(a + 32 + n).value = b"\0"
+    _release_dead()
+    _remember(b, n)
+    return b
+
+
 def _fill(dst, src_addr, n, threads, huge_min, piece):
     if n >= huge_min:
         lo = (dst + _HUGE - 1) // _HUGE * _HUGE

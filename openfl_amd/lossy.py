@@ -268,15 +268,22 @@ def gzip_ranks(x):
     # pinned output sized for a rank stream (a quarter of the input: rank
     # streams compress to 0.05-0.2); the worst-case bound (1.5x the input)
     # only after an OFL_ESPACE
+    # the payload `bytes` is filled batch by batch while the GPU encodes the
+    # next batch (ofl_gzip_ranks_to); small streams are copied afterwards
     for cap in (min(bound, n + (1 << 20)), bound):
         out = _buf("host", "gz_out", cap, pinned=True)
         ln = ctypes.c_size_t()
-        rc = L.ofl_gzip_ranks(x.data_ptr(), n, out.data_ptr(), cap, ctypes.byref(ln), ws.data_ptr(), ws.numel(),
-                              _stream(x.device))
+        dst = hostmem.new_payload(cap)
+        if dst is not None:
+            rc = L.ofl_gzip_ranks_to(x.data_ptr(), n, out.data_ptr(), cap, dst[1], cap, _GZ_COPY_THREADS,
+                                     ctypes.byref(ln), ws.data_ptr(), ws.numel(), _stream(x.device))
+        else:
+            rc = L.ofl_gzip_ranks(x.data_ptr(), n, out.data_ptr(), cap, ctypes.byref(ln), ws.data_ptr(), ws.numel(),
+                                  _stream(x.device))
         if rc != _lib.OFL_ESPACE or cap == bound:
             break
     _lib.check_gzip(rc)
-    payload = hostmem.bytes_from(out.data_ptr(), ln.value)
+    payload = hostmem.seal_payload(dst[0], ln.value) if dst is not None else hostmem.bytes_from(out.data_ptr(), ln.value)
     _trim_bufs()
     return payload
 
@@ -421,6 +428,7 @@ def gunzip_device(data, out):
 
 
 _H2D_THREADS = int(os.environ.get("OFL_H2D_THREADS", "2"))  # host threads staging a large pageable payload (0: one plain hipMemcpyAsync)
+_GZ_COPY_THREADS = int(os.environ.get("OFL_GZ_COPY_THREADS", "8"))  # host threads filling the gzip payload
 
 
 def _h2d(L, dst, src, nbytes, stream):

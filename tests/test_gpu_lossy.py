@@ -663,6 +663,34 @@ def test_gzip_ranks_deterministic_repeats(case):
         assert lossy.gzip_ranks(xd) == z
 
 
+def test_gzip_ranks_to_matches_pinned_path():
+    """The payload filled batch by batch while the GPU encodes
+    (ofl_gzip_ranks_to, lossy.gzip_ranks' path above 8 MiB) is byte for byte
+    the stream ofl_gzip_ranks leaves in pinned memory, over three full batches
+    of 512 members and a ragged fourth; it decodes with gzip.decompress."""
+    import ctypes
+    from openfl_amd import _lib, lossy
+    n = 3 * (1 << 26) + 12345
+    g = torch.Generator(device=DEV).manual_seed(5)
+    p = torch.tensor([0.1, 0.2, 0.4, 0.2, 0.1], device=DEV)
+    x = torch.empty(n, dtype=torch.float32, device=DEV)
+    for o in range(0, n, 1 << 24):
+        m = min(1 << 24, n - o)
+        x[o:o + m] = torch.multinomial(p, m, replacement=True, generator=g).to(torch.float32)
+    z = lossy.gzip_ranks(x)
+    L = _lib.lib()
+    cap = int(L.ofl_gzip_ranks_bound(n))
+    out = torch.empty(cap, dtype=torch.uint8).pin_memory()
+    ws = torch.empty(int(L.ofl_gzip_ranks_workspace_bytes(n)), dtype=torch.uint8, device=DEV)
+    ln = ctypes.c_size_t()
+    _lib.check_gzip(L.ofl_gzip_ranks(x.data_ptr(), n, out.data_ptr(), cap, ctypes.byref(ln), ws.data_ptr(),
+                                     ws.numel(), torch.cuda.current_stream().cuda_stream))
+    assert type(z) is bytes and len(z) == ln.value
+    assert z == out[:ln.value].numpy().tobytes()
+    assert hash(z) == hash(bytes(memoryview(z)))
+    assert gzip.decompress(z) == x.cpu().numpy().tobytes()
+
+
 def test_gzip_ranks_full_size_kc_set():
     """BASELINE config 3 at its full size (2^28 ranks = the 1 GiB set): the
     device gzip's stream is a valid gzip stream whose gzip.decompress is the

@@ -189,3 +189,35 @@ def test_release_pauses_inside_quiet(monkeypatch):
         t_open = time.monotonic()
     assert done.wait(5)
     assert len(calls) >= 3 and min(calls) >= t_open   # 8 MiB slices, all after the section closed
+
+
+def test_new_payload_seal(monkeypatch):
+    """new_payload / seal_payload (the gzip payload filled by the producer in
+    place): the sealed object is an ordinary bytes of the written length --
+    content, len, hash, slicing and protobuf use match bytes() of the source;
+    below 8 MiB or with recycling on the helper declines; a length above the
+    capacity is refused."""
+    import ctypes
+    from openfl_amd import protocols
+    monkeypatch.setattr(hostmem, "_RECYCLE", False)
+    hostmem.release_pool()
+    assert hostmem.new_payload((8 << 20) - 1) is None
+    cap, n = 12 << 20, (9 << 20) + 7
+    src = _src(21, n)
+    b, addr = hostmem.new_payload(cap)
+    assert len(b) == cap
+    ctypes.memmove(addr, src.ctypes.data, n)
+    with pytest.raises(ValueError):
+        hostmem.seal_payload(b, cap + 1)
+    assert hostmem.seal_payload(b, n) is b
+    want = src.tobytes()
+    assert len(b) == n and b == want and hash(b) == hash(want)
+    assert b[-7:] == want[-7:] and b[n:] == b""
+    nt = protocols.NamedTensor(name="w", round_number=1, lossless=False, report=False, data_bytes=b)
+    back = protocols.NamedTensor()
+    back.ParseFromString(nt.SerializeToString())
+    assert back.data_bytes == want
+    assert any(e[0] is b for e in hostmem._pool)
+    monkeypatch.setattr(hostmem, "_RECYCLE", True)
+    assert hostmem.new_payload(cap) is None
+    hostmem.release_pool()

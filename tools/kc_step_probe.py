@@ -28,7 +28,7 @@ def main():
     class Timed:
         def __getattr__(self, name):
             f = getattr(real, name)
-            if name not in ("ofl_gzip_ranks", "ofl_gzip_member_index", "ofl_inflate_tlz", "ofl_copy_h2d_staged"):
+            if name not in ("ofl_gzip_ranks", "ofl_gzip_ranks_to", "ofl_gzip_member_index", "ofl_inflate_tlz", "ofl_copy_h2d_staged"):
                 return f
 
             def w(*a):
