@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -881,7 +882,10 @@ constexpr int kPer = kSeg / kNT;                   // positions per thread
 constexpr int kWin = 8192;                         // window, values (32 KiB)
 constexpr int kMaxL = 64, kMinL = 3;               // copy length, values
 #ifndef OFL_TLZ_CAND
-#define OFL_TLZ_CAND 16
+// 12 chain candidates: encode 14.0 -> 12.8 ms per GiB of KC ranks for a 0.3 %
+// larger stream (ratio 0.1165 vs 0.1162 at 16; gzip -9: 0.1173;
+// profiles/r04_tlz_cand_ab2.txt)
+#define OFL_TLZ_CAND 12
 #endif
 #ifndef OFL_TLZ_SWEEPS
 #define OFL_TLZ_SWEEPS 4
@@ -2550,14 +2554,33 @@ static int gzip_ranks_impl(const float* x, int64_t n, uint8_t* out, size_t out_c
         }
         GZHIP(hipMemsetAsync(running, 0, sizeof(uint64_t), st));
         uint64_t copied = 0, bend[2] = {0, 0};  // host_dst holds out[0, copied); batch ends
+        // diagnostics: OFL_GZ_FILL_TRACE=1 prints the host's wait / copy times per call
+        static const bool fill_trace = getenv("OFL_GZ_FILL_TRACE") != nullptr;
+        auto now_us = [] {
+            return (double)std::chrono::duration_cast<std::chrono::microseconds>(
+                       std::chrono::steady_clock::now().time_since_epoch()).count();
+        };
+        const double t_call = fill_trace ? now_us() : 0.0;
+        char trace[512];
+        int tn = 0;
         auto host_copy = [&](uint64_t upto) {  // out[copied, upto) -> host_dst (its DMA complete)
             if (host_dst && upto > copied) {
+                const double t0 = fill_trace ? now_us() : 0.0;
                 void* d = host_dst + copied;
                 const void* src = out + copied;
                 const int64_t nb = (int64_t)(upto - copied);
                 ofl_host_copy_many(1, &d, &src, &nb, nthreads);
                 copied = upto;
+                if (fill_trace && tn < 400)
+                    tn += snprintf(trace + tn, sizeof(trace) - tn, " copy@%.0f+%.0f", t0 - t_call, now_us() - t0);
             }
+        };
+        auto sync_pack = [&](int b) -> hipError_t {
+            const double t0 = fill_trace ? now_us() : 0.0;
+            const hipError_t e = hipEventSynchronize(ev_pack[b]);
+            if (fill_trace && tn < 400)
+                tn += snprintf(trace + tn, sizeof(trace) - tn, " wait@%.0f+%.0f", t0 - t_call, now_us() - t0);
+            return e;
         };
         GZHIP(hipEventRecord(ev_pack[1], st));  // orders the side stream after the memsets
         GZHIP(hipStreamWaitEvent(sd, ev_pack[1], 0));
@@ -2601,7 +2624,7 @@ static int gzip_ranks_impl(const float* x, int64_t n, uint8_t* out, size_t out_c
             GZHIP(hipEventRecord(ev_scan[b], sd));
             if (hipGetLastError() != hipSuccess) err = 1;
             if (host_dst && k >= 1 && !err) {  // batch k - 1's bytes, while batch k encodes
-                GZHIP(hipEventSynchronize(ev_pack[(k - 1) & 1]));
+                GZHIP(sync_pack((int)((k - 1) & 1)));
                 host_copy(bend[(k - 1) & 1]);
             }
         }
@@ -2623,7 +2646,9 @@ static int gzip_ranks_impl(const float* x, int64_t n, uint8_t* out, size_t out_c
         if (badh & 1) return gzfail(OFL_EINVAL, "gzip ranks: values must be float32 integers 0..31");
         if (badh & 2) return gzfail(OFL_ESPACE, "gzip ranks: output buffer too small");
         total = tot;
+        if (fill_trace && tn < 400) tn += snprintf(trace + tn, sizeof(trace) - tn, " sync@%.0f", now_us() - t_call);
         host_copy(total);
+        if (fill_trace) fprintf(stderr, "gzip fill (us):%s end@%.0f\n", trace, now_us() - t_call);
     }
     for (int64_t c0 = 0; !dout && c0 < L.members; c0 += L.batch) {
         const int nb = (int)std::min<int64_t>(L.batch, L.members - c0);

@@ -273,7 +273,7 @@ def gzip_ranks(x):
     for cap in (min(bound, n + (1 << 20)), bound):
         out = _buf("host", "gz_out", cap, pinned=True)
         ln = ctypes.c_size_t()
-        dst = hostmem.new_payload(cap)
+        dst = hostmem.new_payload(cap) if _GZ_FILL else None
         if dst is not None:
             rc = L.ofl_gzip_ranks_to(x.data_ptr(), n, out.data_ptr(), cap, dst[1], cap, _GZ_COPY_THREADS,
                                      ctypes.byref(ln), ws.data_ptr(), ws.numel(), _stream(x.device))
@@ -429,6 +429,7 @@ def gunzip_device(data, out):
 
 _H2D_THREADS = int(os.environ.get("OFL_H2D_THREADS", "2"))  # host threads staging a large pageable payload (0: one plain hipMemcpyAsync)
 _GZ_COPY_THREADS = int(os.environ.get("OFL_GZ_COPY_THREADS", "8"))  # host threads filling the gzip payload
+_GZ_FILL = os.environ.get("OFL_GZ_FILL", "1") != "0"  # 0: copy the payload after the call (A/B)
 
 
 def _h2d(L, dst, src, nbytes, stream):
