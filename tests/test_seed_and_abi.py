@@ -247,3 +247,18 @@ def test_one_call_host_entry_points_check_their_block_layout():
     assert L.ofl_eden_decode_host(p.handle, a, a, 8192, 256, 256, a, a, 4000, None, 0, None) == _lib.OFL_EINVAL
     assert L.ofl_eden_decode_host(p.handle, a, a, 8192, 256, 1024, a, a, 4004, None, 0, None) == _lib.OFL_EINVAL
     assert L.ofl_eden_encode_host(None, a, a, 8192, 4096, a, a, 8192, 1024, None, 0, None) == _lib.OFL_EINVAL
+
+
+def test_gzip_ranks_to_checks_its_host_buffer():
+    """ofl_gzip_ranks_to refuses a missing or too small host destination
+    before touching the GPU (OFL_EINVAL, with a message)."""
+    import ctypes
+    from openfl_amd import _lib
+    L = _lib.lib()
+    buf = ctypes.create_string_buffer(1 << 12)
+    a = ctypes.addressof(buf)
+    ln = ctypes.c_size_t()
+    assert L.ofl_gzip_ranks_to(a, 1000, a, 4096, None, 4096, 8, ctypes.byref(ln), a, 4096, None) == _lib.OFL_EINVAL
+    assert b"host_dst" in L.ofl_gzip_last_error()
+    assert L.ofl_gzip_ranks_to(a, 1000, a, 4096, a, 4095, 8, ctypes.byref(ln), a, 4096, None) == _lib.OFL_EINVAL
+    assert b"host_cap" in L.ofl_gzip_last_error()
