@@ -893,6 +893,7 @@ constexpr int kMaxL = 64, kMinL = 3;               // copy length, values
 constexpr int kCand = OFL_TLZ_CAND;                // chain candidates per position (A/B: -DOFL_TLZ_CAND)
 constexpr int kBuckets = 512;                      // 3-gram buckets: exact for values < 8, hashed (into the same) above
 constexpr int kBucketBits = 9;
+static_assert(kBuckets == 1 << kBucketBits, "bucket ids are kBucketBits wide");
 constexpr int kSweeps = OFL_TLZ_SWEEPS;            // DP sweeps (segments of kPer = 4 positions; tools/tlz_proto.c)
 constexpr int kRing = 16384;                       // value ring (ids), + 8 mirrored bytes
 constexpr int kLitMax = 11, kDistMax = 10;         // code length limits = the inflate's table bits
@@ -1186,7 +1187,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             const int bk = act ? bucket(S.tok, p) : 0;
             uint64_t m = __ballot(act);
 #pragma unroll
-            for (int b = 0; b < 10; ++b) {
+            for (int b = 0; b < kBucketBits; ++b) {  // buckets < 2^kBucketBits
                 const bool on = ((bk >> b) & 1) != 0;
                 const uint64_t bb = __ballot(act && on);
                 m &= on ? bb : ~bb;
