@@ -2564,26 +2564,7 @@ static int gzip_ranks_impl(const float* x, int64_t n, uint8_t* out, size_t out_c
         const double t_call = fill_trace ? now_us() : 0.0;
         char trace[512];
         int tn = 0;
-        // the next batch's pages of host_dst are faulted in while the GPU still
-        // encodes it (a write per 4 KiB; the bytes are overwritten by its copy),
-        // so the copy after the last batch runs on resident pages
-        uint64_t faulted = 0;
-        auto prefault = [&](uint64_t upto) {
-            upto = std::min<uint64_t>(upto, host_cap);
-            if (!host_dst || upto <= std::max(faulted, copied)) return;
-            const uint64_t lo = std::max(faulted, copied);
-            const int nt = std::max(1, std::min(nthreads, (int)((upto - lo) >> 22) + 1));
-            auto touch = [&](int t) {
-                const uint64_t a = lo + (upto - lo) * t / nt, e = lo + (upto - lo) * (t + 1) / nt;
-                for (uint64_t i = a; i < e; i = (i | 4095u) + 1) host_dst[i] = 0;
-            };
-            std::vector<std::thread> th;
-            for (int t = 1; t < nt; ++t) th.emplace_back(touch, t);
-            touch(0);
-            for (auto& x : th) x.join();
-            faulted = upto;
-        };
-        auto host_copy = [&](uint64_t upto, bool ahead) {  // out[copied, upto) -> host_dst (its DMA complete)
+        auto host_copy = [&](uint64_t upto) {  // out[copied, upto) -> host_dst (its DMA complete)
             if (host_dst && upto > copied) {
                 const double t0 = fill_trace ? now_us() : 0.0;
                 void* d = host_dst + copied;
@@ -2591,7 +2572,6 @@ static int gzip_ranks_impl(const float* x, int64_t n, uint8_t* out, size_t out_c
                 const int64_t nb = (int64_t)(upto - copied);
                 ofl_host_copy_many(1, &d, &src, &nb, nthreads);
                 copied = upto;
-                if (ahead) prefault(copied + nb + nb / 4);
                 if (fill_trace && tn < 400)
                     tn += snprintf(trace + tn, sizeof(trace) - tn, " copy@%.0f+%.0f", t0 - t_call, now_us() - t0);
             }
@@ -2646,7 +2626,7 @@ static int gzip_ranks_impl(const float* x, int64_t n, uint8_t* out, size_t out_c
             if (hipGetLastError() != hipSuccess) err = 1;
             if (host_dst && k >= 1 && !err) {  // batch k - 1's bytes, while batch k encodes
                 GZHIP(sync_pack((int)((k - 1) & 1)));
-                host_copy(bend[(k - 1) & 1], true);
+                host_copy(bend[(k - 1) & 1]);
             }
         }
         if (!err)
@@ -2668,7 +2648,7 @@ static int gzip_ranks_impl(const float* x, int64_t n, uint8_t* out, size_t out_c
         if (badh & 2) return gzfail(OFL_ESPACE, "gzip ranks: output buffer too small");
         total = tot;
         if (fill_trace && tn < 400) tn += snprintf(trace + tn, sizeof(trace) - tn, " sync@%.0f", now_us() - t_call);
-        host_copy(total, false);
+        host_copy(total);
         if (fill_trace) fprintf(stderr, "gzip fill (us):%s end@%.0f\n", trace, now_us() - t_call);
     }
     for (int64_t c0 = 0; !dout && c0 < L.members; c0 += L.batch) {
