@@ -138,15 +138,27 @@ def _drop_later(objs):
 
 
 def _release_dead():
-    """Default mode: hand tracked payloads nobody else references (and those
-    tracked longer than _POOL_IDLE_S) to the release thread."""
+    """Default mode: hand tracked payloads nobody else references to the
+    release thread (their pages are discarded there).  Payloads tracked longer
+    than _POOL_IDLE_S that someone still references are only forgotten: the
+    pool drops its reference and the caller's own references free the object
+    as usual, untouched.  Only a refcount-1 object (the pool's entry is its
+    last reference, so nothing outside this module can reach it) is ever
+    handed to _release."""
     import time
     now = time.monotonic()
+    dead = []
     with _pool_lock:
-        dead = [e[0] for e in _pool if _refcount_is_pool_only(e) or now - e[2] > _POOL_IDLE_S]
-        if dead:
-            keep = [e for e in _pool if not any(e[0] is d for d in dead)]
+        keep = []
+        for i in range(len(_pool)):
+            if _refcount_is_pool_only(_pool[i]):
+                dead.append(_pool[i][0])
+            elif now - _pool[i][2] <= _POOL_IDLE_S:
+                keep.append(_pool[i])
+            # else: live and idle -> forgotten (its reference dropped with the old list)
+        if len(keep) != len(_pool):
             _pool[:] = keep
+        keep = None
     _drop_later(dead)
 
 

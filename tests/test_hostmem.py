@@ -147,6 +147,71 @@ def test_default_mode_never_rewrites_a_payload(monkeypatch):
     assert k1 is not None
 
 
+def _wait_release_thread():
+    if hostmem._reaper is not None:
+        hostmem._reaper.submit(lambda: None).result(30)
+
+
+@needs_layout
+@pytest.mark.parametrize("holder", ["local", "attribute"])
+def test_idle_payloads_still_held_are_never_discarded(monkeypatch, holder):
+    """A payload the caller still holds past the pool's idle window (here
+    0.1 s) is only forgotten by the pool, never discarded: a bytes_from
+    payload and a seal_payload payload, held directly or only through a plain
+    attribute (a pure-python protobuf-style holder), keep their bytes while
+    two more large payloads are made after the window has passed."""
+    import ctypes
+    import time
+    monkeypatch.setattr(hostmem, "_RECYCLE", False)
+    monkeypatch.setattr(hostmem, "_POOL_IDLE_S", 0.1)
+    hostmem.release_pool()
+    _wait_release_thread()
+    n = 9 << 20
+    a, c = _src(31, n), _src(32, n + 11)
+    b1 = hostmem.bytes_from(a.ctypes.data, n)
+    b2, addr = hostmem.new_payload(n + 4096)
+    ctypes.memmove(addr, c.ctypes.data, n + 11)
+    hostmem.seal_payload(b2, n + 11)
+
+    class Holder:   # what a pure-python message does with a bytes field
+        pass
+    h = Holder()
+    if holder == "attribute":
+        h.data_bytes, h.other = b1, b2
+        del b1, b2
+        get = lambda: (h.data_bytes, h.other)   # noqa: E731
+    else:
+        get = lambda: (b1, b2)   # noqa: E731
+    time.sleep(0.25)
+    for k in range(2):
+        s = _src(40 + k, n)
+        assert hostmem.bytes_from(s.ctypes.data, n) == s.tobytes()
+    _wait_release_thread()
+    x1, x2 = get()
+    assert x1 == a.tobytes() and x2 == c.tobytes()
+    assert not any(e[0] is x1 or e[0] is x2 for e in hostmem._pool)   # forgotten, not freed
+    hostmem.release_pool()
+
+
+@needs_layout
+def test_idle_entry_aged_by_hand_is_not_discarded(monkeypatch):
+    """The advisor's recipe: age a held payload's pool entry by hand, make
+    another payload, check the held bytes."""
+    monkeypatch.setattr(hostmem, "_RECYCLE", False)
+    hostmem.release_pool()
+    _wait_release_thread()
+    n = 8 << 20
+    a, c = _src(51, n), _src(52, n)
+    held = hostmem.bytes_from(a.ctypes.data, n)
+    for e in hostmem._pool:
+        if e[0] is held:
+            e[2] -= 10 * hostmem._POOL_IDLE_S + 1
+    hostmem.bytes_from(c.ctypes.data, n)
+    _wait_release_thread()
+    assert held == a.tobytes()
+    hostmem.release_pool()
+
+
 def test_release_pool_drops_tracked_payloads(monkeypatch):
     monkeypatch.setattr(hostmem, "_RECYCLE", False)
     hostmem.release_pool()
