@@ -1758,7 +1758,7 @@ struct DecSmem {
     uint8_t lens[320];
 };
 struct DecArgs {
-    const uint8_t* src;      // device stream (readable 32 bytes past every member)
+    const uint8_t* src;      // device stream (readable 64 bytes past every member: BitIn's look-ahead at the end bound)
     const int64_t* idx;      // per member: data offset, data length | kind << 62, output offset, isize | crc << 32
     int64_t nmem;
     uint8_t* out;
@@ -1840,6 +1840,19 @@ __global__ __launch_bounds__(64) void k_tlz_ops(DecArgs a) {
         return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
     };
     const uint64_t dbit = 8ull * (uint64_t)doff;  // the data's first bit in the stream
+    // the segment table is untrusted input: every entry must lie inside the
+    // member's data and the entries must increase, or no lane may start a
+    // decoder there (a bad entry would send BitIn far outside the stream)
+    const uint64_t ebit = dbit + 8ull * (uint64_t)in_len;  // one past the data's last bit
+    {
+        const uint32_t sb = lane < nseg ? seg_bit(lane) : 0u;
+        const uint32_t sp = lane > 0 && lane < nseg ? seg_bit(lane - 1) : 0u;
+        const bool bad = lane < nseg && ((uint64_t)sb >= 8ull * (uint64_t)in_len || (lane > 0 && sb <= sp));
+        if (__ballot(bad)) {
+            if (lane == 0) atomicOr(a.status, kInfCorrupt);
+            return;
+        }
+    }
     // ---- the block header, on every lane (wave-uniform) ----
     BitIn in;
     in.start(a.src, dbit);
@@ -1862,6 +1875,7 @@ __global__ __launch_bounds__(64) void k_tlz_ops(DecArgs a) {
         const int total = nlit + ndist;
         int i = 0;
         while (!err && i < total) {
+            if (in.pos() > ebit) { err = kInfCorrupt; break; }  // ran past the data (wave-uniform)
             in.fill();
             const uint32_t e = S.lit.fast[in.peek() & (uint32_t)(DecLit::kSize - 1)];
             const int l = (int)(e & 15u);
@@ -1943,6 +1957,9 @@ __global__ __launch_bounds__(64) void k_tlz_ops(DecArgs a) {
             ++nops;
         };
         while (produced < T) {
+            // a corrupt segment must not decode on past its member: one op
+            // reads at most ~48 bytes beyond pos (the stream is padded for that)
+            if (in.pos() > ebit) { err = kInfCorrupt; break; }
             in.fill();
             uint32_t e = S.lit.fast[in.peek() & (uint32_t)(DecLit::kSize - 1)];
             int l = (int)(e & 15u);
@@ -2319,6 +2336,7 @@ size_t member_at(const uint8_t* src, size_t n, size_t pos, GzMember& m) {
     if (12 + xlen > n - pos) return 0;
     size_t bsize = 0;
     bool tlz = false;
+    const uint8_t* zf = nullptr;  // the OZ subfield's payload
     for (size_t q = 12; q + 4 <= 12 + xlen;) {
         const size_t sl = (size_t)h[q + 2] | ((size_t)h[q + 3] << 8);
         if (q + 4 + sl > 12 + xlen) return 0;
@@ -2330,6 +2348,7 @@ size_t member_at(const uint8_t* src, size_t n, size_t pos, GzMember& m) {
             // the segment table must end where the deflate data starts
             tlz = z[0] == 1 && z[1] == gz::tlz::kSegLog && sl == 12 + 4 * nseg && q + 4 + sl == 12 + xlen &&
                   nseg >= 1 && nseg <= (size_t)gz::tlz::kMemSeg;
+            zf = tlz ? z : nullptr;
         }
         q += 4 + sl;
     }
@@ -2341,7 +2360,7 @@ size_t member_at(const uint8_t* src, size_t n, size_t pos, GzMember& m) {
     m.isize = (uint32_t)t[4] | ((uint32_t)t[5] << 8) | ((uint32_t)t[6] << 16) | ((uint32_t)t[7] << 24);
     // a TLZ member's value count (the OZ field) must match its ISIZE
     if (tlz) {
-        const uint8_t* z = h + 16;
+        const uint8_t* z = zf;
         const size_t ntok = (size_t)z[8] | ((size_t)z[9] << 8) | ((size_t)z[10] << 16) | ((size_t)z[11] << 24);
         const size_t nseg = (size_t)z[2] | ((size_t)z[3] << 8);
         tlz = (m.isize & 3u) == 0 && ntok == m.isize / 4 && nseg == (ntok + gz::tlz::kSeg - 1) / gz::tlz::kSeg;
@@ -2548,6 +2567,18 @@ static int gzip_ranks_impl(const float* x, int64_t n, uint8_t* out, size_t out_c
         GZHIP(gz_pinned_info(&hinfo));  // [2][2]: a batch's first offset and end
         const int64_t nbatch = (L.members + L.batch - 1) / L.batch;
         hipEvent_t ev_enc[2] = {}, ev_pack[2] = {}, ev_scan[2] = {};
+        // every exit (the GZHIP / finish error returns included) waits for the
+        // work queued on both streams -- scan, pack and D2H read ws and write
+        // out -- before the caller may reuse those buffers, then frees the events
+        bool drained = false;
+        ofl_util::ScopeExit cleanup([&] {
+            if (!drained) { (void)hipStreamSynchronize(sd); (void)hipStreamSynchronize(st); }
+            for (int i = 0; i < 2; ++i) {
+                if (ev_enc[i]) (void)hipEventDestroy(ev_enc[i]);
+                if (ev_pack[i]) (void)hipEventDestroy(ev_pack[i]);
+                if (ev_scan[i]) (void)hipEventDestroy(ev_scan[i]);
+            }
+        });
         for (int i = 0; i < 2; ++i) {
             GZHIP(hipEventCreateWithFlags(&ev_enc[i], hipEventDisableTiming));
             GZHIP(hipEventCreateWithFlags(&ev_pack[i], hipEventDisableTiming));
@@ -2638,11 +2669,7 @@ static int gzip_ranks_impl(const float* x, int64_t n, uint8_t* out, size_t out_c
         GZHIP(hipMemcpyAsync(&tot, running, 8, hipMemcpyDeviceToHost, st));
         GZHIP(hipMemcpyAsync(&badh, bad, sizeof(int), hipMemcpyDeviceToHost, st));
         GZHIP(hipStreamSynchronize(st));
-        for (int i = 0; i < 2; ++i) {
-            (void)hipEventDestroy(ev_enc[i]);
-            (void)hipEventDestroy(ev_pack[i]);
-            (void)hipEventDestroy(ev_scan[i]);
-        }
+        drained = true;  // st waited for everything sd ran
         if (err) return gzfail(OFL_EHIP, "gzip ranks: kernel launch failed");
         if (badh & 1) return gzfail(OFL_EINVAL, "gzip ranks: values must be float32 integers 0..31");
         if (badh & 2) return gzfail(OFL_ESPACE, "gzip ranks: output buffer too small");

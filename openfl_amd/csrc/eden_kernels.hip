@@ -46,6 +46,7 @@
 #include <map>
 #include <set>
 #include <atomic>
+#include <condition_variable>
 #include <mutex>
 #include <thread>
 #include <string>
@@ -3599,20 +3600,47 @@ int ofl_copy_h2d_async(void* dst_dev, const void* src_host, size_t bytes, void* 
 }
 
 namespace {
-// Pinned staging ring of ofl_copy_h2d_staged: kStageSlots slots per thread,
-// each with the event of the DMA that last read it.  Process-wide, allocated
-// on first use and kept (hipHostMalloc is slow; 64 MiB at most).
+// Pinned staging rings of ofl_copy_h2d_staged: a ring is kStageSlots slots
+// per thread, each with the event of the DMA that last read it.  Rings belong
+// to one device (their events do) and are lent to one call at a time from
+// that device's pool: concurrent calls -- on different GPUs, or several on one
+// -- take different rings and never hold a common lock while they copy; up to
+// kStageRings rings per device are made (a caller beyond that waits for one to
+// come back).  Allocated on first use and kept (hipHostMalloc is slow; 64 MiB
+// per ring at most).
 constexpr size_t kStageChunk = 4u << 20;
-constexpr int kStageSlots = 2, kStageMaxThreads = 8;
+constexpr int kStageSlots = 2, kStageMaxThreads = 8, kStageRings = 4;
 struct StageRing {
-    std::mutex mu;
-    int device = -1;
     char* slot[kStageMaxThreads][kStageSlots] = {};
     hipEvent_t ev[kStageMaxThreads][kStageSlots] = {};
     bool used[kStageMaxThreads][kStageSlots] = {};
-    static StageRing& get() {  // a member: the enclosing extern "C" block gives free functions C linkage
-        static StageRing* r = new StageRing;  // never destroyed (pinned memory outlives static teardown order)
-        return *r;
+};
+struct StagePool {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::map<int, std::vector<StageRing*>> idle;
+    std::map<int, int> made;
+    static StagePool& get() {  // a member: the enclosing extern "C" block gives free functions C linkage
+        static StagePool* p = new StagePool;  // never destroyed (pinned memory outlives static teardown order)
+        return *p;
+    }
+    StageRing* take(int dev) {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return !idle[dev].empty() || made[dev] < kStageRings; });
+        if (!idle[dev].empty()) {
+            StageRing* r = idle[dev].back();
+            idle[dev].pop_back();
+            return r;
+        }
+        ++made[dev];
+        return new StageRing;
+    }
+    void give(int dev, StageRing* r) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            idle[dev].push_back(r);
+        }
+        cv.notify_one();
     }
 };
 }  // namespace
@@ -3624,22 +3652,11 @@ int ofl_copy_h2d_staged(void* dst_dev, const void* src_host, size_t bytes, int n
     hipStream_t st = static_cast<hipStream_t>(stream);
     const size_t nchunk = (bytes + kStageChunk - 1) / kStageChunk;
     const int nt = (int)std::min<size_t>(nchunk, (size_t)std::max(1, std::min(nthreads, kStageMaxThreads)));
-    StageRing& R = StageRing::get();
-    std::lock_guard<std::mutex> g(R.mu);
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
-    if (R.device != dev) {  // events belong to a device: a call on another one rebuilds them
-        for (int t = 0; t < kStageMaxThreads; ++t)
-            for (int s = 0; s < kStageSlots; ++s) {
-                if (R.ev[t][s]) {
-                    HIP_TRY(hipEventSynchronize(R.ev[t][s]));
-                    HIP_TRY(hipEventDestroy(R.ev[t][s]));
-                    R.ev[t][s] = nullptr;
-                }
-                R.used[t][s] = false;
-            }
-        R.device = dev;
-    }
+    StagePool& P = StagePool::get();
+    StageRing& R = *P.take(dev);
+    ofl_util::ScopeExit back([&] { P.give(dev, &R); });
     for (int t = 0; t < nt; ++t)
         for (int s = 0; s < kStageSlots; ++s) {
             if (!R.slot[t][s]) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&R.slot[t][s]), kStageChunk, hipHostMallocDefault));

@@ -26,6 +26,16 @@ hipError_t per_device_once(F f) {
     return r;
 }
 
+// runs f() when the scope ends, on every return path
+template <typename F>
+struct ScopeExit {
+    F f;
+    explicit ScopeExit(F fn) : f(fn) {}
+    ~ScopeExit() { f(); }
+    ScopeExit(const ScopeExit&) = delete;
+    ScopeExit& operator=(const ScopeExit&) = delete;
+};
+
 }  // namespace ofl_util
 
 namespace ofl {

@@ -378,8 +378,9 @@ def gunzip_device(data, out):
     nm, tot, mx, tl = ctypes.c_int64(), ctypes.c_size_t(), ctypes.c_uint32(), ctypes.c_int()
     # the stream goes H2D straight from the payload, on a pool thread while
     # this one indexes the members (both release the GIL); the inflate
-    # kernels read up to 32 bytes past the stream, hence the padding
-    d_in = _buf(dev, "gz_in", src.size + 64)
+    # kernels read up to ~48 bytes past a member's data (its 8-byte trailer
+    # included) before they stop on corrupt data, hence the padding
+    d_in = _buf(dev, "gz_in", src.size + 128)
     # d_in belongs to the caller's current stream, and the inflate runs there:
     # the pool thread enqueues the copy on that same stream
     caller_stream = torch.cuda.current_stream(dev)

@@ -427,6 +427,34 @@ def test_tlz_rejects_corrupt_streams():
     bad[28 + 4] ^= 0x01
     assert gzip.decompress(bytes(bad)) == x.tobytes()
     assert lossy.gunzip_device(bytes(bad), out).cpu().numpy().tobytes() == x.tobytes()
+    # the segment table is untrusted: entries far past the member (high byte
+    # flipped), non-increasing entries, every entry misaligned by 3 bits, and
+    # the last member's last entry on its final bit must neither fault nor
+    # decode wrongly (the TLZ decoder refuses them, the generic inflate reads
+    # the plain deflate data, which is intact)
+    starts = [0]
+    while starts[-1] < len(z):
+        starts.append(starts[-1] + int.from_bytes(z[starts[-1] + 20:starts[-1] + 24], "little"))
+    assert starts[-1] == len(z) and len(starts) >= 3
+    ns = _nseg(z)
+    cases = []
+    b = bytearray(z); b[28 + 4 + 3] ^= 0xFF; cases.append(b)                      # noqa: E702
+    b = bytearray(z); b[28 + 8:28 + 12] = b[28 + 4:28 + 8]; cases.append(b)       # noqa: E702
+    b = bytearray(z)
+    for s in range(1, ns):   # entry 0 is checked against the header's end
+        e = 28 + 4 * s
+        b[e:e + 4] = (int.from_bytes(b[e:e + 4], "little") + 3).to_bytes(4, "little")
+    cases.append(b)
+    last = starts[-2]
+    nl = int.from_bytes(z[last + 18:last + 20], "little")
+    in_len = (starts[-1] - last) - (28 + 4 * nl) - 8
+    b = bytearray(z)
+    e = last + 28 + 4 * (nl - 1)
+    b[e:e + 4] = (8 * in_len - 1).to_bytes(4, "little")
+    cases.append(b)
+    for b in cases:
+        assert gzip.decompress(bytes(b)) == x.tobytes()
+        assert lossy.gunzip_device(bytes(b), out).cpu().numpy().tobytes() == x.tobytes()
 
 
 def test_gzip_ranks_rejects_non_ranks():
@@ -639,6 +667,37 @@ def test_copy_h2d_staged(n, threads):
         torch.cuda.synchronize()
         assert d[:n].cpu().numpy().tobytes() == arr.tobytes()
         assert bool(d[n:].eq(7).all())
+
+
+def test_copy_h2d_staged_concurrent_threads():
+    """Four threads copying at once, each on its own stream and buffer (the
+    staging rings are lent per call from a per-device pool, so no call waits
+    for another's copy or rebuilds another's events): every copy byte-exact,
+    the bytes past each copy untouched, over several rounds of mixed sizes
+    and thread counts."""
+    from concurrent.futures import ThreadPoolExecutor
+    from openfl_amd import _lib
+    L = _lib.lib()
+    sizes = [(9 << 20) + 5, (17 << 20) + 4093, 12 << 20, (33 << 20) + 1]
+
+    def job(i):
+        rng = np.random.default_rng(100 + i)
+        st = torch.cuda.Stream(DEV)
+        ok = True
+        with torch.cuda.stream(st):
+            d = torch.full((max(sizes) + 64,), 7, dtype=torch.uint8, device=DEV)
+            for rep in range(4):
+                n = sizes[(i + rep) % len(sizes)]
+                arr = rng.integers(0, 256, n, dtype=np.uint8)
+                d.fill_(7)
+                _lib.check(L.ofl_copy_h2d_staged(d.data_ptr(), arr.ctypes.data, n, 1 + (i + rep) % 4,
+                                                 st.cuda_stream))
+                st.synchronize()
+                ok &= d[:n].cpu().numpy().tobytes() == arr.tobytes()
+                ok &= bool(d[n:].eq(7).all())
+        return ok
+    with ThreadPoolExecutor(4) as ex:
+        assert all(ex.map(job, range(4)))
 
 
 @pytest.mark.parametrize("case", ["ternary", "kc6", "runs"])
