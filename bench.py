@@ -372,6 +372,11 @@ def kc_pipeline(steps, warmup, dev, extras=True):
     # (the opt-in host-memory policy, openfl_amd.hostmem.keep_large_blocks,
     # is process-wide, so it is not applied here: tools/kc_bench.py --hostmem
     # times it in a process of its own)
+    # cpu_baseline: the restated CPU pipeline (oracle/kc.py: sklearn KMeans
+    # k=6 n_init=6 -> ranks -> gzip -9, then gunzip -> LUT, per tensor as the
+    # reference calls it) on a bounded sample -- the first KC_CPU_SAMPLE
+    # elements of the first four tensors -- extrapolated linearly to the set
+    cpu = kc_cpu_baseline(x, offs, numels, cores)
     # host inflate variant (native threads into pinned staging, then H2D of the ranks)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -391,9 +396,31 @@ def kc_pipeline(steps, warmup, dev, extras=True):
             "host_inflate_variant": {"inflate_h2d_ms": round(1e3 * t_host_inflate, 3),
                                      "scope": f"ofl_gunzip_members on {cores} host threads + H2D of the ranks, "
                                               "in place of the device inflate"},
+            "cpu_baseline": cpu,
             "tensors": len(numels), "bytes": nbytes, "steps": steps, "host_threads": cores,
             "scope": "KCPipeline forward+backward of the set, gzip in the timed region (one member-indexed "
                      "stream for the arena; each tensor's payload is its run of members)"}
+
+
+KC_CPU_SAMPLE = 1 << 18  # elements per sampled tensor (4 tensors: 4 MiB, ~10-20 s of CPU work)
+
+
+def kc_cpu_baseline(x, offs, numels, cores, per=KC_CPU_SAMPLE, ntens=4):
+    """The restated KC pipeline (oracle/kc.py) timed on the host on a bounded
+    sample: the first `per` elements of the first `ntens` tensors of the set,
+    each as one tensor through forward + backward, in order.  sklearn's KMeans
+    runs on its OpenMP threads (OMP_NUM_THREADS, 16 on the GPU box), gzip -9 on
+    one thread, as in the reference.  The rate extrapolates linearly to the
+    set (every tensor of the set has the same size and distribution)."""
+    from oracle import kc as K
+    sample = [x[offs[j]:offs[j] + min(per, numels[j])].cpu().numpy() for j in range(min(ntens, len(numels)))]
+    t_f, t_b, zb = K.time_pipeline(sample)
+    nb = sum(4 * s.size for s in sample)
+    return {"value": round(nb / 2 ** 30 / (t_f + t_b), 6), "unit": "GiB/s", "cores": cores, "kind": "port",
+            "sample": f"first {per} elements of tensors 0..{len(sample) - 1} ({nb / 2 ** 20:.1f} MiB) through "
+                      f"oracle/kc.py (sklearn KMeans k=6 n_init=6 on {cores} OpenMP threads, ranks, gzip -9 and "
+                      f"gunzip single-threaded, LUT) as the reference's per-tensor calls; forward {t_f:.2f} s, "
+                      f"backward {t_b:.2f} s, wire ratio {zb / nb:.4f}; extrapolated linearly to the 1 GiB set"}
 
 
 # ---------------------------------------------------------------- dry run ---

@@ -81,6 +81,25 @@ DEVI int len_code(uint32_t l) {
     const int b = 31 - __builtin_clz(m);
     return 4 * (b - 1) + (int)((m >> (b - 2)) & 3u);
 }
+// a length's / distance's code with its extra bits computed (no table
+// loads: the tables are in constant memory, and a per-lane index into them is
+// a vector memory load per lookup): l, d in bytes, l in 11..258, d >= 1
+DEVI void len_sym(uint32_t l, int& lc, int& ne, uint32_t& ev) {
+    const uint32_t m = l - 3u;
+    if (m < 8u) { lc = (int)m; ne = 0; ev = 0; return; }
+    const int b = 31 - __builtin_clz(m);
+    lc = 4 * (b - 1) + (int)((m >> (b - 2)) & 3u);
+    ne = b - 2;
+    ev = m & ((1u << ne) - 1u);
+}
+DEVI void dist_sym(uint32_t d, int& dc, int& ne, uint32_t& ev) {
+    const uint32_t m = d - 1u;
+    if (d <= 4u) { dc = (int)m; ne = 0; ev = 0; return; }
+    const int b = 31 - __builtin_clz(m);
+    dc = 2 * b + (int)((m >> (b - 1)) & 1u);
+    ne = b - 1;
+    ev = m & ((1u << ne) - 1u);
+}
 // advance by 2^k zero bytes (k uniform: the matrix columns are scalar loads)
 DEVI uint32_t crc_adv_pow2(uint32_t v, int k) {
     uint32_t r = 0;
@@ -856,16 +875,16 @@ __global__ __launch_bounds__(64, OFL_INF_WAVES) void k_inflate_members(InfArgs a
 //     | values (u32) | nseg x u32 segment bit offsets
 //   deflate data (one block, BFINAL = 1, BTYPE = 2) | CRC-32 | ISIZE
 //
-// Encoder (k_tlz_encode, one 256-thread block per member, a segment at a
+// Encoder (k_tlz_encode, one 512-thread block per member, a segment at a
 // time): 3-gram chains (per-wave ballot matching, then the waves' and the
 // earlier segments' last occurrences), the longest-match frontier of every
-// position over 16 chain candidates (1 <= 3 (length, distance) pairs), an
-// optimal parse by a segmented backward DP (each thread its 8 positions, the
-// other threads' costs from the previous sweep, 3 sweeps) under a cost model
-// re-estimated from the member's symbol counts after every segment, the DP's
-// path followed by Jacobi rounds (every thread walks its 8 positions from
-// its left neighbour's exit until no entry changes), then one Huffman code per
-// member and the bits.  The parse is what gzip -9 lacks: 0.115 of the input
+// position over kCand (12) chain candidates (1 <= 3 (length, distance)
+// pairs), an optimal parse by a segmented backward DP (each thread its 4
+// positions, the other threads' costs from the previous sweep, 4 sweeps)
+// under a cost model re-estimated from the member's symbol counts after every
+// segment, the DP's path followed by Jacobi rounds (every thread walks its 4
+// positions from its left neighbour's exit until no entry changes), then one
+// Huffman code per member and the bits.  The parse is what gzip -9 lacks: 0.115 of the input
 // on KC ranks against gzip -9's 0.117 (tools/tlz_proto.c simulates it).
 // Decoder: k_tlz_ops (one wavefront per member, one lane per segment:
 // Huffman decode from the segment's bit offset with the member's tables in
@@ -910,7 +929,7 @@ struct EncSmem {
             uint16_t prev[kRing];                  // distance to the previous same-bucket position (0: none), by position mod kRing
             union {
                 uint16_t lastw[kNT / 64][kBuckets];  // chains: per wave, this segment: position - range start + 1
-                uint16_t cost[2][kSeg + 8];        // then the DP's costs to the segment end, 1/8 bit, mod 2^16
+                uint32_t cost[2][kSeg + 8];        // then the DP's costs to the segment end, 1/8 bit
                 uint32_t hw[kNT / 64][(kLit + kDist + 1) / 2];  // then per-wave symbol counts of the segment, two u16 per word
             };
         } m;
@@ -918,6 +937,9 @@ struct EncSmem {
             HScratch h;
             uint32_t hdrw[kHdrW];
             uint8_t hb[kHdrFixed + 4 * kMemSeg];
+            // the bit emission's tables (code | extra bits) << 0 | n << 24:
+            // a literal value's first two and last two bytes, a copy length
+            uint32_t litlo[32], lithi[32], lenw[kMaxL + 1];
         } f;
     } u;
     uint32_t head[2][kBuckets];                    // last position + 1 per bucket (earlier segments); segment c reads [c & 1], writes [~c & 1]
@@ -929,7 +951,7 @@ struct EncSmem {
     uint16_t litc[32], lenc[kMaxL + 1], dcst[kDist];
     uint8_t ll[kLit], ld[kDist], lc[kCL];
     uint16_t kl[kLit], kd[kDist], kc[kCL];
-    uint32_t crct[4][256];                         // slicing-by-4 CRC-32 tables
+    uint32_t crct[1][256];                         // CRC-32 byte table (the word tables went to the DP's 32-bit costs)
     uint32_t adv13[8][16];                         // CRC advance by a segment's 8 KiB, per input nibble
     uint32_t cid4[kPer][32];                       // raw CRC of a thread's 16 bytes with only value q = id (from 0)
     uint32_t segop[kMemSeg + 1], segbit[kMemSeg];
@@ -980,9 +1002,13 @@ DEVI int match_len(const uint8_t* tok, int i, int j, int lim) {
     }
     return min(L, lim);
 }
+// raw CRC-32 of one little-endian word, a byte at a time (T: the byte table);
+// used only at set-up and for a member's partial last piece
 DEVI uint32_t crc4(const uint32_t (*T)[256], uint32_t c, uint32_t w) {
     c ^= w;
-    return T[3][c & 0xffu] ^ T[2][(c >> 8) & 0xffu] ^ T[1][(c >> 16) & 0xffu] ^ T[0][c >> 24];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c = (c >> 8) ^ T[0][c & 0xffu];
+    return c;
 }
 // 1/8 bit: -log2(count / total) >= 1 bit, an unseen symbol log2(total + 1) + 2
 // bits, at most 15 bits
@@ -1079,13 +1105,6 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     if (tid < kCL) S.hc[tid] = 0;
     if (tid == 0) { S.totl = S.totd = 0; S.ops_n = 0; S.crc_raw = 0; S.bad = 0; }
     __syncthreads();
-    for (int k = 1; k < 4; ++k) {
-        if (tid < 256) {
-            const uint32_t p = S.crct[k - 1][tid];
-            S.crct[k][tid] = (p >> 8) ^ S.crct[0][p & 0xffu];
-        }
-        __syncthreads();
-    }
     // the raw CRC is linear: a thread's 16 bytes (4 values, ids < 32) hash to
     // the XOR of one table entry per value, 4 independent reads instead of
     // 16 dependent ones
@@ -1345,14 +1364,19 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         }
         PH(3);
         // ---- D: segmented backward DP (kSweeps sweeps) ----
-        // The per-position state is kept packed, so that the whole segment
-        // loop fits the 128 VGPRs of two blocks per CU: unpacked (13
-        // registers per position) it spilled, and the spills' scratch
-        // traffic reached HBM (3.6 GB per 512-member launch, PMC).
-        //   pk[q]  = La | Lb << 7 | (Lm + 1) << 14 | literal cost << 21
-        //   dc3[q] = distance costs of entries a | b << 8 | c << 16 (each <= 224)
-        //   lx0/lx1[q] = the entries' own long lengths (> kU) and their
-        //            length + distance costs, (l | cost << 7) in 16 bits
+        // Costs are absolute (1/8 bit to the segment end, < 2^20: 2048 values
+        // x 4 literals x 15 bits x 8), so a candidate is one 32-bit key
+        // (cost << 3 | candidate index) and the best of a position is a plain
+        // min: the index orders the candidates as the old strict-less scan
+        // did (literal, lengths kMinL..kU, the three frontier entries), so
+        // ties keep the earlier one and the parse is unchanged.  The sweep-
+        // invariant part of every candidate is precomputed per position, 16
+        // bits each (0xffff: no such candidate; a candidate's cost differs
+        // from the literal's by < 3100, so it then never wins):
+        //   cA[q] = literal | length 3 << 16, cB[q] = 4 | 5 << 16,
+        //   cC[q] = 6 | entry a << 16, cD[q] = entry b | entry c << 16;
+        //   a length l: its length + distance cost; an entry (its own length
+        //   > kU): l | cost << 7, 0 = none
         uint32_t dc3[kPer];
 #pragma unroll
         for (int q = 0; q < kPer; ++q) {
@@ -1364,7 +1388,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         __syncthreads();  // the wave tables are dead: the DP's costs take their memory
         for (int k = tid; k <= kSeg; k += kNT) {
             const int rem = max(0, send - c0 - k);
-            S.u.m.cost[1][k] = (uint16_t)(32u * (uint32_t)rem);  // sweep 0's estimate beyond a thread's positions: 4 bits per value
+            S.u.m.cost[1][k] = 32u * (uint32_t)rem;  // sweep 0's estimate beyond a thread's positions: 4 bits per value
             if (k >= send - c0) S.u.m.cost[0][k] = 0;
         }
         __syncthreads();
@@ -1376,17 +1400,25 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             // this thread's positions come from the previous sweep
             constexpr int kU = 6;              // lengths unrolled: kMinL .. kU (longer: only the entries' own lengths; the same ratio, tools/tlz_proto.c)
             constexpr int kW = kU;             // costs beyond this thread's positions within reach
+            static_assert(kU == 6 && kMinL == 3, "the packed candidate table holds lengths 3..6");
+            constexpr uint32_t kNone = 0xffffu;
             uint32_t lenr[kU + 1];
 #pragma unroll
             for (int l = kMinL; l <= kU; ++l) lenr[l] = S.lenc[l];
-            uint32_t pk[kPer], lx0[kPer], lx1[kPer];
+            uint32_t cA[kPer], cB[kPer], cC[kPer], cD[kPer];
+            bool live[kPer];
 #pragma unroll
             for (int q = 0; q < kPer; ++q) {
                 const uint32_t lit = min(511u, (uint32_t)S.litc[(idw[q >> 2] >> (8 * (q & 3))) & 0xffu]);
                 const int La = (int)(fa[q] & 127u), Lb = (int)(fb[q] & 127u);
-                int Lm = nf[q] == 0 ? 0 : (int)((nf[q] == 1 ? fa[q] : nf[q] == 2 ? fb[q] : fc[q]) & 127u);
-                if (c0 + klo + q >= send) Lm = -1;  // no such position
-                pk[q] = (uint32_t)La | ((uint32_t)Lb << 7) | ((uint32_t)(Lm + 1) << 14) | (lit << 21);
+                const int Lm = nf[q] == 0 ? 0 : (int)((nf[q] == 1 ? fa[q] : nf[q] == 2 ? fb[q] : fc[q]) & 127u);
+                live[q] = c0 + klo + q < send;
+                uint32_t lc[kU + 1];
+#pragma unroll
+                for (int l = kMinL; l <= kU; ++l) {
+                    const uint32_t e = l <= La ? 0u : l <= Lb ? 1u : 2u;
+                    lc[l] = l <= Lm ? lenr[l] + ((dc3[q] >> (8 * e)) & 255u) : kNone;
+                }
                 uint32_t E[3];
 #pragma unroll
                 for (int e = 0; e < 3; ++e) {
@@ -1395,51 +1427,79 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                     const uint32_t dcost = (dc3[q] >> (8 * e)) & 255u;
                     E[e] = use ? (uint32_t)l | (min(511u, (uint32_t)S.lenc[l] + dcost) << 7) : 0u;
                 }
-                lx0[q] = E[0] | (E[1] << 16);
-                lx1[q] = E[2];
+                cA[q] = lit | (lc[3] << 16);
+                cB[q] = lc[4] | (lc[5] << 16);
+                cC[q] = lc[6] | (E[0] << 16);
+                cD[q] = E[1] | (E[2] << 16);
             }
 #pragma unroll 1
             for (int sw = 0; sw < kSweeps; ++sw) {
-                uint16_t* cur = S.u.m.cost[sw & 1];
-                const uint16_t* prv = S.u.m.cost[(sw + 1) & 1];
+                uint32_t* cur = S.u.m.cost[sw & 1];
+                const uint32_t* prv = S.u.m.cost[(sw + 1) & 1];
                 uint32_t pw[kW + 1];
 #pragma unroll
                 for (int u = 0; u <= kW; ++u) pw[u] = prv[min(klo + kPer + u, kSeg)];
-                uint32_t cr[kPer];
-                uint32_t chs[kPer];
+                // the frontier entries read costs of the previous sweep only:
+                // their reads are issued here, before the chain, unconditionally
+                // (el = 0 reads the position's own cost, then discarded:
+                // behind a branch each cost ~5 scalar instructions of exec
+                // juggling), and each position's best entry key is formed
+                uint32_t me[kPer];
+#pragma unroll
+                for (int h = 0; h < kPer; h += 2) {  // two positions' six reads at a time (registers)
+                    uint32_t pe[2][3];
+#pragma unroll
+                    for (int u = 0; u < 2; ++u)
+#pragma unroll
+                        for (int e = 0; e < 3; ++e) {
+                            const int q = h + u;
+                            const uint32_t En = e == 0 ? (cC[q] >> 16) : e == 1 ? (cD[q] & 0xffffu) : (cD[q] >> 16);
+                            pe[u][e] = prv[min(klo + q + (int)(En & 127u), kSeg)];
+                        }
+                    asm volatile("" : "+v"(pe[0][0]), "+v"(pe[0][1]), "+v"(pe[0][2]), "+v"(pe[1][0]), "+v"(pe[1][1]),
+                                 "+v"(pe[1][2]));
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const int q = h + u;
+                        me[q] = 0xffffffffu;
+#pragma unroll
+                        for (int e = 0; e < 3; ++e) {
+                            const uint32_t En = e == 0 ? (cC[q] >> 16) : e == 1 ? (cD[q] & 0xffffu) : (cD[q] >> 16);
+                            const uint32_t cc = (((En >> 7) + pe[u][e]) << 3) | (uint32_t)(5 + e);
+                            me[q] = min(me[q], (En & 127u) != 0u ? cc : 0xffffffffu);
+                        }
+                    }
+                }
+                uint32_t cr[kPer], key[kPer];
 #pragma unroll
                 for (int q = kPer - 1; q >= 0; --q) {
                     auto CV = [&](int kk) -> uint32_t { return kk < kPer ? cr[kk] : pw[kk - kPer]; };  // kk = q + l
-                    const uint32_t P = pk[q];
-                    const int La = (int)(P & 127u), Lb = (int)((P >> 7) & 127u), Lm = (int)((P >> 14) & 127u) - 1;
-                    const uint32_t D = dc3[q];
-                    uint32_t best = (P >> 21) + CV(q + 1);
-                    uint32_t ch = 0;
-#pragma unroll
-                    for (int l = kMinL; l <= kU; ++l) {
-                        const uint32_t e = l <= La ? 0u : l <= Lb ? 1u : 2u;
-                        const uint32_t cc = lenr[l] + ((D >> (8 * e)) & 255u) + CV(q + l);
-                        const bool take = l <= Lm && lt16(cc, best);
-                        best = take ? cc : best;
-                        ch = take ? ((uint32_t)l | (e << 8)) : ch;
-                    }
-#pragma unroll
-                    for (int e = 0; e < 3; ++e) {
-                        const uint32_t En = e == 0 ? (lx0[q] & 0xffffu) : e == 1 ? (lx0[q] >> 16) : lx1[q];
-                        const int el = (int)(En & 127u);
-                        const uint32_t cc = (En >> 7) + prv[min(klo + q + el, kSeg)];
-                        const bool take = el != 0 && lt16(cc, best);
-                        best = take ? cc : best;
-                        ch = take ? ((uint32_t)el | ((uint32_t)e << 8)) : ch;
-                    }
-                    cr[q] = Lm < 0 ? 0u : best;
-                    chs[q] = ch;
+                    uint32_t best = min((((cA[q] & 0xffffu) + CV(q + 1)) << 3), me[q]);
+                    best = min(best, (((cA[q] >> 16) + CV(q + 3)) << 3) | 1u);
+                    best = min(best, (((cB[q] & 0xffffu) + CV(q + 4)) << 3) | 2u);
+                    best = min(best, (((cB[q] >> 16) + CV(q + 5)) << 3) | 3u);
+                    best = min(best, (((cC[q] & 0xffffu) + CV(q + 6)) << 3) | 4u);
+                    cr[q] = live[q] ? best >> 3 : 0u;
+                    key[q] = best;
                 }
+                // (a position past the segment's values stores 0: its cost already)
 #pragma unroll
-                for (int q = 0; q < kPer; ++q) {
-                    if ((int)((pk[q] >> 14) & 127u) == 0) continue;  // Lm < 0: no such position
-                    cur[klo + q] = (uint16_t)cr[q];
-                    if (sw == kSweeps - 1) S.dec[klo + q] = (uint16_t)chs[q];
+                for (int q = 0; q < kPer; ++q) cur[klo + q] = cr[q];
+                if (sw == kSweeps - 1) {  // the choices: length | frontier entry << 8 (0: literal)
+#pragma unroll
+                    for (int q = 0; q < kPer; ++q) {
+                        if (!live[q]) continue;
+                        const uint32_t k = key[q] & 7u;
+                        uint32_t ch = 0;
+                        if (k >= 5u) {
+                            const uint32_t ent = k == 5u ? fa[q] : k == 6u ? fb[q] : fc[q];
+                            ch = (ent & 127u) | ((k - 5u) << 8);
+                        } else if (k >= 1u) {
+                            const uint32_t l = k + 2u, La = fa[q] & 127u, Lb = fb[q] & 127u;
+                            ch = l | ((l <= La ? 0u : l <= Lb ? 1u : 2u) << 8);
+                        }
+                        S.dec[klo + q] = (uint16_t)ch;
+                    }
                 }
                 __syncthreads();
             }
@@ -1641,30 +1701,51 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 
     PH(8);
     // ---- H: bits of the ops (a block scan of their costs), segment offsets ----
+    // every op's code and extra bits come from small LDS tables (a literal
+    // value: its four codes in two words; a length: code | extra bits) and
+    // the distance's code index and extra bits by arithmetic
+    if (tid < 32) {
+        const uint32_t bb = __float_as_uint((float)tid);
+        uint32_t v[2] = {0, 0}, n[2] = {0, 0};
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+            const uint32_t by = (bb >> (8 * y)) & 0xffu;
+            v[y >> 1] |= (uint32_t)S.kl[by] << n[y >> 1];
+            n[y >> 1] += S.ll[by];
+        }
+        S.u.f.litlo[tid] = v[0] | (n[0] << 24);
+        S.u.f.lithi[tid] = v[1] | (n[1] << 24);
+    } else if (tid >= 64 && tid < 64 + kMaxL + 1) {
+        const int l = tid - 64;
+        uint32_t w = 0;
+        if (l >= kMinL) {
+            int lc, ne;
+            uint32_t ev;
+            len_sym(4u * (uint32_t)l, lc, ne, ev);
+            const uint32_t cl = S.ll[257 + lc];
+            w = ((uint32_t)S.kl[257 + lc] | (ev << cl)) | ((cl + (uint32_t)ne) << 24);
+        }
+        S.u.f.lenw[l] = w;
+    }
+    __syncthreads();
     const uint32_t nops = S.ops_n, H = S.hdr_bits;
     const uint32_t o_lo = (uint32_t)((uint64_t)nops * tid / kNT), o_hi = (uint32_t)((uint64_t)nops * (tid + 1) / kNT);
+    auto dist_w = [&](uint32_t dv) -> uint32_t {  // code | extra bits, n << 24 (n <= 10 + 13)
+        int dc, ne;
+        uint32_t ev;
+        dist_sym(4u * dv, dc, ne, ev);
+        const uint32_t cd = S.ld[dc];
+        return ((uint32_t)S.kd[dc] | (ev << cd)) | ((cd + (uint32_t)ne) << 24);
+    };
     auto op_bits = [&](uint32_t rec) -> uint32_t {
-        if (rec >> 31) {
-            const uint32_t b = __float_as_uint((float)(rec & 31u));
-            return (uint32_t)S.ll[b & 0xffu] + S.ll[(b >> 8) & 0xffu] + S.ll[(b >> 16) & 0xffu] + S.ll[b >> 24];
-        }
-        const uint32_t l = rec & 127u, d = rec >> 7;
-        const int lc = len_code(4u * l), dc = dist_code(4u * d);
-        return (uint32_t)S.ll[257 + lc] + c_lext[lc] + S.ld[dc] + c_dext[dc];
+        if (rec >> 31) return (S.u.f.litlo[rec & 31u] >> 24) + (S.u.f.lithi[rec & 31u] >> 24);
+        return (S.u.f.lenw[rec & 127u] >> 24) + (dist_w(rec >> 7) >> 24);
     };
     uint32_t mine = 0;
+#pragma unroll 4
     for (uint32_t o = o_lo; o < o_hi; ++o) mine += op_bits(ops[o]);
     uint32_t tot;
     const uint32_t pos0 = H + block_scan<kNT>(mine, S.scan, &tot);
-    {
-        int sidx = 0;
-        while (sidx < nseg && S.segop[sidx] < o_lo) ++sidx;
-        uint32_t pos = pos0;
-        for (uint32_t o = o_lo; o < o_hi && sidx < nseg; ++o) {
-            if (S.segop[sidx] == o) S.segbit[sidx++] = pos;
-            pos += op_bits(ops[o]);
-        }
-    }
     if (tid == 0) S.total_bits = H + tot;
     const uint32_t D = (uint32_t)(kHdrFixed + 4 * nseg);  // header bytes (a multiple of 4)
     uint32_t* const slot = reinterpret_cast<uint32_t*>(a.slots + (int64_t)blockIdx.x * a.slot_bytes);
@@ -1677,13 +1758,18 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     if (tid == 0)
         for (uint32_t i = 0; i < (H + 31u) / 32u; ++i) atomicOr(&dw[i], S.u.f.hdrw[i]);
     {
+        // the segments whose first op lies in this thread's range get their
+        // bit offset here, as the emission passes that op
+        int sidx = 0;
+        while (sidx < nseg && S.segop[sidx] < o_lo) ++sidx;
+        uint32_t next_seg = sidx < nseg ? S.segop[sidx] : 0xffffffffu;
         uint64_t acc = 0;
         int nb = (int)(pos0 & 31u);
         uint32_t wi = pos0 >> 5;
         bool first = true;
-        auto put = [&](uint32_t v, int n) {
-            acc |= (uint64_t)v << nb;
-            nb += n;
+        auto put = [&](uint32_t w) {  // code | extra bits, n << 24 (n <= 24)
+            acc |= (uint64_t)(w & 0xffffffu) << nb;
+            nb += (int)(w >> 24);
             if (nb >= 32) {
                 if (first) { atomicOr(&dw[wi], (uint32_t)acc); first = false; }
                 else dw[wi] = (uint32_t)acc;
@@ -1692,22 +1778,19 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                 nb -= 32;
             }
         };
+#pragma unroll 2
         for (uint32_t o = o_lo; o < o_hi; ++o) {
+            if (o == next_seg) {
+                S.segbit[sidx++] = 32u * wi + (uint32_t)nb;
+                next_seg = sidx < nseg ? S.segop[sidx] : 0xffffffffu;
+            }
             const uint32_t rec = ops[o];
             if (rec >> 31) {
-                const uint32_t b = __float_as_uint((float)(rec & 31u));
-#pragma unroll
-                for (int y = 0; y < 4; ++y) {
-                    const uint32_t by = (b >> (8 * y)) & 0xffu;
-                    put(S.kl[by], S.ll[by]);
-                }
+                put(S.u.f.litlo[rec & 31u]);
+                put(S.u.f.lithi[rec & 31u]);
             } else {
-                const uint32_t l = 4u * (rec & 127u), d = 4u * (rec >> 7);
-                const int lc = len_code(l), dc = dist_code(d);
-                put(S.kl[257 + lc], S.ll[257 + lc]);
-                put(l - c_lbase[lc], c_lext[lc]);
-                put(S.kd[dc], S.ld[dc]);
-                put(d - c_dbase[dc], c_dext[dc]);
+                put(S.u.f.lenw[rec & 127u]);
+                put(dist_w(rec >> 7));
             }
         }
         if (nb > 0) atomicOr(&dw[wi], (uint32_t)acc);
@@ -2211,12 +2294,8 @@ __global__ __launch_bounds__(kRNT) void k_tlz_resolve(DecArgs a) {
 // aligned 16-byte one (the source realigned with alignbyte; slots are 4-byte
 // aligned), only the < 16 bytes at either end of a member are byte stores.
 // (Byte stores for the 3 in 4 members that start misaligned ran at 8.5 GB/s.)
-__global__ __launch_bounds__(256) void k_gzip_pack(const uint8_t* slots, uint64_t stride, const uint32_t* sizes,
-                                                   const uint64_t* off, uint8_t* packed) {
-    if (off[blockIdx.x] == ~0ull) return;  // the batch does not fit the output (reported by the scan)
-    const uint8_t* src = slots + (int64_t)blockIdx.x * stride;
-    uint8_t* dst = packed + off[blockIdx.x];
-    const uint32_t n = sizes[blockIdx.x];
+// one member's bytes from its slot to dst (256 threads; 16-byte stores)
+DEVI void pack_member(const uint8_t* src, uint8_t* dst, uint32_t n) {
     const uint32_t head = (uint32_t)((16u - (reinterpret_cast<uintptr_t>(dst) & 15u)) & 15u);
     if (n <= head + 16u) {
         for (uint32_t i = threadIdx.x; i < n; i += 256) dst[i] = src[i];
@@ -2243,6 +2322,26 @@ __global__ __launch_bounds__(256) void k_gzip_pack(const uint8_t* slots, uint64_
         }
         d[i] = v;
     }
+}
+
+__global__ __launch_bounds__(256) void k_gzip_pack(const uint8_t* slots, uint64_t stride, const uint32_t* sizes,
+                                                   const uint64_t* off, uint8_t* packed) {
+    if (off[blockIdx.x] == ~0ull) return;  // the batch does not fit the output (reported by the scan)
+    pack_member(slots + (int64_t)blockIdx.x * stride, packed + off[blockIdx.x], sizes[blockIdx.x]);
+}
+
+// the batched path's pack, enqueued right behind the batch's scan with no
+// host round trip: the batch's first offset and end come from the scan's
+// output (off[0], off[nb]); a batch that fits the device staging goes there
+// (stage + off - first, then one DMA), a larger one (nearly incompressible
+// ranks) straight into the mapped pinned output at its offsets
+__global__ __launch_bounds__(256) void k_gzip_pack_batch(const uint8_t* slots, uint64_t stride, const uint32_t* sizes,
+                                                         const uint64_t* off, int nb, uint8_t* stage,
+                                                         uint64_t stage_cap, uint8_t* mapped) {
+    const uint64_t first = off[0], end = off[nb];
+    if (first == ~0ull || off[blockIdx.x] == ~0ull) return;  // the batch does not fit the output (reported by the scan)
+    uint8_t* dst = end - first <= stage_cap ? stage + (off[blockIdx.x] - first) : mapped + off[blockIdx.x];
+    pack_member(slots + (int64_t)blockIdx.x * stride, dst, sizes[blockIdx.x]);
 }
 
 }  // namespace gz
@@ -2566,7 +2665,7 @@ static int gzip_ranks_impl(const float* x, int64_t n, uint8_t* out, size_t out_c
         uint64_t* hinfo = nullptr;
         GZHIP(gz_pinned_info(&hinfo));  // [2][2]: a batch's first offset and end
         const int64_t nbatch = (L.members + L.batch - 1) / L.batch;
-        hipEvent_t ev_enc[2] = {}, ev_pack[2] = {}, ev_scan[2] = {};
+        hipEvent_t ev_pack[2] = {}, ev_scan[2] = {};
         // every exit (the GZHIP / finish error returns included) waits for the
         // work queued on both streams -- scan, pack and D2H read ws and write
         // out -- before the caller may reuse those buffers, then frees the events
@@ -2574,18 +2673,16 @@ static int gzip_ranks_impl(const float* x, int64_t n, uint8_t* out, size_t out_c
         ofl_util::ScopeExit cleanup([&] {
             if (!drained) { (void)hipStreamSynchronize(sd); (void)hipStreamSynchronize(st); }
             for (int i = 0; i < 2; ++i) {
-                if (ev_enc[i]) (void)hipEventDestroy(ev_enc[i]);
                 if (ev_pack[i]) (void)hipEventDestroy(ev_pack[i]);
                 if (ev_scan[i]) (void)hipEventDestroy(ev_scan[i]);
             }
         });
         for (int i = 0; i < 2; ++i) {
-            GZHIP(hipEventCreateWithFlags(&ev_enc[i], hipEventDisableTiming));
             GZHIP(hipEventCreateWithFlags(&ev_pack[i], hipEventDisableTiming));
             GZHIP(hipEventCreateWithFlags(&ev_scan[i], hipEventDisableTiming));
         }
         GZHIP(hipMemsetAsync(running, 0, sizeof(uint64_t), st));
-        uint64_t copied = 0, bend[2] = {0, 0};  // host_dst holds out[0, copied); batch ends
+        uint64_t copied = 0;  // host_dst holds out[0, copied)
         // diagnostics: OFL_GZ_FILL_TRACE=1 prints the host's wait / copy times per call
         static const bool fill_trace = getenv("OFL_GZ_FILL_TRACE") != nullptr;
         auto now_us = [] {
@@ -2607,70 +2704,103 @@ static int gzip_ranks_impl(const float* x, int64_t n, uint8_t* out, size_t out_c
                     tn += snprintf(trace + tn, sizeof(trace) - tn, " copy@%.0f+%.0f", t0 - t_call, now_us() - t0);
             }
         };
-        auto sync_pack = [&](int b) -> hipError_t {
+        auto wait_ev = [&](hipEvent_t e, const char* what) -> hipError_t {
             const double t0 = fill_trace ? now_us() : 0.0;
-            const hipError_t e = hipEventSynchronize(ev_pack[b]);
+            const hipError_t r = hipEventSynchronize(e);
             if (fill_trace && tn < 400)
-                tn += snprintf(trace + tn, sizeof(trace) - tn, " wait@%.0f+%.0f", t0 - t_call, now_us() - t0);
-            return e;
+                tn += snprintf(trace + tn, sizeof(trace) - tn, " %s@%.0f+%.0f", what, t0 - t_call, now_us() - t0);
+            return r;
         };
-        GZHIP(hipEventRecord(ev_pack[1], st));  // orders the side stream after the memsets
-        GZHIP(hipStreamWaitEvent(sd, ev_pack[1], 0));
-        int err = 0;
-        auto finish = [&](int64_t k) -> int {  // batch k: scan known -> pack + D2H on the side stream
+        // Batch k on the caller's stream: encode, scan, pack -- the scan and
+        // the pack (tens of us with the whole chip free) run before the next
+        // batch's encode, so nothing of a batch waits for CUs behind the next
+        // one (on a side stream they queued behind its 80 KiB-LDS blocks for
+        // up to 2.3 ms).  Only the DMA of batch k (its size is known once the
+        // host has read the scan) goes on the side stream, beside the encode
+        // of batch k + 1, and the host copies batch k into host_dst meanwhile.
+        // The last batch crosses PCIe in pieces, each copied as it lands.
+        hipEvent_t ev_dma[2] = {};
+        ofl_util::ScopeExit cleanup2([&] {
+            for (int i = 0; i < 2; ++i)
+                if (ev_dma[i]) (void)hipEventDestroy(ev_dma[i]);
+        });
+        for (int i = 0; i < 2; ++i) GZHIP(hipEventCreateWithFlags(&ev_dma[i], hipEventDisableTiming));
+        constexpr int kTailPieces = 4;
+        hipEvent_t ev_tail[kTailPieces] = {};
+        ofl_util::ScopeExit cleanup3([&] {
+            for (auto& e : ev_tail)
+                if (e) (void)hipEventDestroy(e);
+        });
+        for (auto& e : ev_tail) GZHIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        uint64_t bfirst[2] = {0, 0}, bend[2] = {0, 0};
+        // batch k's DMA (after its scan result is on the host); pieces > 1 for the last batch
+        auto issue_dma = [&](int64_t k, int pieces) -> int {
             const int b = (int)(k & 1);
-            const int nb = (int)std::min<int64_t>(L.batch, L.members - k * L.batch);
-            GZHIP(hipEventSynchronize(ev_scan[b]));
+            GZHIP(wait_ev(ev_scan[b], "scan"));
             const uint64_t first = hinfo[2 * b], end = hinfo[2 * b + 1];
+            bfirst[b] = first == ~0ull ? 0 : first;
             bend[b] = first == ~0ull ? 0 : end;
-            gzprof_begin(sd);
-            if (first != ~0ull && end - first <= L.stage) {
-                hipLaunchKernelGGL(gz::k_gzip_pack, dim3(nb), dim3(256), 0, sd, slots2[b], (uint64_t)L.slot, sizes2[b],
-                                   off2[b], reinterpret_cast<uint8_t*>(reinterpret_cast<uintptr_t>(stage2[b]) - first));
-                gzprof_end(sd, "k_gzip_pack");
-                gzprof_begin(sd);
-                if (end > first) GZHIP(hipMemcpyAsync(out + first, stage2[b], end - first, hipMemcpyDeviceToHost, sd));
-                gzprof_end(sd, "gzip D2H (DMA)");
-            } else {  // (an overflowing batch is reported by the scan: the pack skips it)
-                hipLaunchKernelGGL(gz::k_gzip_pack, dim3(nb), dim3(256), 0, sd, slots2[b], (uint64_t)L.slot, sizes2[b],
-                                   off2[b], dout);
-                gzprof_end(sd, "k_gzip_pack");
+            GZHIP(hipStreamWaitEvent(sd, ev_pack[b], 0));
+            if (first != ~0ull && end > first && end - first <= L.stage) {
+                const uint64_t n = end - first;
+                for (int p = 0; p < pieces; ++p) {
+                    const uint64_t lo = n * (uint64_t)p / (uint64_t)pieces, hi = n * (uint64_t)(p + 1) / (uint64_t)pieces;
+                    gzprof_begin(sd);
+                    if (hi > lo) GZHIP(hipMemcpyAsync(out + first + lo, stage2[b] + lo, hi - lo, hipMemcpyDeviceToHost, sd));
+                    gzprof_end(sd, "gzip D2H (DMA)");
+                    if (pieces > 1) GZHIP(hipEventRecord(ev_tail[p], sd));
+                }
             }
-            GZHIP(hipEventRecord(ev_pack[b], sd));
+            GZHIP(hipEventRecord(ev_dma[b], sd));
             return OFL_OK;
         };
-        for (int64_t k = 0; k < nbatch && !err; ++k) {
+        for (int64_t k = 0; k < nbatch; ++k) {
             const int64_t c0 = k * L.batch;
             const int b = (int)(k & 1);
             const int nb = (int)std::min<int64_t>(L.batch, L.members - c0);
-            if (k >= 2) GZHIP(hipStreamWaitEvent(st, ev_pack[b], 0));  // slots[b] and stage[b] free
             enc(c0, nb, slots2[b], sizes2[b]);
-            GZHIP(hipEventRecord(ev_enc[b], st));
-            if (k >= 1)
-                if (int rc = finish(k - 1)) return rc;
-            GZHIP(hipStreamWaitEvent(sd, ev_enc[b], 0));
-            hipLaunchKernelGGL(gz::k_gzip_scan, dim3(1), dim3(1024), 0, sd, sizes2[b], nb, off2[b], running,
+            gzprof_begin(st);
+            hipLaunchKernelGGL(gz::k_gzip_scan, dim3(1), dim3(1024), 0, st, sizes2[b], nb, off2[b], running,
                                (uint64_t)out_cap, bad);
-            GZHIP(hipMemcpyAsync(hinfo + 2 * b, off2[b], 8, hipMemcpyDeviceToHost, sd));
-            GZHIP(hipMemcpyAsync(hinfo + 2 * b + 1, off2[b] + nb, 8, hipMemcpyDeviceToHost, sd));
-            GZHIP(hipEventRecord(ev_scan[b], sd));
-            if (hipGetLastError() != hipSuccess) err = 1;
-            if (host_dst && k >= 1 && !err) {  // batch k - 1's bytes, while batch k encodes
-                GZHIP(sync_pack((int)((k - 1) & 1)));
-                host_copy(bend[(k - 1) & 1]);
+            gzprof_end(st, "k_gzip_scan");
+            GZHIP(hipMemcpyAsync(hinfo + 2 * b, off2[b], 8, hipMemcpyDeviceToHost, st));
+            GZHIP(hipMemcpyAsync(hinfo + 2 * b + 1, off2[b] + nb, 8, hipMemcpyDeviceToHost, st));
+            GZHIP(hipEventRecord(ev_scan[b], st));
+            if (k >= 2) GZHIP(hipStreamWaitEvent(st, ev_dma[b], 0));  // stage[b]'s previous DMA has read it
+            gzprof_begin(st);
+            hipLaunchKernelGGL(gz::k_gzip_pack_batch, dim3(nb), dim3(256), 0, st, slots2[b], (uint64_t)L.slot, sizes2[b],
+                               off2[b], nb, stage2[b], (uint64_t)L.stage, dout);
+            gzprof_end(st, "k_gzip_pack");
+            GZHIP(hipEventRecord(ev_pack[b], st));
+            if (hipGetLastError() != hipSuccess) return gzfail(OFL_EHIP, "gzip ranks: kernel launch failed");
+            if (k >= 1) {  // batch k - 1: its DMA and its bytes to host_dst, beside this batch's encode
+                if (int rc = issue_dma(k - 1, 1)) return rc;
+                if (host_dst) {
+                    GZHIP(wait_ev(ev_dma[(k - 1) & 1], "dma"));
+                    host_copy(bend[(k - 1) & 1]);
+                }
             }
         }
-        if (!err)
-            if (int rc = finish(nbatch - 1)) return rc;
+        if (int rc = issue_dma(nbatch - 1, host_dst ? kTailPieces : 1)) return rc;
+        {  // the last batch, piece by piece as its DMA lands
+            const int b = (int)((nbatch - 1) & 1);
+            const uint64_t first = bfirst[b], end = bend[b];
+            if (host_dst && end > first && end - first <= L.stage) {
+                const uint64_t n = end - first;
+                for (int p = 0; p < kTailPieces; ++p) {
+                    GZHIP(wait_ev(ev_tail[p], "tail"));
+                    host_copy(first + n * (uint64_t)(p + 1) / (uint64_t)kTailPieces);
+                }
+            }
+        }
         GZHIP(hipEventRecord(ev_pack[0], sd));
-        GZHIP(hipStreamWaitEvent(st, ev_pack[0], 0));  // the caller's stream sees every pack and copy
+        GZHIP(hipStreamWaitEvent(st, ev_pack[0], 0));  // the caller's stream sees every copy
         uint64_t tot = 0;
         int badh = 0;
         GZHIP(hipMemcpyAsync(&tot, running, 8, hipMemcpyDeviceToHost, st));
         GZHIP(hipMemcpyAsync(&badh, bad, sizeof(int), hipMemcpyDeviceToHost, st));
         GZHIP(hipStreamSynchronize(st));
         drained = true;  // st waited for everything sd ran
-        if (err) return gzfail(OFL_EHIP, "gzip ranks: kernel launch failed");
         if (badh & 1) return gzfail(OFL_EINVAL, "gzip ranks: values must be float32 integers 0..31");
         if (badh & 2) return gzfail(OFL_ESPACE, "gzip ranks: output buffer too small");
         total = tot;
