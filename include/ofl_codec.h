@@ -464,6 +464,12 @@ int ofl_inflate_tlz_async(const uint8_t* src, const int64_t* index, int64_t firs
                           size_t out_cap, void* ws, size_t ws_bytes, void* stream);
 int ofl_inflate_tlz_wait(const uint8_t* src, const int64_t* index, int64_t nmembers, uint8_t* out, size_t out_cap,
                          void* ws, size_t ws_bytes, void* stream);
+/* ofl_inflate_tlz_async without the status reset: pieces launched on several
+ * streams as their bytes land (the caller resets the status once, e.g. with
+ * ofl_inflate_tlz_async(first = 0, count = 0), orders every piece after it
+ * and joins the streams before ofl_inflate_tlz_wait). */
+int ofl_inflate_tlz_launch(const uint8_t* src, const int64_t* index, int64_t first, int64_t count, uint8_t* out,
+                           size_t out_cap, void* ws, size_t ws_bytes, void* stream);
 int ofl_inflate_members(const uint8_t* src, const int64_t* index, int64_t nmembers, uint32_t max_isize, uint8_t* out,
                         size_t out_cap, void* ws, size_t ws_bytes, void* stream);
 /* Per-kernel timing of the gzip / inflate launches (bench.py): enable (1)

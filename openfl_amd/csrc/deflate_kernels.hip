@@ -901,10 +901,12 @@ constexpr int kPer = kSeg / kNT;                   // positions per thread
 constexpr int kWin = 8192;                         // window, values (32 KiB)
 constexpr int kMaxL = 64, kMinL = 3;               // copy length, values
 #ifndef OFL_TLZ_CAND
-// 12 chain candidates: encode 14.0 -> 12.8 ms per GiB of KC ranks for a 0.3 %
-// larger stream (ratio 0.1165 vs 0.1162 at 16; gzip -9: 0.1173;
-// profiles/r04_tlz_cand_ab2.txt)
-#define OFL_TLZ_CAND 12
+// 11 chain candidates (round 5, after the DP rework made the frontier the
+// largest phase): KC gzip phase 12.5 -> 12.1 ms per GiB for ratio 0.1165 ->
+// 0.1167 (10: 11.9 ms, 0.1170; gzip -9: 0.1171-0.1174;
+// profiles/r05_tlz_cand_sweep_ab.txt).  Round 4: 12 instead of 16, encode
+// 14.0 -> 12.8 ms (profiles/r04_tlz_cand_ab2.txt)
+#define OFL_TLZ_CAND 11
 #endif
 #ifndef OFL_TLZ_SWEEPS
 #define OFL_TLZ_SWEEPS 4
@@ -2925,8 +2927,8 @@ size_t ofl_inflate_tlz_workspace_bytes(int64_t nmembers) {
     return 256 + 4 * (size_t)std::max<int64_t>(nmembers, 1) * gz::tlz::kMemSeg;
 }
 
-int ofl_inflate_tlz_async(const uint8_t* src, const int64_t* index, int64_t first, int64_t count, uint8_t* out,
-                          size_t out_cap, void* ws, size_t ws_bytes, void* stream) {
+static int inflate_tlz_enqueue(const uint8_t* src, const int64_t* index, int64_t first, int64_t count, uint8_t* out,
+                               size_t out_cap, void* ws, size_t ws_bytes, void* stream, bool reset) {
     if (first < 0 || count < 0 || (count && (!src || !index || !out))) return gzfail(OFL_EINVAL, "inflate: null argument");
     if (!ws || ws_bytes < ofl_inflate_tlz_workspace_bytes(first + count)) return gzfail(OFL_ESPACE, "inflate: workspace too small");
     GZHIP(ofl_util::per_device_once([] {
@@ -2937,7 +2939,7 @@ int ofl_inflate_tlz_async(const uint8_t* src, const int64_t* index, int64_t firs
     hipStream_t st = static_cast<hipStream_t>(stream);
     int* status = static_cast<int*>(ws);
     uint32_t* cnt = reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + 256) + first * gz::tlz::kMemSeg;
-    if (first == 0) GZHIP(hipMemsetAsync(status, 0, sizeof(int), st));
+    if (reset) GZHIP(hipMemsetAsync(status, 0, sizeof(int), st));
     if (count == 0) return OFL_OK;
     gz::tlz::DecArgs a{src, index + 4 * first, count, out, (uint64_t)out_cap, cnt, status};
     gzprof_begin(st);
@@ -2948,6 +2950,16 @@ int ofl_inflate_tlz_async(const uint8_t* src, const int64_t* index, int64_t firs
     gzprof_end(st, "tlz::k_tlz_resolve");
     GZHIP(hipGetLastError());
     return OFL_OK;
+}
+
+int ofl_inflate_tlz_async(const uint8_t* src, const int64_t* index, int64_t first, int64_t count, uint8_t* out,
+                          size_t out_cap, void* ws, size_t ws_bytes, void* stream) {
+    return inflate_tlz_enqueue(src, index, first, count, out, out_cap, ws, ws_bytes, stream, first == 0);
+}
+
+int ofl_inflate_tlz_launch(const uint8_t* src, const int64_t* index, int64_t first, int64_t count, uint8_t* out,
+                           size_t out_cap, void* ws, size_t ws_bytes, void* stream) {
+    return inflate_tlz_enqueue(src, index, first, count, out, out_cap, ws, ws_bytes, stream, false);
 }
 
 int ofl_inflate_tlz_wait(const uint8_t* src, const int64_t* index, int64_t nmembers, uint8_t* out, size_t out_cap,

@@ -3878,6 +3878,9 @@ int ofl_host_copy_many(int n, void* const* dst, const void* const* src, const in
             acc += b;
         }
     };
+    // on the persistent native pool (a thread start per call cost ~0.1 ms per
+    // copy); fresh threads only when every pool is busy with another caller
+    if (nt > 1 && ofl::pool_run(nt, nt - 1, work)) return OFL_OK;
     std::vector<std::thread> th;
     for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
     work(0);

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
 #include <map>
 #include <mutex>
 
@@ -39,6 +40,10 @@ struct ScopeExit {
 }  // namespace ofl_util
 
 namespace ofl {
+// f(0..n-1) on the caller and at least `workers` threads of a persistent
+// native pool (csrc/serial_sum.cpp); false when every pool is busy with
+// another caller (then nothing ran)
+bool pool_run(int n, int workers, const std::function<void(int)>& f);
 // exact serial float32 sum (csrc/serial_sum.cpp): s <- fl(s + x[i]) left to
 // right, evaluated on up to nthreads threads (<= 0: the default); dst (or
 // NULL) receives a copy of x, after which after_copy(ctx) (or NULL) runs on

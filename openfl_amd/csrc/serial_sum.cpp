@@ -276,6 +276,8 @@ int default_threads() {
 }  // namespace
 
 namespace ofl {
+bool pool_run(int n, int workers, const std::function<void(int)>& f) { return Pool::run(n, workers, f); }
+
 float serial_sum_f32_mt_cb(const float* x, int64_t n, float* dst, int nthreads, void (*after_copy)(void*),
                            void* ctx) {
     if (nthreads <= 0) nthreads = default_threads();

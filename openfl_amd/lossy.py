@@ -385,13 +385,34 @@ def gunzip_device(data, out):
     # the pool thread enqueues the copy on that same stream
     caller_stream = torch.cuda.current_stream(dev)
 
+    # the stream crosses PCIe in pieces (large payloads): each piece's TLZ
+    # members inflate on a side stream as soon as their bytes have landed,
+    # beside the H2D of the next piece
+    npieces = _INFLATE_PIECES if src.size >= (_INFLATE_PIECE_MIN << 20) else 1
+    bounds = [0] + [min(src.size, (src.size * k // npieces + (4 << 20) - 1) // (4 << 20) * (4 << 20))
+                    for k in range(1, npieces)] + [src.size]
+    landed = [threading.Event() for _ in range(npieces)]
+    piece_ev = [None] * npieces
+
     def h2d():
         # straight from the immutable payload through the C ABI (no torch
         # wrapper of a read-only buffer); the caller's stream orders it
         # (no page freeing meanwhile: hostmem.quiet)
-        if src.size:
-            with torch.cuda.device(dev), hostmem.quiet():
-                _lib.check(_h2d(L, d_in.data_ptr(), src.ctypes.data, src.size, caller_stream.cuda_stream))
+        try:
+            if src.size:
+                with torch.cuda.device(dev), hostmem.quiet():
+                    for k in range(npieces):
+                        lo, hi = bounds[k], bounds[k + 1]
+                        if hi > lo:
+                            _lib.check(_h2d(L, d_in.data_ptr() + lo, src.ctypes.data + lo, hi - lo,
+                                            caller_stream.cuda_stream))
+                        ev = torch.cuda.Event()
+                        ev.record(caller_stream)
+                        piece_ev[k] = ev
+                        landed[k].set()
+        finally:
+            for e in landed:
+                e.set()
     # one pass over the headers: a member takes >= 26 bytes, so n // 26 + 1
     # entries always suffice (untouched pages of the array cost nothing)
     cap = src.size // 26 + 1
@@ -401,8 +422,11 @@ def gunzip_device(data, out):
         rc = L.ofl_gzip_member_index(src.ctypes.data if src.size else None, src.size, idx.ctypes.data, cap,
                                      ctypes.byref(nm), ctypes.byref(tot), ctypes.byref(mx), ctypes.byref(tl)) \
             if src.size else _lib.OFL_EFORMAT
-    finally:
+        if rc != _lib.OFL_OK or not tl.value or npieces == 1:
+            copy.result()
+    except BaseException:
         copy.result()
+        raise
     if rc == _lib.OFL_EFORMAT:
         raw = np.frombuffer(gzip.decompress(bytes(data)), np.uint8)
         if raw.size > out.numel():
@@ -410,17 +434,49 @@ def gunzip_device(data, out):
         if raw.size:
             out[:raw.size].copy_(torch.from_numpy(raw.copy()))
         return out[:raw.size]
+    if rc != _lib.OFL_OK:
+        copy.result()
     _lib.check_gzip(rc)
     if tot.value > out.numel():
+        copy.result()
         raise _lib.CodecError("gunzip_device: output buffer too small")
     idx = idx[:nm.value]
     d_idx = _buf(dev, "gz_idx", max(idx.nbytes, 8))
     d_idx[:idx.nbytes].copy_(torch.from_numpy(idx.view(np.uint8).reshape(-1)))
     if tl.value:
         ws = _buf(dev, "gz_status", int(L.ofl_inflate_tlz_workspace_bytes(nm.value)))
-        _lib.check_gzip(L.ofl_inflate_tlz(d_in.data_ptr(), d_idx.data_ptr(), nm.value, out.data_ptr(), out.numel(),
-                                          ws.data_ptr(), ws.numel(), _stream(dev)))
+        args = (d_in.data_ptr(), d_idx.data_ptr())
+        tail = (out.data_ptr(), out.numel(), ws.data_ptr(), ws.numel())
+        if npieces == 1:
+            _lib.check_gzip(L.ofl_inflate_tlz(*args, nm.value, *tail, _stream(dev)))
+        else:
+            # status reset and the index on the caller's stream, then every
+            # piece on a side stream after its bytes and that reset
+            _lib.check_gzip(L.ofl_inflate_tlz_async(*args, 0, 0, *tail, caller_stream.cuda_stream))
+            ready = torch.cuda.Event()
+            ready.record(caller_stream)
+            ends = idx[:, 0] + (idx[:, 1] & ((1 << 62) - 1)) + 8   # member end (trailer included)
+            sides = _side_streams(dev)
+            first = 0
+            try:
+                for k in range(npieces):
+                    landed[k].wait()
+                    if piece_ev[k] is None:   # the copy failed: its error surfaces below
+                        break
+                    last = nm.value if k == npieces - 1 else int(np.searchsorted(ends, bounds[k + 1], "right"))
+                    if last > first:
+                        st = sides[k % len(sides)]
+                        st.wait_event(ready)
+                        st.wait_event(piece_ev[k])
+                        _lib.check_gzip(L.ofl_inflate_tlz_launch(*args, first, last - first, *tail, st.cuda_stream))
+                        first = last
+            finally:
+                copy.result()
+                for st in sides:
+                    caller_stream.wait_stream(st)
+            _lib.check_gzip(L.ofl_inflate_tlz_wait(*args, nm.value, *tail, caller_stream.cuda_stream))
     else:
+        copy.result()
         ws = _buf(dev, "gz_status", 256)
         _lib.check_gzip(L.ofl_inflate_members(d_in.data_ptr(), d_idx.data_ptr(), nm.value, mx.value, out.data_ptr(),
                                               out.numel(), ws.data_ptr(), ws.numel(), _stream(dev)))
@@ -428,6 +484,8 @@ def gunzip_device(data, out):
     return out[:tot.value]
 
 
+_INFLATE_PIECES = int(os.environ.get("OFL_INFLATE_PIECES", "4"))  # H2D pieces of a large TLZ payload, each inflated as it lands
+_INFLATE_PIECE_MIN = 32  # MiB: smaller payloads cross in one piece
 _H2D_THREADS = int(os.environ.get("OFL_H2D_THREADS", "2"))  # host threads staging a large pageable payload (0: one plain hipMemcpyAsync)
 _GZ_COPY_THREADS = int(os.environ.get("OFL_GZ_COPY_THREADS", "8"))  # host threads filling the gzip payload
 _GZ_FILL = os.environ.get("OFL_GZ_FILL", "1") != "0"  # 0: copy the payload after the call (A/B)
@@ -442,6 +500,16 @@ def _h2d(L, dst, src, nbytes, stream):
 
 
 _h2d_executor = None
+_sides = {}
+
+
+def _side_streams(dev):
+    """Two side streams per device for the pieces of a pipelined inflate."""
+    with _pool_lock:
+        key = str(dev)
+        if key not in _sides:
+            _sides[key] = [torch.cuda.Stream(device=dev) for _ in range(2)]
+        return _sides[key]
 
 
 def _h2d_pool():
