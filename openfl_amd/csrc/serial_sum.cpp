@@ -21,14 +21,20 @@
 //   phase B (threads): per sub-chunk, with the estimated e: the prefix sums of
 //           R relative to the sub-chunk start, their min / max, and every tie
 //           (its relative prefix and the other candidate's direction);
-//   phase C (one thread, in order): with the exact s at the sub-chunk start,
+//           Where the estimated partial sums leave that binade the
+//           sub-chunk is cut into up to three runs at the elements that
+//           cross, each summarised in the binade the estimate is in there;
+//   phase C (one thread, in order): with the exact s at a run's start,
 //           if s is in the guessed binade and every partial sum
 //           S0 + prefix (+- the ties' corrections) stays strictly inside
 //           [2^23 + 1, 2^24 - 1] in magnitude -- so the exact s + x is in the
 //           binade too and the grid u applies -- the ties are resolved in
-//           order by parity and s = (S0 + prefix_end + corrections) * u;
-//           otherwise (binade crossing, zero / subnormal / non-finite values,
-//           many ties) the sub-chunk runs the plain serial loop.
+//           order by parity and s = (S0 + prefix_end + corrections) * u,
+//           and the element that crosses into the next run is one scalar
+//           add; otherwise (a wrong guess, more crossings, zero / subnormal /
+//           non-finite values, many ties) the rest of the sub-chunk runs the
+//           plain serial loop (N(0, 0.01) data at 2^21: 1053 -> ~370 of 8192
+//           sub-chunks).
 // Phase C touches each sub-chunk once in O(1 + ties); the serial loop only
 // runs where the partial sums cross a binade.  Bit-identical to the plain
 // loop by construction (tests/test_serial_sum.py checks it on adversarial
@@ -57,13 +63,23 @@ constexpr int kG = 256;      // sub-chunk
 constexpr int kTieCap = 6;   // ties per sub-chunk resolved in phase C (more: serial loop)
 constexpr int64_t kLo = (1ll << 23) + 1, kHi = (1ll << 24) - 1;
 
-struct Sub {
+// one run of a sub-chunk summarised in one binade: elements [j0, j1); the
+// element j1 (if j1 < len) takes the partial sums across a binade boundary and
+// is added by one scalar step in phase C
+struct Part {
     int64_t pre_end, lo, hi;
     int64_t tpre[kTieCap];
     int8_t tdel[kTieCap];
     int16_t ntie;
-    int16_t e;   // guessed binade; kNoBinade: none (phase C runs the serial loop)
+    int16_t e;   // guessed binade
+    int16_t j0, j1;
     float up, down;  // 2^(23 - e), 2^(e - 23)
+};
+constexpr int kParts = 3;  // runs per sub-chunk (a sub-chunk crossing more binades runs the serial loop)
+struct Sub {
+    Part p[kParts];
+    int8_t nparts;  // 0: the whole sub-chunk runs the serial loop
+    int16_t jend;   // elements from here on (after the parts) run the serial loop
     double dsum;
 };
 // biased exponent field of a float (1..254: normal)
@@ -169,32 +185,56 @@ float serial_loop(const float* x, int64_t n, float s) {
     return s;
 }
 
-void phase_b(const float* x, int len, Sub& b) {
-    const float f = (float)b.dsum;  // estimate of the serial sum at the sub-chunk start
-    b.e = kNoBinade;
-    const int be = expo(f);
-    if (be == 0 || be == 255) return;  // zero / subnormal / non-finite: serial loop
-    const int e = be - 127;
-    if (e < -103) return;  // u = 2^(e-23) must be a normal float
-    const float scale = pow2f(23 - e);
-    // R and the tie flags: a branch-free loop the compiler vectorises.  An
-    // element with |x/u| > 2^22 (a step of more than a quarter of the sum)
-    // sends the sub-chunk to the serial loop, so the relative prefix fits
-    // int32 (|prefix| <= 256 * 2^22).
-    alignas(64) int32_t R[kG + 4];
-    alignas(64) int32_t tie[kG + 4];
+// (an AVX2 clone beside the baseline, picked at load time: the two loops
+// below are the multi-threaded sum's largest phase.  This file is host code;
+// hipcc also runs it through the gfx950 pass, which has no clones.)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define OFL_HOST_CLONES
+#else
+#define OFL_HOST_CLONES __attribute__((target_clones("avx2", "default")))
+#endif
+// R = x / u rounded half-even and each tie's other candidate (+1 / -1, 0: no
+// tie), for j in [j0, len); false if some |x / u| > 2^22 (a step of more than
+// a quarter of the sum: the relative prefix would leave int32)
+OFL_HOST_CLONES bool steps(const float* x, int j0, int len, float scale, int32_t* R, int32_t* tie) {
     int bad = 0;
-    for (int j = 0; j < len; ++j) {
+    for (int j = j0; j < len; ++j) {
         const float q = x[j] * scale;  // exact (power-of-two scaling)
         bad |= !(std::fabs(q) <= 0x1p22f);  // also NaN
         // round half even: the 1.5 * 2^23 shift rounds in the FPU's default mode
         const float qc = std::fabs(q) <= 0x1p22f ? q : 0.0f;
         const float r = (qc + 0x1.8p23f) - 0x1.8p23f;
-        // a tie's other candidate: +1 if q lies above r, -1 below (0: no tie)
         tie[j] = std::fabs(qc - r) == 0.5f ? (qc > r ? 1 : -1) : 0;
         R[j] = (int32_t)r;
     }
-    if (bad) return;
+    return !bad;
+}
+// the binade of a float estimate (kNoBinade: zero / subnormal / non-finite, or
+// a grid u below the normal range)
+int binade(double est) {
+    const int be = expo((float)est);
+    if (be == 0 || be == 255) return kNoBinade;
+    const int e = be - 127;
+    return e < -103 ? kNoBinade : e;
+}
+bool inside(double S, int64_t lo, int64_t hi, int64_t nt) {  // a start S's partial sums stay in its binade
+    return S > 0 ? (S + (double)(lo - nt) >= (double)kLo && S + (double)(hi + nt) <= (double)kHi)
+                 : (S + (double)(hi + nt) <= -(double)kLo && S + (double)(lo - nt) >= -(double)kHi);
+}
+
+// Phase B of one sub-chunk: the whole sub-chunk as one run in the binade of
+// the estimate at its start (the common case, vectorised); where the
+// estimated partial sums leave that binade, up to kParts runs split at the
+// elements that cross, each in the binade the estimate is in there.
+OFL_HOST_CLONES void phase_b(const float* x, int len, Sub& b) {
+    b.nparts = 0;
+    b.jend = 0;
+    int e = binade(b.dsum);
+    if (e == kNoBinade) return;
+    float scale = pow2f(23 - e);
+    alignas(64) int32_t R[kG + 4];
+    alignas(64) int32_t tie[kG + 4];
+    if (!steps(x, 0, len, scale, R, tie)) return;
     for (int j = len; j < ((len + 3) & ~3); ++j) R[j] = tie[j] = 0;  // ragged tail: zero steps
     // the inclusive prefix, four lanes at a time, and its envelope
     typedef int32_t i4 __attribute__((ext_vector_type(4)));
@@ -215,33 +255,80 @@ void phase_b(const float* x, int len, Sub& b) {
         anytie |= (t.x | t.y | t.z | t.w);
     }
     // (lanes past len in a ragged last group hold P[len - 1]: a real partial sum)
-    int64_t lo = std::min(std::min(mn.x, mn.y), std::min(mn.z, mn.w));
-    int64_t hi = std::max(std::max(mx.x, mx.y), std::max(mx.z, mx.w));
-    const int64_t p = P[len - 1];
+    const int64_t lo = std::min(std::min(mn.x, mn.y), std::min(mn.z, mn.w));
+    const int64_t hi = std::max(std::max(mx.x, mx.y), std::max(mx.z, mx.w));
     int nt = 0;
     if (anytie)
-        for (int j = 0; j < len; ++j)
-            if (tie[j]) {
-                if (nt < kTieCap) {
-                    b.tpre[nt] = P[j] - R[j];  // the prefix before element j
-                    b.tdel[nt] = (int8_t)tie[j];
+        for (int j = 0; j < len; ++j) nt += tie[j] != 0;
+    if (nt <= kTieCap && inside(b.dsum * (double)scale, lo, hi, nt)) {  // one run
+        Part& p = b.p[0];
+        int t = 0;
+        if (anytie)
+            for (int j = 0; j < len; ++j)
+                if (tie[j]) {
+                    p.tpre[t] = P[j] - R[j];  // the prefix before element j
+                    p.tdel[t++] = (int8_t)tie[j];
                 }
-                ++nt;
+        p.pre_end = P[len - 1];
+        p.lo = lo;
+        p.hi = hi;
+        p.ntie = (int16_t)nt;
+        p.e = (int16_t)e;
+        p.up = scale;
+        p.down = pow2f(e - 23);
+        p.j0 = 0;
+        p.j1 = (int16_t)len;
+        b.nparts = 1;
+        b.jend = (int16_t)len;
+        return;
+    }
+    // runs split where the estimate crosses a binade boundary (scalar: rare)
+    double est = b.dsum;
+    int j0 = 0;
+    while (j0 < len && b.nparts < kParts) {
+        if (b.nparts > 0) {  // the grid of this run's binade
+            e = binade(est);
+            if (e == kNoBinade) break;
+            scale = pow2f(23 - e);
+            if (!steps(x, j0, len, scale, R, tie)) break;
+        }
+        Part& p = b.p[b.nparts];
+        const double S = est * (double)scale;  // the estimated integer start
+        int64_t acc = 0, plo = INT64_MAX, phi = INT64_MIN;
+        int t = 0, j = j0;
+        for (; j < len; ++j) {
+            const int64_t a = acc + R[j];
+            const int64_t ntn = t + (tie[j] != 0);
+            if (ntn > kTieCap || !inside(S, std::min(plo, a), std::max(phi, a), ntn)) break;
+            if (tie[j]) {
+                p.tpre[t] = acc;
+                p.tdel[t++] = (int8_t)tie[j];
             }
-    if (nt > kTieCap) return;
-    b.pre_end = p;
-    b.lo = lo;
-    b.hi = hi;
-    b.ntie = (int16_t)nt;
-    b.up = scale;
-    b.down = pow2f(e - 23);
-    b.e = (int16_t)e;
+            acc = a;
+            plo = std::min(plo, a);
+            phi = std::max(phi, a);
+        }
+        p.pre_end = acc;
+        p.lo = j > j0 ? plo : 0;
+        p.hi = j > j0 ? phi : 0;
+        p.ntie = (int16_t)t;
+        p.e = (int16_t)e;
+        p.up = scale;
+        p.down = pow2f(e - 23);
+        p.j0 = (int16_t)j0;
+        p.j1 = (int16_t)j;
+        ++b.nparts;
+        for (int k = j0; k <= j && k < len; ++k) est += (double)x[k];  // through the crossing element
+        j0 = j + 1;
+        b.jend = (int16_t)std::min(j0, len);
+    }
 }
 
-// exact continuation of s over one sub-chunk through its phase-B summary;
-// false: the summary does not apply (the caller runs the serial loop)
-bool phase_c(const Sub& b, float& s) {
-    if (b.e == kNoBinade || expo(s) - 127 != b.e) return false;  // also rejects 0 / subnormal / Inf / NaN
+// exact continuation of s over one run through its summary; false: the
+// summary does not apply (the caller runs the serial loop from the run's start)
+bool run_c(const Part& b, float& s) {
+    if (b.j1 == b.j0) return true;  // an empty run (the first element crossed)
+    if (expo(s) - 127 != b.e) return false;  // also rejects 0 / subnormal / Inf / NaN
     const int64_t S0 = (int64_t)(s * b.up);  // exact integer in [2^23, 2^24) in magnitude
     const int64_t nt = b.ntie;
     if (S0 > 0 ? !(S0 + b.lo - nt >= kLo && S0 + b.hi + nt <= kHi)
@@ -251,6 +338,24 @@ bool phase_c(const Sub& b, float& s) {
     for (int t = 0; t < nt; ++t)
         if ((S0 + b.tpre[t] + c) & 1) c += b.tdel[t];
     s = (float)(S0 + b.pre_end + c) * b.down;  // |S| < 2^24, a power-of-two scale: exact
+    return true;
+}
+
+// phase C of one sub-chunk of len elements at x; returns false if some of it
+// ran the serial loop
+bool phase_c(const Sub& b, const float* x, int len, float& s) {
+    for (int t = 0; t < b.nparts; ++t) {
+        const Part& p = b.p[t];
+        if (!run_c(p, s)) {
+            s = serial_loop(x + p.j0, len - p.j0, s);
+            return false;
+        }
+        if (p.j1 < len) s = s + x[p.j1];  // the crossing element
+    }
+    if (b.jend < len) {
+        s = serial_loop(x + b.jend, len - b.jend, s);
+        return false;
+    }
     return true;
 }
 
@@ -265,7 +370,7 @@ bool debug_on() {
 int default_threads() {
     static const int n = [] {
         const char* v = std::getenv("OFL_SUM_THREADS");
-        int t = v ? std::atoi(v) : 8;
+        int t = v ? std::atoi(v) : 16;  // (8 -> 16 on the GPU box's 16 cores: 553 -> 502 us at 2^21)
         const int hw = (int)std::thread::hardware_concurrency();
         if (hw > 0) t = std::min(t, hw);
         return std::max(1, std::min(t, 64));
@@ -291,7 +396,9 @@ float serial_sum_f32_mt_cb(const float* x, int64_t n, float* dst, int nthreads, 
     // any n); the estimate and the exact sum carry over from chunk to chunk
     constexpr int64_t kChunk = (int64_t)1 << 24;
     const int64_t Kmax = (std::min(n, kChunk) + kG - 1) / kG;
-    std::vector<Sub> subs(Kmax);
+    thread_local std::vector<Sub> subs_tl;  // kept per calling thread: no fresh pages every call
+    if ((int64_t)subs_tl.size() < Kmax) subs_tl.resize(Kmax);
+    std::vector<Sub>& subs = subs_tl;
     double run = 0.0;  // float64 running sum: the estimate at each sub-chunk's start
     float s = 0.0f;    // the exact serial sum so far
     int64_t serial = 0;
@@ -350,10 +457,7 @@ float serial_sum_f32_mt_cb(const float* x, int64_t n, float* dst, int nthreads, 
         // phase C: in order, exact
         const double t2 = debug_on() ? now_s() : 0.0;
         for (int64_t k = 0; k < K; ++k)
-            if (!phase_c(subs[k], s)) {
-                s = serial_loop(xc + k * kG, std::min<int64_t>(kG, nc - k * kG), s);
-                ++serial;
-            }
+            serial += !phase_c(subs[k], xc + k * kG, (int)std::min<int64_t>(kG, nc - k * kG), s);
         if (debug_on()) {
             ta += t1 - t0;
             tb += t2 - t1;

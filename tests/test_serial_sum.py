@@ -36,6 +36,10 @@ def _cases():
         "inf - inf": np.where(idx == 10, np.inf, np.where(idx == 99_999, -np.inf, 1.0)).astype(np.float32),
         "ragged": (rng.standard_normal(1_234_567) * 0.01).astype(np.float32),
         "short": (rng.standard_normal(300) * 0.01).astype(np.float32),
+        # the multi-run phase B: partial sums crossing binades inside sub-chunks
+        "ramp N(.05,.001) (crossings mid sub-chunk)": (rng.standard_normal(n) * 0.001 + 0.05).astype(np.float32),
+        "ramp down through zero": (0.5 - idx * (1.0 / n) + rng.standard_normal(n) * 1e-4).astype(np.float32),
+        "ties walk (k / 8)": (rng.integers(-8, 9, n) / 8 + 0.125).astype(np.float32),
     }
 
 
