@@ -604,7 +604,7 @@ def _batch_decode(eden, items):
 class EdenTransformer(Transformer):
     """Eden quantising transformer (:723-818)."""
 
-    def __init__(self, n_bits=8, dim_threshold=100, device="cpu", seed_mode="reference", combine=False):
+    def __init__(self, n_bits=8, dim_threshold=100, device="cpu", seed_mode="reference"):
         self.lossy = True
         self.eden = Eden(nbits=n_bits, device=device)
         self.dim_threshold = dim_threshold
@@ -612,24 +612,6 @@ class EdenTransformer(Transformer):
         if seed_mode not in ("reference", "fast"):
             raise ValueError("seed_mode must be 'reference' or 'fast'")
         self.seed_mode = seed_mode
-        # combine=True: concurrent per-tensor calls (the gRPC pool's threads)
-        # are merged into batches, one per device slot (openfl_amd/combining.py).
-        # Off by default: measured on ResNet-50 with 2 collaborator threads the
-        # merged batches (1.5 calls on average) ran at 0.92 GiB/s against 3.08
-        # for the same threads calling independently, whose host work (staging,
-        # serial sums) runs in parallel (profiles/r04_e2e_resnet50_2collab.json)
-        self.combine = bool(combine)
-        self._comb_lock = threading.Lock()
-        self._fwd_comb, self._bwd_comb = {}, {}
-
-    def _combiner(self, table, run):
-        slot = self.eden._thread_devices.slot() if getattr(self.eden, "_thread_devices", None) is not None else 0
-        with self._comb_lock:
-            c = table.get(slot)
-            if c is None:
-                from openfl_amd.combining import Combiner
-                c = table[slot] = Combiner(run)
-            return c
 
     def _metadata(self, shape, seed, total_dim, scales, dims):
         md = {"int_list": list(shape), "int_to_float": {0: float(seed), 1: float(total_dim)}}
@@ -653,33 +635,14 @@ class EdenTransformer(Transformer):
         payload = b if isinstance(b, bytes) and len(b) == int_array.nbytes else int_array.tobytes()
         return payload, self._metadata(data.shape, seed, total_dim, scale_list, dim_list)
 
-    def _forward_items(self, items):
-        """The combiner's batch: [(array, draw)] -> [(bytes, metadata)]."""
-        if len(items) == 1:
-            return [self._forward_one(*items[0])]
-        return self._forward_many([a for a, _ in items], [r for _, r in items])
-
-    def _backward_items(self, items):
-        """The combiner's batch: [(bytes, metadata)] -> [array]."""
-        if len(items) == 1:
-            data, md = items[0]
-            out = self.eden.decompress(np.frombuffer(data, dtype=np.uint8), md["int_to_float"])
-            return [out.reshape(list(md["int_list"]))]
-        return self.backward_batch(items)
-
     def forward(self, data, **kwargs):
         if data.size > self.dim_threshold:
-            if not self.combine:
-                return self._forward_one(data)
-            draw = np.random.randint(1, 2 ** 16)  # this call's draw, in call order
-            return self._combiner(self._fwd_comb, self._forward_items).call((data, draw))
+            return self._forward_one(data)
         eden_seed(data, self.seed_mode)  # the reference draws its RNG value for every tensor (:771)
         return self.no_comp.forward(data)
 
     def backward(self, data, metadata, **kwargs):
         if np.prod(metadata["int_list"]) > self.dim_threshold:  # reference: >= (:808), see module doc
-            if self.combine:
-                return self._combiner(self._bwd_comb, self._backward_items).call((data, metadata))
             out = self.eden.decompress(np.frombuffer(data, dtype=np.uint8), metadata["int_to_float"])
             # already a fresh float32 array: astype would only copy it again
             return out.reshape(list(metadata["int_list"]))
@@ -727,8 +690,8 @@ class EdenPipeline(TransformationPipeline):
     """plan.yaml: template openfl_amd.pipelines.EdenPipeline, settings n_bits /
     dim_threshold / device (:821-851); extra keyword seed_mode."""
 
-    def __init__(self, n_bits=8, dim_threshold=100, device="cpu", seed_mode="reference", combine=False, **kwargs):
-        transformers = [EdenTransformer(n_bits, dim_threshold, device, seed_mode, combine)]
+    def __init__(self, n_bits=8, dim_threshold=100, device="cpu", seed_mode="reference", **kwargs):
+        transformers = [EdenTransformer(n_bits, dim_threshold, device, seed_mode)]
         super().__init__(transformers=transformers, **kwargs)
 
     def forward(self, data, **kwargs):

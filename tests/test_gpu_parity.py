@@ -695,16 +695,14 @@ def test_small_set_bit_identical(nbits):
         assert torch.equal(a, b)
 
 
-def test_concurrent_plugin_calls_combine():
+def test_concurrent_plugin_calls():
     """Concurrent per-tensor forward / backward calls (the gRPC pool's threads,
-    aggregator_server.py:305) go through the combining queue
-    (openfl_amd/combining.py): each caller gets exactly the bytes, metadata and
+    aggregator_server.py:305): each caller gets exactly the bytes, metadata and
     values the serial per-tensor path gives for its seed, and the seeds use
     the np.random draws of the calls (one per call, as the reference)."""
     from openfl_amd.pipelines import EdenPipeline
     from openfl_amd.pipelines.eden_pipeline import _serial_sum
-    assert not EdenPipeline(n_bits=8, device=DEV).transformers[0].combine  # opt-in
-    pipe = EdenPipeline(n_bits=8, device=DEV, combine=True)
+    pipe = EdenPipeline(n_bits=8, device=DEV)
     tr = pipe.transformers[0]
     rng = np.random.default_rng(29)
     xs = [(rng.standard_normal(int(n)) * 0.01).astype(np.float32) for n in rng.integers(200, 300_000, 48)]

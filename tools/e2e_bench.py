@@ -7,9 +7,7 @@ Modes (wall-clock, both collaborators, second of two rounds):
   plugin   openfl_amd.pipelines.EdenPipeline per tensor (what TensorCodec calls):
            H2D + encode + D2H per tensor, then H2D + decode + D2H per tensor
   plugin_concurrent  the same per-tensor calls with every collaborator on its
-           own thread, as the gRPC server runs them; concurrent calls are
-           merged into batches by the plugin (openfl_amd/combining.py);
-           plugin_concurrent_nocombine: the same threads, combine=False
+           own thread, as the gRPC server runs them
   batched  EdenPipeline.forward_batch / backward_batch over the whole state
            dict: seeds' serial sums on host threads, one pinned H2D, one
            encode launch sequence, one D2H of the planes arena; the receiver
@@ -173,14 +171,11 @@ def main():
         for _, a in sds[0]:
             cnt[_bucket(a.size)] = cnt.get(_bucket(a.size), 0) + len(sds)
         res["plugin"]["tensors_per_bucket"] = cnt
-    for key, combine in (("plugin_concurrent", True), ("plugin_concurrent_nocombine", False)):
+    if "plugin_concurrent" in modes:
         # the gRPC pattern: each collaborator's tensors on its own handler
-        # thread (aggregator_server.py:305), per-tensor calls, concurrently;
-        # the plugin merges concurrent calls into batches (combine=True)
-        if key not in modes and "plugin_concurrent" not in modes:
-            continue
+        # thread (aggregator_server.py:305), per-tensor calls, concurrently
         from concurrent.futures import ThreadPoolExecutor
-        pipe = EdenPipeline(n_bits=8, dim_threshold=100, device="cuda:0", combine=combine)
+        pipe = EdenPipeline(n_bits=8, dim_threshold=100, device="cuda:0")
         rounds = []
         with ThreadPoolExecutor(max_workers=len(sds)) as ex:
             for r in range(int(os.environ.get("E2E_ROUNDS", "5"))):
@@ -191,12 +186,9 @@ def main():
         # the median of the rounds after the first (single rounds vary by
         # up to 2x with the host's scheduling of the two caller threads)
         dt = float(np.median(rounds[1:])) if len(rounds) > 1 else rounds[0]
-        c = pipe.transformers[0]
-        nb = sum(x.batches for x in list(c._fwd_comb.values()) + list(c._bwd_comb.values()))
-        ni = sum(x.items for x in list(c._fwd_comb.values()) + list(c._bwd_comb.values()))
-        res[key] = {"s": round(dt, 4), "GiB_s": round(in_bytes / dt / 2 ** 30, 3), "threads": len(sds),
-                    "wire_bytes": sum(o[1] for o in outs), "rel_err": round(rel_err(sds[0], outs[0][0]), 6),
-                    "combined_calls_per_batch": round(ni / nb, 3) if nb else None, "round_s": rounds}
+        res["plugin_concurrent"] = {"s": round(dt, 4), "GiB_s": round(in_bytes / dt / 2 ** 30, 3), "threads": len(sds),
+                                    "wire_bytes": sum(o[1] for o in outs),
+                                    "rel_err": round(rel_err(sds[0], outs[0][0]), 6), "round_s": rounds}
     if "batched" in modes:
         for mode in ("reference", "fast"):
             pipe = EdenPipeline(n_bits=8, dim_threshold=100, device="cuda:0", seed_mode=mode)
