@@ -470,6 +470,19 @@ int ofl_inflate_tlz_wait(const uint8_t* src, const int64_t* index, int64_t nmemb
  * and joins the streams before ofl_inflate_tlz_wait). */
 int ofl_inflate_tlz_launch(const uint8_t* src, const int64_t* index, int64_t first, int64_t count, uint8_t* out,
                            size_t out_cap, void* ws, size_t ws_bytes, void* stream);
+/* The KC backward fused (kc_pipeline.py:152-156 then :65-86): the same
+ * launch, but the values stored are lut_tab[t * 32 + rank] for the element's
+ * tensor t, tensors being the element ranges [lut_start[t], lut_end[t]) of the
+ * float32 output (sorted, disjoint; device arrays); elements between tensors
+ * store the rank.  lut_tab[t] is the tensor's int_to_float map applied to
+ * every rank 0..31 in the reference's sequential order.  Finish with
+ * ofl_inflate_tlz_check, which returns OFL_EFORMAT where the TLZ decoder
+ * refused a member (the caller then runs ofl_inflate_members and the LUT
+ * itself; no fallback runs inside). */
+int ofl_inflate_tlz_launch_lut(const uint8_t* src, const int64_t* index, int64_t first, int64_t count, uint8_t* out,
+                               size_t out_cap, void* ws, size_t ws_bytes, const float* lut_tab, const int64_t* lut_start,
+                               const int64_t* lut_end, int32_t lut_n, void* stream);
+int ofl_inflate_tlz_check(int64_t nmembers, void* ws, size_t ws_bytes, void* stream);
 int ofl_inflate_members(const uint8_t* src, const int64_t* index, int64_t nmembers, uint32_t max_isize, uint8_t* out,
                         size_t out_cap, void* ws, size_t ws_bytes, void* stream);
 /* Per-kernel timing of the gzip / inflate launches (bench.py): enable (1)

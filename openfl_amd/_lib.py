@@ -37,7 +37,7 @@ EXPORTS = (
     "ofl_apply_delta_ranges", "ofl_wavg_delta32_ranges", "ofl_sub_f32_f64",
     "ofl_gzip_last_error", "ofl_gzip_ranks_workspace_bytes", "ofl_gzip_ranks_bound", "ofl_gzip_ranks", "ofl_gzip_ranks_to",
     "ofl_gunzip_members", "ofl_gzip_member_index", "ofl_inflate_members", "ofl_inflate_tlz_workspace_bytes",
-    "ofl_inflate_tlz", "ofl_inflate_tlz_async", "ofl_inflate_tlz_wait", "ofl_inflate_tlz_launch", "ofl_gzip_profile", "ofl_gzip_profile_collect",
+    "ofl_inflate_tlz", "ofl_inflate_tlz_async", "ofl_inflate_tlz_wait", "ofl_inflate_tlz_launch", "ofl_inflate_tlz_launch_lut", "ofl_inflate_tlz_check", "ofl_gzip_profile", "ofl_gzip_profile_collect",
 )
 
 
@@ -195,6 +195,10 @@ def _bind(L):
     L.ofl_inflate_tlz_wait.restype = i32
     L.ofl_inflate_tlz_launch.argtypes = [vp, vp, i64, i64, vp, sz, vp, sz, vp]
     L.ofl_inflate_tlz_launch.restype = i32
+    L.ofl_inflate_tlz_launch_lut.argtypes = [vp, vp, i64, i64, vp, sz, vp, sz, vp, vp, vp, i32, vp]
+    L.ofl_inflate_tlz_launch_lut.restype = i32
+    L.ofl_inflate_tlz_check.argtypes = [i64, vp, sz, vp]
+    L.ofl_inflate_tlz_check.restype = i32
     L.ofl_gzip_profile.argtypes = [i32]
     L.ofl_gzip_profile.restype = i32
     L.ofl_gzip_profile_collect.argtypes = [vp, sz, vp, vp, i32, vp]

@@ -1850,6 +1850,14 @@ struct DecArgs {
     uint64_t out_cap;
     uint32_t* cnt;           // [nmem][kMemSeg] ops per segment
     int* status;
+    // the fused LUT decode (k_tlz_resolve<true>): the values stored are
+    // lut_tab[t][rank] for the element's tensor t (elements [lut_start[t],
+    // lut_end[t]) of the stream's float32 output, sorted); elements between
+    // tensors store the rank itself
+    const float* lut_tab;
+    const int64_t* lut_start;
+    const int64_t* lut_end;
+    int32_t lut_n;
 };
 
 // bytes of the stream (any alignment) through a 128-bit block register pair
@@ -2115,6 +2123,7 @@ __global__ __launch_bounds__(64) void k_tlz_ops(DecArgs a) {
 // value's source (pointer jumping in LDS; sources before the segment are in
 // the value ring), the values as float32, CRC-32 of the member, ISIZE.
 constexpr int kRNT = 256, kRPer = kSeg / kRNT;     // resolve: threads per member block, values per thread
+constexpr int kLutSlots = 4;                       // fused LUT: tensor tables per segment in LDS
 // resolve's CRC advances: table i advances by 2^(5 + i) bytes for i < 7 (a
 // thread's 32 bytes .. a wave's 2 KiB), table 7 by a segment's 8 KiB
 static_assert(kSegLog == 11, "resolve's CRC tables assume 2048-value segments");
@@ -2130,7 +2139,20 @@ struct ResSmem {
     uint32_t scan[kRNT / 64];
     uint32_t crc_w[kRNT / 64];
     uint32_t crc_raw;
+    float lt[kLutSlots][32];       // fused LUT: the tables of the segment's first kLutSlots tensors
+    int64_t ls[kLutSlots], le[kLutSlots];
+    int32_t lt0, ln;               // the first of those tensors, how many
 };
+// the tensor of element g (-1: none), by binary search over the sorted starts
+DEVI int lut_find(const DecArgs& a, int64_t g) {
+    int lo = 0, hi = a.lut_n - 1, t = -1;
+    while (lo <= hi) {
+        const int mid = (lo + hi) >> 1;
+        if (a.lut_start[mid] <= g) { t = mid; lo = mid + 1; } else hi = mid - 1;
+    }
+    return t >= 0 && g < a.lut_end[t] ? t : -1;
+}
+template <bool LUT>
 __global__ __launch_bounds__(kRNT) void k_tlz_resolve(DecArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     ResSmem& S = *reinterpret_cast<ResSmem*>(smem_raw);
@@ -2187,6 +2209,22 @@ __global__ __launch_bounds__(kRNT) void k_tlz_resolve(DecArgs a) {
         float* const yo = reinterpret_cast<float*>(a.out + out_off) + c0;
         const uint32_t* opi = reinterpret_cast<const uint32_t*>(yo);
         for (uint32_t k = tid; k < nops; k += kRNT) S.opr[k] = opi[k];
+        const int64_t g0 = out_off / 4 + c0;  // the segment's first element of the stream
+        if (LUT) {  // the tables of the tensors from the one holding (or following) g0
+            if (tid == 0) {
+                int lo = 0, hi = a.lut_n - 1, t = a.lut_n;
+                while (lo <= hi) {  // the first tensor ending after g0
+                    const int mid = (lo + hi) >> 1;
+                    if (a.lut_end[mid] > g0) { t = mid; hi = mid - 1; } else lo = mid + 1;
+                }
+                S.lt0 = t;
+                S.ln = min(kLutSlots, a.lut_n - t);
+            }
+            __syncthreads();
+            const int t0 = S.lt0, ln = S.ln;
+            for (int k = tid; k < ln * 32; k += kRNT) S.lt[k >> 5][k & 31] = a.lut_tab[(int64_t)(t0 + (k >> 5)) * 32 + (k & 31)];
+            if (tid < ln) { S.ls[tid] = a.lut_start[t0 + tid]; S.le[tid] = a.lut_end[t0 + tid]; }
+        }
         __syncthreads();
         // positions: each thread a contiguous run of ops
         const uint32_t o_lo = nops * tid / kRNT, o_hi = nops * (tid + 1) / kRNT;
@@ -2246,6 +2284,24 @@ __global__ __launch_bounds__(kRNT) void k_tlz_resolve(DecArgs a) {
 #pragma unroll
                 for (int q = 0; q < kRPer; ++q)
                     if (q < nv) crc = crc4(S.crct, crc, __float_as_uint(f[q]));
+            }
+            if (LUT) {  // the values through the element's tensor table (the CRC above is the ranks')
+                const int ln = S.ln;
+#pragma unroll
+                for (int q = 0; q < kRPer; ++q) {
+                    const int64_t g = g0 + k0 + q;
+                    const uint32_t id = __float_as_uint(f[q]) ? (uint32_t)f[q] : 0u;
+                    int j = 0;
+                    while (j < ln && g >= S.le[j]) ++j;
+                    float v = f[q];
+                    if (j < ln) {
+                        if (g >= S.ls[j]) v = S.lt[j][id];
+                    } else if (ln == kLutSlots) {  // past the tables in LDS: a segment over many small tensors
+                        const int t = lut_find(a, g);
+                        if (t >= 0) v = a.lut_tab[(int64_t)t * 32 + id];
+                    }
+                    f[q] = v;
+                }
             }
             if (nv == kRPer && (reinterpret_cast<uintptr_t>(yo + k0) & 15u) == 0) {
                 float4* y4 = reinterpret_cast<float4*>(yo + k0);
@@ -2927,8 +2983,10 @@ size_t ofl_inflate_tlz_workspace_bytes(int64_t nmembers) {
     return 256 + 4 * (size_t)std::max<int64_t>(nmembers, 1) * gz::tlz::kMemSeg;
 }
 
+struct LutDev { const float* tab; const int64_t* start; const int64_t* end; int32_t n; };
 static int inflate_tlz_enqueue(const uint8_t* src, const int64_t* index, int64_t first, int64_t count, uint8_t* out,
-                               size_t out_cap, void* ws, size_t ws_bytes, void* stream, bool reset) {
+                               size_t out_cap, void* ws, size_t ws_bytes, void* stream, bool reset,
+                               const LutDev* lut = nullptr) {
     if (first < 0 || count < 0 || (count && (!src || !index || !out))) return gzfail(OFL_EINVAL, "inflate: null argument");
     if (!ws || ws_bytes < ofl_inflate_tlz_workspace_bytes(first + count)) return gzfail(OFL_ESPACE, "inflate: workspace too small");
     GZHIP(ofl_util::per_device_once([] {
@@ -2941,12 +2999,18 @@ static int inflate_tlz_enqueue(const uint8_t* src, const int64_t* index, int64_t
     uint32_t* cnt = reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + 256) + first * gz::tlz::kMemSeg;
     if (reset) GZHIP(hipMemsetAsync(status, 0, sizeof(int), st));
     if (count == 0) return OFL_OK;
-    gz::tlz::DecArgs a{src, index + 4 * first, count, out, (uint64_t)out_cap, cnt, status};
+    gz::tlz::DecArgs a{src, index + 4 * first, count, out, (uint64_t)out_cap, cnt, status,
+                       lut ? lut->tab : nullptr, lut ? lut->start : nullptr, lut ? lut->end : nullptr, lut ? lut->n : 0};
     gzprof_begin(st);
     hipLaunchKernelGGL(gz::tlz::k_tlz_ops, dim3((unsigned)count), dim3(64), sizeof(gz::tlz::DecSmem), st, a);
     gzprof_end(st, "tlz::k_tlz_ops");
     gzprof_begin(st);
-    hipLaunchKernelGGL(gz::tlz::k_tlz_resolve, dim3((unsigned)count), dim3(gz::tlz::kRNT), sizeof(gz::tlz::ResSmem), st, a);
+    if (lut)
+        hipLaunchKernelGGL(gz::tlz::k_tlz_resolve<true>, dim3((unsigned)count), dim3(gz::tlz::kRNT), sizeof(gz::tlz::ResSmem),
+                           st, a);
+    else
+        hipLaunchKernelGGL(gz::tlz::k_tlz_resolve<false>, dim3((unsigned)count), dim3(gz::tlz::kRNT),
+                           sizeof(gz::tlz::ResSmem), st, a);
     gzprof_end(st, "tlz::k_tlz_resolve");
     GZHIP(hipGetLastError());
     return OFL_OK;
@@ -2960,6 +3024,26 @@ int ofl_inflate_tlz_async(const uint8_t* src, const int64_t* index, int64_t firs
 int ofl_inflate_tlz_launch(const uint8_t* src, const int64_t* index, int64_t first, int64_t count, uint8_t* out,
                            size_t out_cap, void* ws, size_t ws_bytes, void* stream) {
     return inflate_tlz_enqueue(src, index, first, count, out, out_cap, ws, ws_bytes, stream, false);
+}
+
+int ofl_inflate_tlz_launch_lut(const uint8_t* src, const int64_t* index, int64_t first, int64_t count, uint8_t* out,
+                               size_t out_cap, void* ws, size_t ws_bytes, const float* lut_tab, const int64_t* lut_start,
+                               const int64_t* lut_end, int32_t lut_n, void* stream) {
+    if (lut_n < 1 || !lut_tab || !lut_start || !lut_end) return gzfail(OFL_EINVAL, "inflate lut: empty table");
+    const LutDev lut{lut_tab, lut_start, lut_end, lut_n};
+    return inflate_tlz_enqueue(src, index, first, count, out, out_cap, ws, ws_bytes, stream, false, &lut);
+}
+
+int ofl_inflate_tlz_check(int64_t nmembers, void* ws, size_t ws_bytes, void* stream) {
+    if (nmembers == 0) return OFL_OK;
+    if (!ws || ws_bytes < ofl_inflate_tlz_workspace_bytes(nmembers)) return gzfail(OFL_ESPACE, "inflate: workspace too small");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    int h = 0;
+    GZHIP(hipMemcpyAsync(&h, static_cast<int*>(ws), sizeof(int), hipMemcpyDeviceToHost, st));
+    GZHIP(hipStreamSynchronize(st));
+    if (h & gz::kInfRange) return gzfail(OFL_ESPACE, "inflate: a member's output falls outside out");
+    if (h) return gzfail(OFL_EFORMAT, "inflate: the TLZ decoder refused a member (the generic inflate decides)");
+    return OFL_OK;
 }
 
 int ofl_inflate_tlz_wait(const uint8_t* src, const int64_t* index, int64_t nmembers, uint8_t* out, size_t out_cap,

@@ -359,8 +359,34 @@ def _buf(device, name, nbytes, pinned=False):
     return b
 
 
+def lut_tables(offsets, numels, maps, device):
+    """The fused LUT of gunzip_device(lut=...): per tensor t, its int_to_float
+    map (the reference's sequential key -> value replacement,
+    kc_pipeline.py:79-83) applied to every rank 0..31, in float32 as
+    lut_decode_batch compares and assigns; with the tensors' element ranges
+    [offsets[t], offsets[t] + numels[t]) of the decoded arena."""
+    T = len(numels)
+    tab = np.empty((T, 32), np.float32)
+    for t, m in enumerate(maps):
+        keys = np.asarray([float(k) for k in m.keys()], np.float32)
+        vals = np.asarray([float(v) for v in m.values()], np.float32)
+        for r in range(32):
+            v = np.float32(r)
+            for k, w in zip(keys, vals):
+                if v == k:
+                    v = w
+            tab[t, r] = v
+    start = np.asarray(offsets, np.int64)
+    end = start + np.asarray(numels, np.int64)
+    order = np.argsort(start, kind="stable")
+    dev = torch.device(device)
+    return {"tab": torch.from_numpy(tab[order].reshape(-1).copy()).to(dev),
+            "start": torch.from_numpy(start[order].copy()).to(dev), "end": torch.from_numpy(end[order].copy()).to(dev),
+            "n": T, "offsets": list(offsets), "numels": list(numels), "maps": list(maps)}
+
+
 @_on_device
-def gunzip_device(data, out):
+def gunzip_device(data, out, lut=None):
     """gzip.decompress (kc_pipeline.py:152-156) of `data` into `out`, a uint8
     DEVICE tensor (returns the view of the decompressed bytes).  Member-indexed
     streams inflate on the GPU from the compressed bytes (the index is built
@@ -369,7 +395,10 @@ def gunzip_device(data, out):
     segment, then the copies resolved in LDS; CRC-32 and ISIZE checked), other
     member-indexed streams through ofl_inflate_members (one wavefront per
     member).  Any other gzip stream (e.g. gzip.compress output) is a
-    different format: gzip.decompress on the host, then one H2D."""
+    different format: gzip.decompress on the host, then one H2D.
+    lut (lut_tables(...)): the decoded ranks go through the tensors' LUTs
+    (the lossy pipelines' backward, kc_pipeline.py:79-83) -- fused into the
+    TLZ decoder's stores, or one lut_decode_batch after any other inflate."""
     if not (out.is_cuda and out.dtype == torch.uint8 and out.is_contiguous()):
         raise _lib.CodecError("gunzip_device: out must be a contiguous uint8 device tensor")
     L = _lib.lib()
@@ -433,6 +462,7 @@ def gunzip_device(data, out):
             raise _lib.CodecError("gunzip_device: output buffer too small")
         if raw.size:
             out[:raw.size].copy_(torch.from_numpy(raw.copy()))
+        _apply_lut(out, raw.size, lut)
         return out[:raw.size]
     if rc != _lib.OFL_OK:
         copy.result()
@@ -447,8 +477,20 @@ def gunzip_device(data, out):
         ws = _buf(dev, "gz_status", int(L.ofl_inflate_tlz_workspace_bytes(nm.value)))
         args = (d_in.data_ptr(), d_idx.data_ptr())
         tail = (out.data_ptr(), out.numel(), ws.data_ptr(), ws.numel())
-        if npieces == 1:
+        if lut is not None:
+            lut_args = (lut["tab"].data_ptr(), lut["start"].data_ptr(), lut["end"].data_ptr(), lut["n"])
+
+            def launch(first, count, st):
+                return L.ofl_inflate_tlz_launch_lut(*args, first, count, *tail, *lut_args, st)
+        else:
+            def launch(first, count, st):
+                return L.ofl_inflate_tlz_launch(*args, first, count, *tail, st)
+        if npieces == 1 and lut is None:
             _lib.check_gzip(L.ofl_inflate_tlz(*args, nm.value, *tail, _stream(dev)))
+        elif npieces == 1:
+            _lib.check_gzip(L.ofl_inflate_tlz_async(*args, 0, 0, *tail, caller_stream.cuda_stream))
+            _lib.check_gzip(launch(0, nm.value, caller_stream.cuda_stream))
+            _lut_finish(L, args, tail, nm, mx, out, tot.value, lut, caller_stream)
         else:
             # status reset and the index on the caller's stream, then every
             # piece on a side stream after its bytes and that reset
@@ -468,25 +510,48 @@ def gunzip_device(data, out):
                         st = sides[k % len(sides)]
                         st.wait_event(ready)
                         st.wait_event(piece_ev[k])
-                        _lib.check_gzip(L.ofl_inflate_tlz_launch(*args, first, last - first, *tail, st.cuda_stream))
+                        _lib.check_gzip(launch(first, last - first, st.cuda_stream))
                         first = last
             finally:
                 copy.result()
                 for st in sides:
                     caller_stream.wait_stream(st)
-            _lib.check_gzip(L.ofl_inflate_tlz_wait(*args, nm.value, *tail, caller_stream.cuda_stream))
+            if lut is None:
+                _lib.check_gzip(L.ofl_inflate_tlz_wait(*args, nm.value, *tail, caller_stream.cuda_stream))
+            else:
+                _lut_finish(L, args, tail, nm, mx, out, tot.value, lut, caller_stream)
     else:
         copy.result()
         ws = _buf(dev, "gz_status", 256)
         _lib.check_gzip(L.ofl_inflate_members(d_in.data_ptr(), d_idx.data_ptr(), nm.value, mx.value, out.data_ptr(),
                                               out.numel(), ws.data_ptr(), ws.numel(), _stream(dev)))
+        _apply_lut(out, tot.value, lut)
     _trim_bufs()
     return out[:tot.value]
 
 
 _INFLATE_PIECES = int(os.environ.get("OFL_INFLATE_PIECES", "4"))  # H2D pieces of a large TLZ payload, each inflated as it lands
 _INFLATE_PIECE_MIN = 32  # MiB: smaller payloads cross in one piece
-_H2D_THREADS = int(os.environ.get("OFL_H2D_THREADS", "2"))  # host threads staging a large pageable payload (0: one plain hipMemcpyAsync)
+_H2D_THREADS = int(os.environ.get("OFL_H2D_THREADS", "2"))
+
+
+def _apply_lut(out, nbytes, lut):
+    """The LUT after an inflate that did not fuse it (lut_decode_batch in place)."""
+    if lut is None or nbytes == 0:
+        return
+    y = out[:nbytes].view(torch.float32)
+    lut_decode_batch(y, lut["offsets"], lut["numels"], lut["maps"], y)
+
+
+def _lut_finish(L, args, tail, nm, mx, out, nbytes, lut, stream):
+    """After fused-LUT launches: the TLZ decoder's verdict; where it refused a
+    member, the generic inflate of every member, then the LUT unfused."""
+    rc = L.ofl_inflate_tlz_check(nm.value, tail[2], tail[3], stream.cuda_stream)
+    if rc == _lib.OFL_EFORMAT:
+        _lib.check_gzip(L.ofl_inflate_members(*args, nm.value, mx.value, *tail, stream.cuda_stream))
+        _apply_lut(out, nbytes, lut)
+        return
+    _lib.check_gzip(rc)  # host threads staging a large pageable payload (0: one plain hipMemcpyAsync)
 _GZ_COPY_THREADS = int(os.environ.get("OFL_GZ_COPY_THREADS", "8"))  # host threads filling the gzip payload
 _GZ_FILL = os.environ.get("OFL_GZ_FILL", "1") != "0"  # 0: copy the payload after the call (A/B)
 

@@ -771,3 +771,73 @@ def test_gzip_ranks_full_size_kc_set():
     got = lossy.gunzip_device(z, out)
     assert got.numel() == 4 * n and torch.equal(got.view(torch.float32), x)
     assert lossy.gzip_ranks(x) == z
+
+
+def _lut_case(seed, sizes, gap=64):
+    """A rank arena (tensors 64-aligned with gaps) and per-tensor maps with
+    sequential-replacement chains (a value equal to a later key)."""
+    rng = np.random.default_rng(seed)
+    offs, acc = [], 0
+    for n in sizes:
+        offs.append(acc)
+        acc = (acc + n + gap - 1) // gap * gap
+    x = np.zeros(acc, np.float32)
+    maps = []
+    for t, (o, n) in enumerate(zip(offs, sizes)):
+        k = int(rng.integers(2, 7))
+        x[o:o + n] = rng.choice(k, n, p=np.full(k, 1.0 / k)).astype(np.float32)
+        m = {i: float(rng.standard_normal() * 0.01) for i in range(k)}
+        if t % 3 == 0:
+            m[0] = 2.0          # 0 -> 2 -> m[2]: the reference's in-place chain
+        maps.append(m)
+    gaps = np.ones(acc, bool)
+    for o, n in zip(offs, sizes):
+        gaps[o:o + n] = False
+    x[gaps] = rng.integers(0, 6, int(gaps.sum())).astype(np.float32)
+    return x, offs, list(sizes), maps
+
+
+@pytest.mark.parametrize("case", ["few_large", "many_small", "pipelined"])
+def test_gunzip_fused_lut_matches_unfused(case, monkeypatch):
+    """gunzip_device(lut=lut_tables(...)): the TLZ decoder's stores go through
+    each tensor's LUT -- every tensor element equals the unfused inflate +
+    lut_decode_batch (the reference's sequential replacement), including
+    segments spanning more tensors than the LDS tables hold and a payload
+    large enough for the pipelined (piecewise H2D) inflate."""
+    from openfl_amd import lossy
+    sizes = {"few_large": [300_000, 131_072 * 2 + 17, 5],
+             "many_small": [int(n) for n in np.random.default_rng(3).integers(1, 900, 700)],
+             "pipelined": [1 << 22] * 5}[case]
+    x, offs, nums, maps = _lut_case(11, sizes)
+    z = lossy.gzip_ranks(torch.from_numpy(x).to(DEV))
+    if case == "pipelined":   # several H2D pieces, each inflated as it lands
+        monkeypatch.setattr(lossy, "_INFLATE_PIECE_MIN", 1)
+        assert len(z) >= 4 << 20
+    ref = torch.empty(x.size, dtype=torch.float32, device=DEV)
+    lossy.gunzip_device(z, ref.view(torch.uint8))
+    lossy.lut_decode_batch(ref, offs, nums, maps, ref)
+    got = torch.full((x.size,), -7.0, dtype=torch.float32, device=DEV)
+    lossy.gunzip_device(z, got.view(torch.uint8), lut=lossy.lut_tables(offs, nums, maps, DEV))
+    torch.cuda.synchronize()
+    r, g = ref.cpu().numpy(), got.cpu().numpy()
+    for o, n in zip(offs, nums):
+        np.testing.assert_array_equal(g[o:o + n], r[o:o + n])
+
+
+def test_gunzip_fused_lut_refused_stream_falls_back():
+    """A TLZ stream the fused decoder refuses (a moved segment entry) goes
+    through the generic inflate and the unfused LUT: same values."""
+    from openfl_amd import lossy
+    x, offs, nums, maps = _lut_case(12, [200_000, 70_001])
+    z = bytearray(lossy.gzip_ranks(torch.from_numpy(x).to(DEV)))
+    z[28 + 4] ^= 0x01
+    z = bytes(z)
+    lut = lossy.lut_tables(offs, nums, maps, DEV)
+    got = torch.empty(x.size, dtype=torch.float32, device=DEV)
+    lossy.gunzip_device(z, got.view(torch.uint8), lut=lut)
+    g = got.cpu().numpy()
+    for o, n, m in zip(offs, nums, maps):
+        want = x[o:o + n].copy()
+        for k, v in m.items():
+            want[want == k] = v
+        np.testing.assert_array_equal(g[o:o + n], want)
