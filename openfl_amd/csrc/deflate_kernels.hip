@@ -2140,7 +2140,7 @@ struct ResSmem {
     uint32_t crc_w[kRNT / 64];
     uint32_t crc_raw;
     float lt[kLutSlots][32];       // fused LUT: the tables of the segment's first kLutSlots tensors
-    int64_t ls[kLutSlots], le[kLutSlots];
+    int32_t ls[kLutSlots], le[kLutSlots];  // their element ranges relative to the segment start (clamped)
     int32_t lt0, ln;               // the first of those tensors, how many
 };
 // the tensor of element g (-1: none), by binary search over the sorted starts
@@ -2223,7 +2223,10 @@ __global__ __launch_bounds__(kRNT) void k_tlz_resolve(DecArgs a) {
             __syncthreads();
             const int t0 = S.lt0, ln = S.ln;
             for (int k = tid; k < ln * 32; k += kRNT) S.lt[k >> 5][k & 31] = a.lut_tab[(int64_t)(t0 + (k >> 5)) * 32 + (k & 31)];
-            if (tid < ln) { S.ls[tid] = a.lut_start[t0 + tid]; S.le[tid] = a.lut_end[t0 + tid]; }
+            if (tid < ln) {
+                S.ls[tid] = (int32_t)max<int64_t>(-1, min<int64_t>(kSeg + 1, a.lut_start[t0 + tid] - g0));
+                S.le[tid] = (int32_t)max<int64_t>(-1, min<int64_t>(kSeg + 1, a.lut_end[t0 + tid] - g0));
+            }
         }
         __syncthreads();
         // positions: each thread a contiguous run of ops
@@ -2287,20 +2290,27 @@ __global__ __launch_bounds__(kRNT) void k_tlz_resolve(DecArgs a) {
             }
             if (LUT) {  // the values through the element's tensor table (the CRC above is the ranks')
                 const int ln = S.ln;
+                int j = 0;  // the slot of this thread's first element (segment-relative k0)
+                while (j < ln && k0 >= S.le[j]) ++j;
+                if (j < ln && k0 >= S.ls[j] && k0 + kRPer <= S.le[j]) {  // all its values in one tensor
 #pragma unroll
-                for (int q = 0; q < kRPer; ++q) {
-                    const int64_t g = g0 + k0 + q;
-                    const uint32_t id = __float_as_uint(f[q]) ? (uint32_t)f[q] : 0u;
-                    int j = 0;
-                    while (j < ln && g >= S.le[j]) ++j;
-                    float v = f[q];
-                    if (j < ln) {
-                        if (g >= S.ls[j]) v = S.lt[j][id];
-                    } else if (ln == kLutSlots) {  // past the tables in LDS: a segment over many small tensors
-                        const int t = lut_find(a, g);
-                        if (t >= 0) v = a.lut_tab[(int64_t)t * 32 + id];
+                    for (int q = 0; q < kRPer; ++q) f[q] = S.lt[j][(uint32_t)f[q]];
+                } else {
+#pragma unroll
+                    for (int q = 0; q < kRPer; ++q) {
+                        const int k = k0 + q;
+                        const uint32_t id = (uint32_t)f[q];
+                        int jj = 0;
+                        while (jj < ln && k >= S.le[jj]) ++jj;
+                        float v = f[q];
+                        if (jj < ln) {
+                            if (k >= S.ls[jj]) v = S.lt[jj][id];
+                        } else if (ln == kLutSlots) {  // past the tables in LDS: a segment over many small tensors
+                            const int t = lut_find(a, g0 + k);
+                            if (t >= 0) v = a.lut_tab[(int64_t)t * 32 + id];
+                        }
+                        f[q] = v;
                     }
-                    f[q] = v;
                 }
             }
             if (nv == kRPer && (reinterpret_cast<uintptr_t>(yo + k0) & 15u) == 0) {

@@ -364,24 +364,30 @@ def lut_tables(offsets, numels, maps, device):
     map (the reference's sequential key -> value replacement,
     kc_pipeline.py:79-83) applied to every rank 0..31, in float32 as
     lut_decode_batch compares and assigns; with the tensors' element ranges
-    [offsets[t], offsets[t] + numels[t]) of the decoded arena."""
+    [offsets[t], offsets[t] + numels[t]) of the decoded arena.  One H2D."""
     T = len(numels)
-    tab = np.empty((T, 32), np.float32)
-    for t, m in enumerate(maps):
-        keys = np.asarray([float(k) for k in m.keys()], np.float32)
-        vals = np.asarray([float(v) for v in m.values()], np.float32)
-        for r in range(32):
-            v = np.float32(r)
-            for k, w in zip(keys, vals):
-                if v == k:
-                    v = w
-            tab[t, r] = v
+    lens = [len(m) for m in maps]
+    mk = max(lens + [1])
+    if T and min(lens) == mk:  # every map the same length (the batched k-means': one array each)
+        keys = np.array([list(m.keys()) for m in maps], np.float32)
+        vals = np.array([list(m.values()) for m in maps], np.float32)
+    else:
+        keys = np.full((T, mk), np.nan, np.float32)   # NaN never compares equal: a shorter map's padding
+        vals = np.zeros((T, mk), np.float32)
+        for t, m in enumerate(maps):
+            if m:
+                keys[t, :len(m)] = np.array(list(m.keys()), np.float32)
+                vals[t, :len(m)] = np.array(list(m.values()), np.float32)
+    tab = np.broadcast_to(np.arange(32, dtype=np.float32), (T, 32)).copy()
+    for j in range(mk):   # in map order: a value equal to a later key is replaced again
+        tab = np.where(tab == keys[:, j:j + 1], vals[:, j:j + 1], tab)
     start = np.asarray(offsets, np.int64)
-    end = start + np.asarray(numels, np.int64)
     order = np.argsort(start, kind="stable")
-    dev = torch.device(device)
-    return {"tab": torch.from_numpy(tab[order].reshape(-1).copy()).to(dev),
-            "start": torch.from_numpy(start[order].copy()).to(dev), "end": torch.from_numpy(end[order].copy()).to(dev),
+    blob = np.concatenate([tab[order].reshape(-1).view(np.uint8), start[order].view(np.uint8),
+                           (start + np.asarray(numels, np.int64))[order].view(np.uint8)])
+    d = torch.from_numpy(blob).to(torch.device(device))
+    return {"tab": d[:128 * T].view(torch.float32), "start": d[128 * T:136 * T].view(torch.int64),
+            "end": d[136 * T:144 * T].view(torch.int64),
             "n": T, "offsets": list(offsets), "numels": list(numels), "maps": list(maps)}
 
 
