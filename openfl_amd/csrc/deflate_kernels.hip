@@ -2139,8 +2139,9 @@ struct ResSmem {
     uint32_t scan[kRNT / 64];
     uint32_t crc_w[kRNT / 64];
     uint32_t crc_raw;
-    float lt[kLutSlots][32];       // fused LUT: the tables of the segment's first kLutSlots tensors
-    int32_t ls[kLutSlots], le[kLutSlots];  // their element ranges relative to the segment start (clamped)
+    float lt[kLutSlots][32];       // fused LUT: the tables of kLutSlots tensors from the segment's first
+    int64_t lsa[kLutSlots], lea[kLutSlots];  // their element ranges in the stream
+    int32_t ls[kLutSlots], le[kLutSlots];    // the same relative to the segment start (clamped)
     int32_t lt0, ln;               // the first of those tensors, how many
 };
 // the tensor of element g (-1: none), by binary search over the sorted starts
@@ -2210,22 +2211,36 @@ __global__ __launch_bounds__(kRNT) void k_tlz_resolve(DecArgs a) {
         const uint32_t* opi = reinterpret_cast<const uint32_t*>(yo);
         for (uint32_t k = tid; k < nops; k += kRNT) S.opr[k] = opi[k];
         const int64_t g0 = out_off / 4 + c0;  // the segment's first element of the stream
-        if (LUT) {  // the tables of the tensors from the one holding (or following) g0
+        if (LUT) {
+            // the slots hold the tensors from the one holding (or following)
+            // the segment's first element: loaded for the member's first
+            // segment, then moved on only where a tensor ended before this
+            // segment (a global search per segment cost ~6 us of dependent
+            // loads on every block's critical path)
             if (tid == 0) {
-                int lo = 0, hi = a.lut_n - 1, t = a.lut_n;
-                while (lo <= hi) {  // the first tensor ending after g0
-                    const int mid = (lo + hi) >> 1;
-                    if (a.lut_end[mid] > g0) { t = mid; hi = mid - 1; } else lo = mid + 1;
+                int t = -1;
+                if (s == 0 || (S.ln > 0 && S.lea[0] <= g0 && S.lt0 + 1 < a.lut_n)) {
+                    int lo = s == 0 ? 0 : S.lt0, hi = a.lut_n - 1;
+                    t = a.lut_n;
+                    while (lo <= hi) {  // the first tensor ending after g0
+                        const int mid = (lo + hi) >> 1;
+                        if (a.lut_end[mid] > g0) { t = mid; hi = mid - 1; } else lo = mid + 1;
+                    }
+                    S.lt0 = t;
+                    S.ln = min(kLutSlots, a.lut_n - t);
                 }
-                S.lt0 = t;
-                S.ln = min(kLutSlots, a.lut_n - t);
+                S.scan[0] = t >= 0 ? 1u : 0u;  // reload (the scan words are free until the block scan)
             }
             __syncthreads();
             const int t0 = S.lt0, ln = S.ln;
-            for (int k = tid; k < ln * 32; k += kRNT) S.lt[k >> 5][k & 31] = a.lut_tab[(int64_t)(t0 + (k >> 5)) * 32 + (k & 31)];
+            if (S.scan[0]) {
+                for (int k = tid; k < ln * 32; k += kRNT) S.lt[k >> 5][k & 31] = a.lut_tab[(int64_t)(t0 + (k >> 5)) * 32 + (k & 31)];
+                if (tid < ln) { S.lsa[tid] = a.lut_start[t0 + tid]; S.lea[tid] = a.lut_end[t0 + tid]; }
+            }
+            __syncthreads();
             if (tid < ln) {
-                S.ls[tid] = (int32_t)max<int64_t>(-1, min<int64_t>(kSeg + 1, a.lut_start[t0 + tid] - g0));
-                S.le[tid] = (int32_t)max<int64_t>(-1, min<int64_t>(kSeg + 1, a.lut_end[t0 + tid] - g0));
+                S.ls[tid] = (int32_t)max<int64_t>(-1, min<int64_t>(kSeg + 1, S.lsa[tid] - g0));
+                S.le[tid] = (int32_t)max<int64_t>(-1, min<int64_t>(kSeg + 1, S.lea[tid] - g0));
             }
         }
         __syncthreads();
