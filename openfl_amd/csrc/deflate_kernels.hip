@@ -1290,8 +1290,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             for (int q = 0; q < kPer; ++q) {
                 const int i = lo + q;
                 fa[q] = fb[q] = fc[q] = 0;
-                nf[q] = 0;
-                bl[q] = 0;
+                bl[q] = kMinL - 1;  // an improvement is then also a copy of >= kMinL values
                 lim[q] = min(kMaxL, send - i);
                 const uint32_t pd = lim[q] >= kMinL ? S.u.m.prev[pslot(i)] : 0u;
                 act[q] = pd != 0;
@@ -1348,13 +1347,15 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                         const int i = lo + q;
                         const bool ok = okq[u];
                         const int L = min(Lq[u], lim[q]);
-                        // branch-free (selects, no exec-mask juggling)
-                        const bool imp = ok && L >= kMinL && L > bl[q];
+                        // branch-free (selects, no exec-mask juggling): the
+                        // first two improvements go to fa and fb, and fc
+                        // always takes the latest (the frontier's count is
+                        // read off the three words after the walk)
+                        const bool imp = ok && L > bl[q];
                         const uint32_t e = (uint32_t)L | ((uint32_t)(i - j[q]) << 7);
-                        fa[q] = imp && nf[q] == 0 ? e : fa[q];
-                        fb[q] = imp && nf[q] == 1 ? e : fb[q];
-                        fc[q] = imp && nf[q] >= 2 ? e : fc[q];
-                        nf[q] = imp ? min(nf[q] + 1, 3) : nf[q];
+                        fb[q] = imp && fa[q] != 0u && fb[q] == 0u ? e : fb[q];
+                        fa[q] = imp && fa[q] == 0u ? e : fa[q];
+                        fc[q] = imp ? e : fc[q];
                         bl[q] = imp ? L : bl[q];
                         act[q] = ok && bl[q] < lim[q] && pd[u] != 0;
                         j[q] -= (int)pd[u];
@@ -1363,6 +1364,9 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                 }
                 if (!any) break;
             }
+#pragma unroll
+            for (int q = 0; q < kPer; ++q)  // 0..3 entries; fc repeats fa or fb below three
+                nf[q] = fa[q] == 0u ? 0 : fb[q] == 0u ? 1 : fc[q] == fb[q] ? 2 : 3;
         }
         PH(3);
         // ---- D: segmented backward DP (kSweeps sweeps) ----
