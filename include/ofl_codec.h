@@ -274,6 +274,23 @@ int ofl_kmeans1d_batch(int ntensors, const float* x_arena, const int64_t* offset
                        int n_init, uint64_t seed, int max_exact, int value_f64, float* ranks_out, double* centres,
                        int64_t* counts, double* inertia, int32_t* nuniq, double* uniq, void* ws, size_t ws_bytes,
                        void* stream);
+/* One tensor's labelling rule after ofl_kmeans1d_batch (k <= 8): an element
+ * x of [start, end) is labelled rank[j] for the first j with x <= mid[j]
+ * (mid[j] = float32 midpoint of sorted centres j and j + 1, +inf from k - 1
+ * on) -- the ranks ranks_out receives.  ofl_gzip_label_to reads these
+ * records instead of a rank array. */
+typedef struct {
+    int64_t start, end;  /* arena element range */
+    float mid[8];
+    float rank[8];
+} ofl_label_rec;
+/* ofl_kmeans1d_batch that also writes label_tab (DEVICE, ntensors records,
+ * ascending non-overlapping ranges required; k <= 8), e.g. with ranks_out
+ * NULL, so that the rank array is never written (ofl_gzip_label_to). */
+int ofl_kmeans1d_batch_tab(int ntensors, const float* x_arena, const int64_t* offsets, const int64_t* numels, int k,
+                           int n_init, uint64_t seed, int max_exact, int value_f64, float* ranks_out,
+                           ofl_label_rec* label_tab, double* centres, int64_t* counts, double* inertia,
+                           int32_t* nuniq, double* uniq, void* ws, size_t ws_bytes, void* stream);
 int ofl_kmeans1d_label(const float* x, int64_t n, const double* centres, int k,
                        const float* rank_of_cluster, float* out, void* stream);
 int ofl_sparsify_topk(const float* x, int64_t n, int64_t k, float* sparse_out, float* kept_min,
@@ -422,6 +439,15 @@ int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size
  * kc_pipeline.py:128-141). */
 int ofl_gzip_ranks_to(const float* x, int64_t n, uint8_t* out, size_t out_cap, uint8_t* host_dst, size_t host_cap,
                       int nthreads, size_t* out_len, void* ws, size_t ws_bytes, void* stream);
+/* The k-means labelling fused into the encoder: x is the VALUE arena the
+ * k-means ran on and every value is labelled through label_tab (DEVICE,
+ * ntensors ofl_label_rec from ofl_kmeans1d_batch_tab) as it is loaded, so the
+ * stream equals ofl_gzip_ranks_to of the ranks ranks_out would hold (0 for
+ * elements outside every range).  host_dst may be NULL (then as
+ * ofl_gzip_ranks). */
+int ofl_gzip_label_to(const float* x, int64_t n, const ofl_label_rec* label_tab, int ntensors, uint8_t* out,
+                      size_t out_cap, uint8_t* host_dst, size_t host_cap, int nthreads, size_t* out_len, void* ws,
+                      size_t ws_bytes, void* stream);
 /* GZIPTransformer.backward (kc_pipeline.py:152-156: gzip.decompress) for a
  * stream whose members all carry a size field ('OZ', or BGZF's 'BC'):
  * members are located from their headers and inflated (zlib) on nthreads host

@@ -25,7 +25,7 @@ EXPORTS = (
     "ofl_eden_encode", "ofl_eden_encode_wavg", "ofl_eden_decode", "ofl_eden_decode_add", "ofl_eden_encode_host", "ofl_eden_decode_host", "ofl_eden_encode_mapped", "ofl_eden_decode_mapped", "ofl_eden_encode_seeded", "ofl_copy_h2d_chunked", "ofl_eden_encode_host_x", "ofl_eden_decode_host_x", "ofl_copy_h2d_async", "ofl_copy_h2d_staged", "ofl_eden_plan_profile", "ofl_eden_plan_num_launches",
     "ofl_eden_plan_launch_info", "ofl_eden_plan_profile_collect", "ofl_serial_sum_f32", "ofl_serial_sum_f32_mt", "ofl_serial_sum_copy_f32",
     "ofl_serial_sum_f64", "ofl_host_copy_many", "ofl_serial_sums_many", "ofl_lossy_last_error", "ofl_lossy_workspace_bytes", "ofl_kmeans1d_fit",
-    "ofl_kmeans1d_batch_workspace_bytes", "ofl_kmeans1d_batch",
+    "ofl_kmeans1d_batch_workspace_bytes", "ofl_kmeans1d_batch", "ofl_kmeans1d_batch_tab",
     "ofl_kmeans1d_label", "ofl_sparsify_topk", "ofl_ternary_stats", "ofl_ternary_ranks", "ofl_lut_decode",
     "ofl_lut_decode_batch_workspace_bytes", "ofl_lut_decode_batch",
     "ofl_sparsify_topk_batch_workspace_bytes", "ofl_sparsify_topk_batch",
@@ -35,7 +35,7 @@ EXPORTS = (
     "ofl_py_hash_doubles",
     "ofl_wavg_points_workspace_bytes", "ofl_wavg_delta_points", "ofl_apply_delta",
     "ofl_apply_delta_ranges", "ofl_wavg_delta32_ranges", "ofl_sub_f32_f64",
-    "ofl_gzip_last_error", "ofl_gzip_ranks_workspace_bytes", "ofl_gzip_ranks_bound", "ofl_gzip_ranks", "ofl_gzip_ranks_to",
+    "ofl_gzip_last_error", "ofl_gzip_ranks_workspace_bytes", "ofl_gzip_ranks_bound", "ofl_gzip_ranks", "ofl_gzip_ranks_to", "ofl_gzip_label_to",
     "ofl_gunzip_members", "ofl_gzip_member_index", "ofl_inflate_members", "ofl_inflate_tlz_workspace_bytes",
     "ofl_inflate_tlz", "ofl_inflate_tlz_async", "ofl_inflate_tlz_wait", "ofl_inflate_tlz_launch", "ofl_inflate_tlz_launch_lut", "ofl_inflate_tlz_check", "ofl_gzip_profile", "ofl_gzip_profile_collect",
 )
@@ -121,6 +121,9 @@ def _bind(L):
     L.ofl_kmeans1d_batch.argtypes = [i32, vp, vp, vp, i32, i32, ctypes.c_uint64, i32, i32, vp, vp, vp, vp, vp,
                                      vp, vp, sz, vp]
     L.ofl_kmeans1d_batch.restype = i32
+    L.ofl_kmeans1d_batch_tab.argtypes = [i32, vp, vp, vp, i32, i32, ctypes.c_uint64, i32, i32, vp, vp, vp, vp, vp, vp,
+                                         vp, vp, sz, vp]
+    L.ofl_kmeans1d_batch_tab.restype = i32
     L.ofl_kmeans1d_label.argtypes = [vp, i64, vp, i32, vp, vp, vp]
     L.ofl_kmeans1d_label.restype = i32
     L.ofl_sparsify_topk.argtypes = [vp, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp]
@@ -179,6 +182,8 @@ def _bind(L):
     L.ofl_gzip_ranks.restype = i32
     L.ofl_gzip_ranks_to.argtypes = [vp, i64, vp, sz, vp, sz, i32, vp, vp, sz, vp]
     L.ofl_gzip_ranks_to.restype = i32
+    L.ofl_gzip_label_to.argtypes = [vp, i64, vp, i32, vp, sz, vp, sz, i32, vp, vp, sz, vp]
+    L.ofl_gzip_label_to.restype = i32
     L.ofl_gunzip_members.argtypes = [vp, sz, vp, sz, vp, i32]
     L.ofl_gunzip_members.restype = i32
     L.ofl_gzip_member_index.argtypes = [vp, sz, vp, i64, vp, vp, vp, vp]

@@ -961,6 +961,12 @@ struct EncSmem {
     uint32_t crc_w[kNT / 64];
     uint32_t ops_n, crc_raw, hdr_bits, total_bits, nrle, nlit_ndist;
     int bad;
+    // fused k-means labelling (EncArgs::lab): the records of tensors lab_t0 ..
+    // lab_t0 + 3 (start = end = INT64_MAX past the last); positions below
+    // lab_hi lie in one of them or in no tensor
+    int32_t lab_t0;
+    int64_t lab_s[4], lab_e[4], lab_hi;
+    float lab_m[4][8], lab_r[4][8];
 };
 static_assert(sizeof(EncSmem) <= 80 * 1024, "two member blocks per CU");
 
@@ -975,8 +981,62 @@ struct EncArgs {
     uint32_t slot_bytes, ops_stride;
     int aligned;             // x is 16-byte aligned
     uint64_t* phases;        // diagnostics (OFL_GZ_PHASES): block 0's time per phase (10 ns ticks), else null
+    const ofl_label_rec* lab;  // non-null: x holds values, labelled through these records as they load
+    int32_t lab_n;
 };
 constexpr int kEncPhases = 16;
+
+// k-means label of one value (k_bkm_label's rule, lossy_kernels.hip)
+DEVI float lab_rank(float v, const float* m, const float* r) {
+    float o = r[0];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) o = v > m[j] ? r[j + 1] : o;
+    return o;
+}
+// wave 0: the label window for a segment starting at s0 -- the first tensor
+// ending after s0 (64-way search from the previous window, ends ascending)
+// and the three after it
+DEVI void lab_fill(const EncArgs& a, EncSmem& S, int64_t s0, int lane) {
+    int lo = S.lab_t0, hi = a.lab_n;
+    while (lo < hi) {
+        const int stride = (hi - lo + 63) >> 6;
+        const int i = lo + lane * stride;
+        const int cnt = __popcll(__ballot(i < hi && a.lab[i].end <= s0));
+        if (cnt == 0) break;
+        const int nlo = lo + (cnt - 1) * stride + 1;
+        hi = min(lo + cnt * stride, hi);
+        lo = nlo;
+    }
+    if (lane < 4) {
+        const int t = lo + lane;
+        if (t < a.lab_n) {
+            const ofl_label_rec r = a.lab[t];
+            S.lab_s[lane] = r.start;
+            S.lab_e[lane] = r.end;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { S.lab_m[lane][j] = r.mid[j]; S.lab_r[lane][j] = r.rank[j]; }
+        } else {
+            S.lab_s[lane] = S.lab_e[lane] = INT64_MAX;
+        }
+    }
+    if (lane == 0) {
+        S.lab_t0 = lo;
+        S.lab_hi = lo + 4 < a.lab_n ? a.lab[lo + 4].start : INT64_MAX;
+    }
+}
+// the label of the value v at arena position g (any position of the segment)
+DEVI float lab_one(const EncArgs& a, const EncSmem& S, int64_t g, float v) {
+    const int sl = (g >= S.lab_s[1]) + (g >= S.lab_s[2]) + (g >= S.lab_s[3]);
+    if (g >= S.lab_s[sl] && g < S.lab_e[sl]) return lab_rank(v, S.lab_m[sl], S.lab_r[sl]);
+    if (g < S.lab_hi) return 0.f;  // between tensors
+    int lo = S.lab_t0 + 4, hi = a.lab_n - 1;  // past the window (> 4 tensors in this segment): last start <= g
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (a.lab[mid].start <= g) lo = mid; else hi = mid - 1;
+    }
+    const ofl_label_rec& r = a.lab[lo];
+    return g >= r.start && g < r.end ? lab_rank(v, r.mid, r.rank) : 0.f;
+}
 
 DEVI int pslot(int p) { return p & (kRing - 1); }
 // the DP's costs live modulo 2^16: all candidates of one position lie within
@@ -1105,7 +1165,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     for (int i = tid; i < kLit; i += kNT) S.hl[i] = 0;
     if (tid < kDist) S.hd[tid] = 0;
     if (tid < kCL) S.hc[tid] = 0;
-    if (tid == 0) { S.totl = S.totd = 0; S.ops_n = 0; S.crc_raw = 0; S.bad = 0; }
+    if (tid == 0) { S.totl = S.totd = 0; S.ops_n = 0; S.crc_raw = 0; S.bad = 0; S.lab_t0 = 0; S.lab_hi = INT64_MIN; }
     __syncthreads();
     // the raw CRC is linear: a thread's 16 bytes (4 values, ids < 32) hash to
     // the XOR of one table entry per value, 4 independent reads instead of
@@ -1132,6 +1192,14 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         const int c0 = c << kSegLog;
         const int send = min(c0 + kSeg, ntok);
         const int lo = c0 + kPer * tid;                 // this thread's positions [lo, lo + kPer)
+        if (a.lab) {  // a new label window when this segment reaches past the current one
+            const int64_t lab_hi = S.lab_hi;
+            if (g0 + send > lab_hi) {
+                __syncthreads();
+                if (wv == 0) lab_fill(a, S, g0 + c0, lane);
+                __syncthreads();
+            }
+        }
         // ---- A: values -> ids in the ring, validity, raw CRC-32 ----
         uint32_t idw[kPer / 4] = {};                    // this thread's ids, packed 4 per word
         {
@@ -1147,6 +1215,23 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             } else {
 #pragma unroll
                 for (int q = 0; q < kPer; ++q) v[q] = q < nv ? a.x[g0 + lo + q] : 0.f;
+            }
+            if (a.lab) {  // values -> ranks (the k-means labels the rank array would hold)
+                const int64_t gp = g0 + lo;
+                const int sl = (gp >= S.lab_s[1]) + (gp >= S.lab_s[2]) + (gp >= S.lab_s[3]);
+                if (nv == kPer && gp >= S.lab_s[sl] && gp + kPer <= S.lab_e[sl]) {  // one tensor (the common case)
+                    float m[7], r[8];
+#pragma unroll
+                    for (int j = 0; j < 7; ++j) m[j] = S.lab_m[sl][j];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) r[j] = S.lab_r[sl][j];
+#pragma unroll
+                    for (int q = 0; q < kPer; ++q) v[q] = lab_rank(v[q], m, r);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < kPer; ++q)
+                        if (q < nv) v[q] = lab_one(a, S, gp + q, v[q]);
+                }
             }
             uint32_t crc = 0;
             bool bad = false;
@@ -2675,9 +2760,12 @@ size_t ofl_gzip_ranks_bound(int64_t n) {
 // host_dst (optional): a pageable buffer of host_cap bytes that receives the
 // stream too, each batch copied on nthreads host threads while the next batch
 // encodes (ofl_gzip_ranks_to)
-static int gzip_ranks_impl(const float* x, int64_t n, uint8_t* out, size_t out_cap, uint8_t* host_dst,
-                           size_t host_cap, int nthreads, size_t* out_len, void* ws, size_t ws_bytes, void* stream) {
+// lab (optional, device): x holds values, labelled through lab_n records as they load
+static int gzip_ranks_impl(const float* x, int64_t n, const ofl_label_rec* lab, int lab_n, uint8_t* out,
+                           size_t out_cap, uint8_t* host_dst, size_t host_cap, int nthreads, size_t* out_len, void* ws,
+                           size_t ws_bytes, void* stream) {
     if (n < 1 || !x || !out || !out_len) return gzfail(OFL_EINVAL, "gzip ranks: empty input");
+    if (lab && lab_n < 1) return gzfail(OFL_EINVAL, "gzip label: no label records");
     if (host_dst && host_cap < out_cap) return gzfail(OFL_EINVAL, "gzip ranks: host_cap < out_cap");
     if (!ws || ws_bytes < ofl_gzip_ranks_workspace_bytes(n)) return gzfail(OFL_ESPACE, "gzip ranks: workspace too small");
     GZHIP(ofl_util::per_device_once([] {  // __constant__ tables and attributes are per device
@@ -2732,7 +2820,7 @@ static int gzip_ranks_impl(const float* x, int64_t n, uint8_t* out, size_t out_c
     }
     auto enc = [&](int64_t c0, int nb, uint8_t* sl, uint32_t* sz) {
         gz::tlz::EncArgs a{x, n, c0, sl, ops, sz, bad, (uint32_t)L.slot, (uint32_t)L.ops_stride, aligned,
-                           c0 == 0 ? d_ph : nullptr};
+                           c0 == 0 ? d_ph : nullptr, lab, lab ? lab_n : 0};
         gzprof_begin(st);
         hipLaunchKernelGGL(gz::tlz::k_tlz_encode, dim3(nb), dim3(gz::tlz::kNT), sizeof(gz::tlz::EncSmem), st, a);
         gzprof_end(st, "tlz::k_tlz_encode");
@@ -2931,13 +3019,22 @@ static int gzip_ranks_impl(const float* x, int64_t n, uint8_t* out, size_t out_c
 
 int ofl_gzip_ranks(const float* x, int64_t n, uint8_t* out, size_t out_cap, size_t* out_len, void* ws,
                    size_t ws_bytes, void* stream) {
-    return gzip_ranks_impl(x, n, out, out_cap, nullptr, 0, 1, out_len, ws, ws_bytes, stream);
+    return gzip_ranks_impl(x, n, nullptr, 0, out, out_cap, nullptr, 0, 1, out_len, ws, ws_bytes, stream);
 }
 
 int ofl_gzip_ranks_to(const float* x, int64_t n, uint8_t* out, size_t out_cap, uint8_t* host_dst, size_t host_cap,
                       int nthreads, size_t* out_len, void* ws, size_t ws_bytes, void* stream) {
     if (!host_dst) return gzfail(OFL_EINVAL, "gzip ranks to: null host_dst");
-    return gzip_ranks_impl(x, n, out, out_cap, host_dst, host_cap, std::max(1, nthreads), out_len, ws, ws_bytes, stream);
+    return gzip_ranks_impl(x, n, nullptr, 0, out, out_cap, host_dst, host_cap, std::max(1, nthreads), out_len, ws,
+                           ws_bytes, stream);
+}
+
+int ofl_gzip_label_to(const float* x, int64_t n, const ofl_label_rec* label_tab, int ntensors, uint8_t* out,
+                      size_t out_cap, uint8_t* host_dst, size_t host_cap, int nthreads, size_t* out_len, void* ws,
+                      size_t ws_bytes, void* stream) {
+    if (!label_tab) return gzfail(OFL_EINVAL, "gzip label: null label_tab");
+    return gzip_ranks_impl(x, n, label_tab, ntensors, out, out_cap, host_dst, host_cap, std::max(1, nthreads), out_len,
+                           ws, ws_bytes, stream);
 }
 
 // Host inflate of a member-indexed gzip stream (every member carries the

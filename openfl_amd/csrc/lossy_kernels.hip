@@ -749,6 +749,22 @@ __global__ __launch_bounds__(kBkmAccNT) void k_bkm_label(BkmArgs a) {
     for (int64_t i = a4 + 4 * n4 + threadIdx.x; i < i1; i += kBkmAccNT) out[i] = rank_of(x[i]);
 }
 
+static_assert(sizeof(ofl_label_rec) == 80, "lossy.LabelTable.REC_BYTES");
+// each tensor's labelling rule as an ofl_label_rec (k <= 8): what k_bkm_label
+// applies, for the gzip encoder to apply as it loads the values
+__global__ __launch_bounds__(64) void k_bkm_tab(BkmArgs a, ofl_label_rec* tab) {
+    const int t = (int)(blockIdx.x * 64 + threadIdx.x);
+    if (t >= a.ntensors) return;
+    const BkmState& S = a.st[t];
+    ofl_label_rec r;
+    r.start = a.td[t].off;
+    r.end = a.td[t].off + a.td[t].n;
+    for (int j = 0; j < 8; ++j) {
+        r.mid[j] = j < 7 ? S.mids[j] : INFINITY;
+        r.rank[j] = S.rank[j < a.k ? j : a.k - 1];
+    }
+    tab[t] = r;
+}
 
 // Batched reference backward (kc_pipeline.py:79-83 per tensor): tensor t's
 // float32 ranks -> values by the sequential in-place key->value replacement,
@@ -1224,7 +1240,21 @@ int ofl_kmeans1d_batch(int ntensors, const float* x_arena, const int64_t* offset
                        int n_init, uint64_t seed, int max_exact, int value_f64, float* ranks_out, double* centres,
                        int64_t* counts, double* inertia, int32_t* nuniq, double* uniq, void* ws, size_t ws_bytes,
                        void* stream) {
+    return ofl_kmeans1d_batch_tab(ntensors, x_arena, offsets, numels, k, n_init, seed, max_exact, value_f64, ranks_out,
+                                  nullptr, centres, counts, inertia, nuniq, uniq, ws, ws_bytes, stream);
+}
+
+int ofl_kmeans1d_batch_tab(int ntensors, const float* x_arena, const int64_t* offsets, const int64_t* numels, int k,
+                           int n_init, uint64_t seed, int max_exact, int value_f64, float* ranks_out,
+                           ofl_label_rec* label_tab, double* centres, int64_t* counts, double* inertia,
+                           int32_t* nuniq, double* uniq, void* ws, size_t ws_bytes, void* stream) {
     if (ntensors < 1 || !x_arena || !offsets || !numels) return lfail(OFL_EINVAL, "kmeans: empty batch");
+    if (label_tab) {
+        if (k > 8) return lfail(OFL_EINVAL, "kmeans: label records need k <= 8");
+        for (int t = 0; t < ntensors; ++t)
+            if (offsets[t] < 0 || (t > 0 && offsets[t] < offsets[t - 1] + numels[t - 1]))
+                return lfail(OFL_EINVAL, "kmeans: label records need ascending, non-overlapping tensors");
+    }
     if (k < 1 || k > lossy::kMaxK) return lfail(OFL_EINVAL, "kmeans: need 1 <= k <= 32");
     if (n_init < 1 || n_init > lossy::kBkmMaxInit || max_exact < 0)
         return lfail(OFL_EINVAL, "kmeans: 1 <= n_init <= 16, max_exact >= 0");
@@ -1279,6 +1309,7 @@ int ofl_kmeans1d_batch(int ntensors, const float* x_arena, const int64_t* offset
         else if (k <= 16) bkm_launch_label<15>(L.blocks, st, a);
         else bkm_launch_label<31>(L.blocks, st, a);
     }
+    if (label_tab) hipLaunchKernelGGL(lossy::k_bkm_tab, dim3((ntensors + 63) / 64), dim3(64), 0, st, a, label_tab);
     LHIP(hipGetLastError());
     std::vector<lossy::BkmState> sh(ntensors);
     LHIP(hipMemcpyAsync(sh.data(), w + L.st, sizeof(lossy::BkmState) * ntensors, hipMemcpyDeviceToHost, st));

@@ -83,12 +83,26 @@ def kmeans_fit(x, k=6, n_init=6, seed=0, max_exact=8):
     return c, cnt, inertia.value
 
 
+class LabelTable:
+    """The per-tensor labelling rules of one kmeans_batch (ofl_label_rec
+    records on the device, include/ofl_codec.h): gzip_ranks(x, label=) labels
+    the values as it encodes them, so the rank array is never written."""
+    REC_BYTES = 80
+
+    def __init__(self, ntensors, device):
+        self.n = int(ntensors)
+        self.buf = torch.empty(self.REC_BYTES * self.n, dtype=torch.uint8, device=device)
+
+
 @_on_device
-def kmeans_batch(x_arena, offsets, numels, k=6, n_init=6, seed=0, max_exact=8, value_f64=False, ranks_out=None):
+def kmeans_batch(x_arena, offsets, numels, k=6, n_init=6, seed=0, max_exact=8, value_f64=False, ranks_out=None,
+                 label_out=None):
     """Device k-means of many tensors of one float32 arena (ofl_kmeans1d_batch):
     tensor t = x_arena[offsets[t]:offsets[t] + numels[t]].  Writes float32
     ranks (np.unique order of the used centres, value dtype float64 if
-    value_f64) into ranks_out (a device arena like x_arena) when given.
+    value_f64) into ranks_out (a device arena like x_arena) when given, and
+    the labelling rules into label_out (a LabelTable; k <= 8, ascending
+    tensors) when given.
     -> (centres [T, k], counts [T, k], inertia [T], uniq: list of arrays)."""
     _check_dev(x_arena)
     L = _lib.lib()
@@ -104,11 +118,17 @@ def kmeans_batch(x_arena, offsets, numels, k=6, n_init=6, seed=0, max_exact=8, v
     uq = np.zeros((T, k), np.float64)
     if ranks_out is not None:
         _check_dev(ranks_out)
-    _lib.check_lossy(L.ofl_kmeans1d_batch(T, x_arena.data_ptr(), off.ctypes.data, num.ctypes.data, k, n_init,
-                                          int(seed), max_exact, 1 if value_f64 else 0,
-                                          ranks_out.data_ptr() if ranks_out is not None else None,
-                                          c.ctypes.data, cnt.ctypes.data, inertia.ctypes.data, nu.ctypes.data,
-                                          uq.ctypes.data, ws.data_ptr(), ws.numel(), _stream(x_arena.device)))
+    if label_out is not None:
+        if not label_out.buf.is_cuda:
+            raise _lib.CodecError("label_out must live on the device")
+        if label_out.n != T:
+            raise ValueError(f"label_out holds {label_out.n} records for {T} tensors")
+    _lib.check_lossy(L.ofl_kmeans1d_batch_tab(T, x_arena.data_ptr(), off.ctypes.data, num.ctypes.data, k, n_init,
+                                              int(seed), max_exact, 1 if value_f64 else 0,
+                                              ranks_out.data_ptr() if ranks_out is not None else None,
+                                              label_out.buf.data_ptr() if label_out is not None else None,
+                                              c.ctypes.data, cnt.ctypes.data, inertia.ctypes.data, nu.ctypes.data,
+                                              uq.ctypes.data, ws.data_ptr(), ws.numel(), _stream(x_arena.device)))
     dt = np.float64 if value_f64 else np.float32
     return c, cnt, inertia, [uq[t, :nu[t]].astype(dt) for t in range(T)]
 
@@ -253,12 +273,17 @@ def lut_decode_batch(ranks_arena, offsets, numels, maps, out_arena):
 
 
 @_on_device
-def gzip_ranks(x):
+def gzip_ranks(x, label=None):
     """gzip.compress of a float32 device array of ranks (integers 0..31), on
     the GPU (ofl_gzip_ranks, TLZ: optimal-parse token LZ, one deflate block
     per 512 KiB member): a multi-member gzip stream that gzip.decompress reads
-    back to x's bytes.  Raises CodecError for other values."""
+    back to x's bytes.  Raises CodecError for other values.  label (a
+    LabelTable from kmeans_batch): x holds the VALUES the k-means ran on and
+    the stream is that of the ranks ranks_out would hold (0 between tensors),
+    labelled inside the encoder (ofl_gzip_label_to)."""
     _check_dev(x)
+    if label is not None and not label.buf.is_cuda:
+        raise _lib.CodecError("label records must live on the device")
     L = _lib.lib()
     n = x.numel()
     if n == 0:
@@ -274,7 +299,11 @@ def gzip_ranks(x):
         out = _buf("host", "gz_out", cap, pinned=True)
         ln = ctypes.c_size_t()
         dst = hostmem.new_payload(cap) if _GZ_FILL else None
-        if dst is not None:
+        if label is not None:
+            rc = L.ofl_gzip_label_to(x.data_ptr(), n, label.buf.data_ptr(), label.n, out.data_ptr(), cap,
+                                     dst[1] if dst is not None else None, cap if dst is not None else 0,
+                                     _GZ_COPY_THREADS, ctypes.byref(ln), ws.data_ptr(), ws.numel(), _stream(x.device))
+        elif dst is not None:
             rc = L.ofl_gzip_ranks_to(x.data_ptr(), n, out.data_ptr(), cap, dst[1], cap, _GZ_COPY_THREADS,
                                      ctypes.byref(ln), ws.data_ptr(), ws.numel(), _stream(x.device))
         else:

@@ -841,3 +841,44 @@ def test_gunzip_fused_lut_refused_stream_falls_back():
         for k, v in m.items():
             want[want == k] = v
         np.testing.assert_array_equal(g[o:o + n], want)
+
+
+@pytest.mark.parametrize("case", ["few_large", "many_small", "ragged", "kc_like"])
+def test_gzip_label_fused_matches_rank_array(case):
+    """gzip_ranks(x, label=kmeans_batch(label_out=...)): the k-means labels
+    applied inside the TLZ encoder as it loads the values give byte for byte
+    the stream of the rank array ranks_out receives (zeros between tensors)
+    -- tensors spanning members, segments holding more tensors than the LDS
+    window (4), odd offsets and lengths, a leading gap."""
+    from openfl_amd import lossy
+    rng = np.random.default_rng({"few_large": 1, "many_small": 2, "ragged": 3, "kc_like": 4}[case])
+    sizes = {"few_large": [300_000, 131_072 * 2 + 17, 9],
+             "many_small": [int(n) for n in rng.integers(6, 900, 700)],
+             "ragged": [int(n) for n in rng.integers(6, 40_000, 60)],
+             "kc_like": [1 << 20, 3 << 18, 1 << 21, 1000, 1 << 20]}[case]
+    offs, acc = [], 37 if case == "ragged" else 0
+    for n in sizes:
+        offs.append(acc)
+        acc += n + (int(rng.integers(0, 9)) if case == "ragged" else (-n) % 64)
+    tot = acc + 5
+    x = torch.from_numpy((rng.standard_normal(tot) * 0.01).astype(np.float32)).to(DEV)
+    ranks = torch.zeros(tot, dtype=torch.float32, device=DEV)
+    tab = lossy.LabelTable(len(sizes), DEV)
+    lossy.kmeans_batch(x, offs, sizes, 6, n_init=6, seed=9, ranks_out=ranks, label_out=tab)
+    z_ref = lossy.gzip_ranks(ranks)
+    z = lossy.gzip_ranks(x, label=tab)
+    assert z == z_ref
+    assert gzip.decompress(z) == ranks.cpu().numpy().tobytes()
+
+
+def test_kmeans_label_table_checks():
+    """Label records need k <= 8 and ascending, non-overlapping tensors."""
+    from openfl_amd import lossy
+    from openfl_amd._lib import CodecError
+    x = torch.randn(4096, device=DEV)
+    with pytest.raises(CodecError):
+        lossy.kmeans_batch(x, [0], [4096], 12, n_init=2, label_out=lossy.LabelTable(1, DEV))
+    with pytest.raises(CodecError):
+        lossy.kmeans_batch(x, [2000, 0], [1000, 1000], 6, n_init=2, label_out=lossy.LabelTable(2, DEV))
+    with pytest.raises(ValueError):
+        lossy.kmeans_batch(x, [0], [4096], 6, n_init=2, label_out=lossy.LabelTable(2, DEV))
