@@ -208,7 +208,13 @@ def secondary(name, n_bits, steps, warmup, dev, wave_mib, streams, cpu=False, gr
     return out
 
 
-KC_TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r04_final_kc_pipeline_hbm_traffic.json")
+def _newest_profile(*names):
+    """The first of the committed profile files that exists (newest round first)."""
+    paths = [os.path.join(ROOT, "profiles", n) for n in names]
+    return next((p for p in paths if os.path.exists(p)), paths[-1])
+
+
+KC_TRAFFIC_JSON = _newest_profile("r05_final_kc_pipeline_hbm_traffic.json", "r04_final_kc_pipeline_hbm_traffic.json")
 
 
 def _kc_kernel_profile(encode, decode, dev, steps=2):
@@ -598,9 +604,7 @@ def main(argv=None):
         # PMC counters cannot be read from inside this process: the committed
         # rocprofv3 --pmc passes of this same workload and default schedule
         # (tools/pmc_run.sh), only when this run uses that schedule
-        traffic_src = os.path.join(ROOT, "profiles", "r04_llama3_8b_hbm_traffic.json")
-        if not os.path.exists(traffic_src):
-            traffic_src = os.path.join(ROOT, "profiles", "r03_final_llama3_8b_hbm_traffic.json")
+        traffic_src = _newest_profile("r05_final_llama3_8b_hbm_traffic.json", "r04_llama3_8b_hbm_traffic.json")
     if traffic_src and os.path.exists(traffic_src):
         with open(traffic_src) as f:
             traffic = json.load(f).get("hbm_bytes_per_step")
