@@ -649,7 +649,7 @@ def main(argv=None):
     if world == 1 and args.also:
         for name in [a for a in args.also.split(",") if a]:
             if name == "kc_uniform_1gib":
-                also[name] = kc_pipeline(max(10, args.also_steps // 2), 2, dev)
+                also[name] = kc_pipeline(max(10, args.also_steps // 2), 4, dev)
             else:
                 # a ResNet-50 step is ~0.35 ms: more steps for a stable rate
                 st = max(args.also_steps, 200) if name == "resnet50_fp32" else args.also_steps

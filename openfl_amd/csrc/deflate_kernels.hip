@@ -1947,6 +1947,7 @@ struct DecArgs {
     const int64_t* lut_start;
     const int64_t* lut_end;
     int32_t lut_n;
+    int32_t dbg;             // diagnostics (OFL_TLZ_DEC_STATS): timing printf of every 256th member
 };
 
 // bytes of the stream (any alignment) through a 128-bit block register pair
@@ -2035,6 +2036,7 @@ __global__ __launch_bounds__(64) void k_tlz_ops(DecArgs a) {
             return;
         }
     }
+    const uint64_t t_start = a.dbg ? wall_clock64() : 0;
     // ---- the block header, on every lane (wave-uniform) ----
     BitIn in;
     in.start(a.src, dbit);
@@ -2109,6 +2111,7 @@ __global__ __launch_bounds__(64) void k_tlz_ops(DecArgs a) {
         return;
     }
     __builtin_amdgcn_wave_barrier();
+    const uint64_t t_hdr = a.dbg ? wall_clock64() : 0;
     // ---- lane s: segment s ----
     const int s = lane;
     if (s < nseg) {
@@ -2205,6 +2208,16 @@ __global__ __launch_bounds__(64) void k_tlz_ops(DecArgs a) {
         }
         a.cnt[m * kMemSeg + s] = nops;
         if (err) atomicOr(a.status, err);
+        if (a.dbg && (m & 255) == 0) {
+            uint32_t dt = (uint32_t)(wall_clock64() - t_hdr), no = nops;
+            for (int o = 32; o > 0; o >>= 1) {
+                dt = max(dt, (uint32_t)__shfl_xor((int)dt, o, 64));
+                no = max(no, (uint32_t)__shfl_xor((int)no, o, 64));
+            }
+            if (lane == 0)
+                printf("tlz_ops m=%lld hdr_ticks=%u lanes_max_ticks=%u lane0_ops=%u max_ops=%u\n", (long long)m,
+                       (uint32_t)(t_hdr - t_start), dt, nops, no);
+        }
     }
 }
 
@@ -2218,13 +2231,17 @@ constexpr int kLutSlots = 4;                       // fused LUT: tensor tables p
 static_assert(kSegLog == 11, "resolve's CRC tables assume 2048-value segments");
 static_assert(kRPer * 32 == kRNT, "one thread per (value slot, id) entry of the resolve's CRC table");
 DEVI int adv_k(int i) { return i < 7 ? 5 + i : 13; }
+// the resolve's value ring: the window and one segment (LDS per block decides
+// how many member blocks share a CU: 4 at < 40 KiB)
+constexpr uint32_t kVRing = kWin + kSeg;
 struct ResSmem {
     uint32_t adv[8][8][16];        // CRC advance by 2^adv_k(i) bytes, per input nibble (table form of c_adv)
     uint32_t cid[kRPer][32];       // raw CRC of a thread's 32 bytes with only value q = id (from 0)
-    uint8_t v[kRing];              // ids by member position (ring)
+    uint8_t v[kVRing];             // ids by member position mod kVRing
     uint32_t opr[kSeg];            // the segment's op records
     uint16_t e[kSeg];              // 0x8000 | id (resolved) or the distance to the source
-    uint32_t crct[4][256];
+    uint32_t cnt[kMemSeg];         // ops per segment (k_tlz_ops)
+    uint32_t crct[1][256];
     uint32_t scan[kRNT / 64];
     uint32_t crc_w[kRNT / 64];
     uint32_t crc_raw;
@@ -2270,12 +2287,8 @@ __global__ __launch_bounds__(kRNT) void k_tlz_resolve(DecArgs a) {
         for (int b = 0; b < 4; ++b) r ^= ((v >> b) & 1) ? c_adv[adv_k(i)][4 * j + b] : 0u;
         S.adv[i][j][v] = r;
     }
+    if (tid < kMemSeg) S.cnt[tid] = tid < nseg ? a.cnt[m * kMemSeg + tid] : 0u;
     __syncthreads();
-    for (int k = 1; k < 4; ++k) {
-        const uint32_t p = S.crct[k - 1][tid];
-        S.crct[k][tid] = (p >> 8) ^ S.crct[0][p & 0xffu];
-        __syncthreads();
-    }
     {  // the raw CRC is linear: a thread's 32 bytes hash to the XOR of one entry per value
         const int q = tid >> 5;
         const uint32_t bits = __float_as_uint((float)(tid & 31));
@@ -2292,13 +2305,32 @@ __global__ __launch_bounds__(kRNT) void k_tlz_resolve(DecArgs a) {
         return r;
     };
     int bad = 0;
+    // a segment's op records (over its own output bytes) are loaded one
+    // segment ahead, into registers, so that their latency overlaps the
+    // previous segment's resolve (they were the loop's first dependent loads)
+    constexpr int kOpPer = kSeg / kRNT;  // >= one op per value: nops <= kSeg
+    uint32_t pre[kOpPer];
+    auto fetch = [&](int sg) {
+        const uint32_t n = sg < nseg ? S.cnt[sg] : 0u;
+        const uint32_t* opi = reinterpret_cast<const uint32_t*>(a.out + out_off) + ((int64_t)sg << kSegLog);
+#pragma unroll
+        for (int i = 0; i < kOpPer; ++i) {
+            const uint32_t k = (uint32_t)(tid + i * kRNT);
+            pre[i] = k < n ? opi[k] : 0u;
+        }
+    };
+    fetch(0);
+    uint64_t t_a = a.dbg ? wall_clock64() : 0, d_pre = 0, d_jump = 0, d_val = 0;
+    uint32_t jumps = 0;
     for (int s = 0; s < nseg; ++s) {
         const int c0 = s << kSegLog;
         const int T = (int)min((uint32_t)kSeg, ntok - (uint32_t)c0);
-        const uint32_t nops = a.cnt[m * kMemSeg + s];
+        const uint32_t nops = S.cnt[s];
+        if (nops > (uint32_t)T) { bad = kInfCorrupt; break; }  // (block-uniform)
         float* const yo = reinterpret_cast<float*>(a.out + out_off) + c0;
-        const uint32_t* opi = reinterpret_cast<const uint32_t*>(yo);
-        for (uint32_t k = tid; k < nops; k += kRNT) S.opr[k] = opi[k];
+#pragma unroll
+        for (int i = 0; i < kOpPer; ++i) S.opr[tid + i * kRNT] = pre[i];
+        fetch(s + 1);
         const int64_t g0 = out_off / 4 + c0;  // the segment's first element of the stream
         if (LUT) {
             // the slots hold the tensors from the one holding (or following)
@@ -2351,17 +2383,20 @@ __global__ __launch_bounds__(kRNT) void k_tlz_resolve(DecArgs a) {
             }
         }
         __syncthreads();
+        uint64_t t_b = a.dbg ? wall_clock64() : 0;
+        if (a.dbg) d_pre += t_b - t_a;
         // pointer jumping: an unresolved entry points at its source; a source
         // before the segment is a value of the ring
 #pragma unroll 1
         for (;;) {
+            ++jumps;
             int pend = 0;
             for (int k = tid; k < T; k += kRNT) {
                 const uint32_t e = S.e[k];
                 if (e & 0x8000u) continue;
                 const int src = k - (int)e;
                 uint32_t ne;
-                if (src < 0) ne = 0x8000u | S.v[(c0 + src) & (kRing - 1)];
+                if (src < 0) ne = 0x8000u | S.v[(uint32_t)(c0 + src) % kVRing];
                 else {
                     const uint32_t es = S.e[src];
                     ne = (es & 0x8000u) ? es : e + es;
@@ -2371,6 +2406,7 @@ __global__ __launch_bounds__(kRNT) void k_tlz_resolve(DecArgs a) {
             }
             if (!__syncthreads_or(pend)) break;
         }
+        if (a.dbg) { const uint64_t t = wall_clock64(); d_jump += t - t_b; t_b = t; }
         // values: ring, output (float32), raw CRC-32
         {
             const int k0 = kRPer * tid;
@@ -2382,7 +2418,7 @@ __global__ __launch_bounds__(kRNT) void k_tlz_resolve(DecArgs a) {
                 const uint32_t id = q < nv ? (uint32_t)(S.e[k0 + q] & 31u) : 0u;
                 f[q] = (float)id;
                 if (q < nv) {
-                    S.v[(c0 + k0 + q) & (kRing - 1)] = (uint8_t)id;
+                    S.v[(uint32_t)(c0 + k0 + q) % kVRing] = (uint8_t)id;
                     crc ^= S.cid[q][id];
                 }
             }
@@ -2453,7 +2489,11 @@ __global__ __launch_bounds__(kRNT) void k_tlz_resolve(DecArgs a) {
             }
         }
         __syncthreads();
+        if (a.dbg) { const uint64_t t = wall_clock64(); d_val += t - t_b; t_a = t; }
     }
+    if (a.dbg && (m & 255) == 0 && tid == 0)
+        printf("tlz_resolve m=%lld load_scan_ticks=%llu jump_ticks=%llu values_ticks=%llu jump_rounds=%u segs=%d\n",
+               (long long)m, (unsigned long long)d_pre, (unsigned long long)d_jump, (unsigned long long)d_val, jumps, nseg);
     if (tid == 0) {
         if (bad) atomicOr(a.status, bad);
         else if ((crc_adv(0xffffffffu, isize) ^ S.crc_raw ^ 0xffffffffu) != want_crc) atomicOr(a.status, kInfCrc);
@@ -3125,8 +3165,10 @@ static int inflate_tlz_enqueue(const uint8_t* src, const int64_t* index, int64_t
     uint32_t* cnt = reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + 256) + first * gz::tlz::kMemSeg;
     if (reset) GZHIP(hipMemsetAsync(status, 0, sizeof(int), st));
     if (count == 0) return OFL_OK;
+    static const int dbg = getenv("OFL_TLZ_DEC_STATS") != nullptr;
     gz::tlz::DecArgs a{src, index + 4 * first, count, out, (uint64_t)out_cap, cnt, status,
-                       lut ? lut->tab : nullptr, lut ? lut->start : nullptr, lut ? lut->end : nullptr, lut ? lut->n : 0};
+                       lut ? lut->tab : nullptr, lut ? lut->start : nullptr, lut ? lut->end : nullptr, lut ? lut->n : 0,
+                       dbg};
     gzprof_begin(st);
     hipLaunchKernelGGL(gz::tlz::k_tlz_ops, dim3((unsigned)count), dim3(64), sizeof(gz::tlz::DecSmem), st, a);
     gzprof_end(st, "tlz::k_tlz_ops");

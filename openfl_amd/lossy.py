@@ -436,6 +436,7 @@ def gunzip_device(data, out, lut=None):
     TLZ decoder's stores, or one lut_decode_batch after any other inflate."""
     if not (out.is_cuda and out.dtype == torch.uint8 and out.is_contiguous()):
         raise _lib.CodecError("gunzip_device: out must be a contiguous uint8 device tensor")
+    tr = _gunzip_trace("start")
     L = _lib.lib()
     src = np.frombuffer(data, np.uint8)
     dev = out.device
@@ -473,6 +474,7 @@ def gunzip_device(data, out, lut=None):
                         ev = torch.cuda.Event()
                         ev.record(caller_stream)
                         piece_ev[k] = ev
+                        tr and tr(f"h2d{k}")
                         landed[k].set()
         finally:
             for e in landed:
@@ -486,6 +488,7 @@ def gunzip_device(data, out, lut=None):
         rc = L.ofl_gzip_member_index(src.ctypes.data if src.size else None, src.size, idx.ctypes.data, cap,
                                      ctypes.byref(nm), ctypes.byref(tot), ctypes.byref(mx), ctypes.byref(tl)) \
             if src.size else _lib.OFL_EFORMAT
+        tr and tr("index")
         if rc != _lib.OFL_OK or not tl.value or npieces == 1:
             copy.result()
     except BaseException:
@@ -546,6 +549,7 @@ def gunzip_device(data, out, lut=None):
                         st.wait_event(ready)
                         st.wait_event(piece_ev[k])
                         _lib.check_gzip(launch(first, last - first, st.cuda_stream))
+                        tr and tr(f"launch{k}")
                         first = last
             finally:
                 copy.result()
@@ -555,6 +559,7 @@ def gunzip_device(data, out, lut=None):
                 _lib.check_gzip(L.ofl_inflate_tlz_wait(*args, nm.value, *tail, caller_stream.cuda_stream))
             else:
                 _lut_finish(L, args, tail, nm, mx, out, tot.value, lut, caller_stream)
+            tr and tr("checked")
     else:
         copy.result()
         ws = _buf(dev, "gz_status", 256)
@@ -565,9 +570,25 @@ def gunzip_device(data, out, lut=None):
     return out[:tot.value]
 
 
+_GUNZIP_TRACE = os.environ.get("OFL_GUNZIP_TRACE") is not None  # diagnostics: gunzip_device's timeline
+
+
+def _gunzip_trace(first):
+    """OFL_GUNZIP_TRACE: a recorder of (label, perf_counter) marks appended to
+    lossy.gunzip_trace_log (one list per call); otherwise None."""
+    if not _GUNZIP_TRACE:
+        return None
+    import time
+    marks = [(first, time.perf_counter())]
+    gunzip_trace_log.append(marks)
+    return lambda label: marks.append((label, time.perf_counter()))
+
+
+gunzip_trace_log = []
 _INFLATE_PIECES = int(os.environ.get("OFL_INFLATE_PIECES", "4"))  # H2D pieces of a large TLZ payload, each inflated as it lands
 _INFLATE_PIECE_MIN = 32  # MiB: smaller payloads cross in one piece
-_H2D_THREADS = int(os.environ.get("OFL_H2D_THREADS", "2"))
+_INFLATE_SIDES = int(os.environ.get("OFL_INFLATE_SIDES", "2"))  # side streams the pieces' inflates rotate over
+_H2D_THREADS = int(os.environ.get("OFL_H2D_THREADS", "2"))  # host threads staging a large pageable payload (0: one plain hipMemcpyAsync)
 
 
 def _apply_lut(out, nbytes, lut):
@@ -586,7 +607,9 @@ def _lut_finish(L, args, tail, nm, mx, out, nbytes, lut, stream):
         _lib.check_gzip(L.ofl_inflate_members(*args, nm.value, mx.value, *tail, stream.cuda_stream))
         _apply_lut(out, nbytes, lut)
         return
-    _lib.check_gzip(rc)  # host threads staging a large pageable payload (0: one plain hipMemcpyAsync)
+    _lib.check_gzip(rc)
+
+
 _GZ_COPY_THREADS = int(os.environ.get("OFL_GZ_COPY_THREADS", "8"))  # host threads filling the gzip payload
 _GZ_FILL = os.environ.get("OFL_GZ_FILL", "1") != "0"  # 0: copy the payload after the call (A/B)
 
@@ -604,11 +627,11 @@ _sides = {}
 
 
 def _side_streams(dev):
-    """Two side streams per device for the pieces of a pipelined inflate."""
+    """_INFLATE_SIDES side streams per device for the pieces of a pipelined inflate."""
     with _pool_lock:
-        key = str(dev)
+        key = (str(dev), _INFLATE_SIDES)
         if key not in _sides:
-            _sides[key] = [torch.cuda.Stream(device=dev) for _ in range(2)]
+            _sides[key] = [torch.cuda.Stream(device=dev) for _ in range(max(_INFLATE_SIDES, 1))]
         return _sides[key]
 
 
