@@ -33,6 +33,16 @@ import time
 
 import numpy as np
 
+# HIP hands streams its GPU_MAX_HW_QUEUES hardware queues (4 by default) in
+# turn, and streams that share a queue run in order.  By the KC leg this
+# process has made the codec's side streams, graph-capture streams and the
+# gzip's DMA stream; with 4 queues the DMA stream could share the caller's
+# queue and wait behind the next batch's encode (gzip phase 11.9 -> 13.8-14.9
+# ms per GiB in some runs; profiles/r05_kc_hw_queues_ab.txt).  With 8 every
+# stream has its own.  Must be set before the HIP runtime starts (the first
+# torch.cuda call); a deployment sets it in its environment the same way.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -52,6 +62,8 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-budget-s", type=float, default=15.0,
                     help="CPU baseline: oracle time budget on the main workload's tensors")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-numa-bind", action="store_true",
+                    help="leave the process on every allowed CPU (default: the GPU's NUMA node, openfl_amd.numa)")
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="do not record per-launch HIP events in the timed region")
     ap.add_argument("--traffic-json", default=None,
@@ -491,6 +503,9 @@ def main(argv=None):
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if not args.no_numa_bind:  # host buffers and threads on the GPU's socket (openfl_amd.numa)
+        from openfl_amd import numa
+        numa.bind_to_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 

@@ -217,9 +217,15 @@ int ofl_copy_h2d_async(void* dst_dev, const void* src_host, size_t bytes, void* 
  * soon as it is staged, so the host copies and the DMAs run together.
  * Returns when every chunk is staged and enqueued: the source may be
  * released then, and work enqueued on `stream` afterwards sees the data.
- * Calls are serialized on the ring; copies under 8 MiB go straight to
- * hipMemcpyAsync. */
+ * Each device keeps up to 4 rings (concurrent callers each take one, a fifth
+ * waits); copies under 8 MiB go straight to hipMemcpyAsync. */
 int ofl_copy_h2d_staged(void* dst_dev, const void* src_host, size_t bytes, int nthreads, void* stream);
+/* The current device's side stream `index` (0..2), created once per device,
+ * all three together: the Eden plans' side streams and the pipelined
+ * inflate's piece streams (1, 2).  HIP gives streams the GPU_MAX_HW_QUEUES
+ * hardware queues in turn and streams on one queue run in order, so the
+ * library shares these instead of making more. */
+int ofl_side_stream(int index, void** stream);
 
 /* ---- profiling (bench.py) --------------------------------------------------
  * While enabled, every encode/decode of the plan records a HIP event before

@@ -35,7 +35,7 @@ EXPORTS = (
     "ofl_py_hash_doubles",
     "ofl_wavg_points_workspace_bytes", "ofl_wavg_delta_points", "ofl_apply_delta",
     "ofl_apply_delta_ranges", "ofl_wavg_delta32_ranges", "ofl_sub_f32_f64",
-    "ofl_gzip_last_error", "ofl_gzip_ranks_workspace_bytes", "ofl_gzip_ranks_bound", "ofl_gzip_ranks", "ofl_gzip_ranks_to", "ofl_gzip_label_to",
+    "ofl_gzip_last_error", "ofl_gzip_ranks_workspace_bytes", "ofl_gzip_ranks_bound", "ofl_gzip_ranks", "ofl_gzip_ranks_to", "ofl_gzip_label_to", "ofl_side_stream",
     "ofl_gunzip_members", "ofl_gzip_member_index", "ofl_inflate_members", "ofl_inflate_tlz_workspace_bytes",
     "ofl_inflate_tlz", "ofl_inflate_tlz_async", "ofl_inflate_tlz_wait", "ofl_inflate_tlz_launch", "ofl_inflate_tlz_launch_lut", "ofl_inflate_tlz_check", "ofl_gzip_profile", "ofl_gzip_profile_collect",
 )
@@ -184,6 +184,8 @@ def _bind(L):
     L.ofl_gzip_ranks_to.restype = i32
     L.ofl_gzip_label_to.argtypes = [vp, i64, vp, i32, vp, sz, vp, sz, i32, vp, vp, sz, vp]
     L.ofl_gzip_label_to.restype = i32
+    L.ofl_side_stream.argtypes = [i32, ctypes.POINTER(ctypes.c_void_p)]
+    L.ofl_side_stream.restype = i32
     L.ofl_gunzip_members.argtypes = [vp, sz, vp, sz, vp, i32]
     L.ofl_gunzip_members.restype = i32
     L.ofl_gzip_member_index.argtypes = [vp, sz, vp, i64, vp, vp, vp, vp]

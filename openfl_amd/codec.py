@@ -175,6 +175,19 @@ class EdenPlan:
             raise _lib.CodecError(f"buffer must be contiguous {dtype} with >= {min_numel} elements")
 
 
+_capture_streams = {}
+
+
+def _capture_stream(dev):
+    """One capture stream per device for every EdenStepGraph: each new stream
+    takes the next HW queue round robin, and a queue shared with a busy
+    stream serialises (ofl_side_stream in include/ofl_codec.h)."""
+    key = str(dev)
+    if key not in _capture_streams:
+        _capture_streams[key] = torch.cuda.Stream(device=dev)
+    return _capture_streams[key]
+
+
 class EdenStepGraph:
     """One plan's encode + decode over fixed device buffers, captured once as a
     hipGraph (torch.cuda.CUDAGraph around the C-ABI calls; the plan's
@@ -189,7 +202,7 @@ class EdenStepGraph:
         plan.encode(x, seeds, planes, scales, ws)
         plan.decode(planes, seeds, scales, y, ws)
         torch.cuda.synchronize(dev)
-        self._stream = torch.cuda.Stream(device=dev)
+        self._stream = _capture_stream(dev)
         self._stream.wait_stream(torch.cuda.current_stream(dev))
         self._graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self._graph, stream=self._stream):

@@ -2589,8 +2589,13 @@ void gzprof_end(hipStream_t st, const char* name) {
     g_prof_a = nullptr;
 }
 
-// the device's side stream for the gzip's pack launches (created once per
-// device; the pack of batch k overlaps the encode of batch k + 1)
+// the device's stream for the gzip's DMA (created once per device): the
+// DMA of batch k overlaps the encode of batch k + 1 only from another HW
+// queue.  HIP hands normal-priority streams the GPU_MAX_HW_QUEUES queues in
+// turn, so a normal stream made late in a busy process can share the
+// caller's queue (the DMA then waits behind the next encode: gzip phase
+// 11.9 -> 14.9 ms per GiB); a high-priority stream comes from HIP's separate
+// high-priority queues (profiles/r05_kc_hw_queues_ab.txt)
 hipError_t gz_side_stream(hipStream_t* out) {
     static std::mutex m;
     static hipStream_t side[64] = {};
@@ -2599,7 +2604,11 @@ hipError_t gz_side_stream(hipStream_t* out) {
     if (e != hipSuccess) return e;
     if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
     std::lock_guard<std::mutex> g(m);
-    if (!side[dev]) e = hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking);
+    if (!side[dev]) {
+        int least = 0, greatest = 0;
+        e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(&side[dev], hipStreamNonBlocking, greatest);
+    }
     *out = side[dev];
     return e;
 }

@@ -3240,14 +3240,24 @@ int ofl_eden_plan_create(int ntensors, const int64_t* numel, const int64_t* elem
 // stream then waits behind a wave stream.  Runs of different plans on the
 // shared streams stay correct (fork/join events per plan); they may wait for
 // each other's work enqueued in between.
-static int shared_side_streams(int dev, bool two, bool three, hipStream_t& s1, hipStream_t& s2, hipStream_t& s3) {
+// The same streams serve the pipelined inflate's pieces (1, 2)
+// (ofl_side_stream): HIP hands streams the HW queues in turn, so the three
+// are created together, and every stream the library made instead of sharing
+// them pushed a later one onto a queue already in use
+// (profiles/r05_kc_hw_queues_ab.txt).
+static int side_pool(int dev, hipStream_t (&out)[3]) {
     static std::mutex mu;
     static std::map<int, std::array<hipStream_t, 3>> pool;
     std::lock_guard<std::mutex> g(mu);
     auto& e = pool[dev];
-    if (!e[0]) HIP_TRY(hipStreamCreateWithFlags(&e[0], hipStreamNonBlocking));
-    if (two && !e[1]) HIP_TRY(hipStreamCreateWithFlags(&e[1], hipStreamNonBlocking));
-    if (three && !e[2]) HIP_TRY(hipStreamCreateWithFlags(&e[2], hipStreamNonBlocking));
+    for (int i = 0; i < 3; ++i)
+        if (!e[i]) HIP_TRY(hipStreamCreateWithFlags(&e[i], hipStreamNonBlocking));
+    for (int i = 0; i < 3; ++i) out[i] = e[i];
+    return OFL_OK;
+}
+static int shared_side_streams(int dev, bool two, bool three, hipStream_t& s1, hipStream_t& s2, hipStream_t& s3) {
+    hipStream_t e[3];
+    if (int rc = side_pool(dev, e)) return rc;
     s1 = e[0];
     s2 = two ? e[1] : nullptr;
     s3 = three ? e[2] : nullptr;
@@ -3282,6 +3292,16 @@ static int ensure_device(ofl_eden_plan_t pl) {
         if (side4) HIP_TRY(hipEventCreateWithFlags(&pl->ev_join3, hipEventDisableTiming));
     }
     pl->uploaded = true;
+    return OFL_OK;
+}
+
+int ofl_side_stream(int index, void** stream) {
+    if (index < 0 || index > 2 || !stream) return fail(OFL_EINVAL, "side stream: index 0..2, non-null out");
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    hipStream_t e[3];
+    if (int rc = side_pool(dev, e)) return rc;
+    *stream = e[index];
     return OFL_OK;
 }
 

@@ -587,7 +587,6 @@ def _gunzip_trace(first):
 gunzip_trace_log = []
 _INFLATE_PIECES = int(os.environ.get("OFL_INFLATE_PIECES", "4"))  # H2D pieces of a large TLZ payload, each inflated as it lands
 _INFLATE_PIECE_MIN = 32  # MiB: smaller payloads cross in one piece
-_INFLATE_SIDES = int(os.environ.get("OFL_INFLATE_SIDES", "2"))  # side streams the pieces' inflates rotate over
 _H2D_THREADS = int(os.environ.get("OFL_H2D_THREADS", "2"))  # host threads staging a large pageable payload (0: one plain hipMemcpyAsync)
 
 
@@ -627,11 +626,20 @@ _sides = {}
 
 
 def _side_streams(dev):
-    """_INFLATE_SIDES side streams per device for the pieces of a pipelined inflate."""
+    """The side streams of a pipelined inflate's pieces: the library's shared
+    side streams 1 and 2 of the device (ofl_side_stream; a new stream per
+    caller would push later streams onto HW queues already in use)."""
     with _pool_lock:
-        key = (str(dev), _INFLATE_SIDES)
+        key = str(dev)
         if key not in _sides:
-            _sides[key] = [torch.cuda.Stream(device=dev) for _ in range(max(_INFLATE_SIDES, 1))]
+            L = _lib.lib()
+            sides = []
+            with torch.cuda.device(dev):
+                for i in (1, 2):
+                    p = ctypes.c_void_p()
+                    _lib.check(L.ofl_side_stream(i, ctypes.byref(p)))
+                    sides.append(torch.cuda.ExternalStream(p.value, device=dev))
+            _sides[key] = sides
         return _sides[key]
 
 

@@ -23,6 +23,11 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--hostmem", action="store_true")
+    ap.add_argument("--no-numa-bind", action="store_true")
+    ap.add_argument("--extra-streams", type=int, default=0,
+                    help="diagnostics: create and use this many torch streams first (HW queue sharing)")
+    ap.add_argument("--ballast-gib", type=float, default=0.0,
+                    help="diagnostics: hold this much device memory (written once) during the run")
     args = ap.parse_args()
     import torch
     import bench
@@ -31,8 +36,26 @@ def main():
         if not keep_large_blocks():
             raise SystemExit("keep_large_blocks() is not available here")
     torch.cuda.set_device(0)
+    cpus = None
+    if not args.no_numa_bind:
+        from openfl_amd import numa
+        cpus = numa.bind_to_device(0)
+    keep = []
+    for _ in range(args.extra_streams):
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st):
+            keep.append(torch.ones(1024, device="cuda:0") * 2)
+        keep.append(st)
+    torch.cuda.synchronize()
+    ballast = None
+    if args.ballast_gib > 0:
+        ballast = torch.ones(int(args.ballast_gib * 2 ** 28), dtype=torch.float32, device="cuda:0")
+        torch.cuda.synchronize()
     out = bench.kc_pipeline(args.steps, args.warmup, torch.device("cuda", 0), extras=False)
     out["hostmem_policy"] = bool(args.hostmem)
+    out["ballast_gib"] = args.ballast_gib
+    out["numa_cpus"] = f"{cpus[0]}-{cpus[-1]} ({len(cpus)})" if cpus else None
+    del ballast
     print(json.dumps(out), flush=True)
 
 

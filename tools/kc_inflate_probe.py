@@ -40,8 +40,8 @@ def main():
     y = torch.empty_like(x)
     yb = y.view(torch.uint8)
     res = {"payload_bytes": len(z), "calls": [], "configs": {}}
-    for pieces, sides in [(4, 2), (4, 4), (8, 4), (8, 8), (6, 6), (3, 3), (4, 2)]:
-        lossy._INFLATE_PIECES, lossy._INFLATE_SIDES = pieces, sides
+    for pieces in [4, 2, 3, 6, 8, 4]:
+        lossy._INFLATE_PIECES = pieces
         ts, gaps = [], []
         for r in range(7):
             lut = lossy.lut_tables(offs, numels, maps, dev)
@@ -54,9 +54,9 @@ def main():
             m = dict(lossy.gunzip_trace_log[0])
             ts.append(1e3 * (t2 - t0))
             gaps.append(1e3 * (t2 - m[f"h2d{pieces - 1}"]))
-        res["configs"][f"p{pieces}s{sides}"] = {"ms_med": round(float(np.median(ts[1:])), 3),
+        res["configs"][f"p{pieces}"] = {"ms_med": round(float(np.median(ts[1:])), 3),
                                                 "last_landed_to_synced_med": round(float(np.median(gaps[1:])), 3)}
-    lossy._INFLATE_PIECES, lossy._INFLATE_SIDES = 4, 2
+    lossy._INFLATE_PIECES = 4
     for r in range(10):
         lut = lossy.lut_tables(offs, numels, maps, dev)
         torch.cuda.synchronize()
