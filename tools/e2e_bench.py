@@ -128,6 +128,8 @@ def main():
     ap.add_argument("--collaborators", type=int, default=2)
     ap.add_argument("--modes", default="plugin,batched,cpu")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--numa-bind", action="store_true",
+                    help="bind the process to the GPU's NUMA node first (openfl_amd.numa, as bench.py does)")
     ap.add_argument("--heap-policy", action="store_true",
                     help="hostmem.keep_large_blocks() first (the opt-in deployment setting: large host "
                          "blocks stay in the heap, so protobuf copies and fresh arrays do not page-fault)")
@@ -140,6 +142,9 @@ def main():
     from openfl_amd.pipelines import EdenPipeline
     from openfl_amd.workloads import WORKLOADS
     dev = torch.device("cuda", 0)
+    if args.numa_bind:
+        from openfl_amd import numa
+        numa.bind_to_device(0)
     shapes = WORKLOADS[args.workload]()
     sds = [state_dict(shapes, 100 + c) for c in range(args.collaborators)]
     in_bytes = sum(a.nbytes for sd in sds for _, a in sd)
