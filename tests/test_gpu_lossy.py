@@ -455,6 +455,13 @@ def test_tlz_rejects_corrupt_streams():
     for b in cases:
         assert gzip.decompress(bytes(b)) == x.tobytes()
         assert lossy.gunzip_device(bytes(b), out).cpu().numpy().tobytes() == x.tobytes()
+    # a truncated stream (the last member cut inside its data, or just its
+    # trailer) raises on both paths and never faults
+    for cut in (len(z) - 8 - in_len // 2, len(z) - 3):
+        with pytest.raises((_lib.CodecError, EOFError, OSError, zlib.error)):
+            gzip.decompress(z[:cut])
+        with pytest.raises((_lib.CodecError, EOFError, OSError, zlib.error)):
+            lossy.gunzip_device(z[:cut], out)
 
 
 def test_gzip_ranks_rejects_non_ranks():
