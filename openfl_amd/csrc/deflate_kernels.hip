@@ -351,7 +351,6 @@ constexpr int kRing = 512;                 // compressed-input ring per wave (by
 #define OFL_INF_WAVES 1
 #endif
 constexpr int kFastBits = OFL_INF_FASTBITS; // first-level decode table: codes of <= 9 bits
-constexpr int kFast = 1 << kFastBits;
 
 // A first-level table entry says what the symbol means, so the serial decode
 // (scalar-unit bound: one SALU pipe per CU serves all its waves) needs no
