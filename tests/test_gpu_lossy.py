@@ -889,3 +889,26 @@ def test_kmeans_label_table_checks():
         lossy.kmeans_batch(x, [2000, 0], [1000, 1000], 6, n_init=2, label_out=lossy.LabelTable(2, DEV))
     with pytest.raises(ValueError):
         lossy.kmeans_batch(x, [0], [4096], 6, n_init=2, label_out=lossy.LabelTable(2, DEV))
+
+
+def test_side_streams_shared_per_device():
+    """ofl_side_stream: three streams per device, the same objects on every
+    call (the Eden plans' side streams and the pipelined inflate's), distinct
+    from each other and from the caller's stream."""
+    import ctypes
+    from openfl_amd import _lib, lossy
+    L = _lib.lib()
+    got = []
+    for _ in range(2):
+        row = []
+        for i in range(3):
+            p = ctypes.c_void_p()
+            _lib.check(L.ofl_side_stream(i, ctypes.byref(p)))
+            row.append(p.value)
+        got.append(row)
+    assert got[0] == got[1] and len(set(got[0])) == 3 and all(got[0])
+    assert torch.cuda.current_stream().cuda_stream not in got[0]
+    p = ctypes.c_void_p()
+    assert L.ofl_side_stream(3, ctypes.byref(p)) == _lib.OFL_EINVAL
+    sides = lossy._side_streams(torch.device(DEV))
+    assert [s.cuda_stream for s in sides] == got[0][1:]

@@ -60,3 +60,11 @@ def test_shared_mapping_follows():
         t.join()
     assert all(x == y for x, y in seen)
     assert sorted(x for x, _ in seen) == ["d0", "d0", "d1", "d1"]
+
+
+def test_numa_cpulist_parsing():
+    """openfl_amd.numa reads sysfs cpulists ("0-3,8,10-11") into CPU sets."""
+    from openfl_amd import numa
+    assert numa._cpulist("0-3,8,10-11") == {0, 1, 2, 3, 8, 10, 11}
+    assert numa._cpulist("64-127,192-255") == set(range(64, 128)) | set(range(192, 256))
+    assert numa._cpulist("") == set() and numa._cpulist(None) == set()
