@@ -2236,9 +2236,9 @@ constexpr uint32_t kVRing = kWin + kSeg;
 struct ResSmem {
     uint32_t adv[8][8][16];        // CRC advance by 2^adv_k(i) bytes, per input nibble (table form of c_adv)
     uint32_t cid[kRPer][32];       // raw CRC of a thread's 32 bytes with only value q = id (from 0)
-    uint8_t v[kVRing];             // ids by member position mod kVRing
+    alignas(16) uint8_t v[kVRing];  // ids by member position mod kVRing
     uint32_t opr[kSeg];            // the segment's op records
-    uint16_t e[kSeg];              // 0x8000 | id (resolved) or the distance to the source
+    alignas(16) uint16_t e[kSeg];   // 0x8000 | id (resolved) or the distance to the source
     uint32_t cnt[kMemSeg];         // ops per segment (k_tlz_ops)
     uint32_t crct[1][256];
     uint32_t scan[kRNT / 64];
@@ -2386,23 +2386,35 @@ __global__ __launch_bounds__(kRNT) void k_tlz_resolve(DecArgs a) {
         if (a.dbg) d_pre += t_b - t_a;
         // pointer jumping: an unresolved entry points at its source; a source
         // before the segment is a value of the ring
+        const int rb0 = (int)((uint32_t)c0 % kVRing);
+        // (a resolved entry stays resolved: each thread skips the ones it
+        // saw resolved, so later rounds read only the 43 %, 7 %, ... left)
+        uint32_t um = (1u << kRPer) - 1u;
 #pragma unroll 1
         for (;;) {
             ++jumps;
             int pend = 0;
-            for (int k = tid; k < T; k += kRNT) {
+            uint32_t nm = 0;
+#pragma unroll
+            for (int i = 0; i < kRPer; ++i) {
+                const int k = tid + i * kRNT;
+                if (!((um >> i) & 1u) || k >= T) continue;
                 const uint32_t e = S.e[k];
                 if (e & 0x8000u) continue;
                 const int src = k - (int)e;
                 uint32_t ne;
-                if (src < 0) ne = 0x8000u | S.v[(uint32_t)(c0 + src) % kVRing];
+                if (src < 0) {  // a value before the segment: ring slot (c0 + src) mod kVRing, src >= -kWin
+                    const int r = rb0 + src;
+                    ne = 0x8000u | S.v[r < 0 ? r + (int)kVRing : r];
+                }
                 else {
                     const uint32_t es = S.e[src];
                     ne = (es & 0x8000u) ? es : e + es;
                 }
                 S.e[k] = (uint16_t)ne;
-                pend |= !(ne & 0x8000u);
+                if (!(ne & 0x8000u)) { pend = 1; nm |= 1u << i; }
             }
+            um = nm;
             if (!__syncthreads_or(pend)) break;
         }
         if (a.dbg) { const uint64_t t = wall_clock64(); d_jump += t - t_b; t_b = t; }
@@ -2412,14 +2424,24 @@ __global__ __launch_bounds__(kRNT) void k_tlz_resolve(DecArgs a) {
             const int nv = max(0, min(kRPer, T - k0));
             uint32_t crc = 0;
             float f[kRPer];
+            // the thread's 8 entries as one 16-byte read, its 8 ids into the
+            // ring as one 8-byte write (c0 + k0 and kVRing are multiples of 8:
+            // the 8 ring slots never wrap)
+            static_assert(kRPer == 8 && kVRing % 8 == 0, "one b128 read, one b64 ring write per thread");
+            const uint4 ev = *reinterpret_cast<const uint4*>(&S.e[k0]);
+            const uint32_t ew[4] = {ev.x, ev.y, ev.z, ev.w};
+            uint32_t idw[2] = {0u, 0u};
 #pragma unroll
             for (int q = 0; q < kRPer; ++q) {
-                const uint32_t id = q < nv ? (uint32_t)(S.e[k0 + q] & 31u) : 0u;
+                const uint32_t id = q < nv ? ((ew[q >> 1] >> (16 * (q & 1))) & 31u) : 0u;
                 f[q] = (float)id;
-                if (q < nv) {
-                    S.v[(uint32_t)(c0 + k0 + q) % kVRing] = (uint8_t)id;
-                    crc ^= S.cid[q][id];
-                }
+                idw[q >> 2] |= id << (8 * (q & 3));
+                if (q < nv) crc ^= S.cid[q][id];
+            }
+            if (nv == kRPer) {
+                *reinterpret_cast<uint2*>(&S.v[(uint32_t)(c0 + k0) % kVRing]) = make_uint2(idw[0], idw[1]);
+            } else {
+                for (int q = 0; q < nv; ++q) S.v[(uint32_t)(c0 + k0 + q) % kVRing] = (uint8_t)(idw[q >> 2] >> (8 * (q & 3)));
             }
             if (nv < kRPer) {  // a partial last piece: the values' own chain
                 crc = 0;
