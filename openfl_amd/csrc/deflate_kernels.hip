@@ -2140,10 +2140,13 @@ __global__ __launch_bounds__(64) void k_tlz_ops(DecArgs a) {
             }
             ++nops;
         };
+        // a corrupt segment must not decode on past its member: the lane
+        // stops once its bit window's block passes the data's last block + 1
+        // (reads stay within ~48 bytes past the data; the stream is padded
+        // for that), checked on the block index instead of the bit position
+        const int64_t blim = (int64_t)(ebit >> 7) + 1;
         while (produced < T) {
-            // a corrupt segment must not decode on past its member: one op
-            // reads at most ~48 bytes beyond pos (the stream is padded for that)
-            if (in.pos() > ebit) { err = kInfCorrupt; break; }
+            if (in.blk > blim) { err = kInfCorrupt; break; }
             in.fill();
             uint32_t e = S.lit.fast[in.peek() & (uint32_t)(DecLit::kSize - 1)];
             int l = (int)(e & 15u);
@@ -2172,12 +2175,14 @@ __global__ __launch_bounds__(64) void k_tlz_ops(DecArgs a) {
                 in.fill();
                 const uint32_t f = S.dist.fast[in.peek() & (uint32_t)(DecDist::kSize - 1)];
                 const int l2 = (int)(f & 15u);
-                if (!l2 || ((f >> 8) & 3u) != (uint32_t)kKindCopy) { err = kInfCorrupt; break; }
-                in.drop(l2);
+                in.drop(l2);  // (l2 == 0 or a wrong kind fails below, before anything is used)
                 const uint32_t d = (f >> 16) + in.get((int)((f >> 4) & 15u));
                 const uint32_t lt = len >> 2, dt = d >> 2;
-                if ((len & 3u) || (d & 3u) || lt < (uint32_t)kMinL || lt > (uint32_t)kMaxL || produced + lt > T ||
-                    dt > before + produced || dt > (uint32_t)kWin) { err = kInfCorrupt; break; }
+                // every check at once: one branch out instead of one per test
+                const bool bad = (l2 == 0) | (((f >> 8) & 3u) != (uint32_t)kKindCopy) | (((len | d) & 3u) != 0u) |
+                                 (lt - (uint32_t)kMinL > (uint32_t)(kMaxL - kMinL)) | (produced + lt > T) |
+                                 (dt > before + produced) | (dt > (uint32_t)kWin);
+                if (bad) { err = kInfCorrupt; break; }
                 emit(lt | (dt << 7));
                 produced += lt;
             } else {
