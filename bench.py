@@ -227,6 +227,16 @@ def _newest_profile(*names):
 
 
 KC_TRAFFIC_JSON = _newest_profile("r05_final_kc_pipeline_hbm_traffic.json", "r04_final_kc_pipeline_hbm_traffic.json")
+KC_SQ_JSON = _newest_profile("r05_final_kc_sq.json")
+
+
+def _valu_busy(sq):
+    """VALU issue share of a dispatch from rocprofv3 SQ counters (means per
+    dispatch): wave64 VALU instructions x 4 cycles over the 1024 SIMDs,
+    against SQ_BUSY_CYCLES summed over the 32 shader engines (8 XCDs x 4)."""
+    if not sq or not sq.get("SQ_BUSY_CYCLES"):
+        return None
+    return round(sq["SQ_INSTS_VALU"] * 4 / 1024 / (sq["SQ_BUSY_CYCLES"] / 32), 3)
 
 
 def _kc_kernel_profile(encode, decode, dev, steps=2):
@@ -375,6 +385,17 @@ def kc_pipeline(steps, warmup, dev, extras=True):
         pk = next((v for k, v in kern_pmc.items() if name and (k == name or k.endswith("::" + name))), None)
         if pk:
             roof["dominant_kernel"]["traffic_per_launch"] = pk["read_bytes_per_dispatch"] + pk["write_bytes_per_dispatch"]
+    if name and os.path.exists(KC_SQ_JSON):
+        # the dominant kernel is compute-bound, not HBM-bound: its VALU issue
+        # share from the committed SQ counter passes (tools/r05_evidence.sh b)
+        with open(KC_SQ_JSON) as f:
+            sq_all = json.load(f)
+        sq = next((v for k, v in sq_all.items() if k.split("(")[0].endswith(name.split("(")[0])), None)
+        vb = _valu_busy(sq)
+        if vb is not None:
+            roof["dominant_kernel"]["valu_busy"] = vb
+            roof["dominant_kernel"]["limiter"] = ("VALU issue (rocprofv3 SQ_INSTS_VALU / SQ_BUSY_CYCLES, "
+                                                  + os.path.relpath(KC_SQ_JSON, ROOT) + ", not this run)")
     if not extras:
         return {"value": round(nbytes / wall / 2 ** 30, 3), "unit": "GiB/s", "ms_per_step": round(1e3 * wall, 3),
                 "phases_ms": phases, "wire_ratio": round(len(z) / nbytes, 4), "roofline": roof,
