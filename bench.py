@@ -33,16 +33,6 @@ import time
 
 import numpy as np
 
-# HIP hands streams its GPU_MAX_HW_QUEUES hardware queues (4 by default) in
-# turn, and streams that share a queue run in order.  By the KC leg this
-# process has made the codec's side streams, graph-capture streams and the
-# gzip's DMA stream; with 4 queues the DMA stream could share the caller's
-# queue and wait behind the next batch's encode (gzip phase 11.9 -> 13.8-14.9
-# ms per GiB in some runs; profiles/r05_kc_hw_queues_ab.txt).  With 8 every
-# stream has its own.  Must be set before the HIP runtime starts (the first
-# torch.cuda call); a deployment sets it in its environment the same way.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -64,6 +54,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-numa-bind", action="store_true",
                     help="leave the process on every allowed CPU (default: the GPU's NUMA node, openfl_amd.numa)")
+    ap.add_argument("--hw-queues", type=int, default=0,
+                    help="set GPU_MAX_HW_QUEUES before the HIP runtime starts (0 = leave the environment's / "
+                         "HIP's default of 4); recorded in the line's host_env")
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="do not record per-launch HIP events in the timed region")
     ap.add_argument("--traffic-json", default=None,
@@ -354,6 +347,9 @@ def kc_pipeline(steps, warmup, dev, extras=True):
         z, maps = encode()
         decode(z, maps)
     wall = (time.perf_counter() - t0) / steps
+    # quality of the timed path itself: y of the last timed step (label-fused
+    # encode -> pipelined LUT-fused inflate), before anything below rewrites y
+    rel = float(torch.linalg.vector_norm((y - x).double()) / torch.linalg.vector_norm(x.double()))
     phases = {k: round(1e3 * v / steps, 3) for k, v in ph.items()}
     nbytes = 4 * sum(numels)
     # roofline of the pipeline step: its minimum I/O, the Eden line's
@@ -399,7 +395,8 @@ def kc_pipeline(steps, warmup, dev, extras=True):
     if not extras:
         return {"value": round(nbytes / wall / 2 ** 30, 3), "unit": "GiB/s", "ms_per_step": round(1e3 * wall, 3),
                 "phases_ms": phases, "wire_ratio": round(len(z) / nbytes, 4), "roofline": roof,
-                "tensors": len(numels), "bytes": nbytes, "steps": steps, "warmup": warmup}
+                "check_rel_l2": round(rel, 5), "tensors": len(numels), "bytes": nbytes, "steps": steps,
+                "warmup": warmup}
     # device part alone (k-means + ranks, LUT decode; the previous KC line)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -409,7 +406,7 @@ def kc_pipeline(steps, warmup, dev, extras=True):
         lossy.lut_decode_batch(ranks, offs, numels, [{i: u for i, u in enumerate(uq)} for uq in uniq], y)
     torch.cuda.synchronize()
     dev_only = (time.perf_counter() - t0) / steps
-    rel = float(torch.linalg.vector_norm((y - x).double()) / torch.linalg.vector_norm(x.double()))
+    rel_dev = float(torch.linalg.vector_norm((y - x).double()) / torch.linalg.vector_norm(x.double()))
     # host gzip -9 (the reference compressor) on a 4-tensor sample of the ranks, all host cores
     sample = ranks[:4 * numels[0]].cpu().numpy().tobytes()
     t0 = time.perf_counter()
@@ -435,7 +432,9 @@ def kc_pipeline(steps, warmup, dev, extras=True):
     return {"value": round(nbytes / wall / 2 ** 30, 3), "unit": "GiB/s", "ms_per_step": round(1e3 * wall, 3),
             "phases_ms": phases, "roofline": roof,
             "wire_ratio": round(len(z) / nbytes, 4), "check_rel_l2": round(rel, 5),
+            "check_rel_l2_scope": "y of the last timed step (label-fused encode, pipelined LUT-fused inflate)",
             "device_only": {"value": round(nbytes / dev_only / 2 ** 30, 2), "ms_per_step": round(1e3 * dev_only, 3),
+                            "check_rel_l2": round(rel_dev, 5),
                             "scope": "batched k-means fit + ranks and LUT decode, no gzip"},
             "host_gzip9_variant": {"value": round(nbytes / t_host_pipe / 2 ** 30, 4),
                                    "gzip9_GiBps": round(host_gz_gibs, 4), "ratio": round(len(zh) / len(sample), 4),
@@ -505,6 +504,8 @@ def dry_run(args, rank, world):
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse_args(argv)
+    if args.hw_queues > 0:  # before anything starts the HIP runtime (the first torch.cuda call)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(args.gpus, argv, args.master_port)
     rank = int(os.environ.get("RANK", 0))
@@ -524,9 +525,17 @@ def main(argv=None):
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    numa_cpus = None
     if not args.no_numa_bind:  # host buffers and threads on the GPU's socket (openfl_amd.numa)
         from openfl_amd import numa
-        numa.bind_to_device(local)
+        numa_cpus = numa.bind_to_device(local)
+    # the process placement every number of this line was measured under
+    host_env = {"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES"),
+                "GPU_MAX_HW_QUEUES_source": ("bench.py --hw-queues" if args.hw_queues > 0 else
+                                             "environment" if "GPU_MAX_HW_QUEUES" in os.environ else
+                                             "unset (HIP default, 4)"),
+                "numa_bind": (f"CPUs {numa_cpus[0]}-{numa_cpus[-1]} ({len(numa_cpus)}) of the GPU's node"
+                              if numa_cpus else "none" if args.no_numa_bind else "no node found (unbound)")}
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
@@ -720,6 +729,7 @@ def main(argv=None):
             "check_rel_l2": round(rel, 6),
             "roofline": roof,
             "cpu_baseline": cpu,
+            "host_env": host_env,
             "also": also or None,
         }
         print(json.dumps(out), flush=True)

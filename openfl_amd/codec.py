@@ -176,16 +176,23 @@ class EdenPlan:
 
 
 _capture_streams = {}
+_capture_locks = {}
+_capture_guard = threading.Lock()
 
 
 def _capture_stream(dev):
-    """One capture stream per device for every EdenStepGraph: each new stream
-    takes the next HW queue round robin, and a queue shared with a busy
-    stream serialises (ofl_side_stream in include/ofl_codec.h)."""
+    """One capture stream per device for every EdenStepGraph, with the lock
+    that serialises captures on it: each new stream takes the next HW queue
+    round robin, and a queue shared with a busy stream serialises
+    (ofl_side_stream in include/ofl_codec.h); two captures begun on one stream
+    at once would both fail, so EdenStepGraph holds the lock while it
+    captures.  -> (stream, lock)."""
     key = str(dev)
-    if key not in _capture_streams:
-        _capture_streams[key] = torch.cuda.Stream(device=dev)
-    return _capture_streams[key]
+    with _capture_guard:
+        if key not in _capture_streams:
+            _capture_streams[key] = torch.cuda.Stream(device=dev)
+            _capture_locks[key] = threading.Lock()
+        return _capture_streams[key], _capture_locks[key]
 
 
 class EdenStepGraph:
@@ -199,15 +206,20 @@ class EdenStepGraph:
 
     def __init__(self, plan, x, seeds, planes, scales, y, ws):
         dev = x.device
-        plan.encode(x, seeds, planes, scales, ws)
-        plan.decode(planes, seeds, scales, y, ws)
-        torch.cuda.synchronize(dev)
-        self._stream = _capture_stream(dev)
-        self._stream.wait_stream(torch.cuda.current_stream(dev))
-        self._graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self._graph, stream=self._stream):
+        self._stream, lock = _capture_stream(dev)
+        # one construction at a time per device: the captures share the
+        # device's capture stream, and the eager run's synchronize must not
+        # fall inside another thread's capture; thread_local capture mode so
+        # that unrelated threads' calls do not invalidate this capture
+        with lock:
             plan.encode(x, seeds, planes, scales, ws)
             plan.decode(planes, seeds, scales, y, ws)
+            torch.cuda.synchronize(dev)
+            self._stream.wait_stream(torch.cuda.current_stream(dev))
+            self._graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._graph, stream=self._stream, capture_error_mode="thread_local"):
+                plan.encode(x, seeds, planes, scales, ws)
+                plan.decode(planes, seeds, scales, y, ws)
         self._keep = (plan, x, seeds, planes, scales, y, ws)  # the graph holds their addresses
 
     def replay(self):

@@ -1931,7 +1931,12 @@ struct DecSmem {
     uint8_t lens[320];
 };
 struct DecArgs {
-    const uint8_t* src;      // device stream (readable 64 bytes past every member: BitIn's look-ahead at the end bound)
+    // device stream: readable, and already landed, 64 bytes past every
+    // member's trailer (BitIn's look-ahead at the end bound; the pipelined
+    // inflate launches a member only once the H2D piece holding its end plus
+    // those 64 bytes has landed, lossy.gunzip_device / _INFLATE_LOOKAHEAD;
+    // the last piece is followed by 128 bytes of padding)
+    const uint8_t* src;
     const int64_t* idx;      // per member: data offset, data length | kind << 62, output offset, isize | crc << 32
     int64_t nmem;
     uint8_t* out;

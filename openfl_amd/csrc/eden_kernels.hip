@@ -1156,6 +1156,24 @@ __device__ void raw_store_f32(float v, rsrc_t r, int voff, int soff, int aux) __
 constexpr int kLdAux = OFL_LD_AUX;
 constexpr int kStAux = OFL_ST_AUX;
 
+// Ladder builds (diagnostics only, WRONG results; tools/r06_ladder.sh):
+// -DOFL_LADDER=1 the large-slice passes keep only their tile loads and
+// stores (same addresses, layouts and bytes), =2 adds the butterflies and
+// the LDS exchanges, =3 adds the sign generation (D1 hashes, the D2 byte
+// table); 0 (the product) adds the quantiser / plane pack, the centroid
+// unpack and the block reductions.  The partial sums are then written as 1.
+#ifndef OFL_LADDER
+#define OFL_LADDER 0
+#endif
+constexpr int kLadder = OFL_LADDER;
+constexpr bool kLadFly = kLadder == 0 || kLadder >= 2;   // butterflies + exchanges
+constexpr bool kLadSign = kLadder == 0 || kLadder >= 3;  // sign generation
+constexpr bool kLadFull = kLadder == 0;                  // quantiser, unpack, reductions
+// the memory-only rungs' stand-ins: a plane word from 4 values, values from a plane byte
+DEVI uint32_t lad_word(float a, float b, float c, float d) {
+    return __float_as_uint(a) ^ __float_as_uint(b) ^ __float_as_uint(c) ^ __float_as_uint(d);
+}
+
 // word 3 = 0x00020000: 32-bit data format, as the gfx9 family expects
 DEVI rsrc_t mk_rsrc(const void* p, uint32_t bytes) {
     const uint64_t a = reinterpret_cast<uint64_t>(p);
@@ -1310,6 +1328,13 @@ DEVI void store_ws4(const KArgs& a, const SliceDesc& D, uint32_t tile, uint32_t 
     }
 }
 
+// the memory-only ladder rungs' stand-in for unpack_centroids64: a value per
+// byte of the plane words (no bit transposes, no centroid table)
+DEVI void lad_unpack64(const uint64_t (&w)[8], float (&v)[64]) {
+#pragma unroll
+    for (int r = 0; r < 64; ++r) v[r] = (float)((uint32_t)(w[r >> 3] >> (8 * (r & 7))) & 255u);
+}
+
 // the tile's 8-byte word of every plane (planes >= nbits read as 0).  A8: the
 // launch's plane rows are 8-byte aligned; otherwise bytes.
 template <bool A8>
@@ -1357,21 +1382,27 @@ __global__ __launch_bounds__(kRowNT) void k_enc_rowA(KArgs a) {
         fetch_x(a, udesc(a.d, sn), tln, more, base1, nx);
         fix_x(a, D, tile, base1, v);
         const uint32_t b1 = seed_b(sld(a.seeds, D.tensor));
-        float ss = sum_sq(v);
-        apply_signs_direct<RS::L1>(v, tile << kRowLog, base1, D.logp, b1, 1.0f);
-        stages<RS::L1, RS::F1a>(v);
-        exchange<RS::L1, RS::L2>(v, s, tid);
-        stages<RS::L2, RS::F1b>(v);
+        float ss = kLadFull ? sum_sq(v) : 1.0f;
+        if constexpr (kLadSign) apply_signs_direct<RS::L1>(v, tile << kRowLog, base1, D.logp, b1, 1.0f);
+        if constexpr (kLadFly) {
+            stages<RS::L1, RS::F1a>(v);
+            exchange<RS::L1, RS::L2>(v, s, tid);
+            stages<RS::L2, RS::F1b>(v);
+        }
         if constexpr (kRowWs4) {
-            exchange<RS::L2, RS::L3F>(v, s, tid);
-            stages<RS::L3F, RS::F1c>(v);
+            if constexpr (kLadFly) {
+                exchange<RS::L2, RS::L3F>(v, s, tid);
+                stages<RS::L3F, RS::F1c>(v);
+            }
             store_ws4<RS::L3F>(a, D, tile, base3, v);
         } else {
-            exchange<RS::L2, RS::L3>(v, s, tid);
-            stages<RS::L3, RS::F1c>(v);
+            if constexpr (kLadFly) {
+                exchange<RS::L2, RS::L3>(v, s, tid);
+                stages<RS::L3, RS::F1c>(v);
+            }
             store_ws(a, D, tile, base3, v);
         }
-        ss = block_sum<kRowNT>(ss, red);
+        if constexpr (kLadFull) ss = block_sum<kRowNT>(ss, red);
         if (tid == 0) a.part[D.part_off + tile] = ss;
         if (!more) break;
         t = tn; si = sn; tile = tln;
@@ -1405,11 +1436,13 @@ __global__ __launch_bounds__(kRowNT) void k_enc_rowC(KArgs a) {
         tw.at(more ? tn : t, sn, tln);
         const SliceDesc Dn = udesc(a.d, sn);
         fetch_ws(a, Dn, tln, more, base3, nx);
-        stages<RS::L3, RS::F2c>(v);
-        exchange<RS::L3, RS::L4>(v, s, tid);
-        stages<RS::L4, RS::F2d>(v);
-        exchange<RS::L4, RS::L5>(v, s, tid);
-        stages<RS::L5, RS::F2e>(v);
+        if constexpr (kLadFly) {
+            stages<RS::L3, RS::F2c>(v);
+            exchange<RS::L3, RS::L4>(v, s, tid);
+            stages<RS::L4, RS::F2d>(v);
+            exchange<RS::L4, RS::L5>(v, s, tid);
+            stages<RS::L5, RS::F2e>(v);
+        }
         __builtin_amdgcn_sched_barrier(0);  // keep the quantiser out of the butterflies (VGPR cap)
         const float nu = sldf(a.nu, si);
         const float ysc = pow2i(-((D.logp + 1) / 2));
@@ -1417,14 +1450,22 @@ __global__ __launch_bounds__(kRowNT) void k_enc_rowC(KArgs a) {
         uint64_t wd[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) wd[i] = 0;
-        float dot = quant_pack64(v, ysc, zm64, qt, wd);
+        float dot = 1.0f;
+        if constexpr (kLadFull) {
+            dot = quant_pack64(v, ysc, zm64, qt, wd);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                wd[i] = (uint64_t)lad_word(v[8 * i], v[8 * i + 1], v[8 * i + 2], v[8 * i + 3]) |
+                        ((uint64_t)lad_word(v[8 * i + 4], v[8 * i + 5], v[8 * i + 6], v[8 * i + 7]) << 32);
+        }
         if (!(nu > 0.0f)) {
             dot = 0.f;
 #pragma unroll
             for (int i = 0; i < 8; ++i) wd[i] = 0;
         }
         store_planes64(a.pout + D.pl_off, (tile << kRowLog) + base5, D.pl_stride, a.nbits, wd);
-        dot = block_sum<kRowNT>(dot, red);
+        if constexpr (kLadFull) dot = block_sum<kRowNT>(dot, red);
         if (tid == 0) a.part[D.part_off + tile] = dot;
         if (!more) break;
         t = tn; si = sn; tile = tln;
@@ -1449,18 +1490,21 @@ __global__ __launch_bounds__(kRowNT) void k_dec_rowA(KArgs a) {
     fetch_planes<A8>(a, udesc(a.d, si), tile, true, base5, nw);
     for (;;) {
         float v[64];
-        unpack_centroids64(nw, cen, v);
+        if constexpr (kLadFull) unpack_centroids64(nw, cen, v);
+        else lad_unpack64(nw, v);
         const SliceDesc D = udesc(a.d, si);
         const int tn = t + (int)gridDim.x;
         const bool more = tn < tw.total;
         int sn; uint32_t tln;
         tw.at(more ? tn : t, sn, tln);
         fetch_planes<A8>(a, udesc(a.d, sn), tln, more, base5, nw);
-        stages<RS::L5, RS::F2e>(v);
-        exchange<RS::L5, RS::L4>(v, s, tid);
-        stages<RS::L4, RS::F2d>(v);
-        exchange<RS::L4, RS::L3>(v, s, tid);
-        stages<RS::L3, RS::F2c>(v);
+        if constexpr (kLadFly) {
+            stages<RS::L5, RS::F2e>(v);
+            exchange<RS::L5, RS::L4>(v, s, tid);
+            stages<RS::L4, RS::F2d>(v);
+            exchange<RS::L4, RS::L3>(v, s, tid);
+            stages<RS::L3, RS::F2c>(v);
+        }
         // (one more exchange to L3F for float4 stores: 494 -> 533 us per wave,
         // profiles/r03_deca_ws4_ab.txt)
         store_ws(a, D, tile, base3, v);
@@ -1495,20 +1539,23 @@ __global__ __launch_bounds__(kRowNT) void k_dec_rowC(KArgs a) {
         if constexpr (kRowWs4) fetch_ws4<RS::L3F>(a, udesc(a.d, sn), tln, more, base3, nx);
         else fetch_ws(a, udesc(a.d, sn), tln, more, base3, nx);
         const uint32_t b1 = seed_b(sld(a.seeds, D.tensor));
-        if constexpr (kRowWs4) {
-            stages<RS::L3F, RS::F1c>(v);
-            exchange<RS::L3F, RS::L2>(v, s, tid);
-        } else {
-            stages<RS::L3, RS::F1c>(v);
-            exchange<RS::L3, RS::L2>(v, s, tid);
+        if constexpr (kLadFly) {
+            if constexpr (kRowWs4) {
+                stages<RS::L3F, RS::F1c>(v);
+                exchange<RS::L3F, RS::L2>(v, s, tid);
+            } else {
+                stages<RS::L3, RS::F1c>(v);
+                exchange<RS::L3, RS::L2>(v, s, tid);
+            }
+            stages<RS::L2, RS::F1b>(v);
+            exchange<RS::L2, RS::L1>(v, s, tid);
+            stages<RS::L1, RS::F1a>(v);
         }
-        stages<RS::L2, RS::F1b>(v);
-        exchange<RS::L2, RS::L1>(v, s, tid);
-        stages<RS::L1, RS::F1a>(v);
         // scale folded into the 2^-k normalisation: 2^-k is exact, so
         // v * (sc * 2^-k) rounds like (v * 2^-k) * sc (normal range)
         const float sc = sldf(a.scales_in, D.scale_idx);
-        apply_signs_direct<RS::L1>(v, tile << kRowLog, base1, D.logp, b1, sc * pow2i(-((D.logp + 1) / 2)));
+        if constexpr (kLadSign)
+            apply_signs_direct<RS::L1>(v, tile << kRowLog, base1, D.logp, b1, sc * pow2i(-((D.logp + 1) / 2)));
         store_y(a, D, tile, base1, v);
         if (!more) break;
         t = tn; si = sn; tile = tln;
@@ -1767,7 +1814,7 @@ __global__ __launch_bounds__(col6_nt<TL>(), 4) void k_col6(KArgs a) {
     auto map = [&](uint32_t t) -> uint32_t { return tb | (t & ((1u << K) - 1u)) | ((t >> K) << lo); };
     const rsrc_t rw = mk_rsrc(a.ws + D.ws_off, (uint32_t)(4ull << D.logp));
     constexpr uint32_t kTabMask = (1u << (TL - 3)) - 1u;
-    if constexpr (MID) {  // D2 sign bytes of the tile's 2^12 rand_diag words (see k_col)
+    if constexpr (MID && kLadSign) {  // D2 sign bytes of the tile's 2^12 rand_diag words (see k_col)
         const uint32_t b2 = seed_b(sld(a.seeds, D.tensor) + 1u);
         for (uint32_t q = tid; q < (1u << (TL - 3)); q += NT)
             tab[q] = (uint8_t)rd_byte(map(q) & ((1u << (D.logp - 3)) - 1u), b2);
@@ -1792,8 +1839,8 @@ __global__ __launch_bounds__(col6_nt<TL>(), 4) void k_col6(KArgs a) {
         for (int r = 0; r < 64; ++r)
             v[r] = raw_load_f32(rw, (int)vo, (int)uu((LT<CS::L1>::off(r) >> K) << lo) * 4, kLdAux);
     }
-    stages<CS::L1, CS::A1>(v);
-    if constexpr (EXCH) {
+    if constexpr (kLadFly) stages<CS::L1, CS::A1>(v);
+    if constexpr (EXCH && kLadFly) {
         exchange_half<CS::L1, CS::L2, CS::HB>(v, s, tid);  // its barriers also publish tab
         stages<CS::L2, CS::A2>(v);
     } else if constexpr (MID) {
@@ -1806,16 +1853,18 @@ __global__ __launch_bounds__(col6_nt<TL>(), 4) void k_col6(KArgs a) {
         // immediate
         static_assert((LT<LC>::rmask() >> (TL - 3)) == 7u, "top 3 tile bits must be register bits");
         const uint32_t bt = opaque(LT<LC>::base(tid) & kTabMask);
+        if constexpr (kLadSign) {
 #pragma unroll
-        for (int r = 0; r < 64; ++r) {
-            const uint32_t o = LT<LC>::off(r);
-            v[r] = flip_unless(v[r] * m2, ((uint32_t)tab[bt + (o & kTabMask)] >> (o >> (TL - 3))) & 1u);
+            for (int r = 0; r < 64; ++r) {
+                const uint32_t o = LT<LC>::off(r);
+                v[r] = flip_unless(v[r] * m2, ((uint32_t)tab[bt + (o & kTabMask)] >> (o >> (TL - 3))) & 1u);
+            }
         }
-        if constexpr (EXCH) {
+        if constexpr (EXCH && kLadFly) {
             stages<CS::L2, CS::A2>(v);
             exchange_half<CS::L2, CS::L1, CS::HB>(v, s, tid);
         }
-        stages<CS::L1, CS::A1>(v);
+        if constexpr (kLadFly) stages<CS::L1, CS::A1>(v);
         if (perm) {
             const uint32_t vo = opaque(ws_pos(map(base1)) * 4u);
 #pragma unroll
@@ -1954,11 +2003,13 @@ __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowC2(KArgs a) {
         int sn; uint32_t tln;
         locate(more ? tn : t, sn, tln);
         if (!ROLL) fetch_ws<kRowC2LdAux>(a, D, tile, true, base3, v);
-        stages<R::L3, R::F2c>(v);
-        if (!(kDiagRowC2 & 1)) exchange_half_pad<R::L3, R::L4, R::HB>(v, s, tid);
-        stages<R::L4, R::F2d>(v);
-        if (!(kDiagRowC2 & 1)) exchange_half_pad<R::L4, R::L5, R::HB>(v, s, tid);
-        stages<R::L5, R::F2e>(v);
+        if constexpr (kLadFly) {
+            stages<R::L3, R::F2c>(v);
+            if (!(kDiagRowC2 & 1)) exchange_half_pad<R::L3, R::L4, R::HB>(v, s, tid);
+            stages<R::L4, R::F2d>(v);
+            if (!(kDiagRowC2 & 1)) exchange_half_pad<R::L4, R::L5, R::HB>(v, s, tid);
+            stages<R::L5, R::F2e>(v);
+        }
         __builtin_amdgcn_sched_barrier(0);
         const float nu = sldf(a.nu, si);
         const float ysc = pow2i(-((D.logp + 1) / 2));
@@ -1968,7 +2019,12 @@ __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowC2(KArgs a) {
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
             uint32_t w[8];
-            if (kDiagRowC2 & 2) {  // diagnostic: no quantiser (wrong output)
+            if (!kLadFull) {  // ladder rungs: a plane word from 4 values, no quantiser
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    w[i] = lad_word(v[32 * g + 4 * i], v[32 * g + 4 * i + 1], v[32 * g + 4 * i + 2], v[32 * g + 4 * i + 3]);
+                dot = 1.0f;
+            } else if (kDiagRowC2 & 2) {  // diagnostic: no quantiser (wrong output)
 #pragma unroll
                 for (int i = 0; i < 8; ++i) w[i] = __float_as_uint(v[32 * g + 4 * i]) ^ __float_as_uint(v[32 * g + 4 * i + 1]);
                 dot += v[32 * g];
@@ -1987,7 +2043,7 @@ __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowC2(KArgs a) {
                          a.nbits, w);
         }
         if (!pos) dot = 0.f;
-        if (!(kDiagRowC2 & 4)) dot = block_sum<kRowNT>(dot, red);
+        if (!(kDiagRowC2 & 4) && kLadFull) dot = block_sum<kRowNT>(dot, red);
         if (tid == 0) a.part[D.part_off + tile] = dot;
         if (!more) break;
         t = tn; si = sn; tile = tln;
@@ -2201,18 +2257,20 @@ __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowA2(KArgs a) {
                              "+v"(v[r + 5]), "+v"(v[r + 6]), "+v"(v[r + 7]));
         }
         const uint32_t b1 = seed_b(sld(a.seeds, D.tensor));
-        float ss = sum_sq(v);
+        float ss = kLadFull ? sum_sq(v) : 1.0f;
         // the sum is taken here, not sunk past the sign flips (which would keep
         // the 64 unflipped values live through the butterflies and spill them)
         asm volatile("" : "+v"(ss));
-        apply_signs_grouped<R::A1>(v, tile << kRowLog, base1, D.logp, b1, 1.0f);
-        stages<R::A1, R::F1a>(v);
-        exchange_half_pad<R::A1, R::A2, 14>(v, s, tid);
-        stages<R::A2, R::F1b>(v);
-        exchange_half_pad<R::A2, R::A3, 14>(v, s, tid);
-        stages<R::A3, R::F1c>(v);
+        if constexpr (kLadSign) apply_signs_grouped<R::A1>(v, tile << kRowLog, base1, D.logp, b1, 1.0f);
+        if constexpr (kLadFly) {
+            stages<R::A1, R::F1a>(v);
+            exchange_half_pad<R::A1, R::A2, 14>(v, s, tid);
+            stages<R::A2, R::F1b>(v);
+            exchange_half_pad<R::A2, R::A3, 14>(v, s, tid);
+            stages<R::A3, R::F1c>(v);
+        }
         store_ws_l<R::A3>(a, D, tile, base3, v);
-        ss = block_sum<kRowNT>(ss, red);
+        if constexpr (kLadFull) ss = block_sum<kRowNT>(ss, red);
         if (tid == 0) a.part[D.part_off + tile] = ss;
     }
 }
@@ -2236,12 +2294,15 @@ __global__ __launch_bounds__(kRowNT, 4) void k_dec_rowA2(KArgs a) {
         uint64_t w[8];
         fetch_planes<A8>(a, D, tile, true, base1, w);
         float v[64];
-        unpack_centroids64(w, cen, v);
-        stages<R::C1, R::G1>(v);
-        exchange_half_pad<R::C1, R::C2, 5>(v, s, tid);
-        stages<R::C2, R::G2>(v);
-        exchange_half_pad<R::C2, R::C3, 5>(v, s, tid);
-        stages<R::C3, R::G3>(v);
+        if constexpr (kLadFull) unpack_centroids64(w, cen, v);
+        else lad_unpack64(w, v);
+        if constexpr (kLadFly) {
+            stages<R::C1, R::G1>(v);
+            exchange_half_pad<R::C1, R::C2, 5>(v, s, tid);
+            stages<R::C2, R::G2>(v);
+            exchange_half_pad<R::C2, R::C3, 5>(v, s, tid);
+            stages<R::C3, R::G3>(v);
+        }
         store_ws_l<R::C3>(a, D, tile, base3, v);
     }
 }
@@ -2262,15 +2323,18 @@ __global__ __launch_bounds__(kRowNT, 4) void k_dec_rowC2(KArgs a) {
         if constexpr (kRowWs4) fetch_ws4<R::B1>(a, D, tile, true, base1, v);
         else fetch_ws(a, D, tile, true, base1, v);
         const uint32_t b1 = seed_b(sld(a.seeds, D.tensor));
-        stages<R::B1, R::H1>(v);
-        exchange_half_pad<R::B1, R::B2, 10>(v, s, tid);
-        stages<R::B2, R::H2>(v);
-        exchange_half_pad<R::B2, R::B3, 10>(v, s, tid);
-        stages<R::B3, R::H3>(v);
-        exchange_half_pad<R::B3, R::B4, 10>(v, s, tid);
-        stages<R::B4, R::H4>(v);
+        if constexpr (kLadFly) {
+            stages<R::B1, R::H1>(v);
+            exchange_half_pad<R::B1, R::B2, 10>(v, s, tid);
+            stages<R::B2, R::H2>(v);
+            exchange_half_pad<R::B2, R::B3, 10>(v, s, tid);
+            stages<R::B3, R::H3>(v);
+            exchange_half_pad<R::B3, R::B4, 10>(v, s, tid);
+            stages<R::B4, R::H4>(v);
+        }
         const float sc = sldf(a.scales_in, D.scale_idx);
-        apply_signs_grouped<R::B4>(v, tile << kRowLog, base4, D.logp, b1, sc * pow2i(-((D.logp + 1) / 2)));
+        if constexpr (kLadSign)
+            apply_signs_grouped<R::B4>(v, tile << kRowLog, base4, D.logp, b1, sc * pow2i(-((D.logp + 1) / 2)));
         store_y_l<R::B4>(a, D, tile, base4, v);
     }
 }

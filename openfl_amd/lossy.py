@@ -421,7 +421,7 @@ def lut_tables(offsets, numels, maps, device):
 
 
 @_on_device
-def gunzip_device(data, out, lut=None):
+def gunzip_device(data, out, lut=None, expect_bytes=None):
     """gzip.decompress (kc_pipeline.py:152-156) of `data` into `out`, a uint8
     DEVICE tensor (returns the view of the decompressed bytes).  Member-indexed
     streams inflate on the GPU from the compressed bytes (the index is built
@@ -433,7 +433,10 @@ def gunzip_device(data, out, lut=None):
     different format: gzip.decompress on the host, then one H2D.
     lut (lut_tables(...)): the decoded ranks go through the tensors' LUTs
     (the lossy pipelines' backward, kc_pipeline.py:79-83) -- fused into the
-    TLZ decoder's stores, or one lut_decode_batch after any other inflate."""
+    TLZ decoder's stores, or one lut_decode_batch after any other inflate.
+    expect_bytes: the decoded length the caller requires; a stream of any
+    other length raises CodecError before anything is inflated or looked up
+    (with lut, the decoded length must also be whole float32s)."""
     if not (out.is_cuda and out.dtype == torch.uint8 and out.is_contiguous()):
         raise _lib.CodecError("gunzip_device: out must be a contiguous uint8 device tensor")
     tr = _gunzip_trace("start")
@@ -496,6 +499,7 @@ def gunzip_device(data, out, lut=None):
         raise
     if rc == _lib.OFL_EFORMAT:
         raw = np.frombuffer(gzip.decompress(bytes(data)), np.uint8)
+        _check_len(raw.size, expect_bytes, lut)
         if raw.size > out.numel():
             raise _lib.CodecError("gunzip_device: output buffer too small")
         if raw.size:
@@ -505,6 +509,11 @@ def gunzip_device(data, out, lut=None):
     if rc != _lib.OFL_OK:
         copy.result()
     _lib.check_gzip(rc)
+    try:
+        _check_len(tot.value, expect_bytes, lut)   # the members' ISIZE sum, before any launch
+    except _lib.CodecError:
+        copy.result()
+        raise
     if tot.value > out.numel():
         copy.result()
         raise _lib.CodecError("gunzip_device: output buffer too small")
@@ -535,7 +544,11 @@ def gunzip_device(data, out, lut=None):
             _lib.check_gzip(L.ofl_inflate_tlz_async(*args, 0, 0, *tail, caller_stream.cuda_stream))
             ready = torch.cuda.Event()
             ready.record(caller_stream)
-            ends = idx[:, 0] + (idx[:, 1] & ((1 << 62) - 1)) + 8   # member end (trailer included)
+            # a member is launched with the piece in which its end lands PLUS
+            # the decoder's look-ahead (_INFLATE_LOOKAHEAD bytes past the
+            # trailer), so every byte a lane may read -- of a valid or a
+            # corrupt member -- has landed before the launch
+            ends = idx[:, 0] + (idx[:, 1] & ((1 << 62) - 1)) + 8 + _INFLATE_LOOKAHEAD
             sides = _side_streams(dev)
             first = 0
             try:
@@ -587,13 +600,24 @@ def _gunzip_trace(first):
 gunzip_trace_log = []
 _INFLATE_PIECES = int(os.environ.get("OFL_INFLATE_PIECES", "4"))  # H2D pieces of a large TLZ payload, each inflated as it lands
 _INFLATE_PIECE_MIN = 32  # MiB: smaller payloads cross in one piece
+_INFLATE_LOOKAHEAD = 64  # bytes the inflate kernels may read past a member's trailer (d_in keeps 128 of padding)
 _H2D_THREADS = int(os.environ.get("OFL_H2D_THREADS", "2"))  # host threads staging a large pageable payload (0: one plain hipMemcpyAsync)
+
+
+def _check_len(nbytes, expect, lut):
+    """gunzip_device's length checks: the caller's expected decoded length,
+    and whole float32s wherever a LUT will read the bytes as values."""
+    if expect is not None and nbytes != expect:
+        raise _lib.CodecError(f"payload decodes to {nbytes} bytes, expected {expect}")
+    if lut is not None and nbytes % 4:
+        raise _lib.CodecError(f"payload decodes to {nbytes} bytes, not whole float32 values")
 
 
 def _apply_lut(out, nbytes, lut):
     """The LUT after an inflate that did not fuse it (lut_decode_batch in place)."""
     if lut is None or nbytes == 0:
         return
+    _check_len(nbytes, None, lut)
     y = out[:nbytes].view(torch.float32)
     lut_decode_batch(y, lut["offsets"], lut["numels"], lut["maps"], y)
 

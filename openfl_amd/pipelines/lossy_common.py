@@ -67,9 +67,9 @@ def gzip_lut_backward_device(data, int2float_map, n, device):
     -> float32 device tensor of n elements."""
     buf = torch.empty(4 * max(n, 1), dtype=torch.uint8, device=device)
     # the LUT fused into the inflate's stores (one tensor: elements [0, n))
-    raw = lossy.gunzip_device(data, buf, lut=lossy.lut_tables([0], [n], [int2float_map], buf.device) if n else None)
-    if raw.numel() != 4 * n:
-        raise lossy._lib.CodecError(f"payload decodes to {raw.numel()} bytes, expected {4 * n}")
+    # (the length is checked against 4n before anything is inflated or looked up)
+    raw = lossy.gunzip_device(data, buf, lut=lossy.lut_tables([0], [n], [int2float_map], buf.device) if n else None,
+                              expect_bytes=4 * n)
     if n == 0:
         return torch.empty(0, dtype=torch.float32, device=device)
     return raw.view(torch.float32)

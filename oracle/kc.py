@@ -46,11 +46,19 @@ def kc_forward(x, n_cluster=6):
     return gzip.compress(ranks.reshape(quant.shape).astype(np.float32).tobytes()), metadata
 
 
+def lut_sequential(data, int_to_float):
+    """KmeansTransformer.backward's replacement (kc_pipeline.py:79-83), in
+    place on a float32 array: `data[data == key] = value` for every key in
+    map order, so a value equal to a later key is replaced again."""
+    for key in int_to_float:
+        data[data == key] = int_to_float[key]
+    return data
+
+
 def kc_backward(payload, metadata):
     """The tensor back: kc_pipeline.py:152-156, then :65-86."""
     data = np.frombuffer(gzip.decompress(payload), dtype=np.float32).copy()
-    for key in metadata["int_to_float"]:
-        data[data == key] = metadata["int_to_float"][key]
+    lut_sequential(data, metadata["int_to_float"])
     return data.reshape(list(metadata["int_list"]))
 
 

@@ -912,3 +912,99 @@ def test_side_streams_shared_per_device():
     assert L.ofl_side_stream(3, ctypes.byref(p)) == _lib.OFL_EINVAL
     sides = lossy._side_streams(torch.device(DEV))
     assert [s.cuda_stream for s in sides] == got[0][1:]
+
+
+def test_gunzip_wrong_length_payloads():
+    """A payload that does not decode to the caller's 4n bytes raises the
+    pipelines' CodecError before any LUT runs, on every inflate path: a
+    foreign gzip stream (host gzip.decompress) whose length is not whole
+    float32s or is short, and a device-gzip TLZ stream one value short or
+    long; gunzip_device(lut=...) without an expected length still refuses a
+    length that is not whole float32s."""
+    from openfl_amd import _lib, lossy
+    from openfl_amd.pipelines.lossy_common import gzip_lut_backward_device
+    m = {0: 0.5, 1: -0.25, 2: 1.0}
+    for payload, n in ((gzip.compress(bytes(10)), 3), (gzip.compress(bytes(8)), 3), (gzip.compress(bytes(16)), 3)):
+        with pytest.raises(_lib.CodecError, match="payload decodes to"):
+            gzip_lut_backward_device(payload, m, n, torch.device(DEV))
+    x = torch.from_numpy(np.random.default_rng(8).integers(0, 3, 100_001).astype(np.float32)).to(DEV)
+    z = lossy.gzip_ranks(x)
+    for n in (100_000, 100_002):
+        with pytest.raises(_lib.CodecError, match="payload decodes to"):
+            gzip_lut_backward_device(z, m, n, torch.device(DEV))
+    y = gzip_lut_backward_device(z, m, 100_001, torch.device(DEV)).cpu().numpy()
+    want = x.cpu().numpy().copy()
+    for k, v in m.items():
+        want[want == k] = v
+    np.testing.assert_array_equal(y, want)
+    out = torch.empty(64, dtype=torch.uint8, device=DEV)
+    with pytest.raises(_lib.CodecError, match="whole float32"):
+        lossy.gunzip_device(gzip.compress(bytes(10)), out, lut=lossy.lut_tables([0], [3], [m], DEV))
+
+
+def test_kc_bench_composition_full_size():
+    """bench.py's KC line, exactly as it times it, on its own 64 x 2^22 set
+    (BASELINE config 3): kmeans_batch(label_out=...) -> gzip_ranks(x,
+    label=...) (the label-fused encoder, several encode batches) ->
+    gunzip_device(lut=lut_tables(...)) (the pipelined inflate: 4 H2D pieces,
+    each inflated as it lands, LUT fused into the stores).  gzip.decompress of
+    the stream (the reference's GZIPTransformer.backward) equals the device
+    k-means ranks (the same seed through ranks_out), and y equals the
+    reference's sequential replacement (oracle/kc.py:lut_sequential,
+    kc_pipeline.py:79-83) of those ranks, element for element."""
+    from oracle import kc as K
+    from openfl_amd import lossy
+    from openfl_amd.workloads import WORKLOADS, numel
+    numels = [numel(s) for _, s in WORKLOADS["uniform_1gib"]()]
+    offs = list(np.cumsum([0] + [(n + 63) // 64 * 64 for n in numels[:-1]]))
+    tot = int(offs[-1] + numels[-1])
+    x = torch.empty(tot, dtype=torch.float32, device=DEV)
+    g = torch.Generator(device=DEV)
+    for j, (o, n) in enumerate(zip(offs, numels)):
+        g.manual_seed(j)
+        x[o:o + n].normal_(0.0, 0.01, generator=g)
+    tab = lossy.LabelTable(len(numels), DEV)
+    _, _, _, uniq = lossy.kmeans_batch(x, offs, numels, 6, n_init=6, seed=1234, label_out=tab)
+    z = lossy.gzip_ranks(x, label=tab)
+    assert len(z) >= lossy._INFLATE_PIECE_MIN << 20          # the pipelined (4-piece) inflate
+    maps = [{i: u for i, u in enumerate(uq)} for uq in uniq]
+    y = torch.full((tot,), -7.0, dtype=torch.float32, device=DEV)
+    lossy.gunzip_device(z, y.view(torch.uint8), lut=lossy.lut_tables(offs, numels, maps, DEV))
+    ranks = torch.zeros(tot, dtype=torch.float32, device=DEV)
+    _, _, _, uniq2 = lossy.kmeans_batch(x, offs, numels, 6, n_init=6, seed=1234, ranks_out=ranks)
+    assert all(np.array_equal(a, b) for a, b in zip(uniq, uniq2))
+    r = ranks.cpu().numpy()
+    assert np.frombuffer(gzip.decompress(z), np.float32).tobytes() == r.tobytes()
+    yh = y.cpu().numpy()
+    for o, n, m in zip(offs, numels, maps):
+        want = K.lut_sequential(r[o:o + n].copy(), m)
+        np.testing.assert_array_equal(yh[o:o + n], want)
+
+
+def test_gunzip_pipelined_rejects_corrupt_members(monkeypatch):
+    """The pipelined inflate (several H2D pieces, members launched as their
+    bytes land) refuses corrupt members next to every piece boundary as
+    gzip.decompress does, and decodes the intact stream: the members at a
+    boundary are launched only once the look-ahead bytes past their trailer
+    have landed too."""
+    from openfl_amd import _lib, lossy
+    monkeypatch.setattr(lossy, "_INFLATE_PIECE_MIN", 1)
+    x, offs, nums, maps = _lut_case(21, [1 << 22] * 5)
+    z = lossy.gzip_ranks(torch.from_numpy(x).to(DEV))
+    assert len(z) >= 4 << 20
+    out = torch.empty(x.nbytes + 64, dtype=torch.uint8, device=DEV)
+    assert lossy.gunzip_device(z, out).cpu().numpy().tobytes() == x.tobytes()
+    starts = [0]
+    while starts[-1] < len(z):
+        starts.append(starts[-1] + int.from_bytes(z[starts[-1] + 20:starts[-1] + 24], "little"))
+    n = lossy._INFLATE_PIECES
+    bounds = [min(len(z), (len(z) * k // n + (4 << 20) - 1) // (4 << 20) * (4 << 20)) for k in range(1, n)]
+    for b in bounds:
+        j = int(np.searchsorted(starts, b, "right")) - 1       # the member holding the boundary
+        for m in (j - 1, j):
+            bad = bytearray(z)
+            bad[starts[m + 1] - 12] ^= 0xFF                       # last data bytes before the trailer
+            with pytest.raises((_lib.CodecError, EOFError, OSError, zlib.error)):
+                gzip.decompress(bytes(bad))
+            with pytest.raises(_lib.CodecError):
+                lossy.gunzip_device(bytes(bad), out, lut=lossy.lut_tables(offs, nums, maps, DEV))

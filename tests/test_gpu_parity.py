@@ -510,6 +510,51 @@ def test_step_graph_replay_bit_identical():
     assert torch.equal(p0, p1) and torch.equal(s0, s1) and torch.equal(y0, y1)
 
 
+def test_step_graphs_built_concurrently():
+    """Two threads building EdenStepGraphs on one device at once (the graphs
+    share the device's capture stream; construction is serialised by its
+    lock): both captures succeed and replay the eager bytes."""
+    import threading
+    from openfl_amd.codec import EdenPlan, EdenStepGraph
+    numels = [50_000, 1 << 20, 3000]
+    plan = EdenPlan(numels, 8, wave_mib=8, streams=2)
+    g = torch.Generator(device=DEV).manual_seed(4)
+    x = torch.empty(plan.arena_numel, device=DEV).normal_(0, 0.01, generator=g)
+    seeds = torch.tensor([5, 6, 7], dtype=torch.int32, device=DEV)
+    ref = (torch.zeros(plan.planes_bytes, dtype=torch.uint8, device=DEV), torch.zeros_like(x))
+    ws0 = torch.empty(max(plan.ws_bytes, 256), dtype=torch.uint8, device=DEV)
+    s0 = torch.zeros(plan.n_slices, dtype=torch.float32, device=DEV)
+    plan.encode(x, seeds, ref[0], s0, ws0)
+    plan.decode(ref[0], seeds, s0, ref[1], ws0)
+    torch.cuda.synchronize()
+    outs, errs = [], []
+
+    def build():
+        try:
+            torch.cuda.set_device(DEV)
+            p = torch.zeros_like(ref[0])
+            y = torch.zeros_like(x)
+            s = torch.zeros_like(s0)
+            ws = torch.empty_like(ws0)
+            gr = EdenStepGraph(plan, x, seeds, p, s, y, ws)
+            p.zero_()
+            y.zero_()
+            gr.replay()
+            torch.cuda.current_stream().synchronize()
+            outs.append((p, y, gr))
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errs.append(e)
+    ts = [threading.Thread(target=build) for _ in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs
+    torch.cuda.synchronize()
+    for p, y, _ in outs:
+        assert torch.equal(p, ref[0]) and torch.equal(y, ref[1])
+
+
 @pytest.mark.parametrize("setting", ["cuda:all", "two_slots_one_gpu"])
 def test_pipeline_multi_device_threads(setting):
     """device naming several GPUs: each calling thread is bound to one of them

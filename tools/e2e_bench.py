@@ -3,7 +3,9 @@
 ResNet-50-shaped fp32 update; per tensor: host ndarray -> Eden encode ->
 NamedTensor protobuf bytes -> parse -> Eden decode -> host ndarray.
 
-Modes (wall-clock, both collaborators, second of two rounds):
+Modes (wall-clock, both collaborators; every mode runs --rounds rounds and
+reports the median of the rounds after the first, with every round's time in
+round_s):
   plugin   openfl_amd.pipelines.EdenPipeline per tensor (what TensorCodec calls):
            H2D + encode + D2H per tensor, then H2D + decode + D2H per tensor
   plugin_concurrent  the same per-tensor calls with every collaborator on its
@@ -128,6 +130,7 @@ def main():
     ap.add_argument("--collaborators", type=int, default=2)
     ap.add_argument("--modes", default="plugin,batched,cpu")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--rounds", type=int, default=7, help="rounds per mode (the first is a warm-up)")
     ap.add_argument("--numa-bind", action="store_true",
                     help="bind the process to the GPU's NUMA node first (openfl_amd.numa, as bench.py does)")
     ap.add_argument("--heap-policy", action="store_true",
@@ -156,15 +159,22 @@ def main():
         den = sum(float(np.sum(a.astype(np.float64) ** 2)) for _, a in sd)
         return (num / den) ** 0.5
 
+    def rounds_of(fn, n=args.rounds):
+        """fn() per round -> (median seconds of the rounds after the first,
+        every round's seconds, the last round's result)."""
+        times, out = [], None
+        for _ in range(max(n, 2)):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = fn()
+            times.append(round(time.perf_counter() - t0, 4))
+        return float(np.median(times[1:])), times, out
+
     modes = args.modes.split(",")
     if "plugin" in modes:
         pipe = EdenPipeline(n_bits=8, dim_threshold=100, device="cuda:0")
-        for r in range(2):
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            outs = [run_plugin(sd, pipe, P) for sd in sds]
-            dt = time.perf_counter() - t0
-        res["plugin"] = {"s": round(dt, 4), "GiB_s": round(in_bytes / dt / 2 ** 30, 3),
+        dt, rounds, outs = rounds_of(lambda: [run_plugin(sd, pipe, P) for sd in sds])
+        res["plugin"] = {"s": round(dt, 4), "GiB_s": round(in_bytes / dt / 2 ** 30, 3), "round_s": rounds,
                          "wire_bytes": sum(o[1] for o in outs), "rel_err": round(rel_err(sds[0], outs[0][0]), 6)}
         # where a round's time goes (a third, instrumented round)
         ph = {}
@@ -181,31 +191,31 @@ def main():
         # thread (aggregator_server.py:305), per-tensor calls, concurrently
         from concurrent.futures import ThreadPoolExecutor
         pipe = EdenPipeline(n_bits=8, dim_threshold=100, device="cuda:0")
-        rounds = []
+        # (single rounds vary by up to 2x with the host's scheduling of the
+        # two caller threads: the median of the rounds after the first)
         with ThreadPoolExecutor(max_workers=len(sds)) as ex:
-            for r in range(int(os.environ.get("E2E_ROUNDS", "5"))):
-                torch.cuda.synchronize()
-                t0 = time.perf_counter()
-                outs = list(ex.map(lambda sd: run_plugin(sd, pipe, P), sds))
-                rounds.append(round(time.perf_counter() - t0, 4))
-        # the median of the rounds after the first (single rounds vary by
-        # up to 2x with the host's scheduling of the two caller threads)
-        dt = float(np.median(rounds[1:])) if len(rounds) > 1 else rounds[0]
+            dt, rounds, outs = rounds_of(lambda: list(ex.map(lambda sd: run_plugin(sd, pipe, P), sds)))
         res["plugin_concurrent"] = {"s": round(dt, 4), "GiB_s": round(in_bytes / dt / 2 ** 30, 3), "threads": len(sds),
                                     "wire_bytes": sum(o[1] for o in outs),
                                     "rel_err": round(rel_err(sds[0], outs[0][0]), 6), "round_s": rounds}
     if "batched" in modes:
         for mode in ("reference", "fast"):
             pipe = EdenPipeline(n_bits=8, dim_threshold=100, device="cuda:0", seed_mode=mode)
-            for r in range(3):
-                torch.cuda.synchronize()
-                t0 = time.perf_counter()
-                outs = [run_batched(sd, pipe, P) for sd in sds]
-                dt = time.perf_counter() - t0
+            phs = []
+
+            def one():
+                o = []
+                for sd in sds:
+                    o.append(run_batched(sd, pipe, P))
+                    phs.append(dict(run_batched.phases))
+                return o
+            dt, rounds, outs = rounds_of(one)
             key = "batched" if mode == "reference" else "batched_fast_seed"
-            res[key] = {"s": round(dt, 4), "GiB_s": round(in_bytes / dt / 2 ** 30, 3),
+            phs = phs[len(sds):]   # the rounds after the first
+            res[key] = {"s": round(dt, 4), "GiB_s": round(in_bytes / dt / 2 ** 30, 3), "round_s": rounds,
                         "wire_bytes": sum(o[1] for o in outs), "rel_err": round(rel_err(sds[-1], outs[-1][0]), 6),
-                        "last_collaborator_phases": dict(run_batched.phases)}
+                        "phases_ms_median_per_collaborator": {k: round(float(np.median([p[k] for p in phs])), 2)
+                                                              for k in phs[0]}}
     if "cpu" in modes:
         from oracle import eden as O
         cores = O.host_cores()

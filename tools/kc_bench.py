@@ -28,7 +28,10 @@ def main():
                     help="diagnostics: create and use this many torch streams first (HW queue sharing)")
     ap.add_argument("--ballast-gib", type=float, default=0.0,
                     help="diagnostics: hold this much device memory (written once) during the run")
+    ap.add_argument("--hw-queues", type=int, default=0, help="GPU_MAX_HW_QUEUES to set (0: leave HIP's default)")
     args = ap.parse_args()
+    if args.hw_queues > 0:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     import torch
     import bench
     if args.hostmem:
@@ -55,6 +58,7 @@ def main():
     out["hostmem_policy"] = bool(args.hostmem)
     out["ballast_gib"] = args.ballast_gib
     out["numa_cpus"] = f"{cpus[0]}-{cpus[-1]} ({len(cpus)})" if cpus else None
+    out["GPU_MAX_HW_QUEUES"] = os.environ.get("GPU_MAX_HW_QUEUES")
     del ballast
     print(json.dumps(out), flush=True)
 
