@@ -52,8 +52,11 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-budget-s", type=float, default=15.0,
                     help="CPU baseline: oracle time budget on the main workload's tensors")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-numa-bind", action="store_true",
-                    help="leave the process on every allowed CPU (default: the GPU's NUMA node, openfl_amd.numa)")
+    ap.add_argument("--numa-bind", action="store_true",
+                    help="bind the process to the GPU's NUMA node (openfl_amd.numa); default: the OS placement")
+    ap.add_argument("--no-numa-bind", action="store_true", help=argparse.SUPPRESS)  # the default (older scripts)
+    ap.add_argument("--no-kc-numa-variant", action="store_true",
+                    help="skip the KC line's NUMA-bound variant (tools/kc_bench.py in a child process)")
     ap.add_argument("--hw-queues", type=int, default=0,
                     help="set GPU_MAX_HW_QUEUES before the HIP runtime starts (0 = leave the environment's / "
                          "HIP's default of 4); recorded in the line's host_env")
@@ -449,6 +452,22 @@ def kc_pipeline(steps, warmup, dev, extras=True):
                      "stream for the arena; each tensor's payload is its run of members)"}
 
 
+def kc_numa_variant(steps=10, warmup=2):
+    """The KC pipeline steps (tools/kc_bench.py: the same composition as the
+    line) in a child process bound to the GPU's NUMA node, for the line's
+    numa_bound_variant; this process stays on the OS placement."""
+    env = dict(os.environ)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "kc_bench.py"), "--steps", str(steps),
+                        "--warmup", str(warmup)], env=env, capture_output=True, text=True, timeout=300)
+    try:
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return {"error": f"tools/kc_bench.py rc={r.returncode}: {r.stderr[-300:]}"}
+    return {"value": d["value"], "unit": "GiB/s", "ms_per_step": d["ms_per_step"], "phases_ms": d["phases_ms"],
+            "wire_ratio": d["wire_ratio"], "numa_cpus": d.get("numa_cpus"),
+            "scope": "the same KC steps in a child process bound to the GPU's NUMA node (tools/kc_bench.py)"}
+
+
 KC_CPU_SAMPLE = 1 << 18  # elements per sampled tensor (4 tensors: 4 MiB, ~10-20 s of CPU work)
 
 
@@ -525,8 +544,13 @@ def main(argv=None):
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # Host placement: the OS's by default.  Binding to the GPU's NUMA node
+    # (--numa-bind) speeds the host-heavy KC pipeline up (~52 vs ~48 GiB/s)
+    # but measured slower on the device-resident Eden step (422-425 vs 425-438
+    # GiB/s, profiles/r06_env_ab.txt), so the line runs unbound and the KC
+    # entry carries a bound variant measured in a child process.
     numa_cpus = None
-    if not args.no_numa_bind:  # host buffers and threads on the GPU's socket (openfl_amd.numa)
+    if args.numa_bind and not args.no_numa_bind:
         from openfl_amd import numa
         numa_cpus = numa.bind_to_device(local)
     # the process placement every number of this line was measured under
@@ -535,7 +559,8 @@ def main(argv=None):
                                              "environment" if "GPU_MAX_HW_QUEUES" in os.environ else
                                              "unset (HIP default, 4)"),
                 "numa_bind": (f"CPUs {numa_cpus[0]}-{numa_cpus[-1]} ({len(numa_cpus)}) of the GPU's node"
-                              if numa_cpus else "none" if args.no_numa_bind else "no node found (unbound)")}
+                              if numa_cpus else "none (OS placement)" if not args.numa_bind else
+                              "no node found (unbound)")}
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
@@ -695,6 +720,8 @@ def main(argv=None):
         for name in [a for a in args.also.split(",") if a]:
             if name == "kc_uniform_1gib":
                 also[name] = kc_pipeline(max(10, args.also_steps // 2), 4, dev)
+                if not args.no_kc_numa_variant and not numa_cpus:
+                    also[name]["numa_bound_variant"] = kc_numa_variant()
             else:
                 # a ResNet-50 step is ~0.35 ms: more steps for a stable rate
                 st = max(args.also_steps, 200) if name == "resnet50_fp32" else args.also_steps

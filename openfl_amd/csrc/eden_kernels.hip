@@ -1184,6 +1184,90 @@ DEVI rsrc_t mk_rsrc(const void* p, uint32_t bytes) {
     r.w = 0x00020000;
     return r;
 }
+
+// Storage format of the large-slice intermediates.  32 (the product): fp32.
+// A/B stubs of narrower intermediates (WRONG results,
+// memory pattern only, tools/r06_ws_ab.sh): 16 = the high 16 bits of each
+// fp32 (2 B per element), 24 = split planes, the high 16 bits at byte 2e of
+// the slice's ws and the next 8 bits at byte 2P + e (3 B per element).
+#ifndef OFL_WS_FMT
+#define OFL_WS_FMT 32
+#endif
+constexpr int kWsFmt = OFL_WS_FMT;
+static_assert(kWsFmt == 32 || kWsFmt == 24 || kWsFmt == 16, "OFL_WS_FMT: 32, 24 or 16");
+__device__ uint16_t raw_load_u16(rsrc_t r, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.i16");
+__device__ uint8_t raw_load_u8w(rsrc_t r, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.i8");
+__device__ int raw_load_i32w(rsrc_t r, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.i32");
+__device__ i32x2 raw_load_i32x2w(rsrc_t r, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.v2i32");
+__device__ void raw_store_u16(uint16_t v, rsrc_t r, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.store.i16");
+__device__ void raw_store_u8(uint8_t v, rsrc_t r, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.store.i8");
+__device__ void raw_store_i32(int v, rsrc_t r, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.store.i32");
+__device__ void raw_store_i32x2(i32x2 v, rsrc_t r, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.store.v2i32");
+// a view of the intermediate elements [i0, i0 + bytes / 4) of a slice whose
+// ws starts at sw (2^logp elements); offsets below are fp32 byte offsets
+struct WsR { rsrc_t h, l; };
+DEVI WsR ws_rsrc(const float* sw, int logp, size_t i0, uint32_t bytes) {
+    WsR w;
+    if constexpr (kWsFmt == 32) {
+        w.h = mk_rsrc(sw + i0, bytes);
+        w.l = w.h;
+    } else {
+        const uint8_t* b = reinterpret_cast<const uint8_t*>(sw);
+        w.h = mk_rsrc(b + 2 * i0, bytes / 2);
+        w.l = mk_rsrc(b + (2ull << logp) + i0, kWsFmt == 24 ? bytes / 4 : 0u);
+    }
+    return w;
+}
+DEVI float ws_ld1(const WsR& w, uint32_t vo, uint32_t so, int aux) {
+    if constexpr (kWsFmt == 32) return raw_load_f32(w.h, (int)vo, (int)so, aux);
+    uint32_t u = (uint32_t)raw_load_u16(w.h, (int)(vo >> 1), (int)(so >> 1), aux) << 16;
+    if constexpr (kWsFmt == 24) u |= (uint32_t)raw_load_u8w(w.l, (int)(vo >> 2), (int)(so >> 2), aux) << 8;
+    return __uint_as_float(u);
+}
+DEVI void ws_st1(const WsR& w, uint32_t vo, uint32_t so, float v, int aux) {
+    if constexpr (kWsFmt == 32) { raw_store_f32(v, w.h, (int)vo, (int)so, aux); return; }
+    const uint32_t u = __float_as_uint(v);
+    raw_store_u16((uint16_t)(u >> 16), w.h, (int)(vo >> 1), (int)(so >> 1), aux);
+    if constexpr (kWsFmt == 24) raw_store_u8((uint8_t)(u >> 8), w.l, (int)(vo >> 2), (int)(so >> 2), aux);
+}
+DEVI f32x4 ws_ld4(const WsR& w, uint32_t vo, uint32_t so, int aux) {
+    if constexpr (kWsFmt == 32) return raw_load_f32x4(w.h, (int)vo, (int)so, aux);
+    const i32x2 h = raw_load_i32x2w(w.h, (int)(vo >> 1), (int)(so >> 1), aux);
+    uint32_t l = 0;
+    if constexpr (kWsFmt == 24) l = (uint32_t)raw_load_i32w(w.l, (int)(vo >> 2), (int)(so >> 2), aux);
+    const uint32_t h0 = (uint32_t)h.x, h1 = (uint32_t)h.y;
+    f32x4 q;
+    q.x = __uint_as_float((h0 << 16) | ((l & 0xffu) << 8));
+    q.y = __uint_as_float((h0 & 0xffff0000u) | (((l >> 8) & 0xffu) << 8));
+    q.z = __uint_as_float((h1 << 16) | (((l >> 16) & 0xffu) << 8));
+    q.w = __uint_as_float((h1 & 0xffff0000u) | ((l >> 24) << 8));
+    return q;
+}
+DEVI void ws_st4(const WsR& w, uint32_t vo, uint32_t so, f32x4 q, int aux) {
+    if constexpr (kWsFmt == 32) { raw_store_f32x4(q, w.h, (int)vo, (int)so, aux); return; }
+    const uint32_t a0 = __float_as_uint(q.x), a1 = __float_as_uint(q.y), a2 = __float_as_uint(q.z),
+                   a3 = __float_as_uint(q.w);
+    const i32x2 h = {(int)((a0 >> 16) | (a1 & 0xffff0000u)), (int)((a2 >> 16) | (a3 & 0xffff0000u))};
+    raw_store_i32x2(h, w.h, (int)(vo >> 1), (int)(so >> 1), aux);
+    if constexpr (kWsFmt == 24)
+        raw_store_i32((int)(((a0 >> 8) & 0xffu) | (a1 & 0xff00u) | ((a2 & 0xff00u) << 8) | ((a3 & 0xff00u) << 16)),
+                      w.l, (int)(vo >> 2), (int)(so >> 2), aux);
+}
+// element i of a slice's intermediate through a plain pointer (k_col)
+DEVI float ws_pld(const float* sw, int logp, uint32_t i) {
+    if constexpr (kWsFmt == 32) return sw[i];
+    const uint8_t* b = reinterpret_cast<const uint8_t*>(sw);
+    uint32_t u = (uint32_t)reinterpret_cast<const uint16_t*>(b)[i] << 16;
+    if constexpr (kWsFmt == 24) u |= (uint32_t)b[(2ull << logp) + i] << 8;
+    return __uint_as_float(u);
+}
+DEVI void ws_pst(float* sw, int logp, uint32_t i, float v) {
+    if constexpr (kWsFmt == 32) { sw[i] = v; return; }
+    uint8_t* b = reinterpret_cast<uint8_t*>(sw);
+    const uint32_t u = __float_as_uint(v);
+    reinterpret_cast<uint16_t*>(b)[i] = (uint16_t)(u >> 16);
+    if constexpr (kWsFmt == 24) b[(2ull << logp) + i] = (uint8_t)(u >> 8);
+}
 DEVI uint32_t tile_valid(int64_t len) {
     return len <= 0 ? 0u : (len >= (1 << kRowLog) ? (1u << kRowLog) : (uint32_t)len);
 }
@@ -1191,9 +1275,6 @@ DEVI float4 bload4(rsrc_t r, uint32_t e, uint32_t k) {
     const f32x4 q = raw_load_f32x4(r, (int)(e * 4u), (int)(k * 4u), kLdAux);
     return make_float4(q.x, q.y, q.z, q.w);
 }
-template <int AUX = kLdAux>
-DEVI float bload1(rsrc_t r, uint32_t e, uint32_t k) { return raw_load_f32(r, (int)(e * 4u), (int)(k * 4u), AUX); }
-DEVI void bstore1(rsrc_t r, uint32_t e, uint32_t k, float v) { raw_store_f32(v, r, (int)(e * 4u), (int)(k * 4u), kStAux); }
 DEVI void bstore4(rsrc_t r, uint32_t e, uint32_t k, const float* v) {
     const f32x4 q = {v[0], v[1], v[2], v[3]};
     raw_store_f32x4(q, r, (int)(e * 4u), (int)(k * 4u), kStAux);
@@ -1268,33 +1349,37 @@ DEVI void store_y(const KArgs& a, const SliceDesc& D, uint32_t tile, uint32_t ba
 // inserted at position 5 of its element index; L3's register bits (5..10)
 // simply double.
 DEVI constexpr uint32_t ws_row_idx(uint32_t j) { return (j & 31u) | ((j >> 5) << 6); }
-DEVI float* ws_row_base(const KArgs& a, const SliceDesc& D, uint32_t tile) {
-    return D.perm ? a.ws + D.ws_off + ((size_t)(tile >> 1) << (kRowLog + 1)) + ((tile & 1u) << 5)
-                  : a.ws + D.ws_off + ((size_t)tile << kRowLog);
+DEVI size_t ws_row_i0(const SliceDesc& D, uint32_t tile) {
+    return D.perm ? ((size_t)(tile >> 1) << (kRowLog + 1)) + ((tile & 1u) << 5) : ((size_t)tile << kRowLog);
+}
+DEVI float* ws_row_base(const KArgs& a, const SliceDesc& D, uint32_t tile) { return a.ws + D.ws_off + ws_row_i0(D, tile); }
+// the tile's ws view (bytes: fp32 extent of the tile's records)
+DEVI WsR ws_row(const KArgs& a, const SliceDesc& D, uint32_t tile, uint32_t bytes) {
+    return ws_rsrc(a.ws + D.ws_off, D.logp, ws_row_i0(D, tile), bytes);
 }
 template <int AUX = kLdAux>
 DEVI void fetch_ws(const KArgs& a, const SliceDesc& D, uint32_t tile, bool live, uint32_t base3, float (&v)[64]) {
     if (D.perm) {
-        const rsrc_t r = mk_rsrc(ws_row_base(a, D, tile), live ? (4u << (kRowLog + 1)) - 128u : 0u);
+        const WsR r = ws_row(a, D, tile, live ? (4u << (kRowLog + 1)) - 128u : 0u);
         const uint32_t b = ws_row_idx(base3);
 #pragma unroll
-        for (int k = 0; k < 64; ++k) v[k] = bload1<AUX>(r, b, LT<RS::L3>::off(k) << 1);
+        for (int k = 0; k < 64; ++k) v[k] = ws_ld1(r, b * 4u, (LT<RS::L3>::off(k) << 1) * 4u, AUX);
     } else {
-        const rsrc_t r = mk_rsrc(ws_row_base(a, D, tile), live ? (4u << kRowLog) : 0u);
+        const WsR r = ws_row(a, D, tile, live ? (4u << kRowLog) : 0u);
 #pragma unroll
-        for (int k = 0; k < 64; ++k) v[k] = bload1<AUX>(r, base3, LT<RS::L3>::off(k));
+        for (int k = 0; k < 64; ++k) v[k] = ws_ld1(r, base3 * 4u, LT<RS::L3>::off(k) * 4u, AUX);
     }
 }
 DEVI void store_ws(const KArgs& a, const SliceDesc& D, uint32_t tile, uint32_t base3, const float (&v)[64]) {
     if (D.perm) {
-        const rsrc_t r = mk_rsrc(ws_row_base(a, D, tile), (4u << (kRowLog + 1)) - 128u);
+        const WsR r = ws_row(a, D, tile, (4u << (kRowLog + 1)) - 128u);
         const uint32_t b = ws_row_idx(base3);
 #pragma unroll
-        for (int k = 0; k < 64; ++k) bstore1(r, b, LT<RS::L3>::off(k) << 1, v[k]);
+        for (int k = 0; k < 64; ++k) ws_st1(r, b * 4u, (LT<RS::L3>::off(k) << 1) * 4u, v[k], kStAux);
     } else {
-        const rsrc_t r = mk_rsrc(ws_row_base(a, D, tile), 4u << kRowLog);
+        const WsR r = ws_row(a, D, tile, 4u << kRowLog);
 #pragma unroll
-        for (int k = 0; k < 64; ++k) bstore1(r, base3, LT<RS::L3>::off(k), v[k]);
+        for (int k = 0; k < 64; ++k) ws_st1(r, base3 * 4u, LT<RS::L3>::off(k) * 4u, v[k], kStAux);
     }
 }
 // ws tile in layout L (element bits 0, 1 in registers 0, 1) as float4s
@@ -1306,12 +1391,12 @@ template <Lay L>
 DEVI void fetch_ws4(const KArgs& a, const SliceDesc& D, uint32_t tile, bool live, uint32_t base, float (&v)[64]) {
     static_assert(LT<L>::rb(0) == 0 && LT<L>::rb(1) == 1, "float4 loads need element bits 0, 1 in registers 0, 1");
     const bool perm = D.perm;
-    const rsrc_t r = mk_rsrc(ws_row_base(a, D, tile), live ? (perm ? (4u << (kRowLog + 1)) - 128u : 4u << kRowLog) : 0u);
+    const WsR r = ws_row(a, D, tile, live ? (perm ? (4u << (kRowLog + 1)) - 128u : 4u << kRowLog) : 0u);
     const uint32_t b = perm ? ws_row_idx(base) : base;
 #pragma unroll
     for (int k = 0; k < 64; k += 4) {
         const uint32_t o = LT<L>::off(k);
-        const float4 f = bload4(r, b, perm ? ws_row_idx(o) : o);
+        const f32x4 f = ws_ld4(r, b * 4u, (perm ? ws_row_idx(o) : o) * 4u, kLdAux);
         v[k] = f.x; v[k + 1] = f.y; v[k + 2] = f.z; v[k + 3] = f.w;
     }
 }
@@ -1319,12 +1404,13 @@ template <Lay L>
 DEVI void store_ws4(const KArgs& a, const SliceDesc& D, uint32_t tile, uint32_t base, const float (&v)[64]) {
     static_assert(LT<L>::rb(0) == 0 && LT<L>::rb(1) == 1, "float4 stores need element bits 0, 1 in registers 0, 1");
     const bool perm = D.perm;
-    const rsrc_t r = mk_rsrc(ws_row_base(a, D, tile), perm ? (4u << (kRowLog + 1)) - 128u : 4u << kRowLog);
+    const WsR r = ws_row(a, D, tile, perm ? (4u << (kRowLog + 1)) - 128u : 4u << kRowLog);
     const uint32_t b = perm ? ws_row_idx(base) : base;
 #pragma unroll
     for (int k = 0; k < 64; k += 4) {
         const uint32_t o = LT<L>::off(k);
-        bstore4(r, b, perm ? ws_row_idx(o) : o, &v[k]);
+        const f32x4 q = {v[k], v[k + 1], v[k + 2], v[k + 3]};
+        ws_st4(r, b * 4u, (perm ? ws_row_idx(o) : o) * 4u, q, kStAux);
     }
 }
 
@@ -1606,6 +1692,7 @@ DEVI void col_body(const KArgs& a, int b) {
     const uint32_t th = tile >> (lo - K);
     const uint32_t tb = (tl << K) | (th << (lo + M));
     float* w = a.ws + D.ws_off;
+    const int lgp = D.logp;
     auto map = [&](uint32_t t) -> uint32_t { return tb | (t & ((1u << K) - 1u)) | ((t >> K) << lo); };
     // sign-table index of tile element t: the tile bits below the nibble bits
     // (columns, then rows lo .. p-4), i.e. t with its top 3 bits removed
@@ -1618,7 +1705,7 @@ DEVI void col_body(const KArgs& a, int b) {
     float v[32];
     const uint32_t base1 = LT<CS::L1>::base(tid);
 #pragma unroll
-    for (int r = 0; r < 32; ++r) v[r] = w[map(base1 | LT<CS::L1>::off(r))];
+    for (int r = 0; r < 32; ++r) v[r] = ws_pld(w, lgp, map(base1 | LT<CS::L1>::off(r)));
     stages<CS::L1, CS::A1>(v);
     if constexpr (M > 5) {
         exchange<CS::L1, CS::L2>(v, s, tid);  // its barriers also publish tab
@@ -1656,16 +1743,16 @@ DEVI void col_body(const KArgs& a, int b) {
         }
         const uint32_t base1w = opaque(base1);
 #pragma unroll
-        for (int r = 0; r < 32; ++r) w[map(base1w | LT<CS::L1>::off(r))] = v[r];
+        for (int r = 0; r < 32; ++r) ws_pst(w, lgp, map(base1w | LT<CS::L1>::off(r)), v[r]);
     } else {
         if constexpr (M > 5) {
             const uint32_t base2 = opaque(LT<CS::L2>::base(tid));
 #pragma unroll
-            for (int r = 0; r < 32; ++r) w[map(base2 | LT<CS::L2>::off(r))] = v[r];
+            for (int r = 0; r < 32; ++r) ws_pst(w, lgp, map(base2 | LT<CS::L2>::off(r)), v[r]);
         } else {
             const uint32_t base1w = opaque(base1);
 #pragma unroll
-            for (int r = 0; r < 32; ++r) w[map(base1w | LT<CS::L1>::off(r))] = v[r];
+            for (int r = 0; r < 32; ++r) ws_pst(w, lgp, map(base1w | LT<CS::L1>::off(r)), v[r]);
         }
     }
     // The slice norm nu = sqrt(sum of the row pass's partials of x^2)
@@ -1812,7 +1899,7 @@ __global__ __launch_bounds__(col6_nt<TL>(), 4) void k_col6(KArgs a) {
     const uint32_t th = tile >> (lo - K);
     const uint32_t tb = (tl << K) | (th << (lo + M));
     auto map = [&](uint32_t t) -> uint32_t { return tb | (t & ((1u << K) - 1u)) | ((t >> K) << lo); };
-    const rsrc_t rw = mk_rsrc(a.ws + D.ws_off, (uint32_t)(4ull << D.logp));
+    const WsR rw = ws_rsrc(a.ws + D.ws_off, D.logp, 0, (uint32_t)(4ull << D.logp));
     constexpr uint32_t kTabMask = (1u << (TL - 3)) - 1u;
     if constexpr (MID && kLadSign) {  // D2 sign bytes of the tile's 2^12 rand_diag words (see k_col)
         const uint32_t b2 = seed_b(sld(a.seeds, D.tensor) + 1u);
@@ -1832,12 +1919,12 @@ __global__ __launch_bounds__(col6_nt<TL>(), 4) void k_col6(KArgs a) {
         const uint32_t vo = opaque(ws_pos(map(base1)) * 4u);
 #pragma unroll
         for (int r = 0; r < 64; ++r)
-            v[r] = raw_load_f32(rw, (int)vo, (int)ws_pos((LT<CS::L1>::off(r) >> K) << 15) * 4, kLdAux);
+            v[r] = ws_ld1(rw, vo, ws_pos((LT<CS::L1>::off(r) >> K) << 15) * 4u, kLdAux);
     } else {
         const uint32_t vo = opaque(map(base1) * 4u);
 #pragma unroll
         for (int r = 0; r < 64; ++r)
-            v[r] = raw_load_f32(rw, (int)vo, (int)uu((LT<CS::L1>::off(r) >> K) << lo) * 4, kLdAux);
+            v[r] = ws_ld1(rw, vo, uu((LT<CS::L1>::off(r) >> K) << lo) * 4u, kLdAux);
     }
     if constexpr (kLadFly) stages<CS::L1, CS::A1>(v);
     if constexpr (EXCH && kLadFly) {
@@ -1869,14 +1956,14 @@ __global__ __launch_bounds__(col6_nt<TL>(), 4) void k_col6(KArgs a) {
             const uint32_t vo = opaque(ws_pos(map(base1)) * 4u);
 #pragma unroll
             for (int r = 0; r < 64; ++r)
-                raw_store_f32(v[r], rw, (int)vo, (int)ws_pos((LT<CS::L1>::off(r) >> K) << 15) * 4, kStAux);
+                ws_st1(rw, vo, ws_pos((LT<CS::L1>::off(r) >> K) << 15) * 4u, v[r], kStAux);
         } else {
             const uint32_t vo = opaque(map(base1) * 4u);
             int los = lo;
             asm volatile("" : "+s"(los));  // recompute the row offsets: 64 SGPRs kept live would spill
 #pragma unroll
             for (int r = 0; r < 64; ++r)
-                raw_store_f32(v[r], rw, (int)vo, (int)uu((LT<CS::L1>::off(r) >> K) << los) * 4, kStAux);
+                ws_st1(rw, vo, uu((LT<CS::L1>::off(r) >> K) << los) * 4u, v[r], kStAux);
         }
     } else {
         const uint32_t bcw = LT<LC>::base(tid);
@@ -1885,7 +1972,7 @@ __global__ __launch_bounds__(col6_nt<TL>(), 4) void k_col6(KArgs a) {
         asm volatile("" : "+s"(los));
 #pragma unroll
         for (int r = 0; r < 64; ++r)
-            raw_store_f32(v[r], rw, (int)vo, (int)uu((LT<LC>::off(r) >> K) << los) * 4, kStAux);
+            ws_st1(rw, vo, uu((LT<LC>::off(r) >> K) << los) * 4u, v[r], kStAux);
     }
     if (a.do_nu && tile == 0) {  // slice norm, as in k_col
         __shared__ float nred[NT / 64];
@@ -1940,14 +2027,14 @@ template <int H, int AUX = kLdAux>
 DEVI void fetch_ws_half(const KArgs& a, const SliceDesc& D, uint32_t tile, bool live, uint32_t base3,
                         float (&v)[64]) {
     if (D.perm) {
-        const rsrc_t r = mk_rsrc(ws_row_base(a, D, tile), live ? (4u << (kRowLog + 1)) - 128u : 0u);
+        const WsR r = ws_row(a, D, tile, live ? (4u << (kRowLog + 1)) - 128u : 0u);
         const uint32_t b = ws_row_idx(base3);
 #pragma unroll
-        for (int k = 32 * H; k < 32 * H + 32; ++k) v[k] = bload1<AUX>(r, b, LT<RS::L3>::off(k) << 1);
+        for (int k = 32 * H; k < 32 * H + 32; ++k) v[k] = ws_ld1(r, b * 4u, (LT<RS::L3>::off(k) << 1) * 4u, AUX);
     } else {
-        const rsrc_t r = mk_rsrc(ws_row_base(a, D, tile), live ? (4u << kRowLog) : 0u);
+        const WsR r = ws_row(a, D, tile, live ? (4u << kRowLog) : 0u);
 #pragma unroll
-        for (int k = 32 * H; k < 32 * H + 32; ++k) v[k] = bload1<AUX>(r, base3, LT<RS::L3>::off(k));
+        for (int k = 32 * H; k < 32 * H + 32; ++k) v[k] = ws_ld1(r, base3 * 4u, LT<RS::L3>::off(k) * 4u, AUX);
     }
 }
 
@@ -2105,14 +2192,14 @@ constexpr size_t kRow2SmemC = kRowC2Ex + 1024;  // half-exchange buffer + 256 ce
 template <Lay L>
 DEVI void store_ws_l(const KArgs& a, const SliceDesc& D, uint32_t tile, uint32_t base, const float (&v)[64]) {
     if (D.perm) {
-        const rsrc_t r = mk_rsrc(ws_row_base(a, D, tile), (4u << (kRowLog + 1)) - 128u);
+        const WsR r = ws_row(a, D, tile, (4u << (kRowLog + 1)) - 128u);
         const uint32_t b = ws_row_idx(base);
 #pragma unroll
-        for (int k = 0; k < 64; ++k) bstore1(r, b, LT<L>::off(k) << 1, v[k]);
+        for (int k = 0; k < 64; ++k) ws_st1(r, b * 4u, (LT<L>::off(k) << 1) * 4u, v[k], kStAux);
     } else {
-        const rsrc_t r = mk_rsrc(ws_row_base(a, D, tile), 4u << kRowLog);
+        const WsR r = ws_row(a, D, tile, 4u << kRowLog);
 #pragma unroll
-        for (int k = 0; k < 64; ++k) bstore1(r, base, LT<L>::off(k), v[k]);
+        for (int k = 0; k < 64; ++k) ws_st1(r, base * 4u, LT<L>::off(k) * 4u, v[k], kStAux);
     }
 }
 template <Lay L>

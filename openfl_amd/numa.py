@@ -4,17 +4,21 @@ A GPU's PCIe link hangs off one socket.  Host buffers the pipelines touch on
 every call -- the payload `bytes` the device gzip fills, the pinned staging
 of the payload's H2D, the serial seed sum's threads -- run at the local
 socket's memory and PCIe rate only when the threads that first touch them
-run on that socket.  On a two-socket MI355X host whose process may run on
-any CPU, the KC step measured bimodal, 19.4 or 21.2 ms per GiB run to run,
-with the host phases (payload fill, staged H2D, LUT tables) carrying the
-difference (profiles/r05_kc_numa_ab.txt).
+run on that socket.  Measured on a two-socket MI355X host whose process may
+run on any CPU (profiles/r06_env_ab.txt, bench.py alternated, HIP's 4 and
+8 HW queues): the KC pipeline runs 50.5-52.3 GiB/s bound against 46.8-49.9
+unbound, the gzip and inflate phases carrying the difference; the
+device-resident Eden step does not gain (422-425 GiB/s bound, 425-438
+unbound).  bench.py therefore runs on the OS placement and measures the KC
+steps bound in a child process beside it (numa_bound_variant).
 
 bind_to_device(i) restricts every thread of the process (and the threads it
 starts later) to the CPUs of the GPU's NUMA node, within the CPUs the process
 is allowed; memory first touched afterwards is then node-local.  It is
-process-wide, so the framework never calls it by itself: bench.py and the
-tools call it, and a deployment calls it once per process after choosing the
-device (the equivalent of `numactl --cpunodebind`)."""
+process-wide, so the framework never calls it by itself: tools/kc_bench.py
+and bench.py --numa-bind call it, and a deployment that runs the host-heavy
+lossy pipelines calls it once per process after choosing the device (the
+equivalent of `numactl --cpunodebind`)."""
 import os
 
 __all__ = ["device_numa_node", "bind_to_device"]

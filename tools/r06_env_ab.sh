@@ -8,7 +8,7 @@ for r in 1 2; do
   for cfg in q4_bind q4_free q8_bind q8_free; do
     a="--steps 3 --warmup 1 --also uniform_1gib,kc_uniform_1gib --no-cpu-baseline --also-steps 10"
     case $cfg in q8*) a="$a --hw-queues 8";; esac
-    case $cfg in *free) a="$a --no-numa-bind";; esac
+    case $cfg in *bind) a="$a --numa-bind";; esac  # (the A/B ran when binding was the default and free took --no-numa-bind)
     timeout -k 10 240 python -u bench.py $a > $out/${cfg}_$r.json 2> $out/${cfg}_$r.err || exit 1
     python - $out/${cfg}_$r.json <<'PY'
 import json,sys
