@@ -1984,6 +1984,23 @@ __global__ __launch_bounds__(col6_nt<TL>(), 4) void k_col6(KArgs a) {
     }
 }
 
+// block-uniform tile lookup of the non-persistent row launches (scalar loads):
+// one load from the launch's per-tile table when it has one, else a search
+DEVI void row_locate(const KArgs& a, int t, int& si, uint32_t& tile) {
+    if (a.btab) {
+        si = (int)sld(a.btab, 2 * (int64_t)t);
+        tile = sld(a.btab, 2 * (int64_t)t + 1) >> 3;
+        return;
+    }
+    int lo = 0, hi = a.count - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((int)sld(a.tstart, mid) <= t) lo = mid; else hi = mid - 1;
+    }
+    si = (int)sld(a.list, lo);
+    tile = (uint32_t)(t - (int)sld(a.tstart, lo));
+}
+
 // ===========================================================================
 // Encode pass C with two blocks per CU (k_enc_rowC2).  The quantiser makes
 // k_enc_rowC latency-bound at one block per CU (LDS table reads, bank
@@ -2065,15 +2082,7 @@ __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowC2(KArgs a) {
     __syncthreads();
     const int total = (int)sld(a.tstart, a.count);
     const uint32_t base3 = LT<R::L3>::base(tid), base5 = LT<R::L5>::base(tid);
-    auto locate = [&](int t, int& si, uint32_t& tile) {
-        int lo = 0, hi = a.count - 1;  // block-uniform search of the tile table (scalar loads)
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if ((int)sld(a.tstart, mid) <= t) lo = mid; else hi = mid - 1;
-        }
-        si = (int)sld(a.list, lo);
-        tile = (uint32_t)(t - (int)sld(a.tstart, lo));
-    };
+    auto locate = [&](int t, int& si, uint32_t& tile) { row_locate(a, t, si, tile); };
     int t = (int)blockIdx.x;
     if (t >= total) return;
     int si; uint32_t tile;
@@ -2232,16 +2241,6 @@ DEVI void store_y_l(const KArgs& a, const SliceDesc& D, uint32_t tile, uint32_t 
                     if ((uint32_t)q < (nv & 3u)) y[q] = yb ? add_rn(yb[q], v[k + q]) : v[k + q];
             }
     }
-}
-// block-uniform tile lookup of the non-persistent row launches (scalar loads)
-DEVI void row_locate(const KArgs& a, int t, int& si, uint32_t& tile) {
-    int lo = 0, hi = a.count - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if ((int)sld(a.tstart, mid) <= t) lo = mid; else hi = mid - 1;
-    }
-    si = (int)sld(a.list, lo);
-    tile = (uint32_t)(t - (int)sld(a.tstart, lo));
 }
 
 // x tile of the fused round-end encode: per element the delta of the
@@ -2666,6 +2665,8 @@ bool use_btab() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_BTAB"); return !(s && s[0] == '0'); }();
     return on;
 }
+// row launches up to this many tiles carry a per-tile table (8 B per tile)
+constexpr int64_t kRowTabMax = 1 << 16;
 // OFL_EDEN_SPLIT_MIB=m: two-stream plans split their large slices into two
 // waves only above m MiB of intermediates; unset (-1): see build_schedule
 int64_t split_min_bytes() {
@@ -3188,10 +3189,12 @@ void build_schedule(ofl_eden_plan* pl) {
         f.stream = s;
         pl->enc.push_back(f);
     }
-    // column launches: a per-block {slice, tile << 3 | group} table, so a
-    // block finds its tile with one load (a launch of few tiles per CU is
-    // latency-bound, and the prefix search is a chain of dependent loads);
-    // encode and decode share the table of the same list
+    // column launches and the two-blocks-per-CU row launches: a per-block
+    // (per-tile) {slice, tile << 3 | group} table, so a block finds its tile
+    // with one load (a launch of few tiles per CU is latency-bound, and the
+    // prefix search is a chain of dependent loads); encode and decode share
+    // the table of the same list.  The persistent row kernels search their
+    // LDS copy of the prefix and take no table.
     {
         std::map<std::pair<int, int>, int> made;
         auto table = [&](Launch& l) {
@@ -3207,7 +3210,7 @@ void build_schedule(ofl_eden_plan* pl) {
                         t.push_back((k << 3) | g);
                     }
             };
-            if (l.kind == K_COL) {
+            if (l.kind == K_COL || l.kind == K_ROWA || l.kind == K_ROWC) {
                 add_group(l.list_off, l.tstart_off, l.count, 0);
             } else {  // K_COLM / K_COLMSET: l.count groups {M, list, tstart (relative), count, first block}
                 for (int g = 0; g < l.count; ++g) {
@@ -3222,7 +3225,9 @@ void build_schedule(ofl_eden_plan* pl) {
         };
         for (auto* L : {&pl->enc, &pl->dec})
             for (Launch& l : *L)
-                if (l.kind == K_COL || l.kind == K_COLM || l.kind == K_COLMSET) table(l);
+                if (l.kind == K_COL || l.kind == K_COLM || l.kind == K_COLMSET ||
+                    ((l.kind == K_ROWA || l.kind == K_ROWC) && l.blocks <= kRowTabMax))
+                    table(l);
     }
     // per-launch byte accounting (bench / DESIGN.md roofline)
     const int64_t n_bits = pl->nbits;

@@ -212,10 +212,12 @@ def main():
             dt, rounds, outs = rounds_of(one)
             key = "batched" if mode == "reference" else "batched_fast_seed"
             phs = phs[len(sds):]   # the rounds after the first
+            nc = len(sds)
             res[key] = {"s": round(dt, 4), "GiB_s": round(in_bytes / dt / 2 ** 30, 3), "round_s": rounds,
                         "wire_bytes": sum(o[1] for o in outs), "rel_err": round(rel_err(sds[-1], outs[-1][0]), 6),
-                        "phases_ms_median_per_collaborator": {k: round(float(np.median([p[k] for p in phs])), 2)
-                                                              for k in phs[0]}}
+                        # median over the rounds after the first, per collaborator (in call order)
+                        "phases_ms_median": [{k: round(float(np.median([p[k] for p in phs[c::nc]])), 2)
+                                              for k in phs[0]} for c in range(nc)]}
     if "cpu" in modes:
         from oracle import eden as O
         cores = O.host_cores()
