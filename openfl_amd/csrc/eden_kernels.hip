@@ -1166,9 +1166,10 @@ constexpr int kStAux = OFL_ST_AUX;
 #define OFL_LADDER 0
 #endif
 constexpr int kLadder = OFL_LADDER;
+// (=5: the product without the sign generation, the bound of cheaper signs)
 constexpr bool kLadFly = kLadder == 0 || kLadder >= 2;   // butterflies + exchanges
-constexpr bool kLadSign = kLadder == 0 || kLadder >= 3;  // sign generation
-constexpr bool kLadFull = kLadder == 0;                  // quantiser, unpack, reductions
+constexpr bool kLadSign = kLadder == 0 || kLadder == 3;  // sign generation
+constexpr bool kLadFull = kLadder == 0 || kLadder == 5;  // quantiser, unpack, reductions
 // the memory-only rungs' stand-ins: a plane word from 4 values, values from a plane byte
 DEVI uint32_t lad_word(float a, float b, float c, float d) {
     return __float_as_uint(a) ^ __float_as_uint(b) ^ __float_as_uint(c) ^ __float_as_uint(d);
