@@ -222,8 +222,8 @@ def _newest_profile(*names):
     return next((p for p in paths if os.path.exists(p)), paths[-1])
 
 
-KC_TRAFFIC_JSON = _newest_profile("r05_final_kc_pipeline_hbm_traffic.json", "r04_final_kc_pipeline_hbm_traffic.json")
-KC_SQ_JSON = _newest_profile("r05_final_kc_sq.json")
+KC_TRAFFIC_JSON = _newest_profile("r06_final_kc_pipeline_hbm_traffic.json", "r05_final_kc_pipeline_hbm_traffic.json")
+KC_SQ_JSON = _newest_profile("r06_final_kc_sq.json", "r05_final_kc_sq.json")
 
 
 def _valu_busy(sq):
@@ -674,7 +674,7 @@ def main(argv=None):
         # PMC counters cannot be read from inside this process: the committed
         # rocprofv3 --pmc passes of this same workload and default schedule
         # (tools/pmc_run.sh), only when this run uses that schedule
-        traffic_src = _newest_profile("r05_final_llama3_8b_hbm_traffic.json", "r04_llama3_8b_hbm_traffic.json")
+        traffic_src = _newest_profile("r06_final_llama3_8b_hbm_traffic.json", "r05_final_llama3_8b_hbm_traffic.json")
     if traffic_src and os.path.exists(traffic_src):
         with open(traffic_src) as f:
             traffic = json.load(f).get("hbm_bytes_per_step")
