@@ -91,7 +91,8 @@ for f in ("r06_signs.txt", "r06_sgn.txt"):
             print("   " + line.rstrip())
 print("   (u = 1 GiB set, two streams, ms per step last; rn = ResNet-50; full = product, lad5 = no sign work;")
 print("    sgn=1 bitmaps, sgn=0 per-element hashes = the product.  The bitmaps lose: their extra launch per wave")
-print("    and direction costs more than the hashes they save; reverted.)")
+print("    and direction costs more than the hashes they save; reverted.  Written instead by blocks appended to an")
+print("    earlier row launch of the same stream, they lose too: profiles/r06_sign_bitmaps_fused_ab.txt.)")
 print()
 print("## G. Narrower intermediates, memory-pattern stubs on the Llama step (VERDICT r05 item 3; tools/r06_ladder2.sh:")
 print("##    -DOFL_WS_FMT=16 the high 16 bits of each fp32, =24 split planes hi-16 + lo-8; wrong results)")
