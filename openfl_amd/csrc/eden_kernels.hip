@@ -2174,23 +2174,39 @@ struct DecC2Set {  // decode pass C, half bit 10: 7,8,9 | 2..6,10 | 0,1,11,12,13
 // apply_signs_direct in groups of 8 registers whose results are pinned before
 // the next group starts: at the 128-VGPR cap of two blocks per CU the
 // scheduler would otherwise overlap all 64 hash chains and spill
-template <Lay L>
+// ADD = false: the general form only (k_enc_rowA2<true>: its weighted-
+// average loads leave no registers for the second path)
+template <Lay L, bool ADD = true>
 DEVI void apply_signs_grouped(float (&v)[64], uint32_t ebase, uint32_t base, int p, uint32_t b, float mul) {
-    // one code path for every p (the general per-element form of
-    // sgn_elem; no branch whose two sides the register allocator must both
-    // fit), the 64 sign bits first in two mask registers pinned per group of
-    // 8 hashes, then the flips: few live temporaries at the 128-VGPR cap
+    // the 64 sign bits first in two mask registers pinned per group of 8
+    // hashes, then the flips: few live temporaries at the 128-VGPR cap
     const uint32_t jm = (1u << (p - 3)) - 1u;
     const uint32_t ps = (uint32_t)(p - 3);
     uint32_t m[2] = {0u, 0u};
+    if (ADD && p >= 18) {
+        // a row tile (ebase = tile << 15) lies in one nibble of every word,
+        // and its elements' words are j0 + (base | off(r)): the LCG is one
+        // add of a compile-time constant per element (as apply_signs_direct),
+        // one quarter-rate multiply per element fewer than the general form
+        const uint32_t r2b = kLcgA * ((ebase & jm) + base) + b;
+        const uint32_t sh = 4u * (ebase >> ps) + 3u;
 #pragma unroll
-    for (int g = 0; g < 64; g += 8) {
+        for (int g = 0; g < 64; g += 8) {
 #pragma unroll
-        for (int r = g; r < g + 8; ++r) {
-            const uint32_t e = ebase + (base | LT<L>::off(r));
-            m[r >> 5] |= ((rd_word(e & jm, b) >> (4u * (e >> ps) + 3u)) & 1u) << (r & 31);
+            for (int r = g; r < g + 8; ++r)
+                m[r >> 5] |= ((rd_mix(r2b + kLcgA * LT<L>::off(r)) >> sh) & 1u) << (r & 31);
+            asm volatile("" : "+v"(m[0]), "+v"(m[1]));
         }
-        asm volatile("" : "+v"(m[0]), "+v"(m[1]));
+    } else {  // the general per-element form of sgn_elem
+#pragma unroll
+        for (int g = 0; g < 64; g += 8) {
+#pragma unroll
+            for (int r = g; r < g + 8; ++r) {
+                const uint32_t e = ebase + (base | LT<L>::off(r));
+                m[r >> 5] |= ((rd_word(e & jm, b) >> (4u * (e >> ps) + 3u)) & 1u) << (r & 31);
+            }
+            asm volatile("" : "+v"(m[0]), "+v"(m[1]));
+        }
     }
 #pragma unroll
     for (int r = 0; r < 64; ++r) v[r] = flip_unless(v[r] * mul, (m[r >> 5] >> (r & 31)) & 1u);
@@ -2348,7 +2364,7 @@ __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowA2(KArgs a) {
         // the sum is taken here, not sunk past the sign flips (which would keep
         // the 64 unflipped values live through the butterflies and spill them)
         asm volatile("" : "+v"(ss));
-        if constexpr (kLadSign) apply_signs_grouped<R::A1>(v, tile << kRowLog, base1, D.logp, b1, 1.0f);
+        if constexpr (kLadSign) apply_signs_grouped<R::A1, !WAVG>(v, tile << kRowLog, base1, D.logp, b1, 1.0f);
         if constexpr (kLadFly) {
             stages<R::A1, R::F1a>(v);
             exchange_half_pad<R::A1, R::A2, 14>(v, s, tid);
