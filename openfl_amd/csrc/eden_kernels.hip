@@ -2546,8 +2546,14 @@ struct ofl_eden_plan {
 
 namespace {
 
-// Default large-slice schedule (see build_schedule).
-constexpr int64_t kDefaultWaveMiB = 2048;
+// Default large-slice schedule (see build_schedule):
+// waves the size of the 256 MiB Infinity Cache's working half on two streams,
+// with the two-blocks-per-CU row kernels (1-2 tiles per CU per wave).  Since
+// the additive-LCG signs these beat 2 GiB waves on the Llama-3-8B step (429-431
+// vs 426-427 GiB/s) and the 1 GiB set (470-474 vs 458-461); 256 MiB waves lose
+// (420-422 / 450-452), profiles/r06_sched_ab.txt.  Slices above the wave size
+// (the 2^29 ones) are waves of their own and keep the persistent kernels.
+constexpr int64_t kDefaultWaveMiB = 128;
 constexpr int64_t kDefaultStreams = 2;
 
 int64_t low_po2(int64_t n) { int64_t p = 1; while (p * 2 <= n) p *= 2; return n ? p : 0; }
@@ -2624,13 +2630,13 @@ bool use_roll() {
 // Row launches of fewer than row2_max_tiles_per_cu() tiles per CU use the
 // two-blocks-per-CU kernels (k_enc_rowA2 / k_dec_rowA2 / k_dec_rowC2; outputs
 // bit-identical).  OFL_EDEN_ROW2=0: never, =1: always, unset: below the
-// threshold (OFL_EDEN_ROW2_TPC tiles per CU, default 4).
+// threshold (OFL_EDEN_ROW2_TPC tiles per CU, default 5).
 int row2_mode() {
     static const int m = [] { const char* s = getenv("OFL_EDEN_ROW2"); return (s && *s) ? (s[0] == '1' ? 1 : 0) : -1; }();
     return m;
 }
 int64_t row2_max_tiles_per_cu() {
-    static const int64_t v = [] { const char* s = getenv("OFL_EDEN_ROW2_TPC"); return (s && *s) ? strtoll(s, nullptr, 10) : 4ll; }();
+    static const int64_t v = [] { const char* s = getenv("OFL_EDEN_ROW2_TPC"); return (s && *s) ? strtoll(s, nullptr, 10) : 5ll; }();
     return v;
 }
 bool use_row2(int64_t tiles, int ncu, int plan_mode) {
@@ -3015,8 +3021,8 @@ void build_schedule(ofl_eden_plan* pl) {
     for (int32_t si : large) tot += 1ll << pl->slices[si].logp;
     // two streams: at least two waves, so both streams have work -- unless
     // every large slice fits one wave and no small-slice launches could use
-    // the second stream (the 1 GiB set: one wave on one stream, 2.24 vs
-    // 2.29 ms; ResNet-50 keeps its two waves beside the small slices: 360
+    // the second stream (at 2 GiB waves the 1 GiB set ran one wave on one
+    // stream, 2.24 vs 2.29 ms; ResNet-50 keeps its two waves beside the small slices: 360
     // vs 369 us with one wave; OFL_EDEN_SPLIT_MIB=m splits above m MiB)
     // With the small-set launch a plan that fits one wave keeps it whole: the
     // one small-set launch runs beside it on the side stream (ResNet-50 0.288

@@ -135,9 +135,15 @@ def test_two_stream_split_rules():
     assert len(rows) == 2 and abs(rows[0] - rows[1]) <= max(rows) // 4
     # with the small-set launch beside it, a plan that fits one wave keeps it whole
     assert EdenPlan(sizes, 8, streams=2, sset=1).n_waves == 1
-    uni = EdenPlan([numel(s) for _, s in WORKLOADS["uniform_1gib"]()], 8, streams=2)
+    # large slices only, all in one wave: one wave on the caller's stream
+    uni = EdenPlan([numel(s) for _, s in WORKLOADS["uniform_1gib"]()], 8, wave_mib=2048, streams=2)
     assert uni.n_waves == 1
     assert [l["name"] for l in uni.launches(True)].count("ofl::k_finalize") == 1
+    # the default schedule: 128 MiB waves (the 1 GiB set: eight, alternating
+    # streams), one finalize per wave stream
+    uni = EdenPlan([numel(s) for _, s in WORKLOADS["uniform_1gib"]()], 8, streams=2)
+    assert uni.n_waves == 8
+    assert [l["name"] for l in uni.launches(True)].count("ofl::k_finalize") == 2
     # more than one wave of large slices: waves by the wave size, as before
     many = EdenPlan([1 << 22] * 6, 8, wave_mib=32, streams=2)
     assert many.n_waves == 3
