@@ -95,11 +95,18 @@ int ofl_eden_plan_set_schedule(ofl_eden_plan_t plan, int64_t wave_bytes, int str
 int ofl_eden_plan_get_schedule(ofl_eden_plan_t plan, int64_t* wave_bytes, int* streams);
 int ofl_eden_plan_num_waves(ofl_eden_plan_t plan);
 /* Kernel choice for the large slices' row passes (no reference counterpart;
- * outputs bit-identical either way): -1 auto (launches of fewer than 4 tiles
+ * outputs bit-identical either way): -1 auto (launches of fewer than 5 tiles
  * per CU use the two-blocks-per-CU kernels, the rest the persistent
  * prefetching ones; env OFL_EDEN_ROW2 / OFL_EDEN_ROW2_TPC override the auto
  * rule), 0 always persistent, 1 always two blocks per CU. */
 int ofl_eden_plan_set_row2(ofl_eden_plan_t plan, int mode);
+/* Tile pairs in the two-blocks-per-CU row passes that apply the D1 signs
+ * (encode pass A, decode pass C; no reference counterpart, outputs
+ * bit-identical either way): a block runs a tile and the one 2^(p-3)
+ * elements up, whose sign words are the same, and hashes them once.
+ * -1 auto (launches of more tiles than two per CU; env OFL_EDEN_PAIR
+ * overrides), 0 never, 1 whenever the launch holds slices of >= 2^18. */
+int ofl_eden_plan_set_pair(ofl_eden_plan_t plan, int mode);
 /* Launches of the tiny (<= 2^10) and small (2^11..2^15) slices (no reference
  * counterpart; outputs bit-identical either way): 1 one small-set launch of
  * 1024-thread workgroups for all of them, 0 one launch per size class, -1 the

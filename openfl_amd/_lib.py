@@ -20,7 +20,7 @@ OFL_EINVAL, OFL_EHIP, OFL_ESPACE, OFL_EFORMAT = -1, -2, -3, -4
 EXPORTS = (
     "ofl_version", "ofl_last_error", "ofl_eden_slice_plan", "ofl_eden_plan_create",
     "ofl_eden_plan_destroy", "ofl_eden_plan_set_schedule", "ofl_eden_plan_num_waves",
-    "ofl_eden_plan_get_schedule", "ofl_eden_plan_set_row2", "ofl_eden_plan_set_sset", "ofl_eden_plan_set_fuse", "ofl_eden_plan_num_slices", "ofl_eden_plan_planes_bytes",
+    "ofl_eden_plan_get_schedule", "ofl_eden_plan_set_row2", "ofl_eden_plan_set_pair", "ofl_eden_plan_set_sset", "ofl_eden_plan_set_fuse", "ofl_eden_plan_num_slices", "ofl_eden_plan_planes_bytes",
     "ofl_eden_plan_workspace_bytes", "ofl_eden_plan_tensor_info", "ofl_eden_plan_tensor_dims",
     "ofl_eden_encode", "ofl_eden_encode_wavg", "ofl_eden_decode", "ofl_eden_decode_add", "ofl_eden_encode_host", "ofl_eden_decode_host", "ofl_eden_encode_mapped", "ofl_eden_decode_mapped", "ofl_eden_encode_seeded", "ofl_copy_h2d_chunked", "ofl_eden_encode_host_x", "ofl_eden_decode_host_x", "ofl_copy_h2d_async", "ofl_copy_h2d_staged", "ofl_eden_plan_profile", "ofl_eden_plan_num_launches",
     "ofl_eden_plan_launch_info", "ofl_eden_plan_profile_collect", "ofl_serial_sum_f32", "ofl_serial_sum_f32_mt", "ofl_serial_sum_copy_f32",
@@ -59,6 +59,8 @@ def _bind(L):
     L.ofl_eden_plan_set_schedule.restype = i32
     L.ofl_eden_plan_set_row2.argtypes = [vp, i32]
     L.ofl_eden_plan_set_row2.restype = i32
+    L.ofl_eden_plan_set_pair.argtypes = [vp, i32]
+    L.ofl_eden_plan_set_pair.restype = i32
     L.ofl_eden_plan_set_sset.argtypes = [vp, i32]
     L.ofl_eden_plan_set_sset.restype = i32
     L.ofl_eden_plan_set_fuse.argtypes = [vp, i32]

@@ -38,11 +38,12 @@ class EdenPlan:
     """Layout + launch plan for one batch shape (list of numels, optional dims)."""
 
     def __init__(self, numels, n_bits=8, dims=None, elem_offsets=None, wave_mib=None, streams=None, row2=None,
-                 sset=None, fuse=None):
+                 sset=None, fuse=None, pair=None):
         """wave_mib / streams: large-slice schedule (ofl_eden_plan_set_schedule;
         None keeps the library default); row2: row-pass kernels
         (ofl_eden_plan_set_row2: None/-1 auto, 0 persistent, 1 two blocks per
-        CU); sset: tiny / small slices in one launch (ofl_eden_plan_set_sset:
+        CU); pair: tile pairs sharing their D1 sign words in those kernels
+        (ofl_eden_plan_set_pair: None/-1 auto, 0 never, 1 always); sset: tiny / small slices in one launch (ofl_eden_plan_set_sset:
         None/-1 default, 0 one launch per size class, 1 one launch); fuse:
         that launch inside a one-wave plan's column launch on the caller's
         stream (ofl_eden_plan_set_fuse: None/-1 default, 0 no, 1 yes).
@@ -78,6 +79,8 @@ class EdenPlan:
                                                     0 if streams is None else int(streams)))
         if row2 is not None:
             _lib.check(L.ofl_eden_plan_set_row2(h, int(row2)))
+        if pair is not None:
+            _lib.check(L.ofl_eden_plan_set_pair(h, int(pair)))
         if sset is not None:
             _lib.check(L.ofl_eden_plan_set_sset(h, int(sset)))
         if fuse is not None:

@@ -111,6 +111,10 @@ struct KArgs {
     // blocks < sset_first run the small-set groups of table sset
     const int32_t* sset;
     int32_t sset_first;
+    // paired row launches (k_enc_rowA2<false> / k_dec_rowC2, row_locate):
+    // btab holds npair entries {slice, tile << 3 | pair}; pair = 1: the block
+    // also runs tile + 2^(p-18), whose D1 words are the same (0: tstart)
+    int32_t npair;
 };
 
 // Eden centroids in global memory (copied to LDS per workgroup); the
@@ -1987,12 +1991,15 @@ __global__ __launch_bounds__(col6_nt<TL>(), 4) void k_col6(KArgs a) {
 
 // block-uniform tile lookup of the non-persistent row launches (scalar loads):
 // one load from the launch's per-tile table when it has one, else a search
-DEVI void row_locate(const KArgs& a, int t, int& si, uint32_t& tile) {
+DEVI void row_locate(const KArgs& a, int t, int& si, uint32_t& tile, uint32_t* pair = nullptr) {
     if (a.btab) {
         si = (int)sld(a.btab, 2 * (int64_t)t);
-        tile = sld(a.btab, 2 * (int64_t)t + 1) >> 3;
+        const uint32_t e = sld(a.btab, 2 * (int64_t)t + 1);
+        tile = e >> 3;
+        if (pair) *pair = e & 1u;
         return;
     }
+    if (pair) *pair = 0u;
     int lo = 0, hi = a.count - 1;
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
@@ -2211,7 +2218,54 @@ DEVI void apply_signs_grouped(float (&v)[64], uint32_t ebase, uint32_t base, int
 #pragma unroll
     for (int r = 0; r < 64; ++r) v[r] = flip_unless(v[r] * mul, (m[r >> 5] >> (r & 31)) & 1u);
 }
-constexpr size_t kRow2Smem = kRowC2Ex + 64;     // half-exchange buffer + 8 wave partials
+// the D1 signs of a paired row launch (p >= 18).  Word j of a slice serves
+// its elements j + k*2^(p-3), k = 0..7 (bit 4k+3), so the tile one nibble up
+// (tile + 2^(p-18)) reuses this tile's words at bit sh + 4.  mode 1 (the
+// pair's first tile, nibble even): hash once, flip with bit sh, leave bit
+// sh + 4 of the 64 words in the thread's 8 stash bytes; mode 2 (the
+// partner, next in the same block): flip with the stash.  Half the hashes of
+// the unpaired form.  Each group of 8 hashes leaves its own and its partner
+// byte in LDS (bytes 8..15 and 0..7 of the thread's 16), so no mask register
+// is live across the hashes (as many live registers as apply_signs_grouped).
+template <Lay L>
+DEVI void apply_signs_pair(float (&v)[64], uint32_t ebase, uint32_t base, int p, uint32_t b, float mul, uint32_t mode,
+                           uint32_t* stash) {
+    // stash: the block's stash; a thread's 16 bytes at 16 * tid, the address
+    // recomputed at each use (an opaque tid: no register held across the hashes)
+    uint32_t m[2];
+    if (mode == 2u) {
+        const uint2 q = *reinterpret_cast<const uint2*>(stash + 4 * opaque(threadIdx.x));
+        m[0] = q.x;
+        m[1] = q.y;
+    } else {
+        const uint32_t jm = (1u << (p - 3)) - 1u;
+        const uint32_t r2b = kLcgA * ((ebase & jm) + base) + b;
+        const uint32_t sh = 4u * (ebase >> (p - 3)) + 3u;
+#pragma unroll
+        for (int g = 0; g < 64; g += 8) {
+            uint32_t ob = 0u, pb = 0u;
+#pragma unroll
+            for (int r = g; r < g + 8; ++r) {
+                const uint32_t w = rd_mix(r2b + kLcgA * LT<L>::off(r)) >> sh;
+                ob |= (w & 1u) << (r & 7);
+                pb |= ((w >> 4) & 1u) << (r & 7);
+            }
+            asm volatile("" : "+v"(ob), "+v"(pb));
+            uint8_t* sb = reinterpret_cast<uint8_t*>(stash) + 16 * opaque(threadIdx.x) + (g >> 3);
+            sb[0] = (uint8_t)pb;
+            sb[8] = (uint8_t)ob;
+        }
+        const uint2 q = *reinterpret_cast<const uint2*>(stash + 4 * opaque(threadIdx.x) + 2);
+        m[0] = q.x;
+        m[1] = q.y;
+    }
+#pragma unroll
+    for (int r = 0; r < 64; ++r) v[r] = flip_unless(v[r] * mul, (m[r >> 5] >> (r & 31)) & 1u);
+}
+// paired row launches: the D1 bits, 16 bytes per thread (thread i at bytes
+// 16i..16i+15: partner, own), after the 8 wave partials
+constexpr size_t kRow2Stash = kRowC2Ex + 64;
+constexpr size_t kRow2Smem = kRow2Stash + 16 * kRowNT;  // half-exchange buffer + partials + stash
 constexpr size_t kRow2SmemC = kRowC2Ex + 1024;  // half-exchange buffer + 256 centroids
 
 // ws tile store / y tile store in any layout (as store_ws / store_y)
@@ -2339,15 +2393,21 @@ __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowA2(KArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float* s = reinterpret_cast<float*>(smem);
     float* red = reinterpret_cast<float*>(smem + kRowC2Ex);
-    const int total = (int)sld(a.tstart, a.count);
+    uint32_t* stash = reinterpret_cast<uint32_t*>(smem + kRow2Stash);
+    const int total = !WAVG && a.npair ? a.npair : (int)sld(a.tstart, a.count);
     for (int t = (int)blockIdx.x; t < total; t += (int)gridDim.x) {
+      // a pair: this tile, then the one a nibble up (apply_signs_pair); the
+      // entry is re-read per tile (scalar loads: few SGPRs live across tiles)
+      for (uint32_t h = 0;; ++h) {
+        int si; uint32_t tile0, pair;
+        row_locate(a, t, si, tile0, &pair);
+        if (WAVG) pair = 0u;
+        const SliceDesc D = udesc(a.d, si);
         // thread-derived addresses are recomputed every tile (an opaque tid):
         // hoisted out of the loop they stay live across it and spill
         const uint32_t tid = opaque(threadIdx.x);
         const uint32_t base1 = LT<R::A1>::base(tid), base3 = LT<R::A3>::base(tid);
-        int si; uint32_t tile;
-        row_locate(a, t, si, tile);
-        const SliceDesc D = udesc(a.d, si);
+        const uint32_t tile = h ? tile0 + (1u << (D.logp - 18)) : tile0;
         float v[64];
         if constexpr (WAVG) {
             fetch_x_wavg(a, D, tile, base1, v);
@@ -2364,7 +2424,12 @@ __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowA2(KArgs a) {
         // the sum is taken here, not sunk past the sign flips (which would keep
         // the 64 unflipped values live through the butterflies and spill them)
         asm volatile("" : "+v"(ss));
-        if constexpr (kLadSign) apply_signs_grouped<R::A1, !WAVG>(v, tile << kRowLog, base1, D.logp, b1, 1.0f);
+        if constexpr (kLadSign) {
+            if (!WAVG && pair)
+                apply_signs_pair<R::A1>(v, tile << kRowLog, base1, D.logp, b1, 1.0f, 1u + h, stash);
+            else
+                apply_signs_grouped<R::A1, !WAVG>(v, tile << kRowLog, base1, D.logp, b1, 1.0f);
+        }
         if constexpr (kLadFly) {
             stages<R::A1, R::F1a>(v);
             exchange_half_pad<R::A1, R::A2, 14>(v, s, tid);
@@ -2375,11 +2440,16 @@ __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowA2(KArgs a) {
         store_ws_l<R::A3>(a, D, tile, base3, v);
         if constexpr (kLadFull) ss = block_sum<kRowNT>(ss, red);
         if (tid == 0) a.part[D.part_off + tile] = ss;
+        if (h >= pair) break;
+      }
     }
 }
 
-// decode pass A (as k_dec_rowA)
-template <bool A8>
+// decode pass A (as k_dec_rowA).  ROLL: the block's next tile's plane
+// words are loaded into w as soon as this tile's are unpacked, so they are in
+// flight across the butterflies and the ws stores (16 VGPRs; the kernel has
+// the room, 102 of 128).  8-byte aligned planes only (A8).
+template <bool A8, bool ROLL>
 __global__ __launch_bounds__(kRowNT, 4) void k_dec_rowA2(KArgs a) {
     using R = DecA2Set;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -2388,17 +2458,29 @@ __global__ __launch_bounds__(kRowNT, 4) void k_dec_rowA2(KArgs a) {
     if (threadIdx.x < 256) cen[threadIdx.x] = g_centroids[a.nbits - 1][threadIdx.x];
     __syncthreads();
     const int total = (int)sld(a.tstart, a.count);
+    uint64_t w[8];
+    if (ROLL && (int)blockIdx.x < total) {
+        int si; uint32_t tile;
+        row_locate(a, (int)blockIdx.x, si, tile);
+        fetch_planes<A8>(a, udesc(a.d, si), tile, true, LT<R::C1>::base(threadIdx.x), w);
+    }
     for (int t = (int)blockIdx.x; t < total; t += (int)gridDim.x) {
         const uint32_t tid = opaque(threadIdx.x);  // as in k_enc_rowA2
         const uint32_t base1 = LT<R::C1>::base(tid), base3 = LT<R::C3>::base(tid);
         int si; uint32_t tile;
         row_locate(a, t, si, tile);
         const SliceDesc D = udesc(a.d, si);
-        uint64_t w[8];
-        fetch_planes<A8>(a, D, tile, true, base1, w);
+        if (!ROLL) fetch_planes<A8>(a, D, tile, true, base1, w);
         float v[64];
         if constexpr (kLadFull) unpack_centroids64(w, cen, v);
         else lad_unpack64(w, v);
+        if (ROLL) {  // w is free: the next tile's planes (none past the end)
+            const int tn = t + (int)gridDim.x;
+            const bool more = tn < total;
+            int sn; uint32_t tln;
+            row_locate(a, more ? tn : t, sn, tln);
+            fetch_planes<A8>(a, udesc(a.d, sn), tln, more, base1, w);
+        }
         if constexpr (kLadFly) {
             stages<R::C1, R::G1>(v);
             exchange_half_pad<R::C1, R::C2, 5>(v, s, tid);
@@ -2415,13 +2497,16 @@ __global__ __launch_bounds__(kRowNT, 4) void k_dec_rowC2(KArgs a) {
     using R = DecC2Set;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float* s = reinterpret_cast<float*>(smem);
-    const int total = (int)sld(a.tstart, a.count);
+    uint32_t* stash = reinterpret_cast<uint32_t*>(smem + kRow2Stash);
+    const int total = a.npair ? a.npair : (int)sld(a.tstart, a.count);
     for (int t = (int)blockIdx.x; t < total; t += (int)gridDim.x) {
+      for (uint32_t h = 0;; ++h) {  // as in k_enc_rowA2
+        int si; uint32_t tile0, pair;
+        row_locate(a, t, si, tile0, &pair);
+        const SliceDesc D = udesc(a.d, si);
         const uint32_t tid = opaque(threadIdx.x);  // as in k_enc_rowA2
         const uint32_t base1 = LT<R::B1>::base(tid), base4 = LT<R::B4>::base(tid);
-        int si; uint32_t tile;
-        row_locate(a, t, si, tile);
-        const SliceDesc D = udesc(a.d, si);
+        const uint32_t tile = h ? tile0 + (1u << (D.logp - 18)) : tile0;
         float v[64];
         if constexpr (kRowWs4) fetch_ws4<R::B1>(a, D, tile, true, base1, v);
         else fetch_ws(a, D, tile, true, base1, v);
@@ -2436,9 +2521,14 @@ __global__ __launch_bounds__(kRowNT, 4) void k_dec_rowC2(KArgs a) {
             stages<R::B4, R::H4>(v);
         }
         const float sc = sldf(a.scales_in, D.scale_idx);
-        if constexpr (kLadSign)
-            apply_signs_grouped<R::B4>(v, tile << kRowLog, base4, D.logp, b1, sc * pow2i(-((D.logp + 1) / 2)));
+        if constexpr (kLadSign) {
+            const float mul = sc * pow2i(-((D.logp + 1) / 2));
+            if (pair) apply_signs_pair<R::B4>(v, tile << kRowLog, base4, D.logp, b1, mul, 1u + h, stash);
+            else apply_signs_grouped<R::B4>(v, tile << kRowLog, base4, D.logp, b1, mul);
+        }
         store_y_l<R::B4>(a, D, tile, base4, v);
+        if (h >= pair) break;
+      }
     }
 }
 
@@ -2495,6 +2585,8 @@ struct Launch {
     int join = 0;    // the caller's stream waits for the side stream before this launch
     int tl = 15;     // column: log2 of the tile (16: k_col6 with 1024 threads)
     int btab_off = -1;  // column: per-block {slice, tile << 3 | group} table in ints
+    int ptab_off = -1;  // row: the paired table {slice, tile << 3 | pair} in ints (npair entries)
+    int npair = 0;
     int sset_off = -1;  // K_COLMSET: the small-set group table in ints
     int sset_groups = 0;  // K_COLMSET: its groups (the launch's first blocks)
     int64_t bytes_moved = 0;  // fp32/plane bytes this launch reads + writes (intermediates included)
@@ -2522,6 +2614,7 @@ struct ofl_eden_plan {
     int nstreams = 1;           // 2: waves alternate between the caller's and a side stream
     int nwaves = 0;
     int row2 = -1;              // row launches on the two-blocks-per-CU kernels: -1 auto, 0 never, 1 always
+    int pair = -1;              // their tile pairs sharing D1 words: -1 auto, 0 never, 1 whenever possible
     int sset = -1;              // tiny / small slices in one small-set launch: -1 env default, 0 no, 1 yes
     int fuse = -1;              // small-set groups fused into the column launch: -1 env default, 0 no, 1 yes
     bool single = false;        // every launch on the caller's stream (no fork / join) -- K_COLMSET plans
@@ -2682,6 +2775,18 @@ bool use_two_waves() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_TWOWAVES"); return !(s && s[0] == '0'); }();
     return on;
 }
+// k_dec_rowA2 loads a block's next tile's planes during this one's work
+// (OFL_EDEN_DECA_ROLL=1; 0 / unset: per tile, as before)
+bool use_deca_roll() {
+    static const bool on = [] { const char* s = getenv("OFL_EDEN_DECA_ROLL"); return s && s[0] == '1'; }();
+    return on;
+}
+// multi-wave plans pack their large slices largest first (OFL_EDEN_WAVESORT=1;
+// 0 / unset: in batch order)
+bool use_wave_sort() {
+    static const bool on = [] { const char* s = getenv("OFL_EDEN_WAVESORT"); return s && s[0] == '1'; }();
+    return on;
+}
 // column launches find their tile in a per-block table (OFL_EDEN_BTAB=0:
 // binary search over the launch's tile prefix, as before)
 bool use_btab() {
@@ -2690,6 +2795,18 @@ bool use_btab() {
 }
 // row launches up to this many tiles carry a per-tile table (8 B per tile)
 constexpr int64_t kRowTabMax = 1 << 16;
+// two-blocks-per-CU row launches of more tiles than block slots run tile
+// pairs sharing their D1 words (apply_signs_pair; OFL_EDEN_PAIR=0: never,
+// =1: whenever the launch has a paired table)
+int pair_mode() {
+    static const int m = [] { const char* s = getenv("OFL_EDEN_PAIR"); return (s && *s) ? (s[0] == '1' ? 1 : 0) : -1; }();
+    return m;
+}
+bool use_pair(const Launch& l, int ncu, int plan_mode) {
+    if (l.ptab_off < 0 || !use_btab()) return false;
+    const int m = plan_mode >= 0 ? plan_mode : pair_mode();
+    return m >= 0 ? m == 1 : l.blocks > 2 * (int64_t)ncu;
+}
 // OFL_EDEN_SPLIT_MIB=m: two-stream plans split their large slices into two
 // waves only above m MiB of intermediates; unset (-1): see build_schedule
 int64_t split_min_bytes() {
@@ -2746,8 +2863,9 @@ hipError_t set_all_attrs() {
     if ((e = set_lds((const void*)ofl::k_dec_rowC, ofl::kRowSmemA)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_enc_rowA2<false>, ofl::kRow2Smem)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_enc_rowA2<true>, ofl::kRow2Smem)) != hipSuccess) return e;
-    if ((e = set_lds((const void*)ofl::k_dec_rowA2<true>, ofl::kRow2SmemC)) != hipSuccess) return e;
-    if ((e = set_lds((const void*)ofl::k_dec_rowA2<false>, ofl::kRow2SmemC)) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_dec_rowA2<true, false>, ofl::kRow2SmemC)) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_dec_rowA2<false, false>, ofl::kRow2SmemC)) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_dec_rowA2<true, true>, ofl::kRow2SmemC)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_dec_rowC2, ofl::kRow2Smem)) != hipSuccess) return e;
     if ((e = set_col_attr<6>()) != hipSuccess) return e;
     if ((e = set_col_attr<7>()) != hipSuccess) return e;
@@ -2807,6 +2925,7 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
         a.count = l.count;
         a.lo = l.lo;
         a.do_nu = l.nu;
+        a.npair = 0;
         if (evs) HIP_TRY(hipEventRecord((*evs)[2 * li], st));
         hipError_t e = hipSuccess;
         switch (l.kind) {
@@ -2842,10 +2961,16 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
                 break;
             }
             if (use_row2(l.blocks, pl->ncu, pl->row2)) {
-                const int64_t g2 = std::min<int64_t>(l.blocks, 2 * pl->ncu);
+                int64_t g2 = std::min<int64_t>(l.blocks, 2 * pl->ncu);
+                if (enc && use_pair(l, pl->ncu, pl->pair)) {
+                    a.btab = pl->d_ints + l.ptab_off;
+                    a.npair = l.npair;
+                    g2 = std::min<int64_t>(l.npair, 2 * pl->ncu);
+                }
                 e = enc ? launch(ofl::k_enc_rowA2<false>, g2, ofl::kRowNT, ofl::kRow2Smem, st, a)
-                        : a8 ? launch(ofl::k_dec_rowA2<true>, g2, ofl::kRowNT, ofl::kRow2SmemC, st, a)
-                             : launch(ofl::k_dec_rowA2<false>, g2, ofl::kRowNT, ofl::kRow2SmemC, st, a);
+                        : a8 ? (use_deca_roll() ? launch(ofl::k_dec_rowA2<true, true>, g2, ofl::kRowNT, ofl::kRow2SmemC, st, a)
+                                                : launch(ofl::k_dec_rowA2<true, false>, g2, ofl::kRowNT, ofl::kRow2SmemC, st, a))
+                             : launch(ofl::k_dec_rowA2<false, false>, g2, ofl::kRowNT, ofl::kRow2SmemC, st, a);
                 break;
             }
             const int64_t g = std::min<int64_t>(l.blocks, pl->ncu);
@@ -2861,8 +2986,15 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
                                         ofl::kRowC2Smem, st, a)
                                : launch(ofl::k_enc_rowC2<false>, std::min<int64_t>(l.blocks, 2 * pl->ncu), ofl::kRowNT,
                                         ofl::kRowC2Smem, st, a);
-            else if (!enc && use_row2(l.blocks, pl->ncu, pl->row2))
-                e = launch(ofl::k_dec_rowC2, std::min<int64_t>(l.blocks, 2 * pl->ncu), ofl::kRowNT, ofl::kRow2Smem, st, a);
+            else if (!enc && use_row2(l.blocks, pl->ncu, pl->row2)) {
+                int64_t g2 = std::min<int64_t>(l.blocks, 2 * pl->ncu);
+                if (use_pair(l, pl->ncu, pl->pair)) {
+                    a.btab = pl->d_ints + l.ptab_off;
+                    a.npair = l.npair;
+                    g2 = std::min<int64_t>(l.npair, 2 * pl->ncu);
+                }
+                e = launch(ofl::k_dec_rowC2, g2, ofl::kRowNT, ofl::kRow2Smem, st, a);
+            }
             else
                 e = enc ? launch(ofl::k_enc_rowC, g, ofl::kRowNT, ofl::kRowSmemQ, st, a)
                         : launch(ofl::k_dec_rowC, g, ofl::kRowNT, ofl::kRowSmemA, st, a);
@@ -3013,12 +3145,21 @@ void build_schedule(ofl_eden_plan* pl) {
                 common.push_back({K_SMALL, 11 + k, 0, 0, add_list(pl->small[k]), -1, (int)pl->small[k].size(),
                                   (int64_t)pl->small[k].size()});
     }
-    const std::vector<int32_t>& large = pl->large;
     for (auto& D : pl->slices) D.perm = 0;
     std::vector<std::vector<int32_t>> waves;
     int64_t cap = pl->wave_bytes > 0 ? pl->wave_bytes / 4 : INT64_MAX;
     int64_t tot = 0;
-    for (int32_t si : large) tot += 1ll << pl->slices[si].logp;
+    for (int32_t si : pl->large) tot += 1ll << pl->slices[si].logp;
+    // more than one wave by size: the large slices largest first (stable), so
+    // in-order packing fills each wave with slices of one size -- power-of-two
+    // sizes pack whole waves, one column launch per wave (OFL_EDEN_WAVESORT)
+    std::vector<int32_t> sorted_large;
+    if (tot > cap && use_wave_sort()) {
+        sorted_large = pl->large;
+        std::stable_sort(sorted_large.begin(), sorted_large.end(),
+                         [&](int32_t x, int32_t y) { return pl->slices[x].logp > pl->slices[y].logp; });
+    }
+    const std::vector<int32_t>& large = sorted_large.empty() ? pl->large : sorted_large;
     // two streams: at least two waves, so both streams have work -- unless
     // every large slice fits one wave and no small-slice launches could use
     // the second stream (at 2 GiB waves the 1 GiB set ran one wave on one
@@ -3251,6 +3392,37 @@ void build_schedule(ofl_eden_plan* pl) {
                 if (l.kind == K_COL || l.kind == K_COLM || l.kind == K_COLMSET ||
                     ((l.kind == K_ROWA || l.kind == K_ROWC) && l.blocks <= kRowTabMax))
                     table(l);
+        // the sign-applying row launches (encode A, decode C): a paired table,
+        // one entry per tile of nibble-even position (its partner follows in
+        // the same block) and per tile of a slice below 2^18 (unpaired)
+        std::map<std::pair<int, int>, std::pair<int, int>> pmade;
+        auto ptable = [&](Launch& l) {
+            const auto key = std::make_pair(l.list_off, l.tstart_off);
+            auto it = pmade.find(key);
+            if (it != pmade.end()) { l.ptab_off = it->second.first; l.npair = it->second.second; return; }
+            std::vector<int32_t> t;
+            bool any = false;
+            for (int i = 0; i < l.count; ++i) {
+                const int32_t si = ints[l.list_off + i];
+                const int p = pl->slices[si].logp;
+                const int32_t nt = ints[l.tstart_off + i + 1] - ints[l.tstart_off + i];
+                for (int32_t k = 0; k < nt; ++k) {
+                    if (p >= 18 && ((k >> (p - 18)) & 1)) continue;  // a partner
+                    t.push_back(si);
+                    t.push_back((k << 3) | (p >= 18 ? 1 : 0));
+                    any = any || p >= 18;
+                }
+            }
+            if (!any) return;
+            l.ptab_off = (int)ints.size();
+            l.npair = (int)(t.size() / 2);
+            pmade[key] = {l.ptab_off, l.npair};
+            ints.insert(ints.end(), t.begin(), t.end());
+        };
+        for (Launch& l : pl->enc)
+            if (l.kind == K_ROWA && l.tstart_off >= 0 && l.blocks <= kRowTabMax) ptable(l);
+        for (Launch& l : pl->dec)
+            if (l.kind == K_ROWC && l.tstart_off >= 0 && l.blocks <= kRowTabMax) ptable(l);
     }
     // per-launch byte accounting (bench / DESIGN.md roofline)
     const int64_t n_bits = pl->nbits;
@@ -3513,6 +3685,14 @@ int ofl_eden_plan_set_row2(ofl_eden_plan_t pl, int mode) {
     if (mode < -1 || mode > 1) return fail(OFL_EINVAL, "row2 mode must be -1 (auto), 0 or 1");
     std::lock_guard<std::mutex> g(pl->mu);
     pl->row2 = mode;
+    return OFL_OK;
+}
+
+int ofl_eden_plan_set_pair(ofl_eden_plan_t pl, int mode) {
+    if (!pl) return fail(OFL_EINVAL, "null plan");
+    if (mode < -1 || mode > 1) return fail(OFL_EINVAL, "pair mode must be -1 (auto), 0 or 1");
+    std::lock_guard<std::mutex> g(pl->mu);
+    pl->pair = mode;
     return OFL_OK;
 }
 

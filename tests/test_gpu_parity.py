@@ -609,16 +609,20 @@ def test_row2_variants_bit_identical():
     k_dec_rowC2, ofl_eden_plan_set_row2) butterfly the index bits in the same
     order as the persistent ones and load, sum and store the same values: planes,
     scales and decoded values are bit-identical, for 3-pass (incl. the
-    interleaved 2^25 layout) and 5-pass slices, ragged tails and decode_add."""
+    interleaved 2^25 layout) and 5-pass slices, ragged tails and decode_add.
+    The same with tile pairs (ofl_eden_plan_set_pair: a block hashes the D1
+    words of a tile and of the one 2^(p-3) up once), forced on and off, and
+    with 2 MiB waves (every 2^18..2^22 slice in its own paired launch)."""
     from openfl_amd.codec import EdenPlan
-    numels = [(1 << 26) + 777, 1 << 25, (1 << 22) + 12345, (1 << 16) + 5, 3000]
+    numels = [(1 << 26) + 777, 1 << 25, (1 << 22) + 12345, (1 << 16) + 5, 3000, (1 << 18) + 3, (1 << 17) + 1,
+              (1 << 19) - 7]
     g = torch.Generator(device=DEV).manual_seed(21)
     outs = []
-    for row2 in (0, 1):
-        plan = EdenPlan(numels, 8, wave_mib=4096, streams=1, row2=row2)
+    for row2, pair, wave in ((0, 0, 4096), (1, 0, 4096), (1, 1, 4096), (1, 1, 2), (-1, -1, 2)):
+        plan = EdenPlan(numels, 8, wave_mib=wave, streams=1, row2=row2, pair=pair)
         x = torch.empty(plan.arena_numel, device=DEV).normal_(0, 0.01, generator=g.manual_seed(21))
         base = torch.empty(plan.arena_numel, device=DEV).normal_(0, 1.0, generator=g.manual_seed(22))
-        seeds = torch.tensor([5, 6, 7, 8, 9], dtype=torch.int32, device=DEV)
+        seeds = torch.tensor([5, 6, 7, 8, 9, 10, 11, 12], dtype=torch.int32, device=DEV)
         ws = torch.empty(max(plan.ws_bytes, 256), dtype=torch.uint8, device=DEV)
         p = torch.full((plan.planes_bytes,), 0x5A, dtype=torch.uint8, device=DEV)
         s = torch.zeros(plan.n_slices, dtype=torch.float32, device=DEV)
@@ -630,8 +634,9 @@ def test_row2_variants_bit_identical():
         torch.cuda.synchronize()
         outs.append((p.cpu(), s.cpu(), y.cpu(), y2.cpu()))
         del x, base, ws, p, s, y, y2
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
+    for o in outs[1:]:
+        for a, b in zip(o, outs[0]):
+            assert torch.equal(a, b)
 
 
 def test_small_launch_split_bit_identical():

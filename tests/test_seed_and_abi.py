@@ -115,6 +115,10 @@ def test_wave_schedule_layout():
     assert names1.count("ofl::k_dec_rowA2") == 4 and names1.count("ofl::k_dec_rowC2") == 4
     with pytest.raises(_lib.CodecError, match="row2"):
         EdenPlan(numels, 8, row2=2)
+    for pair in (-1, 0, 1):
+        assert EdenPlan(numels, 8, row2=1, pair=pair).n_waves == EdenPlan(numels, 8, row2=1).n_waves
+    with pytest.raises(_lib.CodecError, match="pair"):
+        EdenPlan(numels, 8, pair=2)
     big = EdenPlan([1 << 25, 1 << 22], 8, wave_mib=16, streams=1)   # a slice above the wave size
     assert big.n_waves == 2
     with pytest.raises(_lib.CodecError, match="streams"):
