@@ -2445,11 +2445,8 @@ __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowA2(KArgs a) {
     }
 }
 
-// decode pass A (as k_dec_rowA).  ROLL: the block's next tile's plane
-// words are loaded into w as soon as this tile's are unpacked, so they are in
-// flight across the butterflies and the ws stores (16 VGPRs; the kernel has
-// the room, 102 of 128).  8-byte aligned planes only (A8).
-template <bool A8, bool ROLL>
+// decode pass A (as k_dec_rowA)
+template <bool A8>
 __global__ __launch_bounds__(kRowNT, 4) void k_dec_rowA2(KArgs a) {
     using R = DecA2Set;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -2458,29 +2455,17 @@ __global__ __launch_bounds__(kRowNT, 4) void k_dec_rowA2(KArgs a) {
     if (threadIdx.x < 256) cen[threadIdx.x] = g_centroids[a.nbits - 1][threadIdx.x];
     __syncthreads();
     const int total = (int)sld(a.tstart, a.count);
-    uint64_t w[8];
-    if (ROLL && (int)blockIdx.x < total) {
-        int si; uint32_t tile;
-        row_locate(a, (int)blockIdx.x, si, tile);
-        fetch_planes<A8>(a, udesc(a.d, si), tile, true, LT<R::C1>::base(threadIdx.x), w);
-    }
     for (int t = (int)blockIdx.x; t < total; t += (int)gridDim.x) {
         const uint32_t tid = opaque(threadIdx.x);  // as in k_enc_rowA2
         const uint32_t base1 = LT<R::C1>::base(tid), base3 = LT<R::C3>::base(tid);
         int si; uint32_t tile;
         row_locate(a, t, si, tile);
         const SliceDesc D = udesc(a.d, si);
-        if (!ROLL) fetch_planes<A8>(a, D, tile, true, base1, w);
+        uint64_t w[8];
+        fetch_planes<A8>(a, D, tile, true, base1, w);
         float v[64];
         if constexpr (kLadFull) unpack_centroids64(w, cen, v);
         else lad_unpack64(w, v);
-        if (ROLL) {  // w is free: the next tile's planes (none past the end)
-            const int tn = t + (int)gridDim.x;
-            const bool more = tn < total;
-            int sn; uint32_t tln;
-            row_locate(a, more ? tn : t, sn, tln);
-            fetch_planes<A8>(a, udesc(a.d, sn), tln, more, base1, w);
-        }
         if constexpr (kLadFly) {
             stages<R::C1, R::G1>(v);
             exchange_half_pad<R::C1, R::C2, 5>(v, s, tid);
@@ -2775,16 +2760,10 @@ bool use_two_waves() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_TWOWAVES"); return !(s && s[0] == '0'); }();
     return on;
 }
-// k_dec_rowA2 loads a block's next tile's planes during this one's work
-// (OFL_EDEN_DECA_ROLL=1; 0 / unset: per tile, as before)
-bool use_deca_roll() {
-    static const bool on = [] { const char* s = getenv("OFL_EDEN_DECA_ROLL"); return s && s[0] == '1'; }();
-    return on;
-}
-// multi-wave plans pack their large slices largest first (OFL_EDEN_WAVESORT=1;
-// 0 / unset: in batch order)
+// multi-wave plans pack their large slices largest first (OFL_EDEN_WAVESORT=0:
+// in batch order; profiles/r06_sort_roll_ab.txt)
 bool use_wave_sort() {
-    static const bool on = [] { const char* s = getenv("OFL_EDEN_WAVESORT"); return s && s[0] == '1'; }();
+    static const bool on = [] { const char* s = getenv("OFL_EDEN_WAVESORT"); return !(s && s[0] == '0'); }();
     return on;
 }
 // column launches find their tile in a per-block table (OFL_EDEN_BTAB=0:
@@ -2863,9 +2842,8 @@ hipError_t set_all_attrs() {
     if ((e = set_lds((const void*)ofl::k_dec_rowC, ofl::kRowSmemA)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_enc_rowA2<false>, ofl::kRow2Smem)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_enc_rowA2<true>, ofl::kRow2Smem)) != hipSuccess) return e;
-    if ((e = set_lds((const void*)ofl::k_dec_rowA2<true, false>, ofl::kRow2SmemC)) != hipSuccess) return e;
-    if ((e = set_lds((const void*)ofl::k_dec_rowA2<false, false>, ofl::kRow2SmemC)) != hipSuccess) return e;
-    if ((e = set_lds((const void*)ofl::k_dec_rowA2<true, true>, ofl::kRow2SmemC)) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_dec_rowA2<true>, ofl::kRow2SmemC)) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_dec_rowA2<false>, ofl::kRow2SmemC)) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_dec_rowC2, ofl::kRow2Smem)) != hipSuccess) return e;
     if ((e = set_col_attr<6>()) != hipSuccess) return e;
     if ((e = set_col_attr<7>()) != hipSuccess) return e;
@@ -2968,9 +2946,8 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
                     g2 = std::min<int64_t>(l.npair, 2 * pl->ncu);
                 }
                 e = enc ? launch(ofl::k_enc_rowA2<false>, g2, ofl::kRowNT, ofl::kRow2Smem, st, a)
-                        : a8 ? (use_deca_roll() ? launch(ofl::k_dec_rowA2<true, true>, g2, ofl::kRowNT, ofl::kRow2SmemC, st, a)
-                                                : launch(ofl::k_dec_rowA2<true, false>, g2, ofl::kRowNT, ofl::kRow2SmemC, st, a))
-                             : launch(ofl::k_dec_rowA2<false, false>, g2, ofl::kRowNT, ofl::kRow2SmemC, st, a);
+                        : a8 ? launch(ofl::k_dec_rowA2<true>, g2, ofl::kRowNT, ofl::kRow2SmemC, st, a)
+                             : launch(ofl::k_dec_rowA2<false>, g2, ofl::kRowNT, ofl::kRow2SmemC, st, a);
                 break;
             }
             const int64_t g = std::min<int64_t>(l.blocks, pl->ncu);
@@ -3152,7 +3129,10 @@ void build_schedule(ofl_eden_plan* pl) {
     for (int32_t si : pl->large) tot += 1ll << pl->slices[si].logp;
     // more than one wave by size: the large slices largest first (stable), so
     // in-order packing fills each wave with slices of one size -- power-of-two
-    // sizes pack whole waves, one column launch per wave (OFL_EDEN_WAVESORT)
+    // sizes pack whole waves, one column launch per wave (OFL_EDEN_WAVESORT).
+    // Llama-3-8B: 210 waves of 1024 tiles (but the two 2^29 ones), 637
+    // launches per direction instead of 258 waves of 512-1024 tiles and 909
+    // launches; 434.8-435.4 -> 445.7-448.8 GiB/s
     std::vector<int32_t> sorted_large;
     if (tot > cap && use_wave_sort()) {
         sorted_large = pl->large;

@@ -151,6 +151,13 @@ def test_two_stream_split_rules():
     # more than one wave of large slices: waves by the wave size, as before
     many = EdenPlan([1 << 22] * 6, 8, wave_mib=32, streams=2)
     assert many.n_waves == 3
+    # ... packed largest first, so every wave holds one slice size (batch
+    # order would give [2^22] [2^23] [2^22] [2^23] [2^22 2^22]): one column
+    # launch per wave
+    mixed = EdenPlan([1 << 22, 1 << 23, 1 << 22, 1 << 23, 1 << 22, 1 << 22], 8, wave_mib=32, streams=1)
+    assert mixed.n_waves == 4
+    cols = [l["name"] for l in mixed.launches(True) if "col" in l["name"]]
+    assert len(cols) == 4 and cols.count("ofl::k_col6<8, true, 15>") == 2
 
 
 def test_small_set_launch():
