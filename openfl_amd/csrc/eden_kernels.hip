@@ -2761,11 +2761,12 @@ bool use_two_waves() {
     return on;
 }
 // multi-wave plans pack their large slices largest first (OFL_EDEN_WAVESORT=0:
-// in batch order; profiles/r06_sort_roll_ab.txt)
-bool use_wave_sort() {
-    static const bool on = [] { const char* s = getenv("OFL_EDEN_WAVESORT"); return !(s && s[0] == '0'); }();
-    return on;
+// in batch order, =2: smallest first; profiles/r06_sort_roll_ab.txt)
+int wave_sort_mode() {
+    static const int m = [] { const char* s = getenv("OFL_EDEN_WAVESORT"); return (s && *s) ? (int)(s[0] - '0') : 1; }();
+    return m;
 }
+bool use_wave_sort() { return wave_sort_mode() != 0; }
 // column launches find their tile in a per-block table (OFL_EDEN_BTAB=0:
 // binary search over the launch's tile prefix, as before)
 bool use_btab() {
@@ -3136,8 +3137,10 @@ void build_schedule(ofl_eden_plan* pl) {
     std::vector<int32_t> sorted_large;
     if (tot > cap && use_wave_sort()) {
         sorted_large = pl->large;
-        std::stable_sort(sorted_large.begin(), sorted_large.end(),
-                         [&](int32_t x, int32_t y) { return pl->slices[x].logp > pl->slices[y].logp; });
+        const bool up = wave_sort_mode() == 2;
+        std::stable_sort(sorted_large.begin(), sorted_large.end(), [&](int32_t x, int32_t y) {
+            return up ? pl->slices[x].logp < pl->slices[y].logp : pl->slices[x].logp > pl->slices[y].logp;
+        });
     }
     const std::vector<int32_t>& large = sorted_large.empty() ? pl->large : sorted_large;
     // two streams: at least two waves, so both streams have work -- unless
