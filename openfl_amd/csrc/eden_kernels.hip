@@ -113,7 +113,9 @@ struct KArgs {
     int32_t sset_first;
     // paired row launches (k_enc_rowA2<false> / k_dec_rowC2, row_locate):
     // btab holds npair entries {slice, tile << 3 | pair}; pair = 1: the block
-    // also runs tile + 2^(p-18), whose D1 words are the same (0: tstart)
+    // also runs tile + 2^(p-18), whose D1 words are the same (0: tstart).
+    // The two-blocks-per-CU row kernels all take such a list (pair bits 0
+    // but in those two) for a split 5-pass slice's sub-waves
     int32_t npair;
 };
 
@@ -2088,7 +2090,7 @@ __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowC2(KArgs a) {
     const uint32_t tid = threadIdx.x;
     load_qtable<kRowNT>(qt, a.nbits);
     __syncthreads();
-    const int total = (int)sld(a.tstart, a.count);
+    const int total = a.npair ? a.npair : (int)sld(a.tstart, a.count);  // npair: an explicit tile list
     const uint32_t base3 = LT<R::L3>::base(tid), base5 = LT<R::L5>::base(tid);
     auto locate = [&](int t, int& si, uint32_t& tile) { row_locate(a, t, si, tile); };
     int t = (int)blockIdx.x;
@@ -2394,7 +2396,7 @@ __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowA2(KArgs a) {
     float* s = reinterpret_cast<float*>(smem);
     float* red = reinterpret_cast<float*>(smem + kRowC2Ex);
     uint32_t* stash = reinterpret_cast<uint32_t*>(smem + kRow2Stash);
-    const int total = !WAVG && a.npair ? a.npair : (int)sld(a.tstart, a.count);
+    const int total = a.npair ? a.npair : (int)sld(a.tstart, a.count);
     for (int t = (int)blockIdx.x; t < total; t += (int)gridDim.x) {
       // a pair: this tile, then the one a nibble up (apply_signs_pair); the
       // entry is re-read per tile (scalar loads: few SGPRs live across tiles)
@@ -2454,7 +2456,7 @@ __global__ __launch_bounds__(kRowNT, 4) void k_dec_rowA2(KArgs a) {
     float* cen = reinterpret_cast<float*>(smem + kRowC2Ex);
     if (threadIdx.x < 256) cen[threadIdx.x] = g_centroids[a.nbits - 1][threadIdx.x];
     __syncthreads();
-    const int total = (int)sld(a.tstart, a.count);
+    const int total = a.npair ? a.npair : (int)sld(a.tstart, a.count);  // npair: an explicit tile list
     for (int t = (int)blockIdx.x; t < total; t += (int)gridDim.x) {
         const uint32_t tid = opaque(threadIdx.x);  // as in k_enc_rowA2
         const uint32_t base1 = LT<R::C1>::base(tid), base3 = LT<R::C3>::base(tid);
@@ -2572,6 +2574,11 @@ struct Launch {
     int btab_off = -1;  // column: per-block {slice, tile << 3 | group} table in ints
     int ptab_off = -1;  // row: the paired table {slice, tile << 3 | pair} in ints (npair entries)
     int npair = 0;
+    // a sub-wave launch of a split 5-pass slice (build_schedule): it covers
+    // expl_tiles tiles listed in btab_off ({slice, tile << 3}); row launches
+    // that apply D1 may take the paired list ptab_off (npair entries) instead
+    bool expl = false;
+    int64_t expl_tiles = 0;
     int sset_off = -1;  // K_COLMSET: the small-set group table in ints
     int sset_groups = 0;  // K_COLMSET: its groups (the launch's first blocks)
     int64_t bytes_moved = 0;  // fp32/plane bytes this launch reads + writes (intermediates included)
@@ -2760,6 +2767,12 @@ bool use_two_waves() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_TWOWAVES"); return !(s && s[0] == '0'); }();
     return on;
 }
+// 5-pass slices bigger than a wave run their first two and last two passes
+// in MALL-sized sub-waves (OFL_EDEN_BIGSPLIT=0: whole-slice passes)
+bool use_big_split() {
+    static const bool on = [] { const char* s = getenv("OFL_EDEN_BIGSPLIT"); return !(s && s[0] == '0'); }();
+    return on;
+}
 // multi-wave plans pack their large slices largest first (OFL_EDEN_WAVESORT=0:
 // in batch order, =2: smallest first; profiles/r06_sort_roll_ab.txt)
 int wave_sort_mode() {
@@ -2934,6 +2947,17 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
         }
         case K_ROWA: {
             const bool a8 = l.mid && (reinterpret_cast<uintptr_t>(base.pin) & 7u) == 0;
+            if (l.expl) {  // a sub-wave of a split 5-pass slice: its tile list
+                const bool paired = enc && !base.wx && l.ptab_off >= 0;
+                a.btab = pl->d_ints + (paired ? l.ptab_off : l.btab_off);
+                a.npair = paired ? l.npair : (int)l.expl_tiles;
+                const int64_t g2 = std::min<int64_t>(a.npair, 2 * pl->ncu);
+                e = enc ? (base.wx ? launch(ofl::k_enc_rowA2<true>, g2, ofl::kRowNT, ofl::kRow2Smem, st, a)
+                                   : launch(ofl::k_enc_rowA2<false>, g2, ofl::kRowNT, ofl::kRow2Smem, st, a))
+                        : a8 ? launch(ofl::k_dec_rowA2<true>, g2, ofl::kRowNT, ofl::kRow2SmemC, st, a)
+                             : launch(ofl::k_dec_rowA2<false>, g2, ofl::kRowNT, ofl::kRow2SmemC, st, a);
+                break;
+            }
             if (enc && base.wx) {  // fused round-end encode: x = the weighted-average delta
                 e = launch(ofl::k_enc_rowA2<true>, std::min<int64_t>(l.blocks, 2 * pl->ncu), ofl::kRowNT, ofl::kRow2Smem,
                            st, a);
@@ -2959,6 +2983,16 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
         }
         case K_ROWC: {
             const int64_t g = std::min<int64_t>(l.blocks, pl->ncu);
+            if (l.expl) {  // a sub-wave of a split 5-pass slice: its tile list
+                const bool paired = !enc && l.ptab_off >= 0;
+                a.btab = pl->d_ints + (paired ? l.ptab_off : l.btab_off);
+                a.npair = paired ? l.npair : (int)l.expl_tiles;
+                const int64_t g2 = std::min<int64_t>(a.npair, 2 * pl->ncu);
+                e = !enc ? launch(ofl::k_dec_rowC2, g2, ofl::kRowNT, ofl::kRow2Smem, st, a)
+                    : use_roll() ? launch(ofl::k_enc_rowC2<true>, g2, ofl::kRowNT, ofl::kRowC2Smem, st, a)
+                                 : launch(ofl::k_enc_rowC2<false>, g2, ofl::kRowNT, ofl::kRowC2Smem, st, a);
+                break;
+            }
             if (enc && use_rowc2())
                 e = use_roll() ? launch(ofl::k_enc_rowC2<true>, std::min<int64_t>(l.blocks, 2 * pl->ncu), ofl::kRowNT,
                                         ofl::kRowC2Smem, st, a)
@@ -3238,6 +3272,86 @@ void build_schedule(ofl_eden_plan* pl) {
         int64_t rows = 0;
         const int lo_l = add_list(wl);
         const int rp = add_prefix(wl, ofl::kRowLog, rows);
+        // A 5-pass slice bigger than the wave size (its own wave): passes 1-2
+        // (row bits 0..14, column level 1 bits 15..15+m1-1) touch only a
+        // sub-block of 2^(15+m1) consecutive elements, and so do passes 4-5,
+        // so they run sub-wave by sub-wave (half a wave of nibble-even tiles
+        // and their pair partners 2^(p-18) tiles up), each sub-wave's two
+        // passes back to back while its intermediate sits in the MALL; the
+        // middle pass (column level 2 + D2) spans the slice and runs whole,
+        // writing the slice norm (it follows every row-A sub-wave).  Launches
+        // of one stream run in order, so no other synchronisation.
+        if (wl.size() == 1 && cap != INT64_MAX && use_big_split() && use_rowc2() && use_btab() &&
+            pl->slices[wl[0]].logp - ofl::kRowLog >= 11) {
+            const int32_t si = wl[0];
+            const int p = pl->slices[si].logp, r = p - ofl::kRowLog, m1 = r / 2, m2 = r - m1;
+            const int64_t ntile = 1ll << r, sub = 1ll << m1, P = 1ll << (p - 18);
+            const int64_t cap_t = cap >> ofl::kRowLog;
+            const int64_t half = (cap_t / 2) / sub * sub;
+            if (half >= sub && cap_t < ntile && ntile <= kRowTabMax && use_row2(2 * std::min(half, P), pl->ncu, pl->row2)) {
+                const bool pair = (pl->pair >= 0 ? pl->pair : pair_mode()) != 0;
+                const int lo_c = add_list(wl);
+                int64_t tiles_all = 0;
+                const int tp = add_prefix(wl, ofl::kColLog, tiles_all);
+                struct SubWave { int tab_all, tab_pair; int64_t n_all, n_pair; };
+                std::vector<SubWave> sws;
+                for (int64_t reg = 0; reg < ntile; reg += 2 * P)
+                    for (int64_t c = 0; c < P; c += half) {
+                        const int64_t e = std::min(P, c + half);
+                        SubWave sw;
+                        sw.tab_all = (int)ints.size();
+                        for (int64_t h = 0; h < 2; ++h)
+                            for (int64_t t = reg + c + h * P; t < reg + e + h * P; ++t) {
+                                ints.push_back(si);
+                                ints.push_back((int32_t)(t << 3));
+                            }
+                        sw.n_all = 2 * (e - c);
+                        sw.tab_pair = (int)ints.size();
+                        for (int64_t t = reg + c; t < reg + e; ++t) {
+                            ints.push_back(si);
+                            ints.push_back((int32_t)(t << 3) | 1);
+                        }
+                        sw.n_pair = e - c;
+                        sws.push_back(sw);
+                    }
+                auto rowl = [&](Kind k, const SubWave& sw, bool paired) {
+                    Launch l{k, 0, 0, 0, lo_l, rp, 1, sw.n_all};
+                    l.expl = true;
+                    l.expl_tiles = sw.n_all;
+                    l.btab_off = sw.tab_all;
+                    if (paired) { l.ptab_off = sw.tab_pair; l.npair = (int)sw.n_pair; }
+                    l.stream = s;
+                    return l;
+                };
+                auto coll = [&](const SubWave& sw) {
+                    Launch l{K_COL, m1, ofl::kRowLog, 0, lo_c, tp, 1, sw.n_all};
+                    l.expl = true;
+                    l.expl_tiles = sw.n_all;
+                    l.btab_off = sw.tab_all;
+                    l.stream = s;
+                    return l;
+                };
+                for (int dir = 0; dir < 2; ++dir) {
+                    const bool enc = dir == 1;
+                    std::vector<Launch>& L = enc ? pl->enc : pl->dec;
+                    for (const SubWave& sw : sws) {
+                        Launch ra = rowl(K_ROWA, sw, enc && pair);
+                        if (!enc) ra.mid = a8;
+                        L.push_back(ra);
+                        L.push_back(coll(sw));
+                    }
+                    Launch mid{K_COL, m2, ofl::kRowLog + m1, 1, lo_c, tp, 1, tiles_all};
+                    mid.stream = s;
+                    mid.nu = enc ? 1 : 0;  // after every row-A sub-wave: the slice norm
+                    L.push_back(mid);
+                    for (const SubWave& sw : sws) {
+                        L.push_back(coll(sw));
+                        L.push_back(rowl(K_ROWC, sw, !enc && pair));
+                    }
+                }
+                continue;
+            }
+        }
         std::map<int, std::vector<int32_t>> byp;  // column launches grouped by p
         for (int32_t si : wl) byp[pl->slices[si].logp].push_back(si);
         std::vector<Launch> ce, cd;
@@ -3372,8 +3486,8 @@ void build_schedule(ofl_eden_plan* pl) {
         };
         for (auto* L : {&pl->enc, &pl->dec})
             for (Launch& l : *L)
-                if (l.kind == K_COL || l.kind == K_COLM || l.kind == K_COLMSET ||
-                    ((l.kind == K_ROWA || l.kind == K_ROWC) && l.blocks <= kRowTabMax))
+                if (!l.expl && (l.kind == K_COL || l.kind == K_COLM || l.kind == K_COLMSET ||
+                                ((l.kind == K_ROWA || l.kind == K_ROWC) && l.blocks <= kRowTabMax)))
                     table(l);
         // the sign-applying row launches (encode A, decode C): a paired table,
         // one entry per tile of nibble-even position (its partner follows in
@@ -3403,9 +3517,9 @@ void build_schedule(ofl_eden_plan* pl) {
             ints.insert(ints.end(), t.begin(), t.end());
         };
         for (Launch& l : pl->enc)
-            if (l.kind == K_ROWA && l.tstart_off >= 0 && l.blocks <= kRowTabMax) ptable(l);
+            if (!l.expl && l.kind == K_ROWA && l.tstart_off >= 0 && l.blocks <= kRowTabMax) ptable(l);
         for (Launch& l : pl->dec)
-            if (l.kind == K_ROWC && l.tstart_off >= 0 && l.blocks <= kRowTabMax) ptable(l);
+            if (!l.expl && l.kind == K_ROWC && l.tstart_off >= 0 && l.blocks <= kRowTabMax) ptable(l);
     }
     // per-launch byte accounting (bench / DESIGN.md roofline)
     const int64_t n_bits = pl->nbits;
@@ -3440,6 +3554,10 @@ void build_schedule(ofl_eden_plan* pl) {
                     mv += enc ? 4 * P + pb : 4 * P + 4 * D.ylen; al += enc ? pb : 4 * D.ylen; break;
                 case K_COL: mv += 8 * P; break;
                 default: mv += 4 * (P >> ofl::kRowLog); break;
+                }
+                if (l.expl) {  // a sub-wave: its share of the slice's tiles
+                    mv = mv / (P >> ofl::kRowLog) * l.expl_tiles;
+                    al = al / (P >> ofl::kRowLog) * l.expl_tiles;
                 }
             }
             l.bytes_moved = mv;

@@ -612,13 +612,16 @@ def test_row2_variants_bit_identical():
     interleaved 2^25 layout) and 5-pass slices, ragged tails and decode_add.
     The same with tile pairs (ofl_eden_plan_set_pair: a block hashes the D1
     words of a tile and of the one 2^(p-3) up once), forced on and off, and
-    with 2 MiB waves (every 2^18..2^22 slice in its own paired launch)."""
+    with 2 MiB waves (every 2^18..2^22 slice in its own paired launch); at
+    64 MiB waves the 2^26 slice runs split into MALL sub-waves (passes 1-2
+    and 4-5 per sub-block, explicit tile lists), paired and unpaired."""
     from openfl_amd.codec import EdenPlan
     numels = [(1 << 26) + 777, 1 << 25, (1 << 22) + 12345, (1 << 16) + 5, 3000, (1 << 18) + 3, (1 << 17) + 1,
               (1 << 19) - 7]
     g = torch.Generator(device=DEV).manual_seed(21)
     outs = []
-    for row2, pair, wave in ((0, 0, 4096), (1, 0, 4096), (1, 1, 4096), (1, 1, 2), (-1, -1, 2)):
+    for row2, pair, wave in ((0, 0, 4096), (1, 0, 4096), (1, 1, 4096), (1, 1, 2), (-1, -1, 2), (-1, -1, 64),
+                             (-1, 0, 64)):
         plan = EdenPlan(numels, 8, wave_mib=wave, streams=1, row2=row2, pair=pair)
         x = torch.empty(plan.arena_numel, device=DEV).normal_(0, 0.01, generator=g.manual_seed(21))
         base = torch.empty(plan.arena_numel, device=DEV).normal_(0, 1.0, generator=g.manual_seed(22))
