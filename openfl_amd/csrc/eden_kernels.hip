@@ -2736,6 +2736,13 @@ bool use_col6() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_COL6"); return !(s && s[0] == '0'); }();
     return on;
 }
+// lowest outer (non-middle) column-pass height that runs k_col6
+// (OFL_EDEN_COL6_OUTER, default 8: the 5-pass slices' level-1 passes of
+// heights 5..7 run k_col)
+int col6_outer_min() {
+    static const int v = [] { const char* s = getenv("OFL_EDEN_COL6_OUTER"); return (s && *s) ? atoi(s) : 8; }();
+    return v;
+}
 // interleaved ws layout for 2^25 slices (256-B segments in the middle pass)
 bool use_perm25() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_PERM25"); return !(s && s[0] == '0'); }();
@@ -2771,6 +2778,10 @@ bool use_two_waves() {
 // in MALL-sized sub-waves (OFL_EDEN_BIGSPLIT=0: whole-slice passes)
 bool use_big_split() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_BIGSPLIT"); return !(s && s[0] == '0'); }();
+    return on;
+}
+bool big_last() {
+    static const bool on = [] { const char* s = getenv("OFL_EDEN_BIGLAST"); return s && s[0] == '1'; }();
     return on;
 }
 // multi-wave plans pack their large slices largest first (OFL_EDEN_WAVESORT=0:
@@ -2829,6 +2840,10 @@ bool use_colm6() {
 // lowest middle-pass height that runs k_col6 (7 when height 6 runs col_body<6>:
 // a standalone height-6 launch then uses k_col<6, true> too)
 int col6_mid_min() { return use_colm6() ? 7 : 6; }
+// k_col6 (else k_col) for a column pass of this height
+bool col6_for(int param, bool mid) {
+    return (param >= 8 || (mid ? param >= col6_mid_min() : param >= col6_outer_min())) && param >= 6 && use_col6();
+}
 // one k_col_multi launch per wave for the single-level heights 1..5 (6)
 bool use_colmulti() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_COLMULTI"); return !(s && s[0] == '0'); }();
@@ -3021,7 +3036,7 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
                                           : launch(ofl::k_col6<10, false, 16>, l.blocks, 1024, sm, st, a));
                 break;
             }
-            if ((l.param >= 8 || (l.param >= col6_mid_min() && l.mid)) && use_col6()) {
+            if (col6_for(l.param, l.mid != 0)) {
                 const size_t sm = col6_smem(l.param, l.mid != 0, 15);
 #define COL6CASE(MM)                                                                                 \
     case MM:                                                                                         \
@@ -3089,9 +3104,9 @@ std::string launch_name(const Launch& l, bool enc, int ncu, int row2) {
         return std::string("ofl::k_") + d + "_rowC";
     case K_COL:
         if (l.tl == 16) return "ofl::k_col6<" + std::to_string(l.param) + ", " + (l.mid ? "true" : "false") + ", 16>";
-        return std::string((l.param >= 8 || (l.param >= col6_mid_min() && l.mid)) && use_col6() ? "ofl::k_col6<" : "ofl::k_col<") +
+        return std::string(col6_for(l.param, l.mid != 0) ? "ofl::k_col6<" : "ofl::k_col<") +
                std::to_string(l.param) + ", " + (l.mid ? "true" : "false") +
-               ((l.param >= 8 || (l.param >= col6_mid_min() && l.mid)) && use_col6() ? ", 15>" : ">");
+               (col6_for(l.param, l.mid != 0) ? ", 15>" : ">");
     case K_COLM: return "ofl::k_col_multi";
     case K_COLMSET: return std::string("ofl::k_") + d + "_colm_set";
     default: return "ofl::k_finalize";
@@ -3210,6 +3225,18 @@ void build_schedule(ofl_eden_plan* pl) {
         waves.back().push_back(si);
         acc += P;
         wmax = std::max(wmax, acc);
+    }
+    // OFL_EDEN_BIGLAST=1 (A/B): when the first two waves are both 5-pass
+    // slices (largest first on two streams: both at once), the second one
+    // moves to the end of its stream, so each runs beside the other stream's
+    // MALL-sized waves instead of beside the other's HBM-bound middle pass
+    if (big_last() && pl->nstreams == 2 && waves.size() >= 4 && waves[0].size() == 1 && waves[1].size() == 1 &&
+        pl->slices[waves[1][0]].logp - ofl::kRowLog >= 11) {
+        std::vector<int32_t> b = waves[1];
+        waves.erase(waves.begin() + 1);
+        // keep it on stream 1 (odd index)
+        const size_t at = waves.size() % 2 == 1 ? waves.size() : waves.size() - 1;
+        waves.insert(waves.begin() + (ptrdiff_t)at, b);
     }
     pl->nwaves = (int)waves.size();
     const int nbuf = waves.size() > 1 ? pl->nstreams : 1;
