@@ -2780,10 +2780,6 @@ bool use_big_split() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_BIGSPLIT"); return !(s && s[0] == '0'); }();
     return on;
 }
-bool big_last() {
-    static const bool on = [] { const char* s = getenv("OFL_EDEN_BIGLAST"); return s && s[0] == '1'; }();
-    return on;
-}
 // multi-wave plans pack their large slices largest first (OFL_EDEN_WAVESORT=0:
 // in batch order, =2: smallest first; profiles/r06_sort_roll_ab.txt)
 int wave_sort_mode() {
@@ -3225,18 +3221,6 @@ void build_schedule(ofl_eden_plan* pl) {
         waves.back().push_back(si);
         acc += P;
         wmax = std::max(wmax, acc);
-    }
-    // OFL_EDEN_BIGLAST=1 (A/B): when the first two waves are both 5-pass
-    // slices (largest first on two streams: both at once), the second one
-    // moves to the end of its stream, so each runs beside the other stream's
-    // MALL-sized waves instead of beside the other's HBM-bound middle pass
-    if (big_last() && pl->nstreams == 2 && waves.size() >= 4 && waves[0].size() == 1 && waves[1].size() == 1 &&
-        pl->slices[waves[1][0]].logp - ofl::kRowLog >= 11) {
-        std::vector<int32_t> b = waves[1];
-        waves.erase(waves.begin() + 1);
-        // keep it on stream 1 (odd index)
-        const size_t at = waves.size() % 2 == 1 ? waves.size() : waves.size() - 1;
-        waves.insert(waves.begin() + (ptrdiff_t)at, b);
     }
     pl->nwaves = (int)waves.size();
     const int nbuf = waves.size() > 1 ? pl->nstreams : 1;

@@ -2,7 +2,8 @@
 # r06: k_col6 for the 5-pass slices' level-1 column passes (OFL_EDEN_COL6_OUTER=7:
 # the Llama 2^29 slices' k_col<7, false> sub-wave launches) vs k_col: the
 # five-pass / schedule / row tests with it first, then the Llama step x3;
-# also OFL_EDEN_BIGLAST=1 (the second 2^29 wave at the end of its stream).
+# also OFL_EDEN_BIGLAST=1 (the second 2^29 wave at the end of its stream;
+# removed after this A/B, profiles/r06_col6outer_biglast_ab.txt).
 set -uo pipefail
 R=$PWD; O=$R/gpurun_out/r06_col6outer; mkdir -p $O
 OFL_EDEN_COL6_OUTER=7 OFL_EDEN_BIGLAST=1 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -x --timeout 120 --timeout-method thread -k "five_pass or 2p29 or schedules or row2 or golden or oracle" > $O/pytest.log 2>&1
