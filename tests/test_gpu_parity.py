@@ -792,3 +792,38 @@ def test_concurrent_plugin_calls():
         md = fwd[i][1][0]["int_to_float"]
         ref = tr.eden.decompress(np.frombuffer(fwd[i][0], np.uint8), md)
         np.testing.assert_array_equal(dec[i], ref.reshape(x.shape))
+
+
+def test_wavg_encode_split_bit_identical():
+    """The fused round-end encode (ofl_eden_encode_wavg: x = the weighted-
+    average delta computed in the first row pass) over a 5-pass slice split
+    into MALL sub-waves (64 MiB waves: the row-A sub-waves take explicit tile
+    lists, unpaired in this kernel) gives the same planes and scales as the
+    whole-slice schedule."""
+    import ctypes
+    from openfl_amd import _lib
+    from openfl_amd.codec import EdenPlan
+    numels = [(1 << 26) + 777, 3000, (1 << 20) + 5]
+    g = torch.Generator(device=DEV).manual_seed(41)
+    L = _lib.lib()
+    outs = []
+    for wave in (4096, 64):
+        plan = EdenPlan(numels, 8, wave_mib=wave, streams=2)
+        if not outs:
+            xs = [torch.empty(plan.arena_numel, device=DEV).normal_(0, 0.01, generator=g) for _ in range(2)]
+            base = torch.empty(plan.arena_numel, device=DEV).normal_(0, 0.1, generator=g)
+            delta = torch.empty(plan.arena_numel, device=DEV).normal_(0, 0.01, generator=g)
+        ptrs = torch.tensor([x.data_ptr() for x in xs], dtype=torch.int64, device=DEV)
+        w = torch.tensor([0.3, 0.7], dtype=torch.float64, device=DEV)
+        seeds = torch.tensor([11, 12, 13], dtype=torch.int32, device=DEV)
+        ws = torch.empty(max(plan.ws_bytes, 256), dtype=torch.uint8, device=DEV)
+        p = torch.full((plan.planes_bytes,), 0x5A, dtype=torch.uint8, device=DEV)
+        s = torch.zeros(plan.n_slices, dtype=torch.float32, device=DEV)
+        _lib.check(L.ofl_eden_encode_wavg(plan.handle, ptrs.data_ptr(), w.data_ptr(), 2, ctypes.c_double(1.0),
+                                          base.data_ptr(), delta.data_ptr(), seeds.data_ptr(), p.data_ptr(),
+                                          s.data_ptr(), ws.data_ptr(), ws.numel(), None))
+        torch.cuda.synchronize()
+        outs.append((p.cpu(), s.cpu()))
+        del ws, p, s
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
