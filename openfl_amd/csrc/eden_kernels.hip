@@ -58,6 +58,14 @@
 
 #define DEVI __device__ __forceinline__
 
+// cache policy of the large slices' arena I/O (kIoLdAux / kIoStAux below)
+#ifndef OFL_IO_LD_AUX
+#define OFL_IO_LD_AUX 0
+#endif
+#ifndef OFL_IO_ST_AUX
+#define OFL_IO_ST_AUX 0
+#endif
+
 namespace ofl {
 
 // ---------------------------------------------------------------------------
@@ -518,7 +526,8 @@ DEVI void load_planes64(const uint8_t* plane0, uint32_t e, int64_t stride, int n
 
 DEVI void store_plane_word(uint8_t* p, uint32_t w) {
     if ((reinterpret_cast<uintptr_t>(p) & 3u) == 0) {
-        *reinterpret_cast<uint32_t*>(p) = w;
+        if constexpr ((OFL_IO_ST_AUX & 2) != 0) __builtin_nontemporal_store(w, reinterpret_cast<uint32_t*>(p));
+        else *reinterpret_cast<uint32_t*>(p) = w;
     } else {
         p[0] = (uint8_t)w; p[1] = (uint8_t)(w >> 8); p[2] = (uint8_t)(w >> 16); p[3] = (uint8_t)(w >> 24);
     }
@@ -1161,6 +1170,11 @@ __device__ void raw_store_f32(float v, rsrc_t r, int voff, int soff, int aux) __
 #endif
 constexpr int kLdAux = OFL_LD_AUX;
 constexpr int kStAux = OFL_ST_AUX;
+// ... of the large slices' once-read / once-written arena I/O (x loads, y
+// stores and the yadd loads, bit-plane loads and stores), separately from
+// the intermediates', which MALL-sized waves re-read from the cache
+constexpr int kIoLdAux = OFL_IO_LD_AUX;
+constexpr int kIoStAux = OFL_IO_ST_AUX;
 
 // Ladder builds (diagnostics only, WRONG results; tools/r06_ladder.sh):
 // -DOFL_LADDER=1 the large-slice passes keep only their tile loads and
@@ -1279,12 +1293,12 @@ DEVI uint32_t tile_valid(int64_t len) {
     return len <= 0 ? 0u : (len >= (1 << kRowLog) ? (1u << kRowLog) : (uint32_t)len);
 }
 DEVI float4 bload4(rsrc_t r, uint32_t e, uint32_t k) {
-    const f32x4 q = raw_load_f32x4(r, (int)(e * 4u), (int)(k * 4u), kLdAux);
+    const f32x4 q = raw_load_f32x4(r, (int)(e * 4u), (int)(k * 4u), kIoLdAux);
     return make_float4(q.x, q.y, q.z, q.w);
 }
 DEVI void bstore4(rsrc_t r, uint32_t e, uint32_t k, const float* v) {
     const f32x4 q = {v[0], v[1], v[2], v[3]};
-    raw_store_f32x4(q, r, (int)(e * 4u), (int)(k * 4u), kStAux);
+    raw_store_f32x4(q, r, (int)(e * 4u), (int)(k * 4u), kIoStAux);
 }
 
 // x tile (L1 layout, float4 per register quad); live = false reads nothing
@@ -1437,7 +1451,7 @@ DEVI void fetch_planes(const KArgs& a, const SliceDesc& D, uint32_t tile, bool l
     for (int i = 0; i < 8; ++i) {
         const rsrc_t r = mk_rsrc(p0 + (int64_t)i * D.pl_stride, (live && i < a.nbits) ? (1u << (kRowLog - 3)) : 0u);
         if (A8) {
-            const i32x2 q = raw_load_i32x2(r, (int)(base5 >> 3), 0, kLdAux);
+            const i32x2 q = raw_load_i32x2(r, (int)(base5 >> 3), 0, kIoLdAux);
             w[i] = (uint64_t)(uint32_t)q.x | ((uint64_t)(uint32_t)q.y << 32);
         } else {
             uint64_t x = 0;
