@@ -58,12 +58,16 @@
 
 #define DEVI __device__ __forceinline__
 
-// cache policy of the large slices' arena I/O (kIoLdAux / kIoStAux below)
+// cache policy of the large slices' arena I/O (kIoLdAux / kIoStAux below):
+// nt both ways -- at MALL-sized waves the streamed x / y / plane bytes then
+// do not push a wave's intermediates out of the Infinity Cache (Llama-3-8B
+// 444-447 -> 471-472 GiB/s, the 1 GiB set 473-475 -> 508-509,
+// profiles/r06_io_nt_ab.txt)
 #ifndef OFL_IO_LD_AUX
-#define OFL_IO_LD_AUX 0
+#define OFL_IO_LD_AUX 2
 #endif
 #ifndef OFL_IO_ST_AUX
-#define OFL_IO_ST_AUX 0
+#define OFL_IO_ST_AUX 2
 #endif
 
 namespace ofl {
@@ -1174,6 +1178,11 @@ constexpr int kStAux = OFL_ST_AUX;
 // stores and the yadd loads, bit-plane loads and stores), separately from
 // the intermediates', which MALL-sized waves re-read from the cache
 constexpr int kIoLdAux = OFL_IO_LD_AUX;
+// k_dec_rowC2's intermediate loads: the decode's last read of a wave's ws
+#ifndef OFL_DECC2_LD_AUX
+#define OFL_DECC2_LD_AUX 0
+#endif
+constexpr int kDecC2LdAux = OFL_DECC2_LD_AUX;
 constexpr int kIoStAux = OFL_IO_ST_AUX;
 
 // Ladder builds (diagnostics only, WRONG results; tools/r06_ladder.sh):
@@ -1409,7 +1418,8 @@ DEVI void store_ws(const KArgs& a, const SliceDesc& D, uint32_t tile, uint32_t b
 #endif
 constexpr bool kRowWs4 = OFL_ROW_WS4 != 0;
 template <Lay L>
-DEVI void fetch_ws4(const KArgs& a, const SliceDesc& D, uint32_t tile, bool live, uint32_t base, float (&v)[64]) {
+DEVI void fetch_ws4(const KArgs& a, const SliceDesc& D, uint32_t tile, bool live, uint32_t base, float (&v)[64],
+                    int aux = kLdAux) {
     static_assert(LT<L>::rb(0) == 0 && LT<L>::rb(1) == 1, "float4 loads need element bits 0, 1 in registers 0, 1");
     const bool perm = D.perm;
     const WsR r = ws_row(a, D, tile, live ? (perm ? (4u << (kRowLog + 1)) - 128u : 4u << kRowLog) : 0u);
@@ -1417,7 +1427,7 @@ DEVI void fetch_ws4(const KArgs& a, const SliceDesc& D, uint32_t tile, bool live
 #pragma unroll
     for (int k = 0; k < 64; k += 4) {
         const uint32_t o = LT<L>::off(k);
-        const f32x4 f = ws_ld4(r, b * 4u, (perm ? ws_row_idx(o) : o) * 4u, kLdAux);
+        const f32x4 f = ws_ld4(r, b * 4u, (perm ? ws_row_idx(o) : o) * 4u, aux);
         v[k] = f.x; v[k + 1] = f.y; v[k + 2] = f.z; v[k + 3] = f.w;
     }
 }
@@ -2509,7 +2519,7 @@ __global__ __launch_bounds__(kRowNT, 4) void k_dec_rowC2(KArgs a) {
         const uint32_t base1 = LT<R::B1>::base(tid), base4 = LT<R::B4>::base(tid);
         const uint32_t tile = h ? tile0 + (1u << (D.logp - 18)) : tile0;
         float v[64];
-        if constexpr (kRowWs4) fetch_ws4<R::B1>(a, D, tile, true, base1, v);
+        if constexpr (kRowWs4) fetch_ws4<R::B1>(a, D, tile, true, base1, v, kDecC2LdAux);
         else fetch_ws(a, D, tile, true, base1, v);
         const uint32_t b1 = seed_b(sld(a.seeds, D.tensor));
         if constexpr (kLadFly) {
