@@ -1910,9 +1910,13 @@ DEVI void exchange_half(float (&v)[64], float* s, uint32_t tid) {
     }
 }
 
-template <int M, bool MID, int TL>
+// NTA: the pass streams its intermediate through HBM (the middle pass of a
+// split 5-pass slice): nt loads and stores, so it does not evict the other
+// stream's MALL-resident waves
+template <int M, bool MID, int TL, bool NTA = false>
 __global__ __launch_bounds__(col6_nt<TL>(), 4) void k_col6(KArgs a) {
     using CS = Col6Set<M, TL>;
+    constexpr int kLd = NTA ? 2 : kLdAux, kSt = NTA ? 2 : kStAux;
     constexpr int NT = col6_nt<TL>();
     constexpr int K = CS::K;
     constexpr bool EXCH = M > 6;
@@ -1950,12 +1954,12 @@ __global__ __launch_bounds__(col6_nt<TL>(), 4) void k_col6(KArgs a) {
         const uint32_t vo = opaque(ws_pos(map(base1)) * 4u);
 #pragma unroll
         for (int r = 0; r < 64; ++r)
-            v[r] = ws_ld1(rw, vo, ws_pos((LT<CS::L1>::off(r) >> K) << 15) * 4u, kLdAux);
+            v[r] = ws_ld1(rw, vo, ws_pos((LT<CS::L1>::off(r) >> K) << 15) * 4u, kLd);
     } else {
         const uint32_t vo = opaque(map(base1) * 4u);
 #pragma unroll
         for (int r = 0; r < 64; ++r)
-            v[r] = ws_ld1(rw, vo, uu((LT<CS::L1>::off(r) >> K) << lo) * 4u, kLdAux);
+            v[r] = ws_ld1(rw, vo, uu((LT<CS::L1>::off(r) >> K) << lo) * 4u, kLd);
     }
     if constexpr (kLadFly) stages<CS::L1, CS::A1>(v);
     if constexpr (EXCH && kLadFly) {
@@ -1987,14 +1991,14 @@ __global__ __launch_bounds__(col6_nt<TL>(), 4) void k_col6(KArgs a) {
             const uint32_t vo = opaque(ws_pos(map(base1)) * 4u);
 #pragma unroll
             for (int r = 0; r < 64; ++r)
-                ws_st1(rw, vo, ws_pos((LT<CS::L1>::off(r) >> K) << 15) * 4u, v[r], kStAux);
+                ws_st1(rw, vo, ws_pos((LT<CS::L1>::off(r) >> K) << 15) * 4u, v[r], kSt);
         } else {
             const uint32_t vo = opaque(map(base1) * 4u);
             int los = lo;
             asm volatile("" : "+s"(los));  // recompute the row offsets: 64 SGPRs kept live would spill
 #pragma unroll
             for (int r = 0; r < 64; ++r)
-                ws_st1(rw, vo, uu((LT<CS::L1>::off(r) >> K) << los) * 4u, v[r], kStAux);
+                ws_st1(rw, vo, uu((LT<CS::L1>::off(r) >> K) << los) * 4u, v[r], kSt);
         }
     } else {
         const uint32_t bcw = LT<LC>::base(tid);
@@ -2003,7 +2007,7 @@ __global__ __launch_bounds__(col6_nt<TL>(), 4) void k_col6(KArgs a) {
         asm volatile("" : "+s"(los));
 #pragma unroll
         for (int r = 0; r < 64; ++r)
-            ws_st1(rw, vo, uu((LT<LC>::off(r) >> K) << los) * 4u, v[r], kStAux);
+            ws_st1(rw, vo, uu((LT<LC>::off(r) >> K) << los) * 4u, v[r], kSt);
     }
     if (a.do_nu && tile == 0) {  // slice norm, as in k_col
         __shared__ float nred[NT / 64];
@@ -2603,6 +2607,7 @@ struct Launch {
     // that apply D1 may take the paired list ptab_off (npair entries) instead
     bool expl = false;
     int64_t expl_tiles = 0;
+    bool nt = false;  // column: the intermediate streams through HBM (k_col6<..., true>)
     int sset_off = -1;  // K_COLMSET: the small-set group table in ints
     int sset_groups = 0;  // K_COLMSET: its groups (the launch's first blocks)
     int64_t bytes_moved = 0;  // fp32/plane bytes this launch reads + writes (intermediates included)
@@ -2798,6 +2803,12 @@ bool use_two_waves() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_TWOWAVES"); return !(s && s[0] == '0'); }();
     return on;
 }
+// the whole-slice middle pass of a split 5-pass slice streams its
+// intermediate with nt loads and stores (OFL_EDEN_MIDNT=0: default policy)
+bool use_mid_nt() {
+    static const bool on = [] { const char* s = getenv("OFL_EDEN_MIDNT"); return !(s && s[0] == '0'); }();
+    return on;
+}
 // 5-pass slices bigger than a wave run their first two and last two passes
 // in MALL-sized sub-waves (OFL_EDEN_BIGSPLIT=0: whole-slice passes)
 bool use_big_split() {
@@ -2904,6 +2915,7 @@ hipError_t set_all_attrs() {
     if ((e = set_col6_attr<8, 15>()) != hipSuccess) return e;
     if ((e = set_col6_attr<9, 15>()) != hipSuccess) return e;
     if ((e = set_col6_attr<10, 15>()) != hipSuccess) return e;
+    if ((e = set_lds((const void*)ofl::k_col6<7, true, 15, true>, col6_smem(7, true, 15))) != hipSuccess) return e;
     if ((e = set_col6_attr<9, 16>()) != hipSuccess) return e;
     return set_col6_attr<10, 16>();
 }
@@ -3054,6 +3066,10 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
                                           : launch(ofl::k_col6<9, false, 16>, l.blocks, 1024, sm, st, a))
                                  : (l.mid ? launch(ofl::k_col6<10, true, 16>, l.blocks, 1024, sm, st, a)
                                           : launch(ofl::k_col6<10, false, 16>, l.blocks, 1024, sm, st, a));
+                break;
+            }
+            if (l.nt && l.param == 7 && l.mid && col6_for(7, true)) {
+                e = launch(ofl::k_col6<7, true, 15, true>, l.blocks, 512, col6_smem(7, true, 15), st, a);
                 break;
             }
             if (col6_for(l.param, l.mid != 0)) {
@@ -3377,6 +3393,7 @@ void build_schedule(ofl_eden_plan* pl) {
                     }
                     Launch mid{K_COL, m2, ofl::kRowLog + m1, 1, lo_c, tp, 1, tiles_all};
                     mid.stream = s;
+                    mid.nt = use_mid_nt() && m2 == 7;
                     mid.nu = enc ? 1 : 0;  // after every row-A sub-wave: the slice norm
                     L.push_back(mid);
                     for (const SubWave& sw : sws) {
