@@ -1284,18 +1284,14 @@ DEVI void ws_st4(const WsR& w, uint32_t vo, uint32_t so, f32x4 q, int aux) {
                       w.l, (int)(vo >> 2), (int)(so >> 2), aux);
 }
 // element i of a slice's intermediate through a plain pointer (k_col)
-template <bool NT = false>
 DEVI float ws_pld(const float* sw, int logp, uint32_t i) {
-    if constexpr (kWsFmt == 32 && NT) return __builtin_nontemporal_load(&sw[i]);
     if constexpr (kWsFmt == 32) return sw[i];
     const uint8_t* b = reinterpret_cast<const uint8_t*>(sw);
     uint32_t u = (uint32_t)reinterpret_cast<const uint16_t*>(b)[i] << 16;
     if constexpr (kWsFmt == 24) u |= (uint32_t)b[(2ull << logp) + i] << 8;
     return __uint_as_float(u);
 }
-template <bool NT = false>
 DEVI void ws_pst(float* sw, int logp, uint32_t i, float v) {
-    if constexpr (kWsFmt == 32 && NT) { __builtin_nontemporal_store(v, &sw[i]); return; }
     if constexpr (kWsFmt == 32) { sw[i] = v; return; }
     uint8_t* b = reinterpret_cast<uint8_t*>(sw);
     const uint32_t u = __float_as_uint(v);
@@ -1709,11 +1705,7 @@ template <int M> struct ColSet {
 // LDS (bit k of byte = sign of element k*S + j).  M < 3 hashes per element.
 constexpr size_t kColTab = 4096;
 
-// NTL / NTS: nt intermediate loads / stores (the outer column passes of a
-// split 5-pass slice: level 1 before the middle pass stores what the middle
-// pass reads from HBM much later; level 1 after it loads the middle pass's
-// output from HBM)
-template <int M, bool MID, bool NTL = false, bool NTS = false>
+template <int M, bool MID>
 DEVI void col_body(const KArgs& a, int b) {
     using CS = ColSet<M>;
     constexpr int K = CS::K;
@@ -1744,7 +1736,7 @@ DEVI void col_body(const KArgs& a, int b) {
     float v[32];
     const uint32_t base1 = LT<CS::L1>::base(tid);
 #pragma unroll
-    for (int r = 0; r < 32; ++r) v[r] = ws_pld<NTL>(w, lgp, map(base1 | LT<CS::L1>::off(r)));
+    for (int r = 0; r < 32; ++r) v[r] = ws_pld(w, lgp, map(base1 | LT<CS::L1>::off(r)));
     stages<CS::L1, CS::A1>(v);
     if constexpr (M > 5) {
         exchange<CS::L1, CS::L2>(v, s, tid);  // its barriers also publish tab
@@ -1782,16 +1774,16 @@ DEVI void col_body(const KArgs& a, int b) {
         }
         const uint32_t base1w = opaque(base1);
 #pragma unroll
-        for (int r = 0; r < 32; ++r) ws_pst<NTS>(w, lgp, map(base1w | LT<CS::L1>::off(r)), v[r]);
+        for (int r = 0; r < 32; ++r) ws_pst(w, lgp, map(base1w | LT<CS::L1>::off(r)), v[r]);
     } else {
         if constexpr (M > 5) {
             const uint32_t base2 = opaque(LT<CS::L2>::base(tid));
 #pragma unroll
-            for (int r = 0; r < 32; ++r) ws_pst<NTS>(w, lgp, map(base2 | LT<CS::L2>::off(r)), v[r]);
+            for (int r = 0; r < 32; ++r) ws_pst(w, lgp, map(base2 | LT<CS::L2>::off(r)), v[r]);
         } else {
             const uint32_t base1w = opaque(base1);
 #pragma unroll
-            for (int r = 0; r < 32; ++r) ws_pst<NTS>(w, lgp, map(base1w | LT<CS::L1>::off(r)), v[r]);
+            for (int r = 0; r < 32; ++r) ws_pst(w, lgp, map(base1w | LT<CS::L1>::off(r)), v[r]);
         }
     }
     // The slice norm nu = sqrt(sum of the row pass's partials of x^2)
@@ -1807,9 +1799,9 @@ DEVI void col_body(const KArgs& a, int b) {
         if (tid == 0) a.nu[si] = sqrtf(ss);
     }
 }
-template <int M, bool MID, bool NTL = false, bool NTS = false>
+template <int M, bool MID>
 __global__ __launch_bounds__(kColNT) void k_col(KArgs a) {
-    col_body<M, MID, NTL, NTS>(a, (int)blockIdx.x);
+    col_body<M, MID>(a, (int)blockIdx.x);
 }
 
 // Several single-level middle passes (heights M = 1..6) in one launch: a
@@ -2616,7 +2608,6 @@ struct Launch {
     bool expl = false;
     int64_t expl_tiles = 0;
     bool nt = false;  // column: the intermediate streams through HBM (k_col6<..., true>)
-    bool ntl = false, nts = false;  // column (k_col): nt intermediate loads / stores
     int sset_off = -1;  // K_COLMSET: the small-set group table in ints
     int sset_groups = 0;  // K_COLMSET: its groups (the launch's first blocks)
     int64_t bytes_moved = 0;  // fp32/plane bytes this launch reads + writes (intermediates included)
@@ -2818,12 +2809,6 @@ bool use_mid_nt() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_MIDNT"); return !(s && s[0] == '0'); }();
     return on;
 }
-// ... and its outer column passes stream the HBM side of their intermediate
-// nt (OFL_EDEN_OUTERNT=0: default policy)
-bool use_outer_nt() {
-    static const bool on = [] { const char* s = getenv("OFL_EDEN_OUTERNT"); return !(s && s[0] == '0'); }();
-    return on;
-}
 // 5-pass slices bigger than a wave run their first two and last two passes
 // in MALL-sized sub-waves (OFL_EDEN_BIGSPLIT=0: whole-slice passes)
 bool use_big_split() {
@@ -2931,11 +2916,6 @@ hipError_t set_all_attrs() {
     if ((e = set_col6_attr<9, 15>()) != hipSuccess) return e;
     if ((e = set_col6_attr<10, 15>()) != hipSuccess) return e;
     if ((e = set_lds((const void*)ofl::k_col6<7, true, 15, true>, col6_smem(7, true, 15))) != hipSuccess) return e;
-#define COLNTATTR(MM)                                                                                           \
-    if ((e = set_lds((const void*)ofl::k_col<MM, false, false, true>, col_smem(MM, false))) != hipSuccess) return e; \
-    if ((e = set_lds((const void*)ofl::k_col<MM, false, true, false>, col_smem(MM, false))) != hipSuccess) return e;
-    COLNTATTR(5) COLNTATTR(6) COLNTATTR(7)
-#undef COLNTATTR
     if ((e = set_col6_attr<9, 16>()) != hipSuccess) return e;
     return set_col6_attr<10, 16>();
 }
@@ -3107,16 +3087,6 @@ int run(ofl_eden_plan* pl, bool enc, const ofl::KArgs& base, hipStream_t caller)
                 break;
             }
             const size_t sm = col_smem(l.param, l.mid != 0);
-            if (!l.mid && (l.ntl || l.nts) && l.param >= 5 && l.param <= 7) {
-#define COLNTCASE(MM)                                                                                \
-    case MM:                                                                                         \
-        e = l.nts ? launch(ofl::k_col<MM, false, false, true>, l.blocks, ofl::kColNT, sm, st, a)      \
-                  : launch(ofl::k_col<MM, false, true, false>, l.blocks, ofl::kColNT, sm, st, a);     \
-        break;
-                switch (l.param) { COLNTCASE(5) COLNTCASE(6) COLNTCASE(7) }
-#undef COLNTCASE
-                break;
-            }
 #define COLCASE(MM)                                                                                  \
     case MM:                                                                                         \
         e = l.mid ? launch(ofl::k_col<MM, true>, l.blocks, ofl::kColNT, sm, st, a)                   \
@@ -3404,13 +3374,8 @@ void build_schedule(ofl_eden_plan* pl) {
                     l.stream = s;
                     return l;
                 };
-                auto coll = [&](const SubWave& sw, bool before_mid) {
+                auto coll = [&](const SubWave& sw) {
                     Launch l{K_COL, m1, ofl::kRowLog, 0, lo_c, tp, 1, sw.n_all};
-                    // before the middle pass its output waits in HBM: nt
-                    // stores; after it, the middle pass's output comes from
-                    // HBM: nt loads (the other side stays in the MALL)
-                    l.nts = before_mid && use_outer_nt();
-                    l.ntl = !before_mid && use_outer_nt();
                     l.expl = true;
                     l.expl_tiles = sw.n_all;
                     l.btab_off = sw.tab_all;
@@ -3424,7 +3389,7 @@ void build_schedule(ofl_eden_plan* pl) {
                         Launch ra = rowl(K_ROWA, sw, enc && pair);
                         if (!enc) ra.mid = a8;
                         L.push_back(ra);
-                        L.push_back(coll(sw, true));
+                        L.push_back(coll(sw));
                     }
                     Launch mid{K_COL, m2, ofl::kRowLog + m1, 1, lo_c, tp, 1, tiles_all};
                     mid.stream = s;
@@ -3432,7 +3397,7 @@ void build_schedule(ofl_eden_plan* pl) {
                     mid.nu = enc ? 1 : 0;  // after every row-A sub-wave: the slice norm
                     L.push_back(mid);
                     for (const SubWave& sw : sws) {
-                        L.push_back(coll(sw, false));
+                        L.push_back(coll(sw));
                         L.push_back(rowl(K_ROWC, sw, !enc && pair));
                     }
                 }
