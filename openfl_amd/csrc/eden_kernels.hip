@@ -2105,9 +2105,12 @@ DEVI void fetch_ws_half(const KArgs& a, const SliceDesc& D, uint32_t tile, bool 
 #endif
 constexpr int kDiagRowC2 = OFL_DIAG_ROWC2;
 #ifndef OFL_ROWC2_LD_AUX
-#define OFL_ROWC2_LD_AUX 2
+#define OFL_ROWC2_LD_AUX 0
 #endif
-constexpr int kRowC2LdAux = OFL_ROWC2_LD_AUX;  // nt (A/B: -DOFL_ROWC2_LD_AUX=0)
+// the default policy since the arena I/O went nt (round 6: 478.5-479.2 vs
+// 476.7-478.7 GiB/s with nt, profiles/r06_rowc2ld_ab.txt; nt had won at the
+// 2 GiB waves of round 3, profiles/r03_nt_ab.txt)
+constexpr int kRowC2LdAux = OFL_ROWC2_LD_AUX;
 template <bool ROLL>
 __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowC2(KArgs a) {
     using R = RowC2Set;
@@ -2126,9 +2129,8 @@ __global__ __launch_bounds__(kRowNT, 4) void k_enc_rowC2(KArgs a) {
     int si; uint32_t tile;
     locate(t, si, tile);
     float v[64];
-    // the intermediate is read once: nt loads (r03 A/B, profiles/r03_nt_ab.txt:
-    // 597 -> 572 us per 2 GiB wave; the same policy slows k_enc_rowA and
-    // k_dec_rowC by 8-14 %, so only this kernel uses it)
+    // the intermediate's last read: kRowC2LdAux (nt won at round 3's 2 GiB
+    // waves, the default policy at round 6's MALL-sized ones)
     if (ROLL) fetch_ws<kRowC2LdAux>(a, udesc(a.d, si), tile, true, base3, v);
     for (;;) {
         const SliceDesc D = udesc(a.d, si);
