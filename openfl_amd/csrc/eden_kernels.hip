@@ -58,6 +58,9 @@
 
 #define DEVI __device__ __forceinline__
 
+#ifndef OFL_COL_SC1
+#define OFL_COL_SC1 0
+#endif
 // cache policy of the large slices' arena I/O (kIoLdAux / kIoStAux below):
 // nt both ways -- at MALL-sized waves the streamed x / y / plane bytes then
 // do not push a wave's intermediates out of the Infinity Cache (Llama-3-8B
@@ -1163,14 +1166,19 @@ __device__ uint8_t raw_load_u8(rsrc_t r, int voff, int soff, int aux) __asm("llv
 __device__ void raw_store_f32x4(f32x4 v, rsrc_t r, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.store.v4f32");
 __device__ void raw_store_f32(float v, rsrc_t r, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.store.f32");
 
-// Cache policy of the large-slice passes' streaming buffer accesses (aux
-// operand: bit 1 = nt on gfx950).  Tuning constants for A/B builds
-// (tools/build_variant.sh ... -DOFL_LD_AUX=2), not a platform switch.
+// Cache policy of the large-slice passes' intermediate (ws) buffer accesses
+// (aux operand on gfx950: bit 0 = sc0, bit 1 = nt, bit 4 = sc1).  Tuning
+// constants for A/B builds (tools/build_flags_variant.sh ... -DOFL_LD_AUX=2),
+// not a platform switch.  Stores sc1: the line leaves the XCD's L2 as it is
+// written instead of at the kernel boundary, where a pass would otherwise
+// leave up to 32 MiB of dirty L2 behind for the next launch to wait on
+// (Llama-3-8B 483.7-483.9 -> 486.5-488.1 GiB/s, the 1 GiB set 514.6-517.5 ->
+// 525.2-525.6, profiles/r06_sc1_ab.txt)
 #ifndef OFL_LD_AUX
 #define OFL_LD_AUX 0
 #endif
 #ifndef OFL_ST_AUX
-#define OFL_ST_AUX 0
+#define OFL_ST_AUX 16
 #endif
 constexpr int kLdAux = OFL_LD_AUX;
 constexpr int kStAux = OFL_ST_AUX;
@@ -1292,6 +1300,12 @@ DEVI float ws_pld(const float* sw, int logp, uint32_t i) {
     return __uint_as_float(u);
 }
 DEVI void ws_pst(float* sw, int logp, uint32_t i, float v) {
+    // OFL_COL_SC1 (A/B): the column body's stores sc1 as well (a relaxed
+    // agent-scope store is a global_store ... sc1)
+    if constexpr (kWsFmt == 32 && OFL_COL_SC1) {
+        __hip_atomic_store(&sw[i], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     if constexpr (kWsFmt == 32) { sw[i] = v; return; }
     uint8_t* b = reinterpret_cast<uint8_t*>(sw);
     const uint32_t u = __float_as_uint(v);
