@@ -59,7 +59,7 @@
 #define DEVI __device__ __forceinline__
 
 #ifndef OFL_COL_SC1
-#define OFL_COL_SC1 0
+#define OFL_COL_SC1 1
 #endif
 // cache policy of the large slices' arena I/O (kIoLdAux / kIoStAux below):
 // nt both ways -- at MALL-sized waves the streamed x / y / plane bytes then
@@ -1299,10 +1299,13 @@ DEVI float ws_pld(const float* sw, int logp, uint32_t i) {
     if constexpr (kWsFmt == 24) u |= (uint32_t)b[(2ull << logp) + i] << 8;
     return __uint_as_float(u);
 }
+// SC1: a relaxed agent-scope store, i.e. global_store ... sc1 (as the
+// buffer stores' OFL_ST_AUX): the middle passes of col_body (ResNet-50's
+// small slices: 0.245 -> 0.239 ms; on the 2^29 slices' outer level-1 passes
+// it lost 0.3 %, so those keep plain stores; profiles/r06_colsc1_ab.txt)
+template <bool SC1 = false>
 DEVI void ws_pst(float* sw, int logp, uint32_t i, float v) {
-    // OFL_COL_SC1 (A/B): the column body's stores sc1 as well (a relaxed
-    // agent-scope store is a global_store ... sc1)
-    if constexpr (kWsFmt == 32 && OFL_COL_SC1) {
+    if constexpr (kWsFmt == 32 && SC1 && OFL_COL_SC1) {
         __hip_atomic_store(&sw[i], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
@@ -1788,16 +1791,16 @@ DEVI void col_body(const KArgs& a, int b) {
         }
         const uint32_t base1w = opaque(base1);
 #pragma unroll
-        for (int r = 0; r < 32; ++r) ws_pst(w, lgp, map(base1w | LT<CS::L1>::off(r)), v[r]);
+        for (int r = 0; r < 32; ++r) ws_pst<MID>(w, lgp, map(base1w | LT<CS::L1>::off(r)), v[r]);
     } else {
         if constexpr (M > 5) {
             const uint32_t base2 = opaque(LT<CS::L2>::base(tid));
 #pragma unroll
-            for (int r = 0; r < 32; ++r) ws_pst(w, lgp, map(base2 | LT<CS::L2>::off(r)), v[r]);
+            for (int r = 0; r < 32; ++r) ws_pst<MID>(w, lgp, map(base2 | LT<CS::L2>::off(r)), v[r]);
         } else {
             const uint32_t base1w = opaque(base1);
 #pragma unroll
-            for (int r = 0; r < 32; ++r) ws_pst(w, lgp, map(base1w | LT<CS::L1>::off(r)), v[r]);
+            for (int r = 0; r < 32; ++r) ws_pst<MID>(w, lgp, map(base1w | LT<CS::L1>::off(r)), v[r]);
         }
     }
     // The slice norm nu = sqrt(sum of the row pass's partials of x^2)
