@@ -279,3 +279,23 @@ def test_gzip_ranks_to_checks_its_host_buffer():
     assert b"host_dst" in L.ofl_gzip_last_error()
     assert L.ofl_gzip_ranks_to(a, 1000, a, 4096, a, 4095, 8, ctypes.byref(ln), a, 4096, None) == _lib.OFL_EINVAL
     assert b"host_cap" in L.ofl_gzip_last_error()
+
+
+def test_big_slice_sub_waves():
+    """A 5-pass slice bigger than the wave size runs passes 1-2 and 4-5 in
+    sub-waves (explicit tile lists) around one whole-slice middle pass; the
+    sub-waves cover the slice's tiles once per pass.  Plans whose wave holds
+    the slice keep whole-slice passes."""
+    from openfl_amd.codec import EdenPlan
+    split = [(l["name"], l["blocks"]) for l in EdenPlan([1 << 26], 8, wave_mib=64, streams=1).launches(True)]
+    rows_a = [b for n, b in split if n == "ofl::k_enc_rowA2"]
+    rows_c = [b for n, b in split if n.startswith("ofl::k_enc_rowC2")]
+    outer = [b for n, b in split if n == "ofl::k_col<5, false>"]
+    assert len(rows_a) == 4 and sum(rows_a) == 2048 and sum(rows_c) == 2048 and sum(outer) == 2 * 2048
+    mid = [i for i, (n, _) in enumerate(split) if n == "ofl::k_col<6, true>"]
+    assert len(mid) == 1 and split[mid[0]][1] == 2048
+    # every row-A sub-wave (and its level-1 pass) before the middle pass, every row-C one after
+    assert max(i for i, (n, _) in enumerate(split) if n == "ofl::k_enc_rowA2") < mid[0]
+    assert min(i for i, (n, _) in enumerate(split) if n.startswith("ofl::k_enc_rowC2")) > mid[0]
+    whole = [n for n, _ in [(l["name"], l["blocks"]) for l in EdenPlan([1 << 26], 8, wave_mib=4096, streams=1).launches(True)]]
+    assert whole.count("ofl::k_col<5, false>") == 2 and "ofl::k_enc_rowA2" not in whole
