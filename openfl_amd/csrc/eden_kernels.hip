@@ -2828,6 +2828,10 @@ bool use_mid_nt() {
     static const bool on = [] { const char* s = getenv("OFL_EDEN_MIDNT"); return !(s && s[0] == '0'); }();
     return on;
 }
+int64_t big_sub_mib() {
+    static const int64_t v = [] { const char* s = getenv("OFL_EDEN_BIGSUB_MIB"); return (s && *s) ? strtoll(s, nullptr, 10) : 0ll; }();
+    return v;
+}
 // 5-pass slices bigger than a wave run their first two and last two passes
 // in MALL-sized sub-waves (OFL_EDEN_BIGSPLIT=0: whole-slice passes)
 bool use_big_split() {
@@ -3357,7 +3361,9 @@ void build_schedule(ofl_eden_plan* pl) {
             const int p = pl->slices[si].logp, r = p - ofl::kRowLog, m1 = r / 2, m2 = r - m1;
             const int64_t ntile = 1ll << r, sub = 1ll << m1, P = 1ll << (p - 18);
             const int64_t cap_t = cap >> ofl::kRowLog;
-            const int64_t half = (cap_t / 2) / sub * sub;
+            // sub-wave size: the wave size (OFL_EDEN_BIGSUB_MIB overrides, A/B)
+            const int64_t sw_t = big_sub_mib() > 0 ? (big_sub_mib() << 20) / 4 >> ofl::kRowLog : cap_t;
+            const int64_t half = (sw_t / 2) / sub * sub;
             if (half >= sub && cap_t < ntile && ntile <= kRowTabMax && use_row2(2 * std::min(half, P), pl->ncu, pl->row2)) {
                 const bool pair = (pl->pair >= 0 ? pl->pair : pair_mode()) != 0;
                 const int lo_c = add_list(wl);
